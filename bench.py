@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Headline benchmark: KF predict+update steps/s (whole node), 6-state fp32.
+
+A step is one instance-tick (one correct + one predict of one filter); one timed
+iteration ("tick") is one fused fmskf_tick launch over all instances of a GPU.
+Workload (BASELINE.json configs[1] / SURVEY.md 8(d) cfg 2): 2^20 independent
+6-state fp32 KF instances per GPU, inputs (IMU yaw + gyro z + 4 wheel rpm = 16 B
+per instance-tick) pre-generated into an HBM ring of 64 ticks (not timed).  Every
+`--ensemble-every` ticks each rank reduces its ensemble mean/covariance record and,
+for N > 1, all-gathers it over RCCL (the cfg 4 collective).  Weak scaling: per-GPU
+work is fixed as N grows.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "KF predict+update steps/s (whole node), 6-state fp32, at 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic bytes per instance-tick: x r+w 2*6*4, packed P r+w 2*21*4, input 16
+BYTES_PER_STEP = {"kf6": 2 * 6 * 4 + 2 * 21 * 4 + 16}
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(yaw, gz, rpm, sample_s: float):
+    """The oracle's C restatement of the same KF6 tick (OpenMP over instances, -O3,
+    contraction off) timed on this host on a bounded sample."""
+    import numpy as np
+    import fmskf
+    from oracle import oracle as orc
+    n = yaw.shape[1]
+    T = yaw.shape[0]
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
+    threads = orc.max_threads()
+    res = {}
+    for label, nt, budget in (("all", threads, sample_s), ("one", 1, max(1.0, sample_s / 4))):
+        nn = n if nt > 1 else max(4096, n // 16)
+        x = np.zeros((6, nn), np.float32)
+        P = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], nn, 1).copy()
+        ys, gs, rs = (np.ascontiguousarray(a[:, :nn]) for a in (yaw, gz, rpm))
+        ticks = 0
+        t0 = time.perf_counter()
+        while True:
+            t = ticks % T
+            orc.kf6_tick(x, P, ys[t], gs[t], rs[t], None, prm, nthreads=nt)
+            ticks += 1
+            el = time.perf_counter() - t0
+            if el >= budget and ticks >= 3:
+                break
+        res[label] = (nn * ticks / el, nn, ticks, el)
+    v, nn, ticks, el = res["all"]
+    return {
+        "value": v, "unit": "steps/s", "cores": threads, "kind": "port",
+        "sample": f"{nn} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick, "
+                  f"oracle/fmskf_oracle.c -O3 -ffp-contract=off, OpenMP {threads} threads",
+        "value_1core": res["one"][0],
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--n-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--ring", type=int, default=64)
+    ap.add_argument("--ensemble-every", type=int, default=16)
+    ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
+    ap.add_argument("--cpu-sample-s", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused multi-tick figure")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import fmskf
+    from fmskf.synth import SEED, kf6_ring_torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    n = args.n_per_gpu
+    R = args.ring
+    stream = torch.cuda.current_stream()
+    trig = fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512
+    eng = fmskf.Engine("kf6", n, device=local, trig=trig)
+    eng.set_stream(stream)
+    yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 2 ^ (rank << 8), device=dev)
+    prepared = [eng.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
+    tick_fn = fmskf.load().fmskf_tick
+    rec_len = eng.ensemble_record_len()
+    rec = torch.empty(rec_len, dtype=torch.float64, device=dev)
+    n_events = max(1, (args.steps + args.warmup) // max(1, args.ensemble_every) + 1)
+    gathered = torch.zeros(n_events, world, rec_len, dtype=torch.float64, device=dev)
+    ev_count = [0]
+
+    def step(k):
+        eng.tick_prepared(prepared[k % R], tick_fn)
+        if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
+            eng.ensemble_partial(rec)
+            slot = gathered[ev_count[0] % n_events]
+            if world > 1:
+                dist.all_gather_into_tensor(slot.view(-1), rec)
+            else:
+                slot[0].copy_(rec)
+            ev_count[0] += 1
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    kern_ms_total, kern_cnt = eng.kernel_time_total()
+    eng.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([kern_ms_total / max(1, kern_cnt)], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kern_avg_ms = float(km.item())
+    else:
+        kern_avg_ms = kern_ms_total / max(1, kern_cnt)
+
+    total_steps = n * world * args.steps
+    value = total_steps / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ensemble sanity (outside the timed region): fold the last gathered records in rank order
+    last = gathered[(ev_count[0] - 1) % n_events].cpu().numpy() if ev_count[0] else None
+    ens = None
+    if last is not None:
+        mean, cov = fmskf.ensemble_combine(6, last)
+        ens = {"count": float(last[:, 0].sum()), "mean_theta": float(mean[2]),
+               "var_vx": float(cov[9])}
+    counters = eng.get_counters()
+
+    # secondary figure: the same ring replayed by one fused multi-tick launch per ring pass
+    fused = None
+    if not args.no_fused:
+        e2 = fmskf.Engine("kf6", n, device=local, trig=trig)
+        e2.set_stream(stream)
+        e2.tick_many(R, yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
+        torch.cuda.synchronize()
+        reps = max(1, args.steps // R)
+        ta = time.perf_counter()
+        for _ in range(reps):
+            e2.tick_many(R, yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        fused = {"ticks_per_launch": R, "steps_per_s_per_gpu": n * R * reps / (tb - ta),
+                 "input_bytes_per_step": 16}
+        e2.close()
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("n_instances") == n and tj.get("kernel", "").startswith("k_kf6"):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    bpl = BYTES_PER_STEP["kf6"] * n  # algorithmic bytes per launch (one tick of one GPU)
+    achieved = bpl / (kern_avg_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: WT901 yaw/gyro-z + 4 wheel rpm per robot (fmskf.synth), 64-tick HBM ring",
+        "config": {
+            "workload": "cfg2: 2^20 independent 6-state fp32 KF instances per GPU, fused "
+                        "correct+predict per tick (fmskf_tick)",
+            "instances_per_gpu": n,
+            "global_instances": n * world,
+            "trig": args.trig,
+            "ensemble_every": args.ensemble_every,
+            "parallelism": f"instance-sharded x{world}" + (", RCCL all-gather of ensemble records"
+                                                           if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "bytes_per_step": BYTES_PER_STEP["kf6"],
+            "kernel_ms": kern_avg_ms,
+            "kernel": "k_kf6<false,true,true>",
+        },
+        "cpu_baseline": None,
+        "fused_replay": fused,
+        "ensemble": ens,
+        "nonfinite_instances": int(counters[0]),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        y = yaw[:8, : 1 << 18].cpu().numpy()
+        g = gz[:8, : 1 << 18].cpu().numpy()
+        r = rpm[:8, : 1 << 18].cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline(y, g, r, args.cpu_sample_s)
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

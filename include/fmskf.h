@@ -1,0 +1,206 @@
+/*
+ * fmskf.h -- C ABI of the MI355X batched state-estimation engine (libfmskf.so).
+ *
+ * Drop-in for the IMU + mecanum-odometry fusion path of
+ * Moryu-Io/Roboken-FMSKF-robot-controller, batched over N independent robots
+ * ("instances").  Every per-tick entry point keeps the reference's per-tick call
+ * shape (src/VehicleDrive/VD_task_main.cpp:366-372):
+ *
+ *     can_tx_routine_intr():  set_now_yaw_world(deg2rad(IMT::get_status_now_yaw()));   -> fmskf_correct
+ *                             vhclCtrl.update();                                          -> fmskf_predict
+ *                             (fused: fmskf_tick)
+ *
+ * Plain C: opaque handle, plain pointers and sizes, int status codes, no torch
+ * types, no exceptions across the boundary.  All arrays are caller-owned; the
+ * library never retains a caller pointer after a call returns.  Arrays are
+ * "planes" (structure of arrays): plane k of an array with N instances starts
+ * at element k*N.  `mem` says whether the caller's pointers are host
+ * (FMSKF_MEM_HOST) or device (FMSKF_MEM_DEVICE, on the handle's device).
+ *
+ * Tick entry points are asynchronous on the handle's HIP stream
+ * (fmskf_set_stream); fmskf_sync waits for them.  One handle per host thread;
+ * distinct handles are independent.
+ *
+ * Reference interfaces replaced (file:line in the reference repository):
+ *   IMT::IMU_IF / IMU_IF_WT901C          src/Imu/imu_if_base.hpp:8-32, imu_if_wt901c.hpp:8-42
+ *   IMT::get_status_now_yaw / _imu       src/Imu/imu_task_main.cpp:86-104
+ *   WIT SDK byte input                   lib/wt901c/wit_c_sdk.c:132-198
+ *   VDT::MOTOR_IF_M2006::rx_callback     src/VehicleDrive/VD_motor_if_m2006.cpp:32-72
+ *   VDT::VEHICLE_CTRL::set_now_yaw_world src/VehicleDrive/VD_vehicle_controller.hpp:57
+ *   VDT::VEHICLE_CTRL::update (odometry) src/VehicleDrive/VD_vehicle_controller.cpp:6-51
+ *   VEHICLE_CTRL::get_vehicle_*_latest   src/VehicleDrive/VD_vehicle_controller.hpp:59-60
+ *   VDT::get_status_now_vehicle_pos_world/vel  src/VehicleDrive/VD_task_main.cpp:374-395
+ */
+#ifndef FMSKF_H_
+#define FMSKF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMSKF_ABI_VERSION 1u
+
+/* ---- status codes (every entry point returns one) ------------------------ */
+#define FMSKF_OK 0
+#define FMSKF_EINVAL 1   /* bad argument / shape / state */
+#define FMSKF_ENOMEM 2   /* device or host allocation failed */
+#define FMSKF_EDEVICE 3  /* HIP error, or no usable GPU */
+#define FMSKF_ERCCL 4    /* collective failed (multi-GPU ensemble path) */
+#define FMSKF_ENOTSUP 5  /* entry point not valid for this model */
+
+/* ---- models --------------------------------------------------------------- */
+/* RS: reference semantics.  State = the firmware's VEHICLE_CTRL pose/velocity.
+ *     correct = theta hard overwrite (P == 0, R == 0), predict = the odometry
+ *     integrator bit for bit (VD_vehicle_controller.cpp:11-51).
+ * KF6:  6-state linear KF (px, py, theta, vx, vy, omega), fp32; z = (theta,
+ *       omega, vx_world, vy_world) formed in-kernel from yaw, gyro z, wheel rpm.
+ * EKF9: 9-state EKF (px, py, theta, vbx, vby, omega, gyro bias, abx, aby), fp32,
+ *       nonlinear mecanum f(); z formed in-kernel from 8 raw int16 words.
+ * KF12D: 12-state linear KF in fp64: KF6's base + arm tip (tx, ty, tz, tvx, tvy,
+ *       tvz); z = 8 fp64 (theta, omega, vx_w, vy_w, tx, ty, tz, tvz).          */
+#define FMSKF_MODEL_RS 0u
+#define FMSKF_MODEL_KF6 1u
+#define FMSKF_MODEL_EKF9 2u
+#define FMSKF_MODEL_KF12D 3u
+
+/* sin/cos policy for util_mymath.hpp:44-45 (arm_sin_f32 / arm_cos_f32) */
+#define FMSKF_TRIG_TABLE512 0u /* CMSIS-DSP algorithm: 512-entry table + linear interpolation */
+#define FMSKF_TRIG_LIBM 1u     /* device sinf/cosf */
+
+#define FMSKF_MEM_HOST 0u
+#define FMSKF_MEM_DEVICE 1u
+
+typedef struct fmskf_ctx *fmskf_handle;
+
+typedef struct fmskf_config {
+  uint32_t abi_version;  /* = FMSKF_ABI_VERSION */
+  uint32_t model;        /* FMSKF_MODEL_* */
+  uint64_t n_instances;  /* N */
+  int32_t device;        /* HIP device ordinal */
+  uint32_t trig;         /* FMSKF_TRIG_* */
+  double dt;             /* tick period [s]; the reference ticks at 1 kHz (VD_task_main.cpp:22,165) */
+  /* Noise / initial covariance, packed lower triangle, row-major (k = i*(i+1)/2 + j).
+   * Used by the KF models (n = 6, 9, 12; m = 4, 6, 8); ignored by RS. */
+  double q[78];
+  double r[36];
+  double p0[78];
+  int8_t motor_dir[4];   /* FL, BL, BR, FR: +1 / -1 (VD_task_main.cpp:75-78) */
+  uint32_t imu_read_reg; /* register index for 0x5F REGVALUE frames; init() leaves q0 = 0x51 */
+} fmskf_config;
+
+/* Fill defaults for `model` with `n` instances (dt = 1 ms, TABLE512, reference motor
+ * directions, model-specific Q/R/P0).  Pure host function (no GPU needed). */
+int fmskf_config_init(fmskf_config *cfg, uint32_t model, uint64_t n);
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int fmskf_create(const fmskf_config *cfg, fmskf_handle *out);
+int fmskf_destroy(fmskf_handle h);
+/* Zero-initialised state, as the firmware's static objects at boot
+ * (VD_vehicle_controller.hpp:73-77), P = P0 for KF models. */
+int fmskf_reset(fmskf_handle h);
+int fmskf_set_stream(fmskf_handle h, void *hip_stream); /* hipStream_t; NULL = default */
+int fmskf_sync(fmskf_handle h);
+int fmskf_get_config(fmskf_handle h, fmskf_config *out);
+const char *fmskf_strerror(int status);
+/* last error message of the calling thread ("" if none) */
+const char *fmskf_last_error(void);
+int fmskf_abi_version(void);
+/* state dimension n, measurement dimension m and state element size for a model */
+int fmskf_model_dims(uint32_t model, uint32_t *n, uint32_t *m, uint32_t *elem_bytes);
+
+/* ---- ingest: device boundary --------------------------------------------- */
+/* IMU task tick (IMT::main, imu_task_main.cpp:43-82 at 100 Hz): per instance, feed one
+ * poll's UART bytes through the WT901 parser (wit_c_sdk.c:132-198), then
+ * IMU_IF_WT901C::update (imu_if_wt901c.cpp:83-89): is_error = no quaternion frame
+ * since the last good poll; else refresh the Data page (updateData, :91-129).
+ * bytes: instance i's bytes at bytes + i*stride, len[i] <= stride.
+ * latch_qinit != 0 additionally latches q_init after a good poll (init(), :70-76). */
+int fmskf_ingest_wt901(fmskf_handle h, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
+                       int latch_qinit, uint32_t mem);
+
+/* CAN RX (VD_can_controller.hpp:65-95 -> MOTOR_IF_M2006::rx_callback): frames [N][4][8]
+ * (FL, BL, BR, FR; C610 payload: angle, rpm, current big-endian), stamps [N][4]
+ * (int16 us, micros() & 0x7FFF), present [N] bitmask (bit w = wheel w has a frame;
+ * NULL = all four).  Updates the device-resident motor state. */
+int fmskf_ingest_can(fmskf_handle h, const uint8_t *frames, const int16_t *stamps,
+                     const uint8_t *present, uint32_t mem);
+
+/* ---- per tick -------------------------------------------------------------- */
+/* Inputs of one tick.  Every plane pointer may be NULL: the kernel then reads the
+ * device-resident value the ingest entry points produced (full pipeline). */
+typedef struct fmskf_tick_inputs {
+  uint32_t mem;              /* FMSKF_MEM_HOST or FMSKF_MEM_DEVICE for all pointers below */
+  uint32_t reserved;
+  const float *yaw_deg;      /* [N] IMT::get_status_now_yaw (deg, [-180,180)); RS, KF6 */
+  const float *gyro_z_dps;   /* [N] IMU_IF::Data.gyro[2] (deg/s, as published); KF6 */
+  const int16_t *rpm;        /* [N][4] Status.s16_rawSpeedRpm FL,BL,BR,FR; RS, KF6 */
+  const int64_t *angle_sum;  /* [4][N] MOTOR_IF_M2006::get_rawAngleSum; RS */
+  const int16_t *raw;        /* [N][8] EKF9 words: Yaw, GZ, AX, AY registers, rpm x4 */
+  const double *z;           /* [8][N] KF12D measurements */
+  const uint8_t *valid;      /* [N] measurement present (0 = predict only); NULL = all */
+} fmskf_tick_inputs;
+
+/* correct: RS -> theta = deg2rad(yaw) (VD_task_main.cpp:368); KF models -> update. */
+int fmskf_correct(fmskf_handle h, const fmskf_tick_inputs *in);
+/* predict: RS -> VEHICLE_CTRL::update odometry (VD_vehicle_controller.cpp:11-51);
+ * KF models -> time update (x <- f(x), P <- F P F^T + Q). */
+int fmskf_predict(fmskf_handle h, const fmskf_tick_inputs *in);
+/* fused correct-then-predict, one kernel, one pass over the state (the hot path) */
+int fmskf_tick(fmskf_handle h, const fmskf_tick_inputs *in);
+/* T fused ticks in one launch, state held on chip between ticks.  Inputs are T
+ * consecutive tick records: each plane pointer advances by tick_stride elements
+ * per tick (tick_stride >= N; for [N][k] planes by tick_stride*k). */
+int fmskf_tick_many(fmskf_handle h, const fmskf_tick_inputs *in, uint32_t n_ticks,
+                    uint64_t tick_stride);
+
+/* ---- readout --------------------------------------------------------------- */
+/* VEHICLE_CTRL::get_vehicle_pos_m_latest (x m, y m, th rad).  Any pointer may be NULL. */
+int fmskf_get_pose(fmskf_handle h, float *x, float *y, float *th, uint32_t mem);
+/* VEHICLE_CTRL::get_vehicle_vel_mmps_latest (body frame mm/s, mm/s, rad/s) */
+int fmskf_get_vel(fmskf_handle h, float *vx, float *vy, float *vth, uint32_t mem);
+/* Full model state: x [n][N] and P packed [n(n+1)/2][N] in the model's element type
+ * (float, or double for KF12D); RS: x = (x, y, th, vx, vy, vth) floats, P unused. */
+int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem);
+int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_t mem);
+/* RS: the int64 s64_rawAngleSumPrev [4][N] (VD_vehicle_controller.hpp:75) */
+int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem);
+/* IMU_IF::Data page [16][N] (accel3, gyro3, mag3, angle3, qut4), is_error [N] */
+int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem);
+/* WT901 register file sReg [0x90][N] (int16) and parser bytes pending [N] */
+int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t mem);
+/* Motor state [N][4]: angle, rpm, curr (int16), angle_sum [4][N] int64,
+ * speed_radps [4][N] float (MOTOR_IF_M2006::Status + s64_rawAngleSum) */
+int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr,
+                     int64_t *angle_sum, float *speed_radps, uint32_t mem);
+/* counters: [0] = instances whose state went non-finite (NaN/Inf guard) */
+int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
+
+/* ---- ensemble statistics (mean / covariance of x across instances) --------- */
+/* Record layout: {count, mean[n], M2 packed[n(n+1)/2]} in fp64 (28 doubles for n=6).
+ * fmskf_ensemble_partial writes this rank's record; ranks all-gather the records
+ * (RCCL over xGMI, one process per GPU) and fmskf_ensemble_combine folds them in
+ * rank order -> deterministic.  `out` may be host or device per mem. */
+int fmskf_ensemble_record_len(fmskf_handle h, uint32_t *len);
+int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
+/* host-side: records [n_records][len] -> mean [n], cov packed [n(n+1)/2] (unbiased) */
+int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
+                           double *mean, double *cov_packed);
+
+/* ---- diagnostics ------------------------------------------------------------ */
+/* Evaluate the device sin/cos policy on x[n] (device pointers when mem = DEVICE). */
+int fmskf_eval_trig(fmskf_handle h, const float *x, float *s, float *c, uint64_t n, uint32_t mem);
+/* Per-launch kernel timing with HIP events recorded on the handle's stream around
+ * every tick-kernel launch (enable resets the record).  fmskf_last_kernel_ms: the
+ * last launch; fmskf_kernel_time_total: sum and count of all launches since
+ * enable (waits for the last one).  At most 65536 launches are recorded. */
+int fmskf_set_timing(fmskf_handle h, int enable);
+int fmskf_last_kernel_ms(fmskf_handle h, float *ms);
+int fmskf_kernel_time_total(fmskf_handle h, double *total_ms, uint32_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMSKF_H_ */

@@ -1,0 +1,703 @@
+/*
+ * fmskf_oracle.c -- CPU restatement of the reference hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see fmskf_oracle.h for the parity status of each
+ * row).  Compiled with -ffp-contract=off so every float operation rounds the way
+ * the C++ source of the reference reads (left to right, no fused multiply-add).
+ * Every function cites the reference file:line it restates; paths are relative
+ * to the reference repository root.
+ */
+#include "fmskf_oracle.h"
+
+#include <math.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* Constants                                                                  */
+/* ------------------------------------------------------------------------- */
+/* PI as defined by CMSIS-DSP arm_math.h, used by util_mymath.hpp:13-14 */
+#define ORC_PI_F 3.14159265358979f
+static const float k_deg2rad = ORC_PI_F / 180.0f;                 /* util_mymath.hpp:14 */
+/* VD_motor_if_m2006.hpp:77-82 */
+static const float k_rpm_to_radps = 2.0f * 3.1415926f / 60.0f;
+static const float k_gear_ratio_inv = 1.0f / 36.0f;
+static const float k_out_rad_per_raw = 2.0f * 3.1415926f / 8191.0f;
+#define K_RAW_PER_ROT 8192
+/* VD_vehicle_controller.hpp:82-86 */
+static const float k_wheel_r = 37.5f;
+static const float k_wheel_l = 13.08148f;
+static const float k_sqrtf2 = 1.41421356f;
+/* standard gravity, EKF9 accel scaling (build-defined; the reference keeps g units) */
+static const float k_g0 = 9.80665f;
+
+/* ------------------------------------------------------------------------- */
+/* util_mymath                                                               */
+/* ------------------------------------------------------------------------- */
+float orc_deg2rad(float d) { return d * k_deg2rad; } /* util_mymath.hpp:16 */
+
+/* util_mymath.hpp:18-25 */
+float orc_normalize_rad_0to2pi(float d) {
+  if (d < 0.0f || d >= 2.0f * ORC_PI_F) {
+    int mod = (int)(d / (2.0f * ORC_PI_F));
+    d -= (mod * 2.0f * ORC_PI_F);
+    if (d < 0.0f) d = d + 2.0f * ORC_PI_F;
+  }
+  return d;
+}
+
+/* util_mymath.hpp:27-34 */
+float orc_normalize_deg_0to360(float d) {
+  if (d < 0.0f || d >= 360.0f) {
+    int mod = (int)(d / (360.0f));
+    d -= (mod * 360.0f);
+    if (d < 0.0f) d = d + 360.0f;
+  }
+  return d;
+}
+
+/* CMSIS-DSP arm_sin_f32 / arm_cos_f32 (third-party, absent from the image):
+ * published algorithm = 512-entry sine table over [0, 2pi] plus linear
+ * interpolation.  Table entries computed as (float)sin(2*pi*i/512). */
+static float g_sintab[513];
+static int g_tab_ready = 0;
+
+static void orc_init_tab(void) {
+  if (g_tab_ready) return;
+  for (int i = 0; i <= 512; i++) g_sintab[i] = (float)sin(2.0 * 3.14159265358979323846 * (double)i / 512.0);
+  g_tab_ready = 1;
+}
+
+void orc_sin_table(float out[513]) {
+  orc_init_tab();
+  memcpy(out, g_sintab, sizeof(g_sintab));
+}
+
+static float orc_table_lookup(float in) {
+  int32_t n = (int32_t)in;
+  if (in < 0.0f) n--;
+  in = in - (float)n;
+  float findex = 512.0f * in;
+  uint16_t index = (uint16_t)findex;
+  if (index >= 512) {
+    index = 0;
+    findex -= 512.0f;
+  }
+  float fract = findex - (float)index;
+  float a = g_sintab[index];
+  float b = g_sintab[index + 1];
+  return (1.0f - fract) * a + fract * b;
+}
+
+float orc_sin(float x, int trig) {
+  if (trig == ORC_TRIG_LIBM) return sinf(x);
+  orc_init_tab();
+  return orc_table_lookup(x * 0.159154943092f);
+}
+
+float orc_cos(float x, int trig) {
+  if (trig == ORC_TRIG_LIBM) return cosf(x);
+  orc_init_tab();
+  return orc_table_lookup(x * 0.159154943092f + 0.25f);
+}
+
+void orc_eval_trig(const float *x, float *s, float *c, size_t n, int trig) {
+  for (size_t i = 0; i < n; i++) {
+    s[i] = orc_sin(x[i], trig);
+    c[i] = orc_cos(x[i], trig);
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Mecanum kinematics                                                         */
+/* ------------------------------------------------------------------------- */
+/* VEHICLE_CTRL::conv_Mdir_to_Vdir, VD_vehicle_controller.cpp:126-130 (FL, BL, BR, FR) */
+void orc_mdir_to_vdir(const float m[4], float v[3]) {
+  v[0] = (m[0] + m[1] + m[2] + m[3]) * 0.25f * k_wheel_r;
+  v[1] = (-m[0] + m[1] - m[2] + m[3]) * 0.25f * k_wheel_r;
+  v[2] = (-m[0] - m[1] + m[2] + m[3]) * 0.25f / k_sqrtf2 / k_wheel_l * k_wheel_r;
+}
+
+/* VEHICLE_CTRL::conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 */
+void orc_vdir_to_mdir(const float v[3], float m[4]) {
+  m[0] = (v[0] - v[1] - k_sqrtf2 * k_wheel_l * v[2] * 4.0f) / k_wheel_r;
+  m[1] = (v[0] + v[1] - k_sqrtf2 * k_wheel_l * v[2] * 4.0f) / k_wheel_r;
+  m[2] = (v[0] - v[1] + k_sqrtf2 * k_wheel_l * v[2] * 4.0f) / k_wheel_r;
+  m[3] = (v[0] + v[1] + k_sqrtf2 * k_wheel_l * v[2] * 4.0f) / k_wheel_r;
+}
+
+/* VEHICLE_CTRL::update, VD_vehicle_controller.cpp:21-24: rpm -> motor rad/s */
+static inline float orc_rpm_to_mvel(int16_t rpm) { return (float)rpm * k_rpm_to_radps * k_gear_ratio_inv; }
+
+/* ------------------------------------------------------------------------- */
+/* WT901 parser (lib/wt901c/wit_c_sdk.c) + IMU_IF_WT901C (src/Imu)            */
+/* ------------------------------------------------------------------------- */
+/* register addresses, lib/wt901c/REG.h */
+enum {
+  R_VERSION = 0x2e, R_YYMM = 0x30, R_AX = 0x34, R_AZ = 0x36, R_GX = 0x37, R_GZ = 0x39,
+  R_HX = 0x3a, R_HZ = 0x3c, R_ROLL = 0x3d, R_YAW = 0x3f, R_TEMP = 0x40, R_D0STATUS = 0x41,
+  R_PRESSUREL = 0x45, R_LONL = 0x49, R_GPSHEIGHT = 0x4d, R_Q0 = 0x51, R_Q3 = 0x54, R_SVNUM = 0x55
+};
+/* update flags, imu_if_wt901c.cpp:10-15 */
+enum { F_ACC = 0x01, F_GYRO = 0x02, F_ANGLE = 0x04, F_MAG = 0x08, F_QUAT = 0x10, F_READ = 0x80 };
+
+void orc_wt901_reset(orc_wt901 *s, uint32_t read_reg_index) {
+  memset(s, 0, sizeof(*s));
+  s->read_reg_index = read_reg_index;
+}
+
+/* SensorDataUpdata, imu_if_wt901c.cpp:23-48 */
+static void orc_wt901_cb(orc_wt901 *s, uint32_t reg, uint32_t num) {
+  if (s->ncb < 64) {
+    s->cb_reg[s->ncb] = (uint16_t)reg;
+    s->cb_num[s->ncb] = (uint16_t)num;
+    s->ncb++;
+  }
+  for (uint32_t i = 0; i < num; i++) {
+    switch (reg) {
+      case R_AZ: s->flags |= F_ACC; break;
+      case R_GZ: s->flags |= F_GYRO; break;
+      case R_HZ: s->flags |= F_MAG; break;
+      case R_YAW: s->flags |= F_ANGLE; break;
+      case R_Q3: s->flags |= F_QUAT; break;
+      default: s->flags |= F_READ; break;
+    }
+    reg++;
+  }
+}
+
+/* CopeWitData, wit_c_sdk.c:90-130 */
+static void orc_wt901_cope(orc_wt901 *s, uint8_t type, const uint16_t *data, uint32_t len) {
+  uint32_t reg1 = 0, reg2 = 0, reg1_len = 4, reg2_len = 0;
+  switch (type) {
+    case 0x51: reg1 = R_AX; reg1_len = 3; reg2 = R_TEMP; reg2_len = 1; break;      /* WIT_ACC */
+    case 0x53: reg1 = R_ROLL; reg1_len = 3; reg2 = R_VERSION; reg2_len = 1; break;  /* WIT_ANGLE */
+    case 0x50: reg1 = R_YYMM; break;                                                /* WIT_TIME */
+    case 0x52: reg1 = R_GX; len = 3; break;                                         /* WIT_GYRO */
+    case 0x54: reg1 = R_HX; len = 3; break;                                         /* WIT_MAGNETIC */
+    case 0x55: reg1 = R_D0STATUS; break;                                            /* WIT_DPORT */
+    case 0x56: reg1 = R_PRESSUREL; break;                                           /* WIT_PRESS */
+    case 0x57: reg1 = R_LONL; break;                                                /* WIT_GPS */
+    case 0x58: reg1 = R_GPSHEIGHT; break;                                           /* WIT_VELOCITY */
+    case 0x59: reg1 = R_Q0; break;                                                  /* WIT_QUATER */
+    case 0x5A: reg1 = R_SVNUM; break;                                               /* WIT_GSA */
+    case 0x5F: reg1 = s->read_reg_index; break;                                     /* WIT_REGVALUE */
+    default: return;
+  }
+  if (len == 3) {
+    reg1_len = 3;
+    reg2_len = 0;
+  }
+  if (reg1_len) {
+    for (uint32_t i = 0; i < reg1_len; i++) s->reg[reg1 + i] = (int16_t)data[i];
+    orc_wt901_cb(s, reg1, reg1_len);
+  }
+  if (reg2_len) {
+    for (uint32_t i = 0; i < reg2_len; i++) s->reg[reg2 + i] = (int16_t)data[3 + i];
+    orc_wt901_cb(s, reg2, reg2_len);
+  }
+}
+
+/* 8-bit sum, wit_c_sdk.c:77-83 */
+static uint8_t orc_cali_sum(const uint8_t *d, uint32_t len) {
+  uint8_t c = 0;
+  for (uint32_t i = 0; i < len; i++) c += d[i];
+  return c;
+}
+
+/* WitSerialDataIn, WIT_PROTOCOL_NORMAL branch, wit_c_sdk.c:132-164,197 */
+void orc_wt901_byte(orc_wt901 *s, uint8_t b) {
+  s->buf[s->cnt++] = b;
+  if (s->buf[0] != 0x55) {
+    s->cnt--;
+    memmove(s->buf, &s->buf[1], s->cnt);
+    return;
+  }
+  if (s->cnt >= 11) {
+    uint8_t sum = orc_cali_sum(s->buf, 10);
+    if (sum != s->buf[10]) {
+      s->cnt--;
+      memmove(s->buf, &s->buf[1], s->cnt);
+      return;
+    }
+    uint16_t d[4];
+    d[0] = (uint16_t)(((uint16_t)s->buf[3] << 8) | (uint16_t)s->buf[2]);
+    d[1] = (uint16_t)(((uint16_t)s->buf[5] << 8) | (uint16_t)s->buf[4]);
+    d[2] = (uint16_t)(((uint16_t)s->buf[7] << 8) | (uint16_t)s->buf[6]);
+    d[3] = (uint16_t)(((uint16_t)s->buf[9] << 8) | (uint16_t)s->buf[8]);
+    orc_wt901_cope(s, s->buf[1], d, 4);
+    s->cnt = 0;
+  }
+  if (s->cnt == 256) s->cnt = 0;
+}
+
+/* IMU_IF_WT901C::isComComp, imu_if_wt901c.cpp:132-143 (the GPT1 timeout never fires:
+ * configGENERATE_RUN_TIME_STATS is 0) */
+int orc_wt901_is_com_comp(orc_wt901 *s, const uint8_t *bytes, uint32_t len) {
+  for (uint32_t i = 0; i < len; i++) orc_wt901_byte(s, bytes[i]);
+  if (s->flags & F_QUAT) {
+    s->flags = 0;
+    return 1;
+  }
+  return 0;
+}
+
+/* IMU_IF_WT901C::updateData, imu_if_wt901c.cpp:91-129 */
+void orc_wt901_update_data(orc_wt901 *s) {
+  float acc[3], gyr[3], mag[3], ang[3], q[4];
+  for (int i = 0; i < 3; i++) {
+    acc[i] = (float)s->reg[R_AX + i] / 32768.0f * 16.0f;
+    gyr[i] = (float)s->reg[R_GX + i] / 32768.0f * 2000.0f;
+    mag[i] = (float)s->reg[R_HX + i];
+    ang[i] = (float)s->reg[R_ROLL + i] / 32768.0f * 180.0f;
+  }
+  for (int i = 0; i < 4; i++) q[i] = s->reg[R_Q0 + i] / 32768.0f;
+  float *d = s->data;
+  d[0] = acc[0]; d[1] = -acc[1]; d[2] = -acc[2];
+  d[3] = gyr[0]; d[4] = -gyr[1]; d[5] = -gyr[2];
+  d[6] = mag[0]; d[7] = -mag[1]; d[8] = -mag[2];
+  d[9] = orc_normalize_deg_0to360(ang[0]) - 180.0f;
+  d[10] = ang[1];
+  d[11] = ang[2];
+  const float *qi = s->q_init;
+  d[14] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
+  d[13] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
+  d[12] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
+  d[15] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
+}
+
+/* IMU_IF_WT901C::update, imu_if_wt901c.cpp:83-89; q_init latch per init(), :70-76 */
+void orc_wt901_update(orc_wt901 *s, const uint8_t *bytes, uint32_t len, int latch_qinit) {
+  s->is_error = !orc_wt901_is_com_comp(s, bytes, len);
+  if (!s->is_error) {
+    orc_wt901_update_data(s);
+    if (latch_qinit)
+      for (int i = 0; i < 4; i++) s->q_init[i] = s->reg[R_Q0 + i] / 32768.0f;
+  }
+}
+
+void orc_wt901_update_batch(size_t n, orc_wt901 *s, const uint8_t *bytes, uint32_t stride,
+                            const uint32_t *len, int latch_qinit) {
+  for (size_t i = 0; i < n; i++) orc_wt901_update(&s[i], bytes + i * stride, len[i], latch_qinit);
+}
+
+/* ------------------------------------------------------------------------- */
+/* MOTOR_IF_M2006 (src/VehicleDrive/VD_motor_if_m2006.*)                      */
+/* ------------------------------------------------------------------------- */
+void orc_m2006_reset(orc_m2006 *m, int dir) {
+  memset(m, 0, sizeof(*m));
+  m->dir = (int8_t)dir;
+}
+
+/* couplingU8toS16, VD_motor_if_m2006.hpp:56 */
+static inline int16_t orc_s16(uint8_t h, uint8_t l) { return (int16_t)((h << 8) | l); }
+
+/* int32 multiply with two's-complement wraparound (Cortex-M7 MUL) */
+static inline int32_t orc_mul_wrap(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+/* Cortex-M7 SDIV: x/0 == 0 (CCR.DIV_0_TRP reset value 0), INT_MIN/-1 == INT_MIN */
+static inline int32_t orc_sdiv_arm(int32_t a, int32_t b) {
+  if (b == 0) return 0;
+  if (a == INT32_MIN && b == -1) return INT32_MIN;
+  return a / b;
+}
+
+/* MOTOR_IF_M2006::rx_callback, VD_motor_if_m2006.cpp:32-72.  Only status_buf[status_head]
+ * is observable (get_status_latest, hpp:44-47) and the only other slot rx_callback reads,
+ * so the 3-deep ring is kept as "latest status" plus the head index. */
+void orc_m2006_rx(orc_m2006 *m, const uint8_t f[8], int16_t micro) {
+  uint8_t write_idx = (uint8_t)(m->head + 1);
+  if (write_idx >= 3) write_idx = 0;
+  int16_t old_micro = m->micro, old_angle = m->angle;
+
+  int16_t raw_ang;
+  if (m->dir == 1) raw_ang = orc_s16(f[0], f[1]);
+  else raw_ang = (int16_t)(K_RAW_PER_ROT - orc_s16(f[0], f[1]));
+  int16_t new_angle = raw_ang;
+  int16_t new_rpm = (int16_t)(orc_s16(f[2], f[3]) * m->dir);
+  int16_t new_curr = (int16_t)(orc_s16(f[4], f[5]) * m->dir);
+
+  int32_t raw_ang_dlt = new_angle - old_angle;
+  int32_t usec_dlt = (micro - old_micro);
+  if (raw_ang_dlt > (K_RAW_PER_ROT / 2)) raw_ang_dlt = raw_ang_dlt - K_RAW_PER_ROT;
+  else if (raw_ang_dlt < -(K_RAW_PER_ROT / 2)) raw_ang_dlt = raw_ang_dlt + K_RAW_PER_ROT;
+  if (usec_dlt > 0x7FFF) usec_dlt = usec_dlt - 0x7FFF;
+  else if (usec_dlt < -0x7FFF) usec_dlt = usec_dlt + 0x7FFF;
+
+  int32_t num = orc_mul_wrap(orc_mul_wrap(raw_ang_dlt, 2), 3141593);
+  float x = (float)orc_sdiv_arm(num, usec_dlt) / (float)K_RAW_PER_ROT;
+  /* UTIL::IIR1(0.8, 0.1, 0.1)::update, util_iir.hpp:39-45 */
+  float y = 0.8f * m->iir_prev_y + 0.1f * x + 0.1f * m->iir_prev_x;
+  m->iir_prev_y = y;
+  m->iir_prev_x = x;
+  m->speed_radps = y;
+  m->dlt_out_angle_rad = (float)(new_angle - old_angle) * k_out_rad_per_raw * k_gear_ratio_inv;
+
+  int16_t d = (int16_t)(new_angle - old_angle);
+  d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
+  m->angle_sum = m->angle_sum + d;
+
+  m->micro = micro;
+  m->angle = new_angle;
+  m->rpm = new_rpm;
+  m->curr = new_curr;
+  m->head = write_idx;
+}
+
+void orc_can_ingest_batch(size_t n, orc_m2006 *motors, const uint8_t *frames,
+                          const int16_t *stamps, const uint8_t *present) {
+  for (size_t i = 0; i < n; i++)
+    for (int w = 0; w < 4; w++) {
+      if (present && !((present[i] >> w) & 1)) continue;
+      orc_m2006_rx(&motors[i * 4 + w], frames + (i * 4 + w) * 8, stamps[i * 4 + w]);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Reference-semantics tick: VD_task_main.cpp:366-372 + VEHICLE_CTRL::update   */
+/* ------------------------------------------------------------------------- */
+void orc_rs_tick(size_t n, float *pos, float *vel, int64_t *prev, const float *yaw_deg,
+                 const int64_t *sum, const int16_t *rpm, int trig, int do_correct,
+                 int do_predict) {
+  for (size_t i = 0; i < n; i++) {
+    /* correct: set_now_yaw_world(deg2rad(get_status_now_yaw())), VD_task_main.cpp:368 */
+    if (do_correct) pos[2 * n + i] = orc_deg2rad(yaw_deg[i]);
+    if (!do_predict) continue;
+    /* velocity, VD_vehicle_controller.cpp:21-33 */
+    float mv[4], v[3];
+    for (int w = 0; w < 4; w++) mv[w] = orc_rpm_to_mvel(rpm[i * 4 + w]);
+    orc_mdir_to_vdir(mv, v);
+    vel[i] = v[0];
+    vel[n + i] = v[1];
+    vel[2 * n + i] = v[2];
+    /* odometry, VD_vehicle_controller.cpp:36-51 */
+    float mrad[4], loc[3];
+    for (int w = 0; w < 4; w++) {
+      mrad[w] = (float)((double)(sum[w * n + i] - prev[w * n + i]) * (double)k_out_rad_per_raw *
+                        (double)k_gear_ratio_inv);
+      prev[w * n + i] = sum[w * n + i];
+    }
+    orc_mdir_to_vdir(mrad, loc);
+    float r = orc_normalize_rad_0to2pi(pos[2 * n + i]);
+    float c = orc_cos(r, trig);
+    float s = orc_sin(r, trig);
+    pos[i] = pos[i] + (loc[0] * c - loc[1] * s) * 0.001f;
+    pos[n + i] = pos[n + i] + (loc[0] * s + loc[1] * c) * 0.001f;
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* KF instantiations                                                          */
+/* ------------------------------------------------------------------------- */
+#define REAL float
+#define SFX f32
+#define SQRT sqrtf
+#include "orc_kf_generic.inc"
+#undef REAL
+#undef SFX
+#undef SQRT
+#define REAL double
+#define SFX f64
+#define SQRT sqrt
+#include "orc_kf_generic.inc"
+#undef REAL
+#undef SFX
+#undef SQRT
+
+static inline float orc_wrap_pi_f(float a) {
+  if (a >= ORC_PI_F) a = a - 2.0f * ORC_PI_F;
+  else if (a < -ORC_PI_F) a = a + 2.0f * ORC_PI_F;
+  return a;
+}
+static inline float orc_wrap_innov_f(float a) {
+  if (a > ORC_PI_F) a = a - 2.0f * ORC_PI_F;
+  else if (a < -ORC_PI_F) a = a + 2.0f * ORC_PI_F;
+  return a;
+}
+#define ORC_PI_D 3.141592653589793
+static inline double orc_wrap_pi_d(double a) {
+  if (a >= ORC_PI_D) a = a - 2.0 * ORC_PI_D;
+  else if (a < -ORC_PI_D) a = a + 2.0 * ORC_PI_D;
+  return a;
+}
+static inline double orc_wrap_innov_d(double a) {
+  if (a > ORC_PI_D) a = a - 2.0 * ORC_PI_D;
+  else if (a < -ORC_PI_D) a = a + 2.0 * ORC_PI_D;
+  return a;
+}
+
+/* KF6 measurement frontend: (theta, omega, vx_world, vy_world) from the IMU yaw (deg),
+ * the IMU gyro z as IMU_IF::Data publishes it (deg/s, sign-flipped by
+ * imu_if_wt901c.cpp:113, so omega = -deg2rad(gz)), and the four wheel rpm
+ * (A9/A10 velocity path rotated by the measured heading exactly as the odometry
+ * rotates displacement, VD_vehicle_controller.cpp:47-51). */
+static void orc_kf6_meas1(float yaw, float gz, const int16_t *rpm, int trig, float z[4]) {
+  float th = orc_deg2rad(yaw);
+  float om = -orc_deg2rad(gz);
+  float mv[4], v[3];
+  for (int w = 0; w < 4; w++) mv[w] = orc_rpm_to_mvel(rpm[w]);
+  orc_mdir_to_vdir(mv, v);
+  float r = orc_normalize_rad_0to2pi(th);
+  float c = orc_cos(r, trig), s = orc_sin(r, trig);
+  z[0] = th;
+  z[1] = om;
+  z[2] = (v[0] * c - v[1] * s) * 0.001f;
+  z[3] = (v[0] * s + v[1] * c) * 0.001f;
+}
+
+void orc_kf6_measure(size_t n, const float *yaw_deg, const float *gyro_z_dps,
+                     const int16_t *rpm, float *z, int trig) {
+  for (size_t i = 0; i < n; i++) {
+    float zz[4];
+    orc_kf6_meas1(yaw_deg[i], gyro_z_dps[i], rpm + i * 4, trig, zz);
+    for (int a = 0; a < 4; a++) z[a * n + i] = zz[a];
+  }
+}
+
+static const int k_kf6_h1[4] = {2, 5, 3, 4};
+static const int k_kf6_h2[4] = {-1, -1, -1, -1};
+
+void orc_kf6_tick(size_t n, float *x, float *P, const float *yaw_deg, const float *gyro_z_dps,
+                  const int16_t *rpm, const uint8_t *valid, const orc_kf6_params *prm,
+                  int do_update, int do_predict, int nthreads) {
+  float F[ORC_NMAX][ORC_NMAX];
+  unsigned char pat[ORC_NMAX][ORC_NMAX];
+  memset(F, 0, sizeof(F));
+  memset(pat, 0, sizeof(pat));
+  for (int i = 0; i < 3; i++) {
+    F[i][i + 3] = prm->dt;
+    pat[i][i + 3] = 1;
+  }
+  orc_init_tab();
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+  for (long long ii = 0; ii < (long long)n; ii++) {
+    size_t i = (size_t)ii;
+    float xs[6], Ps[21];
+    for (int k = 0; k < 6; k++) xs[k] = x[k * n + i];
+    for (int k = 0; k < 21; k++) Ps[k] = P[k * n + i];
+    if (do_update && (!valid || valid[i])) {
+      float z[4], y[4];
+      orc_kf6_meas1(yaw_deg[i], gyro_z_dps[i], rpm + i * 4, prm->trig, z);
+      y[0] = orc_wrap_innov_f(z[0] - xs[2]);
+      y[1] = z[1] - xs[5];
+      y[2] = z[2] - xs[3];
+      y[3] = z[3] - xs[4];
+      orc_kf_update_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r);
+    }
+    if (do_predict) {
+      xs[0] = xs[0] + prm->dt * xs[3];
+      xs[1] = xs[1] + prm->dt * xs[4];
+      xs[2] = orc_wrap_pi_f(xs[2] + prm->dt * xs[5]);
+      orc_kf_predict_cov_f32(6, Ps, F, pat, prm->q);
+    }
+    for (int k = 0; k < 6; k++) x[k * n + i] = xs[k];
+    for (int k = 0; k < 21; k++) P[k * n + i] = Ps[k];
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* EKF9: x = (px, py, th, vbx, vby, w, bw, abx, aby), nonlinear mecanum f()   */
+/* ------------------------------------------------------------------------- */
+/* raw words: yaw, gz, ax, ay (WT901 int16 registers Yaw, GZ, AX, AY) + rpm FL BL BR FR */
+static void orc_ekf9_meas1(const int16_t *raw, float z[6]) {
+  /* IMU_IF_WT901C::updateData scaling, imu_if_wt901c.cpp:96-99,107-113 */
+  float yaw = (float)raw[0] / 32768.0f * 180.0f;
+  float gz = (float)raw[1] / 32768.0f * 2000.0f; /* native sensor frame (consistent with yaw) */
+  float ax = (float)raw[2] / 32768.0f * 16.0f;
+  float ay = -((float)raw[3] / 32768.0f * 16.0f);
+  float mv[4], v[3];
+  for (int w = 0; w < 4; w++) mv[w] = orc_rpm_to_mvel(raw[4 + w]);
+  orc_mdir_to_vdir(mv, v);
+  z[0] = orc_deg2rad(yaw);
+  z[1] = orc_deg2rad(gz);
+  z[2] = ax * k_g0;
+  z[3] = ay * k_g0;
+  z[4] = v[0] * 0.001f;
+  z[5] = v[1] * 0.001f;
+}
+
+void orc_ekf9_measure(size_t n, const int16_t *raw, float *z) {
+  for (size_t i = 0; i < n; i++) {
+    float zz[6];
+    orc_ekf9_meas1(raw + i * 8, zz);
+    for (int a = 0; a < 6; a++) z[a * n + i] = zz[a];
+  }
+}
+
+static const int k_ekf9_h1[6] = {2, 5, 7, 8, 3, 4};
+static const int k_ekf9_h2[6] = {-1, 6, -1, -1, -1, -1};
+
+void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8_t *valid,
+                   const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads) {
+  unsigned char pat[ORC_NMAX][ORC_NMAX];
+  memset(pat, 0, sizeof(pat));
+  pat[0][2] = pat[0][3] = pat[0][4] = 1;
+  pat[1][2] = pat[1][3] = pat[1][4] = 1;
+  pat[2][5] = 1;
+  pat[3][7] = 1;
+  pat[4][8] = 1;
+  orc_init_tab();
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+  for (long long ii = 0; ii < (long long)n; ii++) {
+    size_t i = (size_t)ii;
+    float xs[9], Ps[45];
+    for (int k = 0; k < 9; k++) xs[k] = x[k * n + i];
+    for (int k = 0; k < 45; k++) Ps[k] = P[k * n + i];
+    if (do_update && (!valid || valid[i])) {
+      float z[6], y[6];
+      orc_ekf9_meas1(raw + i * 8, z);
+      y[0] = orc_wrap_innov_f(z[0] - xs[2]);
+      y[1] = z[1] - (xs[5] + xs[6]);
+      y[2] = z[2] - xs[7];
+      y[3] = z[3] - xs[8];
+      y[4] = z[4] - xs[3];
+      y[5] = z[5] - xs[4];
+      orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
+    }
+    if (do_predict) {
+      float dt = prm->dt;
+      float r = orc_normalize_rad_0to2pi(xs[2]);
+      float c = orc_cos(r, prm->trig), s = orc_sin(r, prm->trig);
+      float vwx = xs[3] * c - xs[4] * s;
+      float vwy = xs[3] * s + xs[4] * c;
+      float F[ORC_NMAX][ORC_NMAX];
+      memset(F, 0, sizeof(F));
+      F[0][2] = -(vwy * dt);
+      F[0][3] = c * dt;
+      F[0][4] = -(s * dt);
+      F[1][2] = vwx * dt;
+      F[1][3] = s * dt;
+      F[1][4] = c * dt;
+      F[2][5] = dt;
+      F[3][7] = dt;
+      F[4][8] = dt;
+      xs[0] = xs[0] + vwx * dt;
+      xs[1] = xs[1] + vwy * dt;
+      xs[2] = orc_wrap_pi_f(xs[2] + xs[5] * dt);
+      xs[3] = xs[3] + xs[7] * dt;
+      xs[4] = xs[4] + xs[8] * dt;
+      orc_kf_predict_cov_f32(9, Ps, F, pat, prm->q);
+    }
+    for (int k = 0; k < 9; k++) x[k * n + i] = xs[k];
+    for (int k = 0; k < 45; k++) P[k * n + i] = Ps[k];
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* KF12D: base (px,py,th,vx,vy,w) + arm tip (tx,ty,tz,tvx,tvy,tvz), fp64       */
+/* z = (theta, omega, vx_w, vy_w, tx, ty, tz, tvz)                             */
+/* ------------------------------------------------------------------------- */
+static const int k_kf12_h1[8] = {2, 5, 3, 4, 6, 7, 8, 11};
+static const int k_kf12_h2[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+
+void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8_t *valid,
+                    const orc_kf12d_params *prm, int do_update, int do_predict, int nthreads) {
+  double F[ORC_NMAX][ORC_NMAX];
+  unsigned char pat[ORC_NMAX][ORC_NMAX];
+  memset(F, 0, sizeof(F));
+  memset(pat, 0, sizeof(pat));
+  const int pos[6] = {0, 1, 2, 6, 7, 8};
+  for (int a = 0; a < 6; a++) {
+    F[pos[a]][pos[a] + 3] = prm->dt;
+    pat[pos[a]][pos[a] + 3] = 1;
+  }
+#ifdef _OPENMP
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
+  for (long long ii = 0; ii < (long long)n; ii++) {
+    size_t i = (size_t)ii;
+    double xs[12], Ps[78];
+    for (int k = 0; k < 12; k++) xs[k] = x[k * n + i];
+    for (int k = 0; k < 78; k++) Ps[k] = P[k * n + i];
+    if (do_update && (!valid || valid[i])) {
+      double y[8];
+      for (int a = 0; a < 8; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
+      y[0] = orc_wrap_innov_d(y[0]);
+      orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r);
+    }
+    if (do_predict) {
+      for (int a = 0; a < 6; a++) xs[pos[a]] = xs[pos[a]] + prm->dt * xs[pos[a] + 3];
+      xs[2] = orc_wrap_pi_d(xs[2]);
+      orc_kf_predict_cov_f64(12, Ps, F, pat, prm->q);
+    }
+    for (int k = 0; k < 12; k++) x[k * n + i] = xs[k];
+    for (int k = 0; k < 78; k++) P[k * n + i] = Ps[k];
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Ensemble statistics (mean + covariance across instances)                   */
+/* ------------------------------------------------------------------------- */
+size_t orc_ens_record_len(int nx) { return 1 + (size_t)nx + (size_t)nx * (nx + 1) / 2; }
+
+#define ENS_PARTIAL_BODY(GET)                                                     \
+  size_t len = orc_ens_record_len(nx);                                            \
+  memset(rec, 0, len * sizeof(double));                                           \
+  double cnt = (double)(hi - lo);                                                 \
+  rec[0] = cnt;                                                                   \
+  if (hi <= lo) return;                                                           \
+  double *mean = rec + 1, *m2 = rec + 1 + nx;                                     \
+  for (int a = 0; a < nx; a++) {                                                  \
+    double s = 0.0;                                                               \
+    for (size_t i = lo; i < hi; i++) s += (double)GET(a, i);                      \
+    mean[a] = s / cnt;                                                            \
+  }                                                                               \
+  for (int a = 0; a < nx; a++)                                                    \
+    for (int b = 0; b <= a; b++) {                                                \
+      double s = 0.0;                                                             \
+      for (size_t i = lo; i < hi; i++)                                            \
+        s += ((double)GET(a, i) - mean[a]) * ((double)GET(b, i) - mean[b]);       \
+      m2[a * (a + 1) / 2 + b] = s;                                                \
+    }
+
+#define GETX(a, i) x[(size_t)(a) * n + (i)]
+void orc_ens_partial_f32(size_t n, int nx, const float *x, size_t lo, size_t hi, double *rec) {
+  ENS_PARTIAL_BODY(GETX)
+}
+void orc_ens_partial_f64(size_t n, int nx, const double *x, size_t lo, size_t hi, double *rec) {
+  ENS_PARTIAL_BODY(GETX)
+}
+#undef GETX
+
+/* Chan, Golub & LeVeque pairwise combination */
+void orc_ens_combine(int nx, const double *a, const double *b, double *out) {
+  size_t len = orc_ens_record_len(nx);
+  double na = a[0], nb = b[0], nn = na + nb;
+  double tmp[1 + 12 + 78];
+  if (na == 0.0) { memcpy(out, b, len * sizeof(double)); return; }
+  if (nb == 0.0) { memcpy(out, a, len * sizeof(double)); return; }
+  double d[12];
+  for (int i = 0; i < nx; i++) d[i] = b[1 + i] - a[1 + i];
+  tmp[0] = nn;
+  for (int i = 0; i < nx; i++) tmp[1 + i] = a[1 + i] + d[i] * (nb / nn);
+  double f = na * nb / nn;
+  for (int i = 0; i < nx; i++)
+    for (int j = 0; j <= i; j++) {
+      int k = i * (i + 1) / 2 + j;
+      tmp[1 + nx + k] = a[1 + nx + k] + b[1 + nx + k] + d[i] * d[j] * f;
+    }
+  memcpy(out, tmp, len * sizeof(double));
+}
+
+void orc_ens_finalize(int nx, const double *rec, double *mean, double *cov_packed) {
+  double cnt = rec[0];
+  for (int i = 0; i < nx; i++) mean[i] = rec[1 + i];
+  int np = nx * (nx + 1) / 2;
+  for (int k = 0; k < np; k++) cov_packed[k] = cnt > 1.0 ? rec[1 + nx + k] / (cnt - 1.0) : 0.0;
+}
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

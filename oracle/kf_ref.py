@@ -1,0 +1,159 @@
+"""Independent float64 dense restatement of the KF / EKF math (TEST INFRASTRUCTURE ONLY).
+
+The KF path has no reference counterpart (the firmware
+contains no Kalman filter); the north star defines it as
+
+    predict:  x <- F x  (EKF: x <- f(x)),   P <- F P F^T + Q
+    update:   S = H P H^T + R,  K = P H^T S^-1,  x += K y,  P -= K H P
+
+This module evaluates exactly those textbook formulas with dense numpy float64
+matrices (np.linalg.solve for S^-1, Joseph-stabilised P update), independently of
+the Cholesky/packed formulation the oracle and the kernels share, so it checks the
+math of both.  Measurements z are taken as given (the fp32 measurement frontends
+are pinned separately).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def unpack(p, n):
+    M = np.zeros((n, n))
+    k = 0
+    for i in range(n):
+        for j in range(i + 1):
+            M[i, j] = M[j, i] = p[k]
+            k += 1
+    return M
+
+
+def pack(M):
+    n = M.shape[0]
+    return np.array([M[i, j] for i in range(n) for j in range(i + 1)])
+
+
+def wrap_pi(a):
+    return (a + np.pi) % (2 * np.pi) - np.pi
+
+
+def kf_update(x, P, H, R, y):
+    S = H @ P @ H.T + R
+    K = np.linalg.solve(S, H @ P).T          # P H^T S^-1  (S symmetric)
+    x = x + K @ y
+    I_KH = np.eye(len(x)) - K @ H
+    P = I_KH @ P @ I_KH.T + K @ R @ K.T     # Joseph form == P - K H P
+    return x, P
+
+
+# ----------------------------------------------------------------------------- KF6
+def kf6_matrices(dt):
+    F = np.eye(6)
+    for i in range(3):
+        F[i, i + 3] = dt
+    H = np.zeros((4, 6))
+    for a, s in enumerate((2, 5, 3, 4)):
+        H[a, s] = 1.0
+    return F, H
+
+
+def kf6_run(x0, P0p, z_seq, q_packed, r_packed, dt, valid=None):
+    """x0 [6], P0 packed [21], z_seq [T, 4] -> list of (x, P packed) after each tick."""
+    F, H = kf6_matrices(dt)
+    Q, R = unpack(q_packed, 6), unpack(r_packed, 4)
+    x, P = np.array(x0, float), unpack(P0p, 6)
+    out = []
+    for t, z in enumerate(z_seq):
+        if valid is None or valid[t]:
+            y = z - H @ x
+            y[0] = _wrap_innov(y[0])
+            x, P = kf_update(x, P, H, R, y)
+        x = F @ x
+        x[2] = _wrap_state(x[2])
+        P = F @ P @ F.T + Q
+        out.append((x.copy(), pack(P)))
+    return out
+
+
+def _wrap_innov(a):
+    if a > np.pi:
+        return a - 2 * np.pi
+    if a < -np.pi:
+        return a + 2 * np.pi
+    return a
+
+
+def _wrap_state(a):
+    if a >= np.pi:
+        return a - 2 * np.pi
+    if a < -np.pi:
+        return a + 2 * np.pi
+    return a
+
+
+# ----------------------------------------------------------------------------- EKF9
+def ekf9_H():
+    H = np.zeros((6, 9))
+    H[0, 2] = 1
+    H[1, 5] = 1
+    H[1, 6] = 1
+    H[2, 7] = 1
+    H[3, 8] = 1
+    H[4, 3] = 1
+    H[5, 4] = 1
+    return H
+
+
+def ekf9_run(x0, P0p, z_seq, q_packed, r_packed, dt):
+    H = ekf9_H()
+    Q, R = unpack(q_packed, 9), unpack(r_packed, 6)
+    x, P = np.array(x0, float), unpack(P0p, 9)
+    out = []
+    for z in z_seq:
+        y = z - H @ x
+        y[0] = _wrap_innov(y[0])
+        x, P = kf_update(x, P, H, R, y)
+        th, vbx, vby = x[2], x[3], x[4]
+        c, s = np.cos(th), np.sin(th)
+        vwx, vwy = vbx * c - vby * s, vbx * s + vby * c
+        F = np.eye(9)
+        F[0, 2], F[0, 3], F[0, 4] = -vwy * dt, c * dt, -s * dt
+        F[1, 2], F[1, 3], F[1, 4] = vwx * dt, s * dt, c * dt
+        F[2, 5] = dt
+        F[3, 7] = dt
+        F[4, 8] = dt
+        x = x.copy()
+        x[0] += vwx * dt
+        x[1] += vwy * dt
+        x[2] = _wrap_state(x[2] + x[5] * dt)
+        x[3] += x[7] * dt
+        x[4] += x[8] * dt
+        P = F @ P @ F.T + Q
+        out.append((x.copy(), pack(P)))
+    return out
+
+
+# ----------------------------------------------------------------------------- KF12D
+def kf12d_matrices(dt):
+    F = np.eye(12)
+    for p in (0, 1, 2, 6, 7, 8):
+        F[p, p + 3] = dt
+    H = np.zeros((8, 12))
+    for a, s in enumerate((2, 5, 3, 4, 6, 7, 8, 11)):
+        H[a, s] = 1.0
+    return F, H
+
+
+def kf12d_run(x0, P0p, z_seq, q_packed, r_packed, dt):
+    F, H = kf12d_matrices(dt)
+    Q, R = unpack(q_packed, 12), unpack(r_packed, 8)
+    x, P = np.array(x0, float), unpack(P0p, 12)
+    out = []
+    for z in z_seq:
+        y = z - H @ x
+        y[0] = _wrap_innov(y[0])
+        x, P = kf_update(x, P, H, R, y)
+        x = F @ x
+        x[2] = _wrap_state(x[2])
+        P = F @ P @ F.T + Q
+        out.append((x.copy(), pack(P)))
+    return out

@@ -1,0 +1,854 @@
+// fmskf_api.cpp -- the C ABI (include/fmskf.h) over the HIP kernels.
+//
+// Owns the device SoA state of a handle, resolves NULL input planes to the
+// device-resident ingest state (full pipeline), stages host inputs with async
+// copies on the handle's stream, validates shapes, and converts every failure to
+// a status code (no exception crosses the ABI).  No CPU fallback exists: every
+// compute entry point launches a HIP kernel or fails with FMSKF_EDEVICE.
+#include "../../include/fmskf.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "fmskf_internal.hpp"
+
+using namespace fmskf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct ApiError {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string &msg) { throw ApiError{code, msg}; }
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) fail(FMSKF_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+void launch_check(int e, const char *what) { hip_check((hipError_t)e, what); }
+
+template <class F>
+int guarded(F &&f) {
+  try {
+    g_last_error.clear();
+    f();
+    return FMSKF_OK;
+  } catch (const ApiError &e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    g_last_error = "host allocation failed";
+    return FMSKF_ENOMEM;
+  } catch (...) {
+    g_last_error = "unexpected exception";
+    return FMSKF_EDEVICE;
+  }
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+struct Dims {
+  uint32_t nx, m, elem;
+};
+
+Dims dims_of(uint32_t model) {
+  switch (model) {
+    case FMSKF_MODEL_RS: return {6, 0, 4};
+    case FMSKF_MODEL_KF6: return {6, 4, 4};
+    case FMSKF_MODEL_EKF9: return {9, 6, 4};
+    case FMSKF_MODEL_KF12D: return {12, 8, 8};
+    default: fail(FMSKF_EINVAL, "unknown model");
+  }
+}
+
+}  // namespace
+
+struct fmskf_ctx {
+  fmskf_config cfg{};
+  Dims d{};
+  DevState s{};
+  hipStream_t stream = nullptr;
+  std::vector<void *> allocs;
+  // staging for host-resident inputs
+  void *stage = nullptr;
+  size_t stage_bytes = 0;
+  // ensemble scratch
+  double *ens_blocks = nullptr;
+  double *ens_out = nullptr;
+  // readout scratch [6][N] float
+  float *readout = nullptr;
+  // model parameters (fp32 / fp64 copies of cfg)
+  Kf6Params kf6{};
+  Ekf9Params ekf9{};
+  Kf12dParams kf12{};
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // pooled per-launch events (fmskf_kernel_time_total)
+  std::vector<hipEvent_t> tpool;
+  size_t tcount = 0;
+  static constexpr size_t kMaxTimed = 65536;
+
+  void time_begin() {
+    if (!timing) return;
+    if (tcount < kMaxTimed) {
+      while (tpool.size() < 2 * (tcount + 1)) {
+        hipEvent_t e;
+        hip_check(hipEventCreate(&e), "hipEventCreate");
+        tpool.push_back(e);
+      }
+      hip_check(hipEventRecord(tpool[2 * tcount], stream), "hipEventRecord");
+    }
+    hip_check(hipEventRecord(ev0, stream), "hipEventRecord");
+  }
+  void time_end() {
+    if (!timing) return;
+    hip_check(hipEventRecord(ev1, stream), "hipEventRecord");
+    if (tcount < kMaxTimed) {
+      hip_check(hipEventRecord(tpool[2 * tcount + 1], stream), "hipEventRecord");
+      tcount++;
+    }
+  }
+
+  template <typename T>
+  T *alloc(size_t count) {
+    void *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e != hipSuccess) fail(FMSKF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    allocs.push_back(p);
+    return (T *)p;
+  }
+  void *stage_for(size_t bytes) {
+    if (bytes > stage_bytes) {
+      if (stage) {
+        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        hip_check(hipFree(stage), "hipFree");
+        stage = nullptr;
+      }
+      hipError_t e = hipMalloc(&stage, bytes);
+      if (e != hipSuccess) fail(FMSKF_ENOMEM, "staging hipMalloc failed");
+      stage_bytes = bytes;
+    }
+    return stage;
+  }
+  ~fmskf_ctx() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    else (void)hipDeviceSynchronize();
+    for (void *p : allocs) (void)hipFree(p);
+    if (stage) (void)hipFree(stage);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    for (hipEvent_t e : tpool) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+void check_handle(fmskf_handle h) {
+  if (!h) fail(FMSKF_EINVAL, "null handle");
+}
+
+// Host->device staging of a set of planes; returns device pointers.
+struct Stager {
+  fmskf_ctx *h;
+  bool host;
+  std::vector<std::pair<const void **, size_t>> items;
+  Stager(fmskf_ctx *hh, uint32_t mem) : h(hh), host(mem == FMSKF_MEM_HOST) {
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+  }
+  void add(const void **p, size_t bytes) {
+    if (*p && host) items.push_back({p, bytes});
+  }
+  void run() {
+    if (!host || items.empty()) return;
+    size_t total = 0;
+    for (auto &it : items) total += (it.second + 255) & ~size_t(255);
+    char *base = (char *)h->stage_for(total);
+    size_t off = 0;
+    for (auto &it : items) {
+      hip_check(hipMemcpyAsync(base + off, *it.first, it.second, hipMemcpyHostToDevice, h->stream),
+                "stage H2D");
+      *it.first = base + off;
+      off += (it.second + 255) & ~size_t(255);
+    }
+  }
+};
+
+void apply_defaults(fmskf_config *c, uint32_t model, uint64_t n) {
+  memset(c, 0, sizeof(*c));
+  c->abi_version = FMSKF_ABI_VERSION;
+  c->model = model;
+  c->n_instances = n;
+  c->device = 0;
+  c->trig = FMSKF_TRIG_TABLE512;
+  c->dt = 0.001;
+  c->motor_dir[0] = 1;   // FL  (VD_task_main.cpp:75)
+  c->motor_dir[1] = 1;   // BL  (:76)
+  c->motor_dir[2] = -1;  // BR  (:77)
+  c->motor_dir[3] = -1;  // FR  (:78)
+  c->imu_read_reg = 0x51;  // q0: IMU_IF_WT901C::init -> WitReadReg(q0, 4)
+  const double dt = c->dt;
+  auto setq = [&](int i, int j, double v) { c->q[i * (i + 1) / 2 + j] = v; };
+  auto setr = [&](int i, int j, double v) { c->r[i * (i + 1) / 2 + j] = v; };
+  auto setp = [&](int i, double v) { c->p0[i * (i + 1) / 2 + i] = v; };
+  // discretised white-noise-acceleration blocks for a (pos, vel) pair with density qc
+  auto cv_block = [&](int p, int v, double qc) {
+    setq(p, p, qc * dt * dt * dt / 3.0);
+    setq(v, p, qc * dt * dt / 2.0);
+    setq(v, v, qc * dt);
+  };
+  switch (model) {
+    case FMSKF_MODEL_KF6:
+      cv_block(0, 3, 4.0);
+      cv_block(1, 4, 4.0);
+      cv_block(2, 5, 100.0);
+      setr(0, 0, 2.5e-5);  // yaw (5 mrad)^2
+      setr(1, 1, 2.5e-3);  // gyro (0.05 rad/s)^2
+      setr(2, 2, 4e-4);    // wheel velocity (2 cm/s)^2
+      setr(3, 3, 4e-4);
+      setr(3, 2, 1e-5);
+      for (int i = 0; i < 6; i++) setp(i, i < 3 ? 1.0 : 0.25);
+      break;
+    case FMSKF_MODEL_EKF9: {
+      const double qd[9] = {1e-10, 1e-10, 1e-10, 4e-3 * dt, 4e-3 * dt, 100.0 * dt, 1e-12, 2500.0 * dt, 2500.0 * dt};
+      for (int i = 0; i < 9; i++) setq(i, i, qd[i]);
+      const double rd[6] = {2.5e-5, 2.5e-3, 0.25, 0.25, 4e-4, 4e-4};
+      for (int i = 0; i < 6; i++) setr(i, i, rd[i]);
+      for (int i = 0; i < 9; i++) setp(i, i < 3 ? 1.0 : (i == 6 ? 1e-2 : 0.25));
+      break;
+    }
+    case FMSKF_MODEL_KF12D: {
+      cv_block(0, 3, 4.0);
+      cv_block(1, 4, 4.0);
+      cv_block(2, 5, 100.0);
+      cv_block(6, 9, 1.0);
+      cv_block(7, 10, 1.0);
+      cv_block(8, 11, 1.0);
+      const double rd[8] = {2.5e-5, 2.5e-3, 4e-4, 4e-4, 1e-6, 1e-6, 1e-6, 1e-4};
+      for (int i = 0; i < 8; i++) setr(i, i, rd[i]);
+      setr(3, 2, 1e-5);
+      for (int i = 0; i < 12; i++) setp(i, (i % 6) < 3 ? 1.0 : 0.25);
+      break;
+    }
+    default: break;
+  }
+}
+
+void convert_params(fmskf_ctx *h) {
+  const fmskf_config &c = h->cfg;
+  h->kf6.dt = (float)c.dt;
+  for (int k = 0; k < 21; k++) h->kf6.q[k] = (float)c.q[k];
+  for (int k = 0; k < 10; k++) h->kf6.r[k] = (float)c.r[k];
+  h->ekf9.dt = (float)c.dt;
+  for (int k = 0; k < 45; k++) h->ekf9.q[k] = (float)c.q[k];
+  for (int k = 0; k < 21; k++) h->ekf9.r[k] = (float)c.r[k];
+  h->kf12.dt = c.dt;
+  for (int k = 0; k < 78; k++) h->kf12.q[k] = c.q[k];
+  for (int k = 0; k < 36; k++) h->kf12.r[k] = c.r[k];
+}
+
+void do_reset(fmskf_ctx *h) {
+  DevState &s = h->s;
+  const uint64_t n = s.n;
+  const Dims d = h->d;
+  const uint32_t np = d.nx * (d.nx + 1) / 2;
+  hipStream_t st = h->stream;
+  hip_check(hipMemsetAsync(s.x, 0, (size_t)d.nx * n * d.elem, st), "reset x");
+  if (d.m > 0) {
+    hip_check(hipMemsetAsync(s.P, 0, (size_t)np * n * d.elem, st), "reset P");
+    for (uint32_t i = 0; i < d.nx; i++) {
+      for (uint32_t j = 0; j <= i; j++) {
+        const double v = h->cfg.p0[i * (i + 1) / 2 + j];
+        if (v == 0.0) continue;
+        const size_t k = i * (i + 1) / 2 + j;
+        if (d.elem == 4) {
+          float f = (float)v;
+          uint32_t bits;
+          memcpy(&bits, &f, 4);
+          hip_check(hipMemsetD32Async((hipDeviceptr_t)((float *)s.P + k * n), bits, n, st), "reset P0");
+        } else {
+          uint64_t bits;
+          memcpy(&bits, &v, 8);
+          launch_check(launch_fill64((double *)s.P + k * n, bits, n, st), "reset P0");
+        }
+      }
+    }
+  }
+  if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * n * 8, st), "reset prev");
+  hip_check(hipMemsetAsync(s.imu_reg, 0, 0x90 * n * 2, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_parser, 0, 3 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_cnt, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_flags, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_data, 0, 16 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.m_micro, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_angle, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * n * 8, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_dlt, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.counters, 0, 8 * 8, st), "reset counters");
+}
+
+// Resolve the tick inputs of a call (NULL -> device-resident ingest state), stage host
+// planes and validate what the model needs.
+TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, bool need_pred,
+                      uint32_t n_ticks, uint64_t stride) {
+  if (!in) fail(FMSKF_EINVAL, "null inputs");
+  DevState &s = h->s;
+  const uint64_t n = s.n;
+  if (stride < n) fail(FMSKF_EINVAL, "tick_stride < N");
+  if (n_ticks == 0) fail(FMSKF_EINVAL, "n_ticks == 0");
+  TickIn t{};
+  t.yaw_deg = in->yaw_deg;
+  t.gyro_z = in->gyro_z_dps;
+  t.rpm = in->rpm;
+  t.angle_sum = in->angle_sum;
+  t.raw = in->raw;
+  t.z = in->z;
+  t.valid = in->valid;
+  t.sintab = s.sintab;
+  t.stride = stride;
+  t.n_ticks = n_ticks;
+  const uint64_t span = (uint64_t)(n_ticks - 1) * stride + n;  // elements per [N] plane
+  Stager sg(h, in->mem);
+  sg.add((const void **)&t.yaw_deg, span * 4);
+  sg.add((const void **)&t.gyro_z, span * 4);
+  sg.add((const void **)&t.rpm, span * 8);
+  sg.add((const void **)&t.angle_sum, ((uint64_t)(n_ticks - 1) * stride * 4 + 3 * stride + n) * 8);
+  sg.add((const void **)&t.raw, span * 16);
+  sg.add((const void **)&t.z, ((uint64_t)(n_ticks - 1) * stride * 8 + 7 * stride + n) * 8);
+  sg.add((const void **)&t.valid, span);
+  sg.run();
+  const bool many = n_ticks > 1 || stride != n;
+  auto dev_default = [&](const void *p, const char *name) {
+    if (!p && many) fail(FMSKF_EINVAL, std::string("tick_many needs explicit plane ") + name);
+  };
+  switch (h->cfg.model) {
+    case FMSKF_MODEL_RS:
+      if (need_upd) {
+        dev_default(t.yaw_deg, "yaw_deg");
+        if (!t.yaw_deg) t.yaw_deg = s.imu_data + 11 * n;  // IMT::get_status_now_yaw
+      }
+      if (need_pred) {
+        dev_default(t.rpm, "rpm");
+        dev_default(t.angle_sum, "angle_sum");
+        if (!t.rpm) t.rpm = s.m_rpm;
+        if (!t.angle_sum) t.angle_sum = s.m_sum;
+      }
+      break;
+    case FMSKF_MODEL_KF6:
+      if (need_upd) {
+        dev_default(t.yaw_deg, "yaw_deg");
+        dev_default(t.gyro_z, "gyro_z_dps");
+        dev_default(t.rpm, "rpm");
+        if (!t.yaw_deg) t.yaw_deg = s.imu_data + 11 * n;
+        if (!t.gyro_z) t.gyro_z = s.imu_data + 5 * n;
+        if (!t.rpm) t.rpm = s.m_rpm;
+      }
+      break;
+    case FMSKF_MODEL_EKF9:
+      if (need_upd && !t.raw) fail(FMSKF_EINVAL, "EKF9 needs raw words");
+      break;
+    case FMSKF_MODEL_KF12D:
+      if (need_upd && !t.z) fail(FMSKF_EINVAL, "KF12D needs z");
+      break;
+  }
+  return t;
+}
+
+void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, uint32_t n_ticks,
+              uint64_t stride) {
+  check_handle(h);
+  DeviceGuard g(h->cfg.device);
+  TickIn t = resolve_inputs(h, in, upd, pred, n_ticks, stride);
+  const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+  h->time_begin();
+  int e = 0;
+  switch (h->cfg.model) {
+    case FMSKF_MODEL_RS: e = launch_rs(h->s, t, libm, upd, pred, h->stream); break;
+    case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, upd, pred, h->stream); break;
+    case FMSKF_MODEL_EKF9: e = launch_ekf9(h->s, t, h->ekf9, libm, upd, pred, h->stream); break;
+    case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, upd, pred, h->stream); break;
+  }
+  launch_check(e, "tick kernel launch");
+  h->time_end();
+}
+
+void copy_out(fmskf_ctx *h, void *dst, const void *src, size_t bytes, uint32_t mem) {
+  if (!dst) return;
+  if (mem == FMSKF_MEM_HOST) {
+    hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+  } else if (mem == FMSKF_MEM_DEVICE) {
+    hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream), "D2D");
+  } else {
+    fail(FMSKF_EINVAL, "bad mem flag");
+  }
+}
+void finish_out(fmskf_ctx *h, uint32_t mem) {
+  if (mem == FMSKF_MEM_HOST) hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int fmskf_abi_version(void) { return (int)FMSKF_ABI_VERSION; }
+
+const char *fmskf_strerror(int status) {
+  switch (status) {
+    case FMSKF_OK: return "ok";
+    case FMSKF_EINVAL: return "invalid argument";
+    case FMSKF_ENOMEM: return "out of memory";
+    case FMSKF_EDEVICE: return "device error";
+    case FMSKF_ERCCL: return "collective error";
+    case FMSKF_ENOTSUP: return "not supported for this model";
+    default: return "unknown status";
+  }
+}
+
+const char *fmskf_last_error(void) { return g_last_error.c_str(); }
+
+int fmskf_model_dims(uint32_t model, uint32_t *n, uint32_t *m, uint32_t *elem_bytes) {
+  return guarded([&] {
+    Dims d = dims_of(model);
+    if (n) *n = d.nx;
+    if (m) *m = d.m;
+    if (elem_bytes) *elem_bytes = d.elem;
+  });
+}
+
+int fmskf_config_init(fmskf_config *cfg, uint32_t model, uint64_t n) {
+  return guarded([&] {
+    if (!cfg) fail(FMSKF_EINVAL, "null config");
+    (void)dims_of(model);
+    apply_defaults(cfg, model, n);
+  });
+}
+
+int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
+  return guarded([&] {
+    if (!cfg || !out) fail(FMSKF_EINVAL, "null argument");
+    *out = nullptr;
+    if (cfg->abi_version != FMSKF_ABI_VERSION) fail(FMSKF_EINVAL, "ABI version mismatch");
+    const Dims d = dims_of(cfg->model);
+    if (cfg->n_instances == 0) fail(FMSKF_EINVAL, "n_instances == 0");
+    if (cfg->n_instances > (1ull << 34)) fail(FMSKF_EINVAL, "n_instances too large");
+    if (cfg->trig > FMSKF_TRIG_LIBM) fail(FMSKF_EINVAL, "bad trig policy");
+    if (!(cfg->dt > 0.0) || !isfinite(cfg->dt)) fail(FMSKF_EINVAL, "dt must be > 0");
+    if (cfg->imu_read_reg + 4 > 0x90) fail(FMSKF_EINVAL, "imu_read_reg out of range");
+    for (int w = 0; w < 4; w++)
+      if (cfg->motor_dir[w] != 1 && cfg->motor_dir[w] != -1) fail(FMSKF_EINVAL, "motor_dir must be +-1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) fail(FMSKF_EDEVICE, "no HIP device");
+    if (cfg->device < 0 || cfg->device >= ndev) fail(FMSKF_EINVAL, "bad device ordinal");
+    DeviceGuard g(cfg->device);
+    fmskf_ctx *h = new fmskf_ctx();
+    try {
+      h->cfg = *cfg;
+      h->d = d;
+      const uint64_t n = cfg->n_instances;
+      DevState &s = h->s;
+      s.n = n;
+      s.model = cfg->model;
+      const uint32_t np = d.nx * (d.nx + 1) / 2;
+      s.x = h->alloc<char>((size_t)d.nx * n * d.elem);
+      s.P = d.m ? h->alloc<char>((size_t)np * n * d.elem) : nullptr;
+      s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * n) : nullptr;
+      s.imu_reg = h->alloc<int16_t>(0x90 * n);
+      s.imu_parser = h->alloc<uint32_t>(3 * n);
+      s.imu_cnt = h->alloc<uint8_t>(n);
+      s.imu_flags = h->alloc<uint8_t>(n);
+      s.imu_err = h->alloc<uint8_t>(n);
+      s.imu_qinit = h->alloc<float>(4 * n);
+      s.imu_data = h->alloc<float>(16 * n);
+      s.m_micro = h->alloc<int16_t>(4 * n);
+      s.m_angle = h->alloc<int16_t>(4 * n);
+      s.m_rpm = h->alloc<int16_t>(4 * n);
+      s.m_curr = h->alloc<int16_t>(4 * n);
+      s.m_head = h->alloc<uint8_t>(4 * n);
+      s.m_sum = h->alloc<int64_t>(4 * n);
+      s.m_dlt = h->alloc<float>(4 * n);
+      s.m_speed = h->alloc<float>(4 * n);
+      s.m_iir_y = h->alloc<float>(4 * n);
+      s.m_iir_x = h->alloc<float>(4 * n);
+      s.counters = h->alloc<unsigned long long>(8);
+      s.sintab = h->alloc<float>(513);
+      h->ens_blocks = h->alloc<double>((size_t)ensemble_nblocks(n) * 91);
+      h->ens_out = h->alloc<double>(91);
+      h->readout = h->alloc<float>(6 * n);
+      float tab[513];
+      for (int i = 0; i <= 512; i++) tab[i] = (float)sin(2.0 * 3.14159265358979323846 * (double)i / 512.0);
+      hip_check(hipMemcpy(s.sintab, tab, sizeof(tab), hipMemcpyHostToDevice), "sintab upload");
+      hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
+      hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
+      convert_params(h);
+      do_reset(h);
+      hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int fmskf_destroy(fmskf_handle h) {
+  return guarded([&] {
+    if (!h) return;
+    DeviceGuard g(h->cfg.device);
+    delete h;
+  });
+}
+
+int fmskf_reset(fmskf_handle h) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    do_reset(h);
+  });
+}
+
+int fmskf_set_stream(fmskf_handle h, void *stream) {
+  return guarded([&] {
+    check_handle(h);
+    h->stream = (hipStream_t)stream;
+  });
+}
+
+int fmskf_sync(fmskf_handle h) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+  });
+}
+
+int fmskf_get_config(fmskf_handle h, fmskf_config *out) {
+  return guarded([&] {
+    check_handle(h);
+    if (!out) fail(FMSKF_EINVAL, "null out");
+    *out = h->cfg;
+  });
+}
+
+int fmskf_ingest_wt901(fmskf_handle h, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
+                       int latch_qinit, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!bytes || !len) fail(FMSKF_EINVAL, "null bytes/len");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    if (mem == FMSKF_MEM_HOST) {
+      for (uint64_t i = 0; i < n; i++)
+        if (len[i] > stride) fail(FMSKF_EINVAL, "len[i] > stride");
+    }
+    Stager sg(h, mem);
+    const void *b = bytes, *l = len;
+    sg.add(&b, (size_t)stride * n);
+    sg.add(&l, n * 4);
+    sg.run();
+    launch_check(launch_wt901(h->s, (const uint8_t *)b, stride, (const uint32_t *)l, latch_qinit,
+                              h->cfg.imu_read_reg, h->stream),
+                 "wt901 launch");
+  });
+}
+
+int fmskf_ingest_can(fmskf_handle h, const uint8_t *frames, const int16_t *stamps,
+                     const uint8_t *present, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!frames || !stamps) fail(FMSKF_EINVAL, "null frames/stamps");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    Stager sg(h, mem);
+    const void *f = frames, *s = stamps, *p = present;
+    sg.add(&f, n * 32);
+    sg.add(&s, n * 8);
+    sg.add(&p, n);
+    sg.run();
+    launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, (const uint8_t *)p,
+                            h->cfg.motor_dir, h->stream),
+                 "can launch");
+  });
+}
+
+int fmskf_correct(fmskf_handle h, const fmskf_tick_inputs *in) {
+  return guarded([&] { run_tick(h, in, true, false, 1, h ? h->s.n : 0); });
+}
+
+int fmskf_predict(fmskf_handle h, const fmskf_tick_inputs *in) {
+  return guarded([&] { run_tick(h, in, false, true, 1, h ? h->s.n : 0); });
+}
+
+int fmskf_tick(fmskf_handle h, const fmskf_tick_inputs *in) {
+  return guarded([&] { run_tick(h, in, true, true, 1, h ? h->s.n : 0); });
+}
+
+int fmskf_tick_many(fmskf_handle h, const fmskf_tick_inputs *in, uint32_t n_ticks,
+                    uint64_t tick_stride) {
+  return guarded([&] { run_tick(h, in, true, true, n_ticks, tick_stride); });
+}
+
+int fmskf_get_pose(fmskf_handle h, float *x, float *y, float *th, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    launch_check(launch_readout(h->s, h->readout, h->stream), "readout");
+    copy_out(h, x, h->readout, n * 4, mem);
+    copy_out(h, y, h->readout + n, n * 4, mem);
+    copy_out(h, th, h->readout + 2 * n, n * 4, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_vel(fmskf_handle h, float *vx, float *vy, float *vth, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    launch_check(launch_readout(h->s, h->readout, h->stream), "readout");
+    copy_out(h, vx, h->readout + 3 * n, n * 4, mem);
+    copy_out(h, vy, h->readout + 4 * n, n * 4, mem);
+    copy_out(h, vth, h->readout + 5 * n, n * 4, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    const Dims d = h->d;
+    copy_out(h, x, h->s.x, (size_t)d.nx * n * d.elem, mem);
+    if (p_packed) {
+      if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
+      copy_out(h, p_packed, h->s.P, (size_t)(d.nx * (d.nx + 1) / 2) * n * d.elem, mem);
+    }
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    const Dims d = h->d;
+    const hipMemcpyKind k = mem == FMSKF_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    if (x) hip_check(hipMemcpyAsync(h->s.x, x, (size_t)d.nx * n * d.elem, k, h->stream), "set x");
+    if (p_packed) {
+      if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
+      hip_check(hipMemcpyAsync(h->s.P, p_packed, (size_t)(d.nx * (d.nx + 1) / 2) * n * d.elem, k,
+                               h->stream),
+                "set P");
+    }
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!h->s.prev_sum) fail(FMSKF_ENOTSUP, "prev_sum exists in the RS model only");
+    DeviceGuard g(h->cfg.device);
+    copy_out(h, prev, h->s.prev_sum, 4 * h->s.n * 8, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    copy_out(h, data, h->s.imu_data, 16 * h->s.n * 4, mem);
+    copy_out(h, is_error, h->s.imu_err, h->s.n, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    copy_out(h, regs, h->s.imu_reg, 0x90 * h->s.n * 2, mem);
+    copy_out(h, pending, h->s.imu_cnt, h->s.n, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr,
+                     int64_t *angle_sum, float *speed_radps, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
+    copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
+    copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
+    copy_out(h, angle_sum, h->s.m_sum, 4 * n * 8, mem);
+    copy_out(h, speed_radps, h->s.m_speed, 4 * n * 4, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters) {
+  return guarded([&] {
+    check_handle(h);
+    if (!counters || n_counters == 0) return;
+    DeviceGuard g(h->cfg.device);
+    unsigned long long tmp[8];
+    hip_check(hipMemcpyAsync(tmp, h->s.counters, sizeof(tmp), hipMemcpyDeviceToHost, h->stream), "D2H");
+    hip_check(hipStreamSynchronize(h->stream), "sync");
+    for (uint32_t k = 0; k < n_counters && k < 8; k++) counters[k] = tmp[k];
+  });
+}
+
+int fmskf_ensemble_record_len(fmskf_handle h, uint32_t *len) {
+  return guarded([&] {
+    check_handle(h);
+    if (!len) fail(FMSKF_EINVAL, "null len");
+    const uint32_t nx = h->d.nx;
+    *len = 1 + nx + nx * (nx + 1) / 2;
+  });
+}
+
+int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!out) fail(FMSKF_EINVAL, "null out");
+    DeviceGuard g(h->cfg.device);
+    const uint32_t nx = h->d.nx;
+    const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
+    double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
+    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, dst, h->stream),
+                 "ensemble launch");
+    if (mem == FMSKF_MEM_HOST) {
+      copy_out(h, out, h->ens_out, len * 8, mem);
+      finish_out(h, mem);
+    } else if (mem != FMSKF_MEM_DEVICE) {
+      fail(FMSKF_EINVAL, "bad mem flag");
+    }
+  });
+}
+
+int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
+                           double *mean, double *cov_packed) {
+  return guarded([&] {
+    if (n_state == 0 || n_state > 12 || !records) fail(FMSKF_EINVAL, "bad arguments");
+    const uint32_t nx = n_state, np = nx * (nx + 1) / 2, len = 1 + nx + np;
+    std::vector<double> acc(len, 0.0);
+    for (uint32_t r = 0; r < n_records; r++) {  // fixed rank order: deterministic
+      const double *b = records + (size_t)r * len;
+      const double na = acc[0], nb = b[0];
+      if (nb == 0.0) continue;
+      if (na == 0.0) {
+        acc.assign(b, b + len);
+        continue;
+      }
+      const double nn = na + nb;
+      double d[12];
+      for (uint32_t k = 0; k < nx; k++) d[k] = b[1 + k] - acc[1 + k];
+      const double f = na * nb / nn;
+      for (uint32_t k = 0; k < nx; k++) acc[1 + k] = acc[1 + k] + d[k] * (nb / nn);
+      for (uint32_t p = 0; p < nx; p++)
+        for (uint32_t q = 0; q <= p; q++) {
+          const uint32_t k = p * (p + 1) / 2 + q;
+          acc[1 + nx + k] = acc[1 + nx + k] + b[1 + nx + k] + d[p] * d[q] * f;
+        }
+      acc[0] = nn;
+    }
+    if (mean)
+      for (uint32_t k = 0; k < nx; k++) mean[k] = acc[1 + k];
+    if (cov_packed)
+      for (uint32_t k = 0; k < np; k++) cov_packed[k] = acc[0] > 1.0 ? acc[1 + nx + k] / (acc[0] - 1.0) : 0.0;
+  });
+}
+
+int fmskf_eval_trig(fmskf_handle h, const float *x, float *s, float *c, uint64_t n, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!x || !s || !c) fail(FMSKF_EINVAL, "null argument");
+    DeviceGuard g(h->cfg.device);
+    const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+    if (mem == FMSKF_MEM_DEVICE) {
+      launch_check(launch_trig(x, s, c, n, libm, h->s.sintab, h->stream), "trig launch");
+      return;
+    }
+    if (mem != FMSKF_MEM_HOST) fail(FMSKF_EINVAL, "bad mem flag");
+    if (n == 0) return;
+    char *buf = (char *)h->stage_for(3 * n * 4);
+    float *dx = (float *)buf, *ds = dx + n, *dc = ds + n;
+    hip_check(hipMemcpyAsync(dx, x, n * 4, hipMemcpyHostToDevice, h->stream), "H2D");
+    launch_check(launch_trig(dx, ds, dc, n, libm, h->s.sintab, h->stream), "trig launch");
+    hip_check(hipMemcpyAsync(s, ds, n * 4, hipMemcpyDeviceToHost, h->stream), "D2H");
+    hip_check(hipMemcpyAsync(c, dc, n * 4, hipMemcpyDeviceToHost, h->stream), "D2H");
+    hip_check(hipStreamSynchronize(h->stream), "sync");
+  });
+}
+
+int fmskf_set_timing(fmskf_handle h, int enable) {
+  return guarded([&] {
+    check_handle(h);
+    h->timing = enable != 0;
+    h->tcount = 0;
+  });
+}
+
+int fmskf_kernel_time_total(fmskf_handle h, double *total_ms, uint32_t *count) {
+  return guarded([&] {
+    check_handle(h);
+    if (!total_ms || !count) fail(FMSKF_EINVAL, "null argument");
+    DeviceGuard g(h->cfg.device);
+    double sum = 0.0;
+    if (h->tcount) hip_check(hipEventSynchronize(h->tpool[2 * h->tcount - 1]), "hipEventSynchronize");
+    for (size_t k = 0; k < h->tcount; k++) {
+      float ms = 0.f;
+      hip_check(hipEventElapsedTime(&ms, h->tpool[2 * k], h->tpool[2 * k + 1]), "hipEventElapsedTime");
+      sum += ms;
+    }
+    *total_ms = sum;
+    *count = (uint32_t)h->tcount;
+  });
+}
+
+int fmskf_last_kernel_ms(fmskf_handle h, float *ms) {
+  return guarded([&] {
+    check_handle(h);
+    if (!ms) fail(FMSKF_EINVAL, "null ms");
+    if (!h->timing) fail(FMSKF_EINVAL, "timing not enabled");
+    DeviceGuard g(h->cfg.device);
+    hip_check(hipEventSynchronize(h->ev1), "hipEventSynchronize");
+    hip_check(hipEventElapsedTime(ms, h->ev0, h->ev1), "hipEventElapsedTime");
+  });
+}
+
+}  // extern "C"

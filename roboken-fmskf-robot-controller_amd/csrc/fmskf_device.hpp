@@ -1,0 +1,128 @@
+// fmskf_device.hpp -- device-side scalar math of the hot path (gfx950).
+//
+// Every routine restates a reference routine with the same IEEE operation order,
+// and the whole library is compiled with -ffp-contract=off, so results are bit
+// identical to the firmware's C++ semantics (FLT_EVAL_METHOD 0, no FMA
+// contraction) -- the oracle (oracle/fmskf_oracle.c) checks exactly that.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fmskf {
+
+// PI of CMSIS-DSP arm_math.h as used by util_mymath.hpp:13-14
+#define FMSKF_PI_F 3.14159265358979f
+#define FMSKF_PI_D 3.141592653589793
+
+struct K {
+  static constexpr float deg2rad = FMSKF_PI_F / 180.0f;                  // util_mymath.hpp:14
+  static constexpr float two_pi = 2.0f * FMSKF_PI_F;
+  static constexpr float rpm_to_radps = 2.0f * 3.1415926f / 60.0f;       // VD_motor_if_m2006.hpp:77
+  static constexpr float gear_ratio_inv = 1.0f / 36.0f;                  // VD_motor_if_m2006.hpp:81
+  static constexpr float out_rad_per_raw = 2.0f * 3.1415926f / 8191.0f;  // VD_motor_if_m2006.hpp:82
+  static constexpr float wheel_r = 37.5f;                                // VD_vehicle_controller.hpp:82
+  static constexpr float wheel_l = 13.08148f;                            // VD_vehicle_controller.hpp:85
+  static constexpr float sqrtf2 = 1.41421356f;                           // VD_vehicle_controller.hpp:86
+  static constexpr float g0 = 9.80665f;
+  static constexpr int raw_per_rot = 8192;                               // VD_motor_if_m2006.hpp:76
+};
+
+// The 513-entry sine table over [0, 2pi] (CMSIS-DSP sinTable_f32 layout) is a
+// per-handle device buffer filled at fmskf_create from (float)sin(2*pi*i/512);
+// kernels receive it as a pointer (it stays L1/L2 resident: 2 KiB).
+
+__device__ __forceinline__ float deg2rad(float d) { return d * K::deg2rad; }  // util_mymath.hpp:16
+
+// util_mymath.hpp:18-25
+__device__ __forceinline__ float normalize_rad_0to2pi(float d) {
+  if (d < 0.0f || d >= 2.0f * FMSKF_PI_F) {
+    int mod = (int)(d / (2.0f * FMSKF_PI_F));
+    d -= (mod * 2.0f * FMSKF_PI_F);
+    if (d < 0.0f) d = d + 2.0f * FMSKF_PI_F;
+  }
+  return d;
+}
+
+// util_mymath.hpp:27-34
+__device__ __forceinline__ float normalize_deg_0to360(float d) {
+  if (d < 0.0f || d >= 360.0f) {
+    int mod = (int)(d / (360.0f));
+    d -= (mod * 360.0f);
+    if (d < 0.0f) d = d + 360.0f;
+  }
+  return d;
+}
+
+// CMSIS-DSP arm_sin_f32 / arm_cos_f32 published algorithm: scale to turns, floor,
+// 512-entry table, linear interpolation.
+__device__ __forceinline__ float table_lookup(float in, const float *__restrict__ tab) {
+  int32_t n = (int32_t)in;
+  if (in < 0.0f) n--;
+  in = in - (float)n;
+  float findex = 512.0f * in;
+  uint32_t index = (uint16_t)findex;
+  if (index >= 512u) {
+    index = 0;
+    findex -= 512.0f;
+  }
+  float fract = findex - (float)index;
+  float a = tab[index];
+  float b = tab[index + 1];
+  return (1.0f - fract) * a + fract * b;
+}
+
+template <bool LIBM>
+__device__ __forceinline__ float sin_p(float x, const float *tab) {
+  if constexpr (LIBM) return sinf(x);
+  else return table_lookup(x * 0.159154943092f, tab);
+}
+template <bool LIBM>
+__device__ __forceinline__ float cos_p(float x, const float *tab) {
+  if constexpr (LIBM) return cosf(x);
+  else return table_lookup(x * 0.159154943092f + 0.25f, tab);
+}
+
+// VEHICLE_CTRL::update rpm -> motor-output rad/s, VD_vehicle_controller.cpp:21-24
+__device__ __forceinline__ float rpm_to_mvel(int16_t rpm) {
+  return (float)rpm * K::rpm_to_radps * K::gear_ratio_inv;
+}
+
+// VEHICLE_CTRL::conv_Mdir_to_Vdir, VD_vehicle_controller.cpp:126-130 (FL, BL, BR, FR)
+__device__ __forceinline__ void mdir_to_vdir(float fl, float bl, float br, float fr, float &vx,
+                                             float &vy, float &vth) {
+  vx = (fl + bl + br + fr) * 0.25f * K::wheel_r;
+  vy = (-fl + bl - br + fr) * 0.25f * K::wheel_r;
+  vth = (-fl - bl + br + fr) * 0.25f / K::sqrtf2 / K::wheel_l * K::wheel_r;
+}
+
+// heading kept in [-pi, pi)
+__device__ __forceinline__ float wrap_pi(float a) {
+  if (a >= FMSKF_PI_F) a = a - 2.0f * FMSKF_PI_F;
+  else if (a < -FMSKF_PI_F) a = a + 2.0f * FMSKF_PI_F;
+  return a;
+}
+__device__ __forceinline__ float wrap_innov(float a) {
+  if (a > FMSKF_PI_F) a = a - 2.0f * FMSKF_PI_F;
+  else if (a < -FMSKF_PI_F) a = a + 2.0f * FMSKF_PI_F;
+  return a;
+}
+__device__ __forceinline__ double wrap_pi(double a) {
+  if (a >= FMSKF_PI_D) a = a - 2.0 * FMSKF_PI_D;
+  else if (a < -FMSKF_PI_D) a = a + 2.0 * FMSKF_PI_D;
+  return a;
+}
+__device__ __forceinline__ double wrap_innov(double a) {
+  if (a > FMSKF_PI_D) a = a - 2.0 * FMSKF_PI_D;
+  else if (a < -FMSKF_PI_D) a = a + 2.0 * FMSKF_PI_D;
+  return a;
+}
+
+__host__ __device__ constexpr int pk(int i, int j) {
+  return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
+}
+
+template <typename T> __device__ __forceinline__ T dsqrt(T v);
+template <> __device__ __forceinline__ float dsqrt<float>(float v) { return __builtin_sqrtf(v); }
+template <> __device__ __forceinline__ double dsqrt<double>(double v) { return __builtin_sqrt(v); }
+
+}  // namespace fmskf

@@ -1,0 +1,277 @@
+// kernels_ingest.hip -- device boundary ingest kernels for gfx950.
+//
+//  k_wt901: one IMU per lane.  The WIT SDK byte state machine (lib/wt901c/wit_c_sdk.c:
+//           132-198, NORMAL protocol) with its lazy one-byte-per-arrival resync, the
+//           register file sReg (wit_c_sdk.c:13, per instance, SoA int16 planes), the
+//           update-flag callback (imu_if_wt901c.cpp:23-48), isComComp (:132-143) and
+//           updateData (:91-129).  Integer parts bit exact; the parser window (never
+//           more than 11 bytes in NORMAL mode) is held in two 64-bit registers and
+//           shifted, so no per-lane dynamic indexing (no scratch).
+//  k_can:   one wheel per lane (4 lanes per robot).  MOTOR_IF_M2006::rx_callback
+//           (VD_motor_if_m2006.cpp:32-72): big-endian decode, reversed motors, 13-bit
+//           angle unwrap into the int64 sum, and the speed path with Cortex-M7 integer
+//           semantics (wrapping MUL, SDIV x/0 = 0) and its IIR1 low-pass.
+#include "fmskf_device.hpp"
+#include "fmskf_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+// lib/wt901c/REG.h
+enum : uint32_t {
+  R_VERSION = 0x2e, R_YYMM = 0x30, R_AX = 0x34, R_AZ = 0x36, R_GX = 0x37, R_GZ = 0x39, R_HX = 0x3a,
+  R_HZ = 0x3c, R_ROLL = 0x3d, R_YAW = 0x3f, R_TEMP = 0x40, R_D0STATUS = 0x41, R_PRESSUREL = 0x45,
+  R_LONL = 0x49, R_GPSHEIGHT = 0x4d, R_Q0 = 0x51, R_Q3 = 0x54, R_SVNUM = 0x55
+};
+// imu_if_wt901c.cpp:10-15
+enum : uint32_t { F_ACC = 0x01, F_GYRO = 0x02, F_ANGLE = 0x04, F_MAG = 0x08, F_QUAT = 0x10, F_READ = 0x80 };
+
+// SensorDataUpdata for registers [r0, r0 + len)
+__device__ __forceinline__ uint32_t flags_of(uint32_t r0, uint32_t len) {
+  uint32_t f = 0;
+  for (uint32_t k = 0; k < len; k++) {
+    const uint32_t r = r0 + k;
+    f |= r == R_AZ ? F_ACC : r == R_GZ ? F_GYRO : r == R_HZ ? F_MAG : r == R_YAW ? F_ANGLE
+       : r == R_Q3 ? F_QUAT : F_READ;
+  }
+  return f;
+}
+
+struct Wt901Args {
+  uint64_t n;
+  const uint8_t *bytes;
+  uint32_t stride;
+  const uint32_t *len;
+  int latch_qinit;
+  uint32_t read_reg_index;
+  int16_t *reg;
+  uint32_t *parser;
+  uint8_t *cnt;
+  uint8_t *flags;
+  uint8_t *err;
+  float *qinit;
+  float *data;
+};
+
+__global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
+  const uint64_t n = a.n;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint64_t lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
+  uint64_t hi = (uint64_t)a.parser[2 * n + i];
+  uint32_t cnt = a.cnt[i];
+  uint32_t flags = a.flags[i];
+  int16_t *reg = a.reg;
+  const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
+  const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
+  for (uint32_t b = 0; b < len; b++) {
+    const uint64_t byte = p[b];
+    // s_ucWitDataBuff[s_uiWitDataCnt++] = ucData  (bytes >= cnt are kept zero)
+    if (cnt < 8) lo |= byte << (8 * cnt);
+    else hi |= byte << (8 * (cnt - 8));
+    cnt++;
+    bool drop = (lo & 0xFFu) != 0x55u;  // header check, wit_c_sdk.c:142-147
+    if (!drop && cnt >= 11) {
+      uint32_t sum = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) sum += (uint32_t)(lo >> (8 * k)) & 0xFFu;
+      sum += (uint32_t)hi & 0xFFu;
+      sum += (uint32_t)(hi >> 8) & 0xFFu;
+      drop = (sum & 0xFFu) != ((uint32_t)(hi >> 16) & 0xFFu);  // __CaliSum, :150-156
+      if (!drop) {
+        // CopeWitData(type, usData, 4), wit_c_sdk.c:90-130
+        const uint32_t type = (uint32_t)(lo >> 8) & 0xFFu;
+        const uint32_t d[4] = {(uint32_t)(lo >> 16) & 0xFFFFu, (uint32_t)(lo >> 32) & 0xFFFFu,
+                               (uint32_t)(lo >> 48) & 0xFFFFu, (uint32_t)hi & 0xFFFFu};
+        uint32_t reg1 = 0, len1 = 4, reg2 = 0, len2 = 0;
+        bool known = true;
+        switch (type) {
+          case 0x51: reg1 = R_AX; len1 = 3; reg2 = R_TEMP; len2 = 1; break;
+          case 0x53: reg1 = R_ROLL; len1 = 3; reg2 = R_VERSION; len2 = 1; break;
+          case 0x50: reg1 = R_YYMM; break;
+          case 0x52: reg1 = R_GX; len1 = 3; break;
+          case 0x54: reg1 = R_HX; len1 = 3; break;
+          case 0x55: reg1 = R_D0STATUS; break;
+          case 0x56: reg1 = R_PRESSUREL; break;
+          case 0x57: reg1 = R_LONL; break;
+          case 0x58: reg1 = R_GPSHEIGHT; break;
+          case 0x59: reg1 = R_Q0; break;
+          case 0x5A: reg1 = R_SVNUM; break;
+          case 0x5F: reg1 = a.read_reg_index; break;
+          default: known = false; break;
+        }
+        if (known) {
+          for (uint32_t k = 0; k < len1; k++) reg[(reg1 + k) * n + i] = (int16_t)d[k];
+          flags |= flags_of(reg1, len1);
+          if (len2) {
+            reg[reg2 * n + i] = (int16_t)d[3];
+            flags |= flags_of(reg2, 1);
+          }
+        }
+        cnt = 0;
+        lo = 0;
+        hi = 0;
+        continue;
+      }
+    }
+    if (drop) {
+      // s_uiWitDataCnt--; memcpy(buf, &buf[1], cnt)
+      cnt--;
+      lo = (lo >> 8) | (hi << 56);
+      hi >>= 8;
+    }
+  }
+  // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
+  const bool ok = (flags & F_QUAT) != 0;
+  if (ok) flags = 0;
+  a.err[i] = ok ? 0 : 1;
+  a.parser[i] = (uint32_t)lo;
+  a.parser[n + i] = (uint32_t)(lo >> 32);
+  a.parser[2 * n + i] = (uint32_t)hi;
+  a.cnt[i] = (uint8_t)cnt;
+  a.flags[i] = (uint8_t)flags;
+  if (!ok) return;
+  // updateData, imu_if_wt901c.cpp:91-129
+  float acc[3], gyr[3], mag[3], ang[3], q[4], qi[4];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    acc[k] = (float)reg[(R_AX + k) * n + i] / 32768.0f * 16.0f;
+    gyr[k] = (float)reg[(R_GX + k) * n + i] / 32768.0f * 2000.0f;
+    mag[k] = (float)reg[(R_HX + k) * n + i];
+    ang[k] = (float)reg[(R_ROLL + k) * n + i] / 32768.0f * 180.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    q[k] = (float)reg[(R_Q0 + k) * n + i] / 32768.0f;
+    qi[k] = a.qinit[k * n + i];
+  }
+  float *d = a.data;
+  d[0 * n + i] = acc[0];
+  d[1 * n + i] = -acc[1];
+  d[2 * n + i] = -acc[2];
+  d[3 * n + i] = gyr[0];
+  d[4 * n + i] = -gyr[1];
+  d[5 * n + i] = -gyr[2];
+  d[6 * n + i] = mag[0];
+  d[7 * n + i] = -mag[1];
+  d[8 * n + i] = -mag[2];
+  d[9 * n + i] = normalize_deg_0to360(ang[0]) - 180.0f;
+  d[10 * n + i] = ang[1];
+  d[11 * n + i] = ang[2];
+  d[14 * n + i] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
+  d[13 * n + i] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
+  d[12 * n + i] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
+  d[15 * n + i] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
+  if (a.latch_qinit) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) a.qinit[k * n + i] = q[k];
+  }
+}
+
+int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
+                 int latch_qinit, uint32_t read_reg_index, hipStream_t st) {
+  Wt901Args a{s.n,          bytes,          stride,       len,         latch_qinit,
+              read_reg_index, s.imu_reg,    s.imu_parser, s.imu_cnt,   s.imu_flags,
+              s.imu_err,    s.imu_qinit,    s.imu_data};
+  const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
+  k_wt901<<<g, kBlock, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// CAN: MOTOR_IF_M2006::rx_callback
+// ---------------------------------------------------------------------------
+struct CanArgs {
+  uint64_t n;
+  const uint8_t *frames;
+  const int16_t *stamps;
+  const uint8_t *present;
+  int8_t dir[4];
+  int16_t *micro, *angle, *rpm, *curr;
+  uint8_t *head;
+  int64_t *sum;
+  float *dlt, *speed, *iir_y, *iir_x;
+};
+
+__device__ __forceinline__ int16_t s16_of(uint32_t h, uint32_t l) { return (int16_t)((h << 8) | l); }
+__device__ __forceinline__ int32_t mul_wrap(int32_t a, int32_t b) {
+  return (int32_t)((uint32_t)a * (uint32_t)b);
+}
+// Cortex-M7 SDIV: x/0 = 0 (CCR.DIV_0_TRP = 0 at reset), INT_MIN/-1 = INT_MIN
+__device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
+  if (b == 0) return 0;
+  if (a == INT32_MIN && b == -1) return INT32_MIN;
+  return a / b;
+}
+
+__global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
+  const uint64_t n = a.n;
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // (instance, wheel)
+  if (g >= 4 * n) return;
+  const uint64_t i = g >> 2;
+  const int w = (int)(g & 3);
+  if (a.present && !((a.present[i] >> w) & 1)) return;
+  const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
+  const uint32_t b0 = f.x & 0xFF, b1 = (f.x >> 8) & 0xFF, b2 = (f.x >> 16) & 0xFF, b3 = f.x >> 24;
+  const uint32_t b4 = f.y & 0xFF, b5 = (f.y >> 8) & 0xFF;
+  const int16_t micro = a.stamps[g];
+  const int dir = a.dir[w];
+  const int16_t old_micro = a.micro[g], old_angle = a.angle[g];
+  uint32_t head = a.head[g] + 1u;
+  if (head >= 3u) head = 0;
+
+  const int16_t new_angle =
+      dir == 1 ? s16_of(b0, b1) : (int16_t)(K::raw_per_rot - s16_of(b0, b1));
+  const int16_t new_rpm = (int16_t)(s16_of(b2, b3) * dir);
+  const int16_t new_curr = (int16_t)(s16_of(b4, b5) * dir);
+
+  int32_t raw_ang_dlt = new_angle - old_angle;
+  int32_t usec_dlt = micro - old_micro;
+  if (raw_ang_dlt > (K::raw_per_rot / 2)) raw_ang_dlt = raw_ang_dlt - K::raw_per_rot;
+  else if (raw_ang_dlt < -(K::raw_per_rot / 2)) raw_ang_dlt = raw_ang_dlt + K::raw_per_rot;
+  if (usec_dlt > 0x7FFF) usec_dlt = usec_dlt - 0x7FFF;
+  else if (usec_dlt < -0x7FFF) usec_dlt = usec_dlt + 0x7FFF;
+  const int32_t num = mul_wrap(mul_wrap(raw_ang_dlt, 2), 3141593);
+  const float x = (float)sdiv_arm(num, usec_dlt) / (float)K::raw_per_rot;
+  const uint64_t pw = (uint64_t)w * n + i;
+  const float py = a.iir_y[pw], pxv = a.iir_x[pw];
+  const float y = 0.8f * py + 0.1f * x + 0.1f * pxv;  // UTIL::IIR1::update, util_iir.hpp:39-45
+  a.iir_y[pw] = y;
+  a.iir_x[pw] = x;
+  a.speed[pw] = y;
+  a.dlt[pw] = (float)(new_angle - old_angle) * K::out_rad_per_raw * K::gear_ratio_inv;
+  int16_t d = (int16_t)(new_angle - old_angle);
+  d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
+  a.sum[pw] = a.sum[pw] + d;
+  a.micro[g] = micro;
+  a.angle[g] = new_angle;
+  a.rpm[g] = new_rpm;
+  a.curr[g] = new_curr;
+  a.head[g] = (uint8_t)head;
+}
+
+int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
+               const uint8_t *present, const int8_t dir[4], hipStream_t st) {
+  CanArgs a{};
+  a.n = s.n;
+  a.frames = frames;
+  a.stamps = stamps;
+  a.present = present;
+  for (int w = 0; w < 4; w++) a.dir[w] = dir[w];
+  a.micro = s.m_micro;
+  a.angle = s.m_angle;
+  a.rpm = s.m_rpm;
+  a.curr = s.m_curr;
+  a.head = s.m_head;
+  a.sum = s.m_sum;
+  a.dlt = s.m_dlt;
+  a.speed = s.m_speed;
+  a.iir_y = s.m_iir_y;
+  a.iir_x = s.m_iir_x;
+  const dim3 g((unsigned)((4 * s.n + kBlock - 1) / kBlock));
+  k_can<<<g, kBlock, 0, st>>>(a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fmskf

@@ -1,0 +1,93 @@
+// kernels_rs.hip -- reference-semantics tick (mode RS) for gfx950.
+//
+// One robot per lane.  correct = VD_task_main.cpp:368 (theta hard overwrite by the
+// IMU yaw), predict = VEHICLE_CTRL::update's velocity + odometry part
+// (VD_vehicle_controller.cpp:11-51) with its exact numerics: int64 encoder-sum
+// differences scaled in double, narrowed to float, mecanum forward kinematics,
+// rotation by the heading through the selected sin/cos policy, mm -> m.
+// Built with FP contraction off: bit-identical to the oracle restatement.
+//
+// Algorithmic bytes per instance-tick: pos 12 B r+w, prev 32 B r+w,
+// sums 32 B, yaw 4 B, rpm 8 B, vel 12 B w  -> 12*2 + 32*2 + 32 + 4 + 8 + 12 = 144 B.
+#include "fmskf_device.hpp"
+#include "fmskf_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+struct RsArgs {
+  uint64_t n;
+  float *x;          // [6][N]: px, py, th, vx, vy, vth
+  int64_t *prev;     // [4][N]
+  TickIn in;
+};
+
+template <bool LIBM, bool CORR, bool PRED>
+__global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
+  const uint64_t n = a.n;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  float px = a.x[i], py = a.x[n + i], th = a.x[2 * n + i];
+  float vx = 0.f, vy = 0.f, vth = 0.f;
+  int64_t prev[4];
+  if (PRED) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) prev[w] = a.prev[w * n + i];
+  }
+  const uint64_t st = a.in.stride;
+  for (uint32_t t = 0; t < a.in.n_ticks; t++) {
+    const uint64_t j = (uint64_t)t * st + i;
+    if (CORR) th = deg2rad(a.in.yaw_deg[j]);
+    if (PRED) {
+      const uint2 r = reinterpret_cast<const uint2 *>(a.in.rpm)[j];
+      const int16_t r0 = (int16_t)(r.x & 0xFFFFu), r1 = (int16_t)(r.x >> 16);
+      const int16_t r2 = (int16_t)(r.y & 0xFFFFu), r3 = (int16_t)(r.y >> 16);
+      mdir_to_vdir(rpm_to_mvel(r0), rpm_to_mvel(r1), rpm_to_mvel(r2), rpm_to_mvel(r3), vx, vy, vth);
+      float mrad[4];
+      const int64_t *sum = a.in.angle_sum + (uint64_t)t * st * 4;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int64_t s = sum[w * st + i];
+        mrad[w] = (float)((double)(s - prev[w]) * (double)K::out_rad_per_raw *
+                          (double)K::gear_ratio_inv);
+        prev[w] = s;
+      }
+      float lx, ly, lth;
+      mdir_to_vdir(mrad[0], mrad[1], mrad[2], mrad[3], lx, ly, lth);
+      const float rr = normalize_rad_0to2pi(th);
+      const float c = cos_p<LIBM>(rr, a.in.sintab);
+      const float s = sin_p<LIBM>(rr, a.in.sintab);
+      px = px + (lx * c - ly * s) * 0.001f;
+      py = py + (lx * s + ly * c) * 0.001f;
+    }
+  }
+  if (PRED) {
+    a.x[i] = px;
+    a.x[n + i] = py;
+    a.x[3 * n + i] = vx;
+    a.x[4 * n + i] = vy;
+    a.x[5 * n + i] = vth;
+#pragma unroll
+    for (int w = 0; w < 4; w++) a.prev[w * n + i] = prev[w];
+  }
+  if (CORR) a.x[2 * n + i] = th;
+}
+
+int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool predict,
+              hipStream_t st) {
+  RsArgs a{s.n, (float *)s.x, s.prev_sum, in};
+  const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
+  if (libm) {
+    if (correct && predict) k_rs<true, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (correct) k_rs<true, true, false><<<g, kBlock, 0, st>>>(a);
+    else k_rs<true, false, true><<<g, kBlock, 0, st>>>(a);
+  } else {
+    if (correct && predict) k_rs<false, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (correct) k_rs<false, true, false><<<g, kBlock, 0, st>>>(a);
+    else k_rs<false, false, true><<<g, kBlock, 0, st>>>(a);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace fmskf

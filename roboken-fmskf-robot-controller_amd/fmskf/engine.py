@@ -1,0 +1,307 @@
+"""Python host mirror of the C ABI: one Engine = one fmskf handle = N robots.
+
+Inputs may be numpy arrays (host memory; copied to the device on the handle's
+stream) or torch CUDA tensors (device memory, zero copy).  Outputs are numpy
+arrays (host readout synchronises the stream).  Array layouts are the SoA
+planes documented in include/fmskf.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (MEM_DEVICE, MEM_HOST, MODEL_EKF9, MODEL_KF6, MODEL_KF12D, MODEL_NAMES,
+                   MODEL_RS, TRIG_LIBM, TRIG_TABLE512, Config, TickInputs, check, load)
+
+_DTYPES = {
+    "yaw_deg": np.float32, "gyro_z_dps": np.float32, "rpm": np.int16, "angle_sum": np.int64,
+    "raw": np.int16, "z": np.float64, "valid": np.uint8,
+}
+
+
+def _is_torch(a) -> bool:
+    return type(a).__module__.startswith("torch")
+
+
+class _Args:
+    """Collects pointers of one call; all arrays must live in the same memory space."""
+
+    def __init__(self):
+        self.mem = None
+        self.keep = []
+
+    def ptr(self, a, dtype=None):
+        if a is None:
+            return None
+        if _is_torch(a):
+            if not a.is_cuda:
+                a = a.numpy()
+            else:
+                if not a.is_contiguous():
+                    raise ValueError("torch inputs must be contiguous")
+                self._set(MEM_DEVICE)
+                self.keep.append(a)
+                return C.c_void_p(a.data_ptr())
+        arr = np.ascontiguousarray(a, dtype=dtype) if dtype is not None else np.ascontiguousarray(a)
+        self._set(MEM_HOST)
+        self.keep.append(arr)
+        return arr.ctypes.data_as(C.c_void_p)
+
+    def _set(self, mem):
+        if self.mem is None:
+            self.mem = mem
+        elif self.mem != mem:
+            raise ValueError("mixing host and device arrays in one call")
+
+
+class Engine:
+    """Batched IMU + mecanum-odometry estimator over N robots on one GPU."""
+
+    def __init__(self, model="kf6", n=1, device=0, trig=TRIG_TABLE512, dt=None, q=None, r=None,
+                 p0=None, motor_dir=None, imu_read_reg=None):
+        L = load()
+        self.model = MODEL_NAMES[model] if isinstance(model, str) else int(model)
+        self.n = int(n)
+        cfg = Config()
+        check(L.fmskf_config_init(C.byref(cfg), self.model, self.n), "config_init")
+        cfg.device = int(device)
+        cfg.trig = int(trig)
+        if dt is not None:
+            cfg.dt = float(dt)
+        for name, val in (("q", q), ("r", r), ("p0", p0)):
+            if val is not None:
+                dst = getattr(cfg, name)
+                v = np.asarray(val, np.float64).ravel()
+                for k in range(len(dst)):
+                    dst[k] = float(v[k]) if k < v.size else 0.0
+        if motor_dir is not None:
+            for k in range(4):
+                cfg.motor_dir[k] = int(motor_dir[k])
+        if imu_read_reg is not None:
+            cfg.imu_read_reg = int(imu_read_reg)
+        self.cfg = cfg
+        h = C.c_void_p()
+        check(L.fmskf_create(C.byref(cfg), C.byref(h)), "create")
+        self.h = h
+        nx, m, eb = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(L.fmskf_model_dims(self.model, C.byref(nx), C.byref(m), C.byref(eb)), "model_dims")
+        self.nx, self.m, self.elem = nx.value, m.value, eb.value
+        self.np_ = self.nx * (self.nx + 1) // 2
+        self.dtype = np.float64 if self.elem == 8 else np.float32
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "h", None):
+            load().fmskf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def reset(self):
+        check(load().fmskf_reset(self.h), "reset")
+
+    def sync(self):
+        check(load().fmskf_sync(self.h), "sync")
+
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream, a raw hipStream_t (int) or None (default stream)."""
+        if stream is not None and hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        check(load().fmskf_set_stream(self.h, C.c_void_p(stream) if stream else None), "set_stream")
+
+    def set_timing(self, enable=True):
+        check(load().fmskf_set_timing(self.h, int(enable)), "set_timing")
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        check(load().fmskf_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
+        return ms.value
+
+    def kernel_time_total(self):
+        """(sum of per-launch kernel times in ms, number of launches) since set_timing."""
+        tot, cnt = C.c_double(), C.c_uint32()
+        check(load().fmskf_kernel_time_total(self.h, C.byref(tot), C.byref(cnt)),
+              "kernel_time_total")
+        return tot.value, cnt.value
+
+    # ------------------------------------------------------------------ ingest
+    def ingest_wt901(self, data, lens, latch_qinit=False):
+        """data: [N, stride] uint8 (one poll's UART bytes per robot), lens: [N] uint32."""
+        a = _Args()
+        stride = int(data.shape[1]) if hasattr(data, "shape") else 0
+        pb = a.ptr(data, np.uint8)
+        pl = a.ptr(lens, np.uint32)
+        check(load().fmskf_ingest_wt901(self.h, pb, stride, pl, int(latch_qinit), a.mem),
+              "ingest_wt901")
+
+    def ingest_can(self, frames, stamps, present=None):
+        """frames: [N, 4, 8] uint8, stamps: [N, 4] int16, present: [N] uint8 bitmask."""
+        a = _Args()
+        pf = a.ptr(frames, np.uint8)
+        ps = a.ptr(stamps, np.int16)
+        pp = a.ptr(present, np.uint8)
+        check(load().fmskf_ingest_can(self.h, pf, ps, pp, a.mem), "ingest_can")
+
+    # ------------------------------------------------------------------ ticks
+    def _inputs(self, kw):
+        a = _Args()
+        ti = TickInputs()
+        for name in ("yaw_deg", "gyro_z_dps", "rpm", "angle_sum", "raw", "z", "valid"):
+            p = a.ptr(kw.get(name), _DTYPES[name])
+            setattr(ti, name, p.value if p is not None else None)
+        ti.mem = MEM_HOST if a.mem is None else a.mem
+        return ti, a
+
+    def correct(self, **kw):
+        ti, _keep = self._inputs(kw)
+        check(load().fmskf_correct(self.h, C.byref(ti)), "correct")
+
+    def predict(self, **kw):
+        ti, _keep = self._inputs(kw)
+        check(load().fmskf_predict(self.h, C.byref(ti)), "predict")
+
+    def tick(self, **kw):
+        ti, _keep = self._inputs(kw)
+        check(load().fmskf_tick(self.h, C.byref(ti)), "tick")
+
+    def prepare(self, **kw):
+        """Pre-built fmskf_tick_inputs for a hot loop: returns an opaque object to pass to
+        tick_prepared() (keeps the arrays alive)."""
+        ti, keep = self._inputs(kw)
+        return (ti, keep, C.byref(ti))
+
+    def tick_prepared(self, prepared, _tick=None):
+        rc = (_tick or load().fmskf_tick)(self.h, prepared[2])
+        if rc:
+            check(rc, "tick")
+
+    def tick_many(self, n_ticks, tick_stride=None, **kw):
+        ti, _keep = self._inputs(kw)
+        stride = self.n if tick_stride is None else int(tick_stride)
+        check(load().fmskf_tick_many(self.h, C.byref(ti), int(n_ticks), stride), "tick_many")
+
+    # ------------------------------------------------------------------ readout
+    def get_state(self):
+        x = np.empty((self.nx, self.n), self.dtype)
+        P = np.empty((self.np_, self.n), self.dtype) if self.m else None
+        check(load().fmskf_get_state(self.h, x.ctypes.data_as(C.c_void_p),
+                                     P.ctypes.data_as(C.c_void_p) if P is not None else None,
+                                     MEM_HOST), "get_state")
+        return x, P
+
+    def set_state(self, x, P=None):
+        a = _Args()
+        px = a.ptr(x, self.dtype)
+        pP = a.ptr(P, self.dtype) if P is not None else None
+        check(load().fmskf_set_state(self.h, px, pP, a.mem), "set_state")
+
+    def get_pose(self):
+        out = np.empty((3, self.n), np.float32)
+        p = [out[k].ctypes.data_as(C.c_void_p) for k in range(3)]
+        check(load().fmskf_get_pose(self.h, *p, MEM_HOST), "get_pose")
+        return out
+
+    def get_vel(self):
+        out = np.empty((3, self.n), np.float32)
+        p = [out[k].ctypes.data_as(C.c_void_p) for k in range(3)]
+        check(load().fmskf_get_vel(self.h, *p, MEM_HOST), "get_vel")
+        return out
+
+    def get_prev_sum(self):
+        out = np.empty((4, self.n), np.int64)
+        check(load().fmskf_get_prev_sum(self.h, out.ctypes.data_as(C.c_void_p), MEM_HOST),
+              "get_prev_sum")
+        return out
+
+    def get_imu(self):
+        data = np.empty((16, self.n), np.float32)
+        err = np.empty(self.n, np.uint8)
+        check(load().fmskf_get_imu(self.h, data.ctypes.data_as(C.c_void_p),
+                                   err.ctypes.data_as(C.c_void_p), MEM_HOST), "get_imu")
+        return data, err
+
+    def get_imu_regs(self):
+        regs = np.empty((0x90, self.n), np.int16)
+        pend = np.empty(self.n, np.uint8)
+        check(load().fmskf_get_imu_regs(self.h, regs.ctypes.data_as(C.c_void_p),
+                                        pend.ctypes.data_as(C.c_void_p), MEM_HOST), "get_imu_regs")
+        return regs, pend
+
+    def get_motors(self):
+        ang = np.empty((self.n, 4), np.int16)
+        rpm = np.empty((self.n, 4), np.int16)
+        cur = np.empty((self.n, 4), np.int16)
+        s = np.empty((4, self.n), np.int64)
+        spd = np.empty((4, self.n), np.float32)
+        check(load().fmskf_get_motors(self.h, *(a.ctypes.data_as(C.c_void_p)
+                                                for a in (ang, rpm, cur, s, spd)), MEM_HOST),
+              "get_motors")
+        return dict(angle=ang, rpm=rpm, curr=cur, angle_sum=s, speed_radps=spd)
+
+    def get_counters(self):
+        out = (C.c_uint64 * 8)()
+        check(load().fmskf_get_counters(self.h, out, 8), "get_counters")
+        return list(out)
+
+    # ------------------------------------------------------------------ ensemble
+    def ensemble_record_len(self) -> int:
+        v = C.c_uint32()
+        check(load().fmskf_ensemble_record_len(self.h, C.byref(v)), "ensemble_record_len")
+        return v.value
+
+    def ensemble_partial(self, out=None):
+        """This rank's {count, mean, M2} record: numpy (host) or into a torch CUDA tensor."""
+        if out is not None and _is_torch(out) and out.is_cuda:
+            check(load().fmskf_ensemble_partial(self.h, C.c_void_p(out.data_ptr()), MEM_DEVICE),
+                  "ensemble_partial")
+            return out
+        rec = np.empty(self.ensemble_record_len(), np.float64)
+        check(load().fmskf_ensemble_partial(self.h, rec.ctypes.data_as(C.c_void_p), MEM_HOST),
+              "ensemble_partial")
+        return rec
+
+    # ------------------------------------------------------------------ diagnostics
+    def eval_trig(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        s = np.empty_like(x)
+        c = np.empty_like(x)
+        check(load().fmskf_eval_trig(self.h, x.ctypes.data_as(C.c_void_p),
+                                     s.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+                                     x.size, MEM_HOST), "eval_trig")
+        return s, c
+
+
+def ensemble_combine(n_state: int, records) -> tuple[np.ndarray, np.ndarray]:
+    """Fold per-rank records in rank order -> (mean [n], covariance packed [n(n+1)/2])."""
+    recs = np.ascontiguousarray(records, np.float64)
+    nrec = recs.shape[0] if recs.ndim == 2 else 1
+    mean = np.empty(n_state, np.float64)
+    cov = np.empty(n_state * (n_state + 1) // 2, np.float64)
+    check(load().fmskf_ensemble_combine(n_state, recs.ctypes.data_as(C.c_void_p), nrec,
+                                        mean.ctypes.data_as(C.c_void_p),
+                                        cov.ctypes.data_as(C.c_void_p)), "ensemble_combine")
+    return mean, cov
+
+
+def default_config(model="kf6", n=1) -> Config:
+    """Model defaults (pure host call, no GPU needed)."""
+    cfg = Config()
+    m = MODEL_NAMES[model] if isinstance(model, str) else int(model)
+    check(load().fmskf_config_init(C.byref(cfg), m, int(n)), "config_init")
+    return cfg
+
+
+__all__ = ["Engine", "ensemble_combine", "default_config", "MODEL_RS", "MODEL_KF6", "MODEL_EKF9",
+           "MODEL_KF12D", "TRIG_TABLE512", "TRIG_LIBM", "_lib"]

@@ -1,0 +1,88 @@
+"""The C-ABI library loads and exports every symbol include/fmskf.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "fmskf.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fmskf_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import fmskf
+    return fmskf.load()
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "fmskf_tick" in names and "fmskf_correct" in names and "fmskf_predict" in names
+    assert len(names) >= 30
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    from fmskf import _lib
+    assert set(_declared()) == set(_lib.SIGNATURES)
+
+
+def test_abi_version_and_strerror(lib):
+    import fmskf
+    assert lib.fmskf_abi_version() == fmskf.ABI_VERSION
+    assert lib.fmskf_strerror(0) == b"ok"
+    assert lib.fmskf_strerror(3) == b"device error"
+
+
+def test_config_defaults_without_gpu():
+    import fmskf
+    cfg = fmskf.default_config("kf6", 1024)
+    assert cfg.n_instances == 1024 and cfg.model == fmskf.MODEL_KF6
+    assert abs(cfg.dt - 1e-3) < 1e-15
+    assert list(cfg.motor_dir) == [1, 1, -1, -1]       # VD_task_main.cpp:75-78
+    assert cfg.imu_read_reg == 0x51
+    q = np.array(cfg.q[:21])
+    assert q[0] > 0 and q[1 * 2 // 2 + 0] == 0  # packed, lower triangle
+    for m, (n, mm, eb) in {"rs": (6, 0, 4), "kf6": (6, 4, 4), "ekf9": (9, 6, 4),
+                           "kf12d": (12, 8, 8)}.items():
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        assert fmskf.load().fmskf_model_dims(fmskf._lib.MODEL_NAMES[m], C.byref(a), C.byref(b),
+                                             C.byref(c)) == 0
+        assert (a.value, b.value, c.value) == (n, mm, eb)
+
+
+def test_invalid_arguments_are_rejected(lib):
+    import fmskf
+    cfg = fmskf.default_config("kf6", 16)
+    cfg.abi_version = 999
+    h = C.c_void_p()
+    assert lib.fmskf_create(C.byref(cfg), C.byref(h)) == fmskf._lib.EINVAL
+    assert b"ABI" in lib.fmskf_last_error()
+    assert lib.fmskf_tick(None, None) == fmskf._lib.EINVAL
+    assert lib.fmskf_config_init(None, 1, 1) == fmskf._lib.EINVAL
+
+
+def test_host_ensemble_combine_matches_oracle(orc):
+    """fmskf_ensemble_combine is a host routine: check it against the oracle fold."""
+    import fmskf
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(6, 1000)).astype(np.float32) * np.arange(1, 7)[:, None]
+    recs = np.stack([orc.ens_partial(x, lo, hi) for lo, hi in ((0, 300), (300, 301), (301, 1000))])
+    mean, cov = fmskf.ensemble_combine(6, recs)
+    full = orc.ens_partial(x)
+    m2, c2 = orc.ens_finalize(6, full)
+    np.testing.assert_allclose(mean, m2, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(cov, c2, rtol=1e-10)
+    ref = np.cov(x.astype(np.float64))
+    np.testing.assert_allclose(cov[[0, 2, 5, 9, 14, 20]], np.diag(ref), rtol=1e-10)

@@ -1,0 +1,426 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar: bit-exact for every integer / byte path and for every fp32/fp64 path whose
+trig policy is the table (both sides evaluate the identical IEEE operation
+sequence with contraction off).  The LIBM policy compares device sinf/cosf with
+glibc's, which may differ by an ulp; those runs use the north-star tolerance
+(1e-5 relative per physical quantity, as in tests/test_oracle_kf_fp64.py).
+"""
+import numpy as np
+import pytest
+
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory, wt901_frame
+from conftest import iter_golden_streams
+
+pytestmark = pytest.mark.gpu
+
+TABLE, LIBM = fmskf.TRIG_TABLE512, fmskf.TRIG_LIBM
+
+
+def bits_equal(a, b, what=""):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    assert a.shape == b.shape, what
+    if a.dtype.kind == "f":
+        ia = a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+        ib = b.astype(a.dtype).view(ia.dtype)
+        bad = np.nonzero(ia != ib)
+        assert bad[0].size == 0, f"{what}: {bad[0].size} mismatches, first at {tuple(x[0] for x in bad)}: {a[bad][0]!r} vs {b[bad][0]!r}"
+    else:
+        np.testing.assert_array_equal(a, b, err_msg=what)
+
+
+def rel_close(a, b, tol=1e-5, what=""):
+    scale = max(np.abs(b).max(), 1e-3)
+    err = np.abs(a.astype(np.float64) - b.astype(np.float64)).max() / scale
+    assert err <= tol, f"{what}: {err}"
+
+
+# ----------------------------------------------------------------------------- trig
+def test_trig_table_bitexact(orc):
+    x = np.linspace(-50, 50, 100003).astype(np.float32)
+    x = np.concatenate([x, np.float32([0, -0.0, 2 * np.pi, -2 * np.pi, 1e-9, -1e-9, 6.2831855])])
+    with Engine("kf6", 8, trig=TABLE) as e:
+        s, c = e.eval_trig(x)
+    so, co = orc.eval_trig(x, orc.TRIG_TABLE512)
+    bits_equal(s, so, "sin")
+    bits_equal(c, co, "cos")
+
+
+def test_trig_libm_close(orc):
+    x = np.linspace(-10, 10, 10001).astype(np.float32)
+    with Engine("kf6", 8, trig=LIBM) as e:
+        s, c = e.eval_trig(x)
+    assert np.abs(s - np.sin(x.astype(np.float64))).max() < 5e-7
+    assert np.abs(c - np.cos(x.astype(np.float64))).max() < 5e-7
+
+
+# ----------------------------------------------------------------------------- KF6
+def _kf6_setup(n, T, seed):
+    tr = Trajectory(n, T, seed=seed)
+    yaw, gz, rpm = tr.kf6_inputs()
+    rng = np.random.default_rng(seed)
+    valid = (rng.random((T, n)) > 0.1).astype(np.uint8)
+    return tr, yaw, gz, rpm, valid
+
+
+def _kf6_oracle(orc, n, yaw, gz, rpm, valid, trig, ticks):
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]), trig)
+    x = np.zeros((6, n), np.float32)
+    P = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    for t in range(ticks):
+        orc.kf6_tick(x, P, yaw[t], gz[t], rpm[t], None if valid is None else valid[t], prm,
+                     nthreads=0)
+    return x, P
+
+
+@pytest.mark.parametrize("n", [1, 1037])
+def test_kf6_tick_bitexact(orc, n):
+    T = 40
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 21 + n)
+    with Engine("kf6", n, trig=TABLE) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+        x, P = e.get_state()
+        assert e.get_counters()[0] == 0
+    xo, Po = _kf6_oracle(orc, n, yaw, gz, rpm, valid, orc.TRIG_TABLE512, T)
+    bits_equal(x, xo, "x")
+    bits_equal(P, Po, "P")
+
+
+def test_kf6_libm_within_tolerance(orc):
+    n, T = 777, 60
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 5)
+    with Engine("kf6", n, trig=LIBM) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+        x, P = e.get_state()
+    xo, Po = _kf6_oracle(orc, n, yaw, gz, rpm, valid, orc.TRIG_LIBM, T)
+    for grp in [(0, 1), (2,), (3, 4), (5,)]:
+        rel_close(x[list(grp)], xo[list(grp)], 1e-5, f"x{grp}")
+    rel_close(P, Po, 1e-5, "P")
+
+
+def test_kf6_split_equals_fused_and_many():
+    n, T = 1000, 12
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 8)
+    with Engine("kf6", n) as a, Engine("kf6", n) as b, Engine("kf6", n) as c:
+        for t in range(T):
+            a.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+            b.correct(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+            b.predict()
+        c.tick_many(T, yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm, valid=valid)
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        xc, Pc = c.get_state()
+    bits_equal(xa, xb, "split x")
+    bits_equal(Pa, Pb, "split P")
+    bits_equal(xa, xc, "many x")
+    bits_equal(Pa, Pc, "many P")
+
+
+def test_kf6_device_inputs_torch():
+    import torch
+    n, T = 4099, 5
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 9)
+    with Engine("kf6", n) as a, Engine("kf6", n) as b:
+        stream = torch.cuda.current_stream()
+        b.set_stream(stream)
+        dy, dg, dr = (torch.from_numpy(v).cuda() for v in (yaw, gz, rpm))
+        for t in range(T):
+            a.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])
+            b.tick(yaw_deg=dy[t], gyro_z_dps=dg[t], rpm=dr[t])
+        torch.cuda.synchronize()
+        bits_equal(a.get_state()[0], b.get_state()[0], "x")
+        bits_equal(a.get_state()[1], b.get_state()[1], "P")
+
+
+def test_kf6_large_n_sampled_bitexact(orc):
+    """N = 2^20 (the bench config): fused multi-tick launch on device inputs; a sample
+    of 2048 instances is recomputed by the oracle bit for bit, the rest must be finite
+    with a positive covariance diagonal."""
+    import torch
+    n, T = 1 << 20, 8
+    tr = Trajectory(n, T, seed=77)
+    yaw, gz, rpm = tr.kf6_inputs()
+    with Engine("kf6", n) as e:
+        e.tick_many(T, yaw_deg=torch.from_numpy(yaw).cuda(), gyro_z_dps=torch.from_numpy(gz).cuda(),
+                    rpm=torch.from_numpy(rpm).cuda())
+        x, P = e.get_state()
+        assert e.get_counters()[0] == 0
+    assert np.isfinite(x).all() and np.isfinite(P).all()
+    diag = [0, 2, 5, 9, 14, 20]
+    assert (P[diag] > 0).all()
+    idx = np.sort(np.random.default_rng(0).choice(n, 2048, replace=False))
+    xo, Po = _kf6_oracle(orc, idx.size, np.ascontiguousarray(yaw[:, idx]),
+                         np.ascontiguousarray(gz[:, idx]), np.ascontiguousarray(rpm[:, idx]),
+                         None, orc.TRIG_TABLE512, T)
+    bits_equal(x[:, idx], xo, "x sample")
+    bits_equal(P[:, idx], Po, "P sample")
+
+
+def test_nan_guard_counts_bad_instances():
+    n = 512
+    _, yaw, gz, rpm, _ = _kf6_setup(n, 1, 3)
+    yaw = yaw[0].copy()
+    yaw[[5, 100, 300]] = np.nan
+    with Engine("kf6", n) as e:
+        e.tick(yaw_deg=yaw, gyro_z_dps=gz[0], rpm=rpm[0])
+        assert e.get_counters()[0] == 3
+
+
+# ----------------------------------------------------------------------------- RS
+def _rs_oracle(orc, n, yaw, sums, rpm, trig, T):
+    pos = np.zeros((3, n), np.float32)
+    vel = np.zeros((3, n), np.float32)
+    prev = np.zeros((4, n), np.int64)
+    for t in range(T):
+        orc.rs_tick(pos, vel, prev, yaw[t], np.ascontiguousarray(sums[t]), rpm[t], trig)
+    return pos, vel, prev
+
+
+@pytest.mark.parametrize("trig", [TABLE, LIBM])
+def test_rs_tick_bitexact(orc, trig):
+    n, T = 2053, 50
+    tr = Trajectory(n, T, seed=31)
+    yaw, sums, rpm = tr.rs_inputs()
+    with Engine("rs", n, trig=trig) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t])
+        x, _ = e.get_state()
+        prev = e.get_prev_sum()
+        pose = e.get_pose()
+        vel = e.get_vel()
+    pos, velo, prevo = _rs_oracle(orc, n, yaw, sums, rpm, trig, T)
+    bits_equal(prev, prevo, "prev")
+    bits_equal(x[3:6], velo, "vel")
+    bits_equal(pose, pos, "pose")
+    bits_equal(vel, velo, "vel readout")
+    if trig == TABLE:
+        bits_equal(x[:3], pos, "pos")
+    else:  # device sinf/cosf vs glibc: ulp-level differences only
+        rel_close(x[:2], pos[:2], 1e-5, "pos")
+
+
+def test_rs_many_and_split():
+    n, T = 600, 16
+    tr = Trajectory(n, T, seed=32)
+    yaw, sums, rpm = tr.rs_inputs()
+    with Engine("rs", n) as a, Engine("rs", n) as b, Engine("rs", n) as c:
+        for t in range(T):
+            a.tick(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t])
+            b.correct(yaw_deg=yaw[t])
+            b.predict(angle_sum=sums[t], rpm=rpm[t])
+        c.tick_many(T, yaw_deg=yaw, angle_sum=sums, rpm=rpm)
+        for o in (b, c):
+            bits_equal(a.get_state()[0], o.get_state()[0], "x")
+            bits_equal(a.get_prev_sum(), o.get_prev_sum(), "prev")
+
+
+# ----------------------------------------------------------------------------- EKF9 / KF12D
+def test_ekf9_bitexact(orc):
+    n, T = 1500, 30
+    tr = Trajectory(n, T, seed=41)
+    raw = tr.ekf9_raw()
+    cfg = fmskf.default_config("ekf9", n)
+    with Engine("ekf9", n, trig=TABLE) as e:
+        for t in range(T):
+            e.tick(raw=raw[t])
+        x, P = e.get_state()
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((9, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    for t in range(T):
+        orc.ekf9_tick(xo, Po, raw[t], None, prm, nthreads=0)
+    bits_equal(x, xo, "x")
+    bits_equal(P, Po, "P")
+
+
+def test_kf12d_vs_oracle(orc):
+    n, T = 700, 20
+    tr = Trajectory(n, T, seed=51)
+    z = tr.kf12d_z()
+    cfg = fmskf.default_config("kf12d", n)
+    with Engine("kf12d", n) as e:
+        for t in range(T):
+            e.tick(z=z[t])
+        x, P = e.get_state()
+    prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), np.array(cfg.r[:36]))
+    xo = np.zeros((12, n))
+    Po = np.repeat(np.array(cfg.p0[:78])[:, None], n, 1).copy()
+    for t in range(T):
+        orc.kf12d_tick(xo, Po, np.ascontiguousarray(z[t]), None, prm, nthreads=0)
+    # fp64: tolerance 1e-12 relative (config 5); record whether it is also bit exact
+    for k in range(12):
+        rel_close(x[k], xo[k], 1e-12, f"x{k}")
+    rel_close(P, Po, 1e-12, "P")
+
+
+# ----------------------------------------------------------------------------- WT901 ingest
+def test_wt901_ingest_matches_reference_golden(orc, golden_wt901):
+    streams = list(iter_golden_streams(golden_wt901))
+    for rri in sorted({s[0] for s in streams}):
+        group = [s for s in streams if s[0] == rri]
+        n = len(group)
+        maxp = max(len(s[2]) for s in group)
+        stride = max(len(p) for s in group for p in s[2]) + 16
+        orcs = [orc.Wt901(rri) for _ in group]
+        with Engine("rs", n, imu_read_reg=rri) as e:
+            for k in range(maxp):
+                buf = np.zeros((n, stride), np.uint8)
+                lens = np.zeros(n, np.uint32)
+                for i, s in enumerate(group):
+                    if k < len(s[2]):
+                        b = np.frombuffer(s[2][k], np.uint8)
+                        buf[i, :b.size] = b
+                        lens[i] = b.size
+                    orcs[i].update(buf[i, :lens[i]])
+                e.ingest_wt901(buf, lens)
+                regs, pending = e.get_imu_regs()
+                data, err = e.get_imu()
+                for i, s in enumerate(group):
+                    kk = min(k, len(s[2]) - 1)
+                    np.testing.assert_array_equal(regs[:, i], s[3][kk], err_msg=f"{s[1]} poll {k}")
+                    assert err[i] == orcs[i].is_error
+                    assert pending[i] == len(orcs[i].parser)
+                    bits_equal(data[:, i], orcs[i].data, f"data {s[1]} poll {k}")
+
+
+def test_wt901_ingest_random_streams(orc):
+    n, polls, stride = 3000, 6, 96
+    rng = np.random.default_rng(99)
+    orcs = [orc.Wt901(0x51) for _ in range(n)]
+    with Engine("kf6", n) as e:
+        for k in range(polls):
+            buf = np.zeros((n, stride), np.uint8)
+            lens = rng.integers(0, stride + 1, n).astype(np.uint32)
+            for i in range(n):
+                kind = rng.integers(0, 3)
+                if kind == 0:  # clean poll
+                    b = b"".join(wt901_frame(t, rng.integers(0, 65536, 4)) for t in (0x51, 0x52, 0x53, 0x59))
+                    b = np.frombuffer(b, np.uint8)
+                elif kind == 1:  # noisy
+                    b = rng.integers(0, 256, int(lens[i]), dtype=np.uint8)
+                    b[rng.random(b.size) < 0.2] = 0x55
+                else:  # frames with errors
+                    fr = [bytearray(wt901_frame(int(rng.choice([0x51, 0x59, 0x5F, 0x50])), rng.integers(0, 65536, 4))) for _ in range(6)]
+                    for f in fr:
+                        if rng.random() < 0.3:
+                            f[int(rng.integers(0, 11))] ^= 0xA5
+                    b = np.frombuffer(bytes(b"".join(fr)), np.uint8)
+                b = b[:stride]
+                lens[i] = b.size
+                buf[i, :b.size] = b
+                orcs[i].update(b, latch_qinit=(k == 0))
+            e.ingest_wt901(buf, lens, latch_qinit=(k == 0))
+        regs, pending = e.get_imu_regs()
+        data, err = e.get_imu()
+    for i in range(0, n, 7):
+        np.testing.assert_array_equal(regs[:, i], orcs[i].regs)
+        assert pending[i] == len(orcs[i].parser)
+        assert err[i] == orcs[i].is_error
+        bits_equal(data[:, i], orcs[i].data, f"data {i}")
+
+
+# ----------------------------------------------------------------------------- CAN ingest
+def test_can_ingest_bitexact(orc):
+    n, T = 1001, 25
+    rng = np.random.default_rng(7)
+    dirs = [1, 1, -1, -1]
+    motors = [[orc.M2006(d) for d in dirs] for _ in range(n)]
+    with Engine("rs", n) as e:
+        for t in range(T):
+            frames = rng.integers(0, 256, (n, 4, 8), dtype=np.uint8)
+            frames[:, :, 0] &= 0x1F  # mostly in-range 13-bit angles
+            frames[rng.random((n, 4)) < 0.05, 0] |= 0x80  # some out-of-range / negative
+            stamps = rng.integers(0, 0x8000, (n, 4)).astype(np.int16)
+            stamps[rng.random((n, 4)) < 0.05] = 1234  # equal stamps -> usec_dlt == 0
+            present = rng.integers(0, 16, n).astype(np.uint8)
+            e.ingest_can(frames, stamps, present)
+            for i in range(n):
+                for w in range(4):
+                    if (present[i] >> w) & 1:
+                        motors[i][w].rx(frames[i, w], int(stamps[i, w]))
+        m = e.get_motors()
+    for i in range(n):
+        for w in range(4):
+            s = motors[i][w].s
+            assert m["angle"][i, w] == s.angle and m["rpm"][i, w] == s.rpm
+            assert m["curr"][i, w] == s.curr and m["angle_sum"][w, i] == s.angle_sum
+            bits_equal(m["speed_radps"][w, i:i + 1], np.float32([s.speed_radps]), "speed")
+
+
+def test_full_pipeline_rs_device_resident(orc):
+    """CAN ingest every tick + IMU ingest every 10 ticks + tick with NULL planes (the
+    device-resident state), against the same sequence through the oracle."""
+    n, T = 257, 40
+    tr = Trajectory(n, T, seed=61)
+    with Engine("rs", n) as e:
+        imus = [orc.Wt901(0x51) for _ in range(n)]
+        mot = [[orc.M2006(d) for d in (1, 1, -1, -1)] for _ in range(n)]
+        pos = np.zeros((3, n), np.float32)
+        vel = np.zeros((3, n), np.float32)
+        prev = np.zeros((4, n), np.int64)
+        for t in range(T):
+            fr, st = tr.can_frames(t)
+            e.ingest_can(fr, st)
+            for i in range(n):
+                for w in range(4):
+                    mot[i][w].rx(fr[i, w], int(st[i, w]))
+            if t % 10 == 0:
+                buf = np.zeros((n, 48), np.uint8)
+                lens = np.zeros(n, np.uint32)
+                for i in range(n):
+                    b = np.frombuffer(tr.wt901_poll_bytes(t, i), np.uint8)
+                    buf[i, :b.size] = b
+                    lens[i] = b.size
+                    imus[i].update(b, latch_qinit=(t == 0))
+                e.ingest_wt901(buf, lens, latch_qinit=(t == 0))
+            e.tick()
+            yaw = np.array([imus[i].data[11] for i in range(n)], np.float32)
+            sums = np.array([[mot[i][w].s.angle_sum for i in range(n)] for w in range(4)], np.int64)
+            rpm = np.array([[mot[i][w].s.rpm for w in range(4)] for i in range(n)], np.int16)
+            orc.rs_tick(pos, vel, prev, yaw, sums, rpm)
+        x, _ = e.get_state()
+    bits_equal(x[:3], pos, "pose")
+    bits_equal(x[3:], vel, "vel")
+
+
+# ----------------------------------------------------------------------------- ensemble
+@pytest.mark.parametrize("model,n", [("kf6", 100003), ("ekf9", 5000), ("kf12d", 3000)])
+def test_ensemble_partial(orc, model, n):
+    rng = np.random.default_rng(5)
+    with Engine(model, n) as e:
+        x = (rng.normal(size=(e.nx, n)) * np.arange(1, e.nx + 1)[:, None] + 3.0).astype(e.dtype)
+        e.set_state(x, None)
+        r1 = e.ensemble_partial()
+        r2 = e.ensemble_partial()
+    bits_equal(r1, r2, "deterministic")
+    ro = orc.ens_partial(x)
+    assert r1[0] == n
+    np.testing.assert_allclose(r1[1:1 + x.shape[0]], ro[1:1 + x.shape[0]], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(r1[1 + x.shape[0]:], ro[1 + x.shape[0]:], rtol=1e-9)
+
+
+# ----------------------------------------------------------------------------- edge cases
+def test_edge_rpm_extremes_and_single_instance(orc):
+    rpm = np.array([[-32768, 32767, -1, 0]], np.int16)
+    yaw = np.float32([179.99])
+    gz = np.float32([-2000.0])
+    with Engine("kf6", 1) as e:
+        e.tick(yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
+        x, P = e.get_state()
+    xo, Po = _kf6_oracle(orc, 1, yaw[None], gz[None], rpm[None], None, orc.TRIG_TABLE512, 1)
+    bits_equal(x, xo)
+    bits_equal(P, Po)
+
+
+def test_bad_inputs_rejected():
+    with Engine("kf6", 64) as e:
+        with pytest.raises(fmskf.FmskfError):
+            e.tick_many(2, yaw_deg=np.zeros((2, 64), np.float32))  # missing planes
+        with pytest.raises(fmskf.FmskfError):
+            e.get_prev_sum()  # RS only
