@@ -140,25 +140,27 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    eng.set_timing(True)
+    # HIP events on the stream the kernels run on, around exactly the K timed ticks
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
+    ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    kern_ms_total, kern_cnt = eng.kernel_time_total()
-    eng.set_timing(False)
+    region_ms = ev0.elapsed_time(ev1)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, region_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        km = torch.tensor([kern_ms_total / max(1, kern_cnt)], dtype=torch.float64, device=dev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kern_avg_ms = float(km.item())
-    else:
-        kern_avg_ms = kern_ms_total / max(1, kern_cnt)
+        elapsed, region_ms = float(t[0].item()), float(t[1].item())
+    # per-launch average from the event region: includes the ensemble reduction kernels
+    # (1 in --ensemble-every ticks) and inter-kernel gaps, so it bounds the tick kernel's
+    # own duration from above (rocprofv3 reports the kernel alone: profiles/)
+    kern_avg_ms = region_ms / args.steps
 
     total_steps = n * world * args.steps
     value = total_steps / elapsed

@@ -1,0 +1,94 @@
+// fleet_loop.cpp -- the firmware's per-tick call shape, for N robots at once.
+//
+// Mirrors the task structure of the reference: the IMU task polls the WT901 every
+// 10 ms (IMT::main, imu_task_main.cpp:43-82), CAN RX delivers four C610 frames per
+// millisecond (VD_can_controller.hpp:65-95), the 1 kHz ISR corrects with the IMU yaw
+// and predicts from the wheels (VD_task_main.cpp:366-372), and the ROS task reads the
+// pose (RM_task_main.cpp:776-784).  Synthetic traffic: each robot drives its wheels at
+// a constant rpm.  Usage: fleet_loop [N] [ticks]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "fmskf.hpp"
+
+static void wt901_frame(uint8_t *o, uint8_t type, int16_t w0, int16_t w1, int16_t w2, int16_t w3) {
+  const int16_t w[4] = {w0, w1, w2, w3};
+  o[0] = 0x55;
+  o[1] = type;
+  for (int k = 0; k < 4; k++) {
+    o[2 + 2 * k] = (uint8_t)(w[k] & 0xFF);
+    o[3 + 2 * k] = (uint8_t)((uint16_t)w[k] >> 8);
+  }
+  uint8_t s = 0;
+  for (int k = 0; k < 10; k++) s += o[k];
+  o[10] = s;
+}
+
+int main(int argc, char **argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1u << 16);
+  const int ticks = argc > 2 ? atoi(argv[2]) : 1000;
+  try {
+    fmskf::Robots robots(FMSKF_MODEL_RS, n);
+    fmskf::ImuIfWt901c imu(robots);
+    fmskf::MotorIfM2006 motors(robots);
+    fmskf::VehicleCtrl vehicle(robots);
+
+    const uint32_t stride = 48;
+    std::vector<uint8_t> bytes(n * stride);
+    std::vector<uint32_t> len(n, 44);
+    std::vector<uint8_t> frames(n * 32);
+    std::vector<int16_t> stamps(n * 4);
+    std::vector<int64_t> enc(n * 4, 0);
+    std::vector<float> px(n), py(n), pth(n);
+    const int dir[4] = {1, 1, -1, -1};
+
+    auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < ticks; t++) {
+      // CAN RX: wheel i advances (1 + i % 5) counts per tick, all wheels forward
+      for (uint64_t i = 0; i < n; i++) {
+        for (int w = 0; w < 4; w++) {
+          enc[i * 4 + w] += 1 + (int64_t)(i % 5);
+          const int32_t sensor = (int32_t)(((enc[i * 4 + w] * dir[w]) % 8192 + 8192) % 8192);
+          const int16_t rpm = (int16_t)((1 + i % 5) * 7 * dir[w]);
+          uint8_t *f = &frames[(i * 4 + w) * 8];
+          f[0] = (uint8_t)(sensor >> 8);
+          f[1] = (uint8_t)(sensor & 0xFF);
+          f[2] = (uint8_t)((uint16_t)rpm >> 8);
+          f[3] = (uint8_t)(rpm & 0xFF);
+          f[4] = 0;
+          f[5] = 100;
+          f[6] = f[7] = 0;
+          stamps[i * 4 + w] = (int16_t)(((t + 1) * 1000 + 7 * w) & 0x7FFF);
+        }
+      }
+      motors.rx_callback(frames.data(), stamps.data());
+      if (t % 10 == 0) {  // IMU task, 100 Hz: acc, gyro, angle (yaw = 30 deg), quaternion
+        for (uint64_t i = 0; i < n; i++) {
+          uint8_t *b = &bytes[i * stride];
+          wt901_frame(b, 0x51, 0, 0, 2048, 2500);
+          wt901_frame(b + 11, 0x52, 0, 0, 0, 0);
+          wt901_frame(b + 22, 0x53, 0, 0, (int16_t)(30.0 / 180.0 * 32768.0), 0);
+          wt901_frame(b + 33, 0x59, 32767, 0, 0, 0);
+        }
+        if (t == 0) imu.init(bytes.data(), stride, len.data());
+        else imu.update(bytes.data(), stride, len.data());
+      }
+      robots.can_tx_routine();  // correct + predict, device-resident inputs
+      if (t % 60 == 59) vehicle.get_vehicle_pos_m_latest(px.data(), py.data(), pth.data());
+    }
+    robots.sync();
+    auto t1 = std::chrono::steady_clock::now();
+    vehicle.get_vehicle_pos_m_latest(px.data(), py.data(), pth.data());
+    const double s = std::chrono::duration<double>(t1 - t0).count();
+    printf("robots=%llu ticks=%d  %.3f s  (host-fed, PCIe-inclusive %.3g robot-ticks/s)\n",
+           (unsigned long long)n, ticks, s, (double)n * ticks / s);
+    printf("robot 0: x=%.6f m y=%.6f m th=%.6f rad   robot 4: x=%.6f m\n", px[0], py[0], pth[0],
+           n > 4 ? px[4] : 0.f);
+  } catch (const std::exception &e) {
+    fprintf(stderr, "fleet_loop: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -392,18 +392,18 @@ void orc_rs_tick(size_t n, float *pos, float *vel, int64_t *prev, const float *y
 /* ------------------------------------------------------------------------- */
 #define REAL float
 #define SFX f32
-#define SQRT sqrtf
+#define FMA fmaf
 #include "orc_kf_generic.inc"
 #undef REAL
 #undef SFX
-#undef SQRT
+#undef FMA
 #define REAL double
 #define SFX f64
-#define SQRT sqrt
+#define FMA fma
 #include "orc_kf_generic.inc"
 #undef REAL
 #undef SFX
-#undef SQRT
+#undef FMA
 
 static inline float orc_wrap_pi_f(float a) {
   if (a >= ORC_PI_F) a = a - 2.0f * ORC_PI_F;
@@ -430,16 +430,17 @@ static inline double orc_wrap_innov_d(double a) {
 /* KF6 measurement frontend: (theta, omega, vx_world, vy_world) from the IMU yaw (deg),
  * the IMU gyro z as IMU_IF::Data publishes it (deg/s, sign-flipped by
  * imu_if_wt901c.cpp:113, so omega = -deg2rad(gz)), and the four wheel rpm
- * (A9/A10 velocity path rotated by the measured heading exactly as the odometry
- * rotates displacement, VD_vehicle_controller.cpp:47-51). */
+ * (A9/A10 velocity path rotated by the measured heading as the odometry rotates
+ * displacement, VD_vehicle_controller.cpp:47-51).  The sin/cos policies take any
+ * angle, so the heading goes to them directly (no normalize_rad_0to2pi, whose only
+ * purpose in the firmware is that range reduction). */
 static void orc_kf6_meas1(float yaw, float gz, const int16_t *rpm, int trig, float z[4]) {
   float th = orc_deg2rad(yaw);
   float om = -orc_deg2rad(gz);
   float mv[4], v[3];
   for (int w = 0; w < 4; w++) mv[w] = orc_rpm_to_mvel(rpm[w]);
   orc_mdir_to_vdir(mv, v);
-  float r = orc_normalize_rad_0to2pi(th);
-  float c = orc_cos(r, trig), s = orc_sin(r, trig);
+  float c = orc_cos(th, trig), s = orc_sin(th, trig);
   z[0] = th;
   z[1] = om;
   z[2] = (v[0] * c - v[1] * s) * 0.001f;
@@ -489,9 +490,9 @@ void orc_kf6_tick(size_t n, float *x, float *P, const float *yaw_deg, const floa
       orc_kf_update_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r);
     }
     if (do_predict) {
-      xs[0] = xs[0] + prm->dt * xs[3];
-      xs[1] = xs[1] + prm->dt * xs[4];
-      xs[2] = orc_wrap_pi_f(xs[2] + prm->dt * xs[5]);
+      xs[0] = fmaf(prm->dt, xs[3], xs[0]);
+      xs[1] = fmaf(prm->dt, xs[4], xs[1]);
+      xs[2] = orc_wrap_pi_f(fmaf(prm->dt, xs[5], xs[2]));
       orc_kf_predict_cov_f32(6, Ps, F, pat, prm->q);
     }
     for (int k = 0; k < 6; k++) x[k * n + i] = xs[k];
@@ -624,7 +625,7 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
       orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r);
     }
     if (do_predict) {
-      for (int a = 0; a < 6; a++) xs[pos[a]] = xs[pos[a]] + prm->dt * xs[pos[a] + 3];
+      for (int a = 0; a < 6; a++) xs[pos[a]] = fma(prm->dt, xs[pos[a] + 3], xs[pos[a]]);
       xs[2] = orc_wrap_pi_d(xs[2]);
       orc_kf_predict_cov_f64(12, Ps, F, pat, prm->q);
     }

@@ -458,7 +458,7 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
     if (cfg->abi_version != FMSKF_ABI_VERSION) fail(FMSKF_EINVAL, "ABI version mismatch");
     const Dims d = dims_of(cfg->model);
     if (cfg->n_instances == 0) fail(FMSKF_EINVAL, "n_instances == 0");
-    if (cfg->n_instances > (1ull << 34)) fail(FMSKF_EINVAL, "n_instances too large");
+    if (cfg->n_instances > (1ull << 30)) fail(FMSKF_EINVAL, "n_instances > 2^30 per handle");
     if (cfg->trig > FMSKF_TRIG_LIBM) fail(FMSKF_EINVAL, "bad trig policy");
     if (!(cfg->dt > 0.0) || !isfinite(cfg->dt)) fail(FMSKF_EINVAL, "dt must be > 0");
     if (cfg->imu_read_reg + 4 > 0x90) fail(FMSKF_EINVAL, "imu_read_reg out of range");

@@ -121,8 +121,13 @@ __host__ __device__ constexpr int pk(int i, int j) {
   return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
 }
 
-template <typename T> __device__ __forceinline__ T dsqrt(T v);
-template <> __device__ __forceinline__ float dsqrt<float>(float v) { return __builtin_sqrtf(v); }
-template <> __device__ __forceinline__ double dsqrt<double>(double v) { return __builtin_sqrt(v); }
+// explicit fused multiply-add (one rounding: v_fma_f32 / v_fma_f64 == C99 fmaf / fma)
+template <typename T> __device__ __forceinline__ T dfma(T a, T b, T c);
+template <> __device__ __forceinline__ float dfma<float>(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+template <> __device__ __forceinline__ double dfma<double>(double a, double b, double c) {
+  return __builtin_fma(a, b, c);
+}
 
 }  // namespace fmskf

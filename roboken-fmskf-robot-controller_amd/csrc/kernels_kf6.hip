@@ -1,0 +1,277 @@
+// kernels_kf6.hip -- the headline 6-state fp32 KF tick (BASELINE.json configs[1], SURVEY.md
+// 8(d) cfg 2) for gfx950.
+//
+// One robot per lane, x (6) and packed P (21) in VGPRs; a tick = measurement frontend
+// (yaw, gyro z, 4 wheel rpm -> z, the reference's deg2rad / mecanum FK / rotation,
+// VD_vehicle_controller.cpp:21-51) + LDL^T-form update + F P F^T + Q predict, one read and
+// one write of every state byte: 232 algorithmic bytes per instance-tick.
+//
+// Memory-path design (MI355X_MICROARCH.md: s_waitcnt vmcnt is in-order, so any load issued
+// after the state loads makes every later wait cover them):
+//  * the 2 KiB TABLE512 sine table is staged in LDS once per block, so the trig lookups in
+//    the middle of the math wait on lgkmcnt only, never behind the state loads;
+//  * planes are addressed through buffer descriptors built from kernel arguments (T8) with
+//    a 32-bit lane byte offset; when the 21 P planes fit one 4 GiB window (n < 51M, the
+//    SMALL instantiation) one descriptor per array plus a per-plane scalar soffset
+//    addresses every plane, so the loop needs almost no scalar or vector address math;
+//  * whether a validity mask exists is a compile-time choice (no conditional load whose
+//    merge would force a full vmcnt(0) drain);
+//  * tick_many loads the inputs of tick t+1 before computing tick t; the double-buffered
+//    persistent variant loads the next instance's state + inputs before computing the
+//    current one (two register sets, loop unrolled by two: no loop-carried copies).
+#include "kf_generic.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_>
+struct Opt {
+  static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_;
+};
+
+struct Kf6In {
+  float yaw, gz;
+  uint2 rpm;
+  uint32_t valid;
+};
+
+// Buffer descriptor (MI355X SRD, cdna_hip_programming.md T8) from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(base), 0, (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes),
+      0x00020000);
+}
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                       float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
+}
+
+// inputs of one tick; planes of tick t start at t * stride elements
+template <class O>
+__device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint64_t t, uint32_t i) {
+  const uint64_t tb = t * in.stride;
+  Kf6In m;
+  m.yaw = ld_f32(rsrc(in.yaw_deg + tb, n * 4), i * 4u, 0);
+  m.gz = ld_f32(rsrc(in.gyro_z + tb, n * 4), i * 4u, 0);
+  const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + tb * 4, n * 8), i * 8u, 0, 0);
+  m.rpm = make_uint2(rr[0], rr[1]);
+  m.valid = O::VALID ? (uint32_t)in.valid[tb + i] : 1u;
+  return m;
+}
+
+template <class O>
+__device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg, uint64_t n,
+                                               uint32_t i, float (&x)[6], float (&P)[21]) {
+  if constexpr (O::SMALL) {
+    const auto rx = rsrc(xg, n * 24), rp = rsrc(Pg, n * 84);
+    const uint32_t ps = (uint32_t)n * 4u;
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] = ld_f32(rx, i * 4u, k * ps);
+#pragma unroll
+    for (int k = 0; k < 21; k++) P[k] = ld_f32(rp, i * 4u, k * ps);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] = ld_f32(rsrc(xg + k * n, n * 4), i * 4u, 0);
+#pragma unroll
+    for (int k = 0; k < 21; k++) P[k] = ld_f32(rsrc(Pg + k * n, n * 4), i * 4u, 0);
+  }
+}
+
+template <class O>
+__device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t n, uint32_t i,
+                                                const float (&x)[6], const float (&P)[21]) {
+  if constexpr (O::SMALL) {
+    const auto rx = rsrc(xg, n * 24), rp = rsrc(Pg, n * 84);
+    const uint32_t ps = (uint32_t)n * 4u;
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_f32(rx, i * 4u, k * ps, x[k]);
+#pragma unroll
+    for (int k = 0; k < 21; k++) st_f32(rp, i * 4u, k * ps, P[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_f32(rsrc(xg + k * n, n * 4), i * 4u, 0, x[k]);
+#pragma unroll
+    for (int k = 0; k < 21; k++) st_f32(rsrc(Pg + k * n, n * 4), i * 4u, 0, P[k]);
+  }
+}
+
+// z = (deg2rad(yaw), -deg2rad(gz), wheel velocity rotated by the measured heading)
+// (imu_task_main.cpp:102-104, util_mymath.hpp:16, imu_if_wt901c.cpp:113,
+//  VD_vehicle_controller.cpp:21-33,47-51); y = z - H x with the heading innovation wrapped
+template <bool LIBM>
+__device__ __forceinline__ void kf6_innov(const Kf6In &m, const float *tab, const float (&x)[6],
+                                          float (&y)[4]) {
+  int16_t r[4];
+  unpack4(m.rpm, r);
+  const float th = deg2rad(m.yaw);
+  const float om = -deg2rad(m.gz);
+  float vx, vy, vth;
+  mdir_to_vdir(rpm_to_mvel(r[0]), rpm_to_mvel(r[1]), rpm_to_mvel(r[2]), rpm_to_mvel(r[3]), vx, vy,
+               vth);
+  // the sin/cos policies reduce any angle themselves (no normalize_rad_0to2pi needed)
+  const float c = cos_p<LIBM>(th, tab), s = sin_p<LIBM>(th, tab);
+  const float z2 = (vx * c - vy * s) * 0.001f;
+  const float z3 = (vx * s + vy * c) * 0.001f;
+  y[0] = wrap_innov(th - x[2]);
+  y[1] = om - x[5];
+  y[2] = z2 - x[3];
+  y[3] = z3 - x[4];
+}
+
+template <class O>
+__device__ __forceinline__ void kf6_tick1(const Kf6In &m, const float *tab, const Kf6Params &prm,
+                                          float (&x)[6], float (&P)[21]) {
+  if (O::UPD && (!O::VALID || m.valid)) {
+    float y[4];
+    kf6_innov<O::LIBM>(m, tab, x, y);
+    kf_update<MdKF6>(x, P, y, prm.r);
+  }
+  if (O::PRED) {
+    const float dt = prm.dt;
+    x[0] = dfma(dt, x[3], x[0]);
+    x[1] = dfma(dt, x[4], x[1]);
+    x[2] = wrap_pi(dfma(dt, x[5], x[2]));
+    kf_predict_cov<MdKF6>(P, [&](int, int) { return dt; }, prm.q);
+  }
+}
+
+// copy the sine table to LDS: all global loads first, then the LDS writes, one barrier
+template <bool LIBM>
+__device__ __forceinline__ void stage_table(float *stab, const float *g) {
+  if (!LIBM) {
+    const int t = threadIdx.x;
+    const float a = g[t], b = g[t + kBlock];
+    const float c = t == 0 ? g[2 * kBlock] : 0.f;
+    stab[t] = a;
+    stab[t + kBlock] = b;
+    if (t == 0) stab[2 * kBlock] = c;
+    __syncthreads();
+  }
+}
+static_assert(2 * kBlock + 1 == 513, "table staging assumes 256-thread blocks");
+
+// one instance per lane, grid = ceil(N / 256)
+template <int WPE, class O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6(
+    KfArgs<MdKF6, Kf6Params> a) {
+  __shared__ float stab[O::LIBM ? 1 : 513];
+  const uint64_t n = a.n;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i < (uint32_t)n;
+  float x[6], P[21];
+  Kf6In m;
+  if (live) {
+    kf6_load_state<O>(a.x, a.P, n, i, x, P);
+    if (O::UPD) m = kf6_load_in<O>(a.in, n, 0, i);
+  }
+  stage_table<O::LIBM>(stab, a.in.sintab);
+  if (!live) return;
+  for (uint32_t t = 0; t < a.in.n_ticks; t++) {
+    Kf6In mn;
+    if (O::UPD && t + 1 < a.in.n_ticks) mn = kf6_load_in<O>(a.in, n, t + 1, i);
+    kf6_tick1<O>(m, stab, a.prm, x, P);
+    m = mn;
+  }
+  kf6_store_state<O>(a.x, a.P, n, i, x, P);
+  nan_guard(x, P, a.counters);
+}
+
+// Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no
+// loop-carried copies); while set A is computed and stored, set B's loads are in flight.
+// Single-tick launches only.
+template <int WPE, class O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6db(
+    KfArgs<MdKF6, Kf6Params> a) {
+  __shared__ float stab[O::LIBM ? 1 : 513];
+  const uint64_t n = a.n;
+  const uint32_t nn = (uint32_t)n;
+  const uint32_t gs = gridDim.x * kBlock;
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  float xa[6], Pa[21], xb[6], Pb[21];
+  Kf6In ma, mb;
+  if (i < nn) {
+    kf6_load_state<O>(a.x, a.P, n, i, xa, Pa);
+    if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, i);
+  }
+  stage_table<O::LIBM>(stab, a.in.sintab);
+  while (i < nn) {
+    const uint32_t ib = i + gs;
+    if (ib < nn) {
+      kf6_load_state<O>(a.x, a.P, n, ib, xb, Pb);
+      if (O::UPD) mb = kf6_load_in<O>(a.in, n, 0, ib);
+    }
+    kf6_tick1<O>(ma, stab, a.prm, xa, Pa);
+    kf6_store_state<O>(a.x, a.P, n, i, xa, Pa);
+    nan_guard(xa, Pa, a.counters);
+    if (ib >= nn) break;
+    const uint32_t ia = ib + gs;
+    if (ia < nn) {
+      kf6_load_state<O>(a.x, a.P, n, ia, xa, Pa);
+      if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, ia);
+    }
+    kf6_tick1<O>(mb, stab, a.prm, xb, Pb);
+    kf6_store_state<O>(a.x, a.P, n, ib, xb, Pb);
+    nan_guard(xb, Pb, a.counters);
+    i = ia;
+  }
+}
+
+// Variant (FMSKF_KF6_VARIANT, read once) for single-tick launches; default 0:
+//   0: one instance per lane, grid = N/256 (4 waves/SIMD)
+//   1: double-buffered persistent, 2 blocks/CU   2: same, 3 blocks/CU
+static int kf6_variant() {
+  static int v = [] {
+    const char *e = getenv("FMSKF_KF6_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <class O>
+static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
+  const int v = a.in.n_ticks == 1 ? kf6_variant() : 0;
+  if (v == 1 || v == 2) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t g = (uint64_t)cus * (v == 1 ? 2 : 3);
+    const uint64_t need = (a.n + kBlock - 1) / kBlock;
+    k_kf6db<2, O><<<(unsigned)(g < need ? g : need), kBlock, 0, st>>>(a);
+  } else {
+    k_kf6<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);
+  }
+}
+
+template <bool LIBM, bool UPD, bool PRED>
+static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st) {
+  if (small) {
+    if (valid) launch_o<Opt<LIBM, UPD, PRED, true, true>>(a, st);
+    else launch_o<Opt<LIBM, UPD, PRED, true, false>>(a, st);
+  } else {
+    if (valid) launch_o<Opt<LIBM, UPD, PRED, false, true>>(a, st);
+    else launch_o<Opt<LIBM, UPD, PRED, false, false>>(a, st);
+  }
+}
+
+int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool libm, bool upd,
+               bool pred, hipStream_t st) {
+  KfArgs<MdKF6, Kf6Params> a{s.n, (float *)s.x, (float *)s.P, in, s.counters, p};
+  const bool small = s.n * 84 < 0xFFFFFFFFull;
+  const bool valid = upd && in.valid != nullptr;
+  if (libm) {
+    if (upd && pred) launch_lup<true, true, true>(a, small, valid, st);
+    else if (upd) launch_lup<true, true, false>(a, small, valid, st);
+    else launch_lup<true, false, true>(a, small, false, st);
+  } else {
+    if (upd && pred) launch_lup<false, true, true>(a, small, valid, st);
+    else if (upd) launch_lup<false, true, false>(a, small, valid, st);
+    else launch_lup<false, false, true>(a, small, false, st);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace fmskf

@@ -1,12 +1,12 @@
 // kernels_misc.hip -- sin/cos policy evaluation and the ensemble statistics reduction.
 //
-// Ensemble: mean and covariance of the state x across all instances of a rank, in fp64,
-// as a Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]}.  Each thread
-// folds its grid-stride instances with Welford updates, the 64 lanes of a wave fold by
-// DPP-free shuffles (__shfl_down) in a fixed butterfly order, the 4 waves of a block
-// fold through LDS, then one block folds the per-block records in block order.  No
-// atomics anywhere: the result is bitwise reproducible run to run, and ranks combine
-// their records in rank order after the RCCL all-gather.
+// Ensemble: mean and covariance of the state x across all instances of a rank, in fp64.
+// Each thread accumulates shifted moment sums of its grid-stride instances (no division
+// in the streaming loop), waves sum by a fixed xor butterfly, the 4 waves of a block
+// through LDS in wave order, and one block folds the per-block sums in block order and
+// converts them to the Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]}
+// that ranks all-gather and combine in rank order.  No atomics anywhere: the result is
+// bitwise reproducible run to run.
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
 
@@ -42,111 +42,90 @@ struct EnsRec {
   double v[LEN];
 };
 
-// Chan et al. pairwise combination a <- a (+) b  (same formula as oracle orc_ens_combine)
-template <int NX>
-__device__ __forceinline__ void ens_combine(EnsRec<NX> &a, const EnsRec<NX> &b) {
-  const double na = a.v[0], nb = b.v[0];
-  if (nb == 0.0) return;
-  if (na == 0.0) {
-    a = b;
-    return;
-  }
-  const double nn = na + nb;
-  double d[NX];
-#pragma unroll
-  for (int k = 0; k < NX; k++) d[k] = b.v[1 + k] - a.v[1 + k];
-  const double f = na * nb / nn;
-#pragma unroll
-  for (int k = 0; k < NX; k++) a.v[1 + k] = a.v[1 + k] + d[k] * (nb / nn);
-#pragma unroll
-  for (int p = 0; p < NX; p++)
-#pragma unroll
-    for (int q = 0; q <= p; q++) {
-      const int k = p * (p + 1) / 2 + q;
-      a.v[1 + NX + k] = a.v[1 + NX + k] + b.v[1 + NX + k] + d[p] * d[q] * f;
-    }
-  a.v[0] = nn;
-}
-
-template <int NX>
-__device__ __forceinline__ void ens_block_reduce(EnsRec<NX> &r, double *lds) {
-  constexpr int LEN = EnsRec<NX>::LEN;
-  // wave: fixed butterfly-down order
+// Plain sums of a record {count, S1[n], S2 packed} over the block: butterfly over the wave
+// (fixed xor order), then the 4 waves through LDS in wave order.  Deterministic.
+template <int LEN>
+__device__ __forceinline__ void sum_block(double (&v)[LEN], double *lds) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    EnsRec<NX> o;
 #pragma unroll
-    for (int k = 0; k < LEN; k++) o.v[k] = __shfl_down(r.v[k], off, 64);
-    if ((threadIdx.x & 63) < off) ens_combine<NX>(r, o);
+    for (int k = 0; k < LEN; k++) v[k] = v[k] + __shfl_xor(v[k], off, 64);
   }
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int k = 0; k < LEN; k++) lds[wave * LEN + k] = r.v[k];
+    for (int k = 0; k < LEN; k++) lds[wave * LEN + k] = v[k];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int wv = 1; wv < kBlock / 64; wv++) {
-      EnsRec<NX> o;
 #pragma unroll
-      for (int k = 0; k < LEN; k++) o.v[k] = lds[wv * LEN + k];
-      ens_combine<NX>(r, o);
+    for (int k = 0; k < LEN; k++) {
+      double s = lds[k];
+      for (int w = 1; w < kBlock / 64; w++) s = s + lds[w * LEN + k];
+      v[k] = s;
     }
   }
 }
 
+// Shifted moment sums: S1 = sum(x - x0), S2 = sum((x - x0)(x - x0)^T) with the shift x0 =
+// instance 0's state (the same for every block), fp64, no division in the streaming loop.
 template <int NX, typename T>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *x, uint64_t n, double *blocks) {
   constexpr int LEN = EnsRec<NX>::LEN;
   __shared__ double lds[(kBlock / 64) * LEN];
-  EnsRec<NX> r;
+  double sh[NX], v[LEN];
 #pragma unroll
-  for (int k = 0; k < LEN; k++) r.v[k] = 0.0;
+  for (int k = 0; k < NX; k++) sh[k] = (double)x[k * n];
+#pragma unroll
+  for (int k = 0; k < LEN; k++) v[k] = 0.0;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    // Welford: count, mean, co-moment update
-    double xv[NX], d[NX];
-    const double cnt = r.v[0] + 1.0;
+    double d[NX];
 #pragma unroll
     for (int k = 0; k < NX; k++) {
-      xv[k] = (double)x[k * n + i];
-      d[k] = xv[k] - r.v[1 + k];
-      r.v[1 + k] = r.v[1 + k] + d[k] / cnt;
+      d[k] = (double)x[k * n + i] - sh[k];
+      v[1 + k] = v[1 + k] + d[k];
     }
 #pragma unroll
     for (int p = 0; p < NX; p++)
 #pragma unroll
-      for (int q = 0; q <= p; q++) {
-        const int k = p * (p + 1) / 2 + q;
-        r.v[1 + NX + k] = r.v[1 + NX + k] + d[p] * (xv[q] - r.v[1 + q]);
-      }
-    r.v[0] = cnt;
+      for (int q = 0; q <= p; q++) v[1 + NX + p * (p + 1) / 2 + q] += d[p] * d[q];
+    v[0] = v[0] + 1.0;
   }
-  ens_block_reduce<NX>(r, lds);
+  sum_block<LEN>(v, lds);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < LEN; k++) blocks[(uint64_t)blockIdx.x * LEN + k] = r.v[k];
+    for (int k = 0; k < LEN; k++) blocks[(uint64_t)blockIdx.x * LEN + k] = v[k];
   }
 }
 
-template <int NX>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const double *blocks, int nblocks, double *out) {
+// Sum the block records (thread t: blocks t, t+256, ... in order), then convert the
+// shifted sums to the {count, mean, M2} record: mean = x0 + S1/c, M2 = S2 - S1 S1^T / c.
+template <int NX, typename T>
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *x, uint64_t n, const double *blocks,
+                                                     int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
   __shared__ double lds[(kBlock / 64) * LEN];
-  EnsRec<NX> r;
-  // thread t folds blocks t, t + 256, ... sequentially (fixed order)
+  double v[LEN];
 #pragma unroll
-  for (int k = 0; k < LEN; k++) r.v[k] = 0.0;
+  for (int k = 0; k < LEN; k++) v[k] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-    EnsRec<NX> o;
 #pragma unroll
-    for (int k = 0; k < LEN; k++) o.v[k] = blocks[(uint64_t)b * LEN + k];
-    ens_combine<NX>(r, o);
+    for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)b * LEN + k];
   }
-  ens_block_reduce<NX>(r, lds);
+  sum_block<LEN>(v, lds);
   if (threadIdx.x == 0) {
+    const double c = v[0];
+    out[0] = c;
 #pragma unroll
-    for (int k = 0; k < LEN; k++) out[k] = r.v[k];
+    for (int k = 0; k < NX; k++) out[1 + k] = (double)x[k * n] + (c > 0.0 ? v[1 + k] / c : 0.0);
+#pragma unroll
+    for (int p = 0; p < NX; p++)
+#pragma unroll
+      for (int q = 0; q <= p; q++) {
+        const int k = 1 + NX + p * (p + 1) / 2 + q;
+        out[k] = c > 0.0 ? v[k] - v[1 + p] * v[1 + q] / c : 0.0;
+      }
   }
 }
 
@@ -162,13 +141,13 @@ int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double 
   const int nb = ensemble_nblocks(s.n);
   if (nx == 6 && !f64) {
     k_ens_partial<6, float><<<nb, kBlock, 0, st>>>((const float *)s.x, s.n, blocks);
-    k_ens_fold<6><<<1, kBlock, 0, st>>>(blocks, nb, out);
+    k_ens_fold<6, float><<<1, kBlock, 0, st>>>((const float *)s.x, s.n, blocks, nb, out);
   } else if (nx == 9 && !f64) {
     k_ens_partial<9, float><<<nb, kBlock, 0, st>>>((const float *)s.x, s.n, blocks);
-    k_ens_fold<9><<<1, kBlock, 0, st>>>(blocks, nb, out);
+    k_ens_fold<9, float><<<1, kBlock, 0, st>>>((const float *)s.x, s.n, blocks, nb, out);
   } else if (nx == 12 && f64) {
     k_ens_partial<12, double><<<nb, kBlock, 0, st>>>((const double *)s.x, s.n, blocks);
-    k_ens_fold<12><<<1, kBlock, 0, st>>>(blocks, nb, out);
+    k_ens_fold<12, double><<<1, kBlock, 0, st>>>((const double *)s.x, s.n, blocks, nb, out);
   } else {
     return (int)hipErrorInvalidValue;
   }

@@ -1,0 +1,197 @@
+// kf_generic.hpp -- model traits and the generic, fully unrolled KF building blocks
+// shared by the tick kernels (one filter per lane, state in VGPRs).
+//
+// Operation order is the canonical one of oracle/orc_kf_generic.inc (Cholesky form of
+// the update, T = F P then T F^T + Q with ascending-k sums); the library is built with
+// -ffp-contract=off, so GPU and oracle agree bit for bit.
+#pragma once
+#include "fmskf_device.hpp"
+#include "fmskf_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+// ---------------------------------------------------------------------------
+// model traits
+// ---------------------------------------------------------------------------
+// KF6: x = (px, py, th, vx, vy, w); H selects (th, w, vx, vy); F = [[I, dt I], [0, I]]
+struct MdKF6 {
+  using T = float;
+  static constexpr int N = 6, M = 4;
+  __host__ __device__ static constexpr int h1(int a) { return a == 0 ? 2 : a == 1 ? 5 : a == 2 ? 3 : 4; }
+  __host__ __device__ static constexpr int h2(int) { return -1; }
+  __host__ __device__ static constexpr bool pat(int i, int k) { return i < 3 && k == i + 3; }
+};
+// EKF9: x = (px, py, th, vbx, vby, w, bw, abx, aby); h(x) = (th, w+bw, abx, aby, vbx, vby)
+struct MdEKF9 {
+  using T = float;
+  static constexpr int N = 9, M = 6;
+  __host__ __device__ static constexpr int h1(int a) {
+    return a == 0 ? 2 : a == 1 ? 5 : a == 2 ? 7 : a == 3 ? 8 : a == 4 ? 3 : 4;
+  }
+  __host__ __device__ static constexpr int h2(int a) { return a == 1 ? 6 : -1; }
+  __host__ __device__ static constexpr bool pat(int i, int k) {
+    return ((i == 0 || i == 1) && (k == 2 || k == 3 || k == 4)) || (i == 2 && k == 5) ||
+           (i == 3 && k == 7) || (i == 4 && k == 8);
+  }
+};
+// KF12D: KF6 base + arm tip (tx, ty, tz, tvx, tvy, tvz); H selects (th, w, vx, vy, tx, ty, tz, tvz)
+struct MdKF12D {
+  using T = double;
+  static constexpr int N = 12, M = 8;
+  __host__ __device__ static constexpr int h1(int a) {
+    return a == 0 ? 2 : a == 1 ? 5 : a == 2 ? 3 : a == 3 ? 4 : a == 4 ? 6 : a == 5 ? 7 : a == 6 ? 8 : 11;
+  }
+  __host__ __device__ static constexpr int h2(int) { return -1; }
+  __host__ __device__ static constexpr bool pat(int i, int k) {
+    return (i < 3 || (i >= 6 && i < 9)) && k == i + 3;
+  }
+};
+
+template <class Md, typename Prm>
+struct KfArgs {
+  uint64_t n;
+  typename Md::T *x;
+  typename Md::T *P;
+  TickIn in;
+  unsigned long long *counters;
+  Prm prm;
+};
+
+// ---------------------------------------------------------------------------
+// generic update / covariance predict (fully unrolled -> registers only)
+// ---------------------------------------------------------------------------
+template <class Md, typename T = typename Md::T, int N = Md::N, int M = Md::M,
+          int NP = Md::N *(Md::N + 1) / 2>
+__device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M], const T *R) {
+  T HP[M][N];
+#pragma unroll
+  for (int a = 0; a < M; a++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      T v = P[pk(Md::h1(a), j)];
+      if (Md::h2(a) >= 0) v = v + P[pk(Md::h2(a) < 0 ? 0 : Md::h2(a), j)];
+      HP[a][j] = v;
+    }
+  }
+  // S = H P H^T + R = L D L^T (L unit lower, no square roots); E[a][b] = L[a][b] D[b]
+  // is the pre-division value of the recurrence
+  T L[M][M], E[M][M], dinv[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) {
+#pragma unroll
+    for (int b = 0; b <= a; b++) {
+      T s = HP[a][Md::h1(b)];
+      if (Md::h2(b) >= 0) s = s + HP[a][Md::h2(b) < 0 ? 0 : Md::h2(b)];
+      s = s + R[pk(a, b)];
+#pragma unroll
+      for (int k = 0; k < b; k++) s = dfma<T>(-L[a][k], E[b][k], s);
+      if (a == b) {
+        dinv[a] = (T)1 / s;
+      } else {
+        E[a][b] = s;
+        L[a][b] = s * dinv[b];
+      }
+    }
+  }
+  // U = L^-1 HP overwrites HP row by row; w = L^-1 y
+  T w[M];
+#pragma unroll
+  for (int a = 0; a < M; a++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      T s = HP[a][j];
+#pragma unroll
+      for (int k = 0; k < a; k++) s = dfma<T>(-L[a][k], HP[k][j], s);
+      HP[a][j] = s;
+    }
+    T s = y[a];
+#pragma unroll
+    for (int k = 0; k < a; k++) s = dfma<T>(-L[a][k], w[k], s);
+    w[a] = s;
+  }
+  // x += U^T (D^-1 w),  P -= U^T (D^-1 U)
+  T vw[M], V[M][N];
+#pragma unroll
+  for (int a = 0; a < M; a++) {
+    vw[a] = w[a] * dinv[a];
+#pragma unroll
+    for (int j = 0; j < N; j++) V[a][j] = HP[a][j] * dinv[a];
+  }
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    T t = HP[0][j] * vw[0];
+#pragma unroll
+    for (int a = 1; a < M; a++) t = dfma<T>(HP[a][j], vw[a], t);
+    x[j] = x[j] + t;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      T t = HP[0][i] * V[0][j];
+#pragma unroll
+      for (int a = 1; a < M; a++) t = dfma<T>(HP[a][i], V[a][j], t);
+      P[pk(i, j)] = P[pk(i, j)] - t;
+    }
+  }
+}
+
+// P <- F P F^T + Q, F = I + Fv(i,k) on the compile-time pattern Md::pat
+template <class Md, class FV, typename T = typename Md::T, int N = Md::N,
+          int NP = Md::N *(Md::N + 1) / 2>
+__device__ __forceinline__ void kf_predict_cov(T (&P)[NP], const FV &fv, const T *Q) {
+  T Tm[N][N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      T t = P[pk(i, j)];
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(i, k)) t = dfma<T>(fv(i, k), P[pk(k, j)], t);
+      Tm[i][j] = t;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      T t = Tm[i][j];
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(j, k)) t = dfma<T>(fv(j, k), Tm[i][k], t);
+      P[pk(i, j)] = t + Q[pk(i, j)];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-model measurement frontends and time updates
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void unpack4(uint2 r, int16_t (&o)[4]) {
+  o[0] = (int16_t)(r.x & 0xFFFFu);
+  o[1] = (int16_t)(r.x >> 16);
+  o[2] = (int16_t)(r.y & 0xFFFFu);
+  o[3] = (int16_t)(r.y >> 16);
+}
+
+// Count instances whose state became non-finite (one atomic per wave, rare path).
+template <typename T, int N, int NP>
+__device__ __forceinline__ void nan_guard(const T (&x)[N], const T (&P)[NP],
+                                          unsigned long long *counters) {
+  T acc = x[0];
+#pragma unroll
+  for (int k = 1; k < N; k++) acc = acc + x[k];
+#pragma unroll
+  for (int k = 0; k < NP; k++) acc = acc + P[k];
+  const bool bad = !__builtin_isfinite(acc);
+  const unsigned long long m = __ballot(bad);
+  if (m && (threadIdx.x & 63) == __builtin_ctzll(m))
+    atomicAdd(counters, (unsigned long long)__popcll(m));
+}
+
+static inline dim3 grid_for(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+}  // namespace fmskf

@@ -26,8 +26,13 @@ run() {  # name limit cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p pytest_timeout --timeout 600 -rf ;;
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout 600 -rf ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    sweep) for v in ${VARIANTS:-0 2 3 4}; do
+             export FMSKF_KF6_VARIANT=$v
+             run kb_v$v 180 python tools/kbench.py ${KB_ARGS:-}
+           done
+           unset FMSKF_KF6_VARIANT ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-fused ;;
     pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \

@@ -1,0 +1,142 @@
+// membench.hip -- bandwidth ceilings for the KF6 tick's access pattern on MI355X.
+//
+// Streams exactly the bytes of one KF6 tick (27 fp32 state planes read + written,
+// yaw/gyro planes and the [N][4] int16 rpm plane read = 232 B per instance) with no
+// arithmetic, at 1, 2 and 4 instances per lane (dword / dwordx2 / dwordx4 accesses),
+// plus a plain float4 copy of the same byte count.  Prints GB/s of algorithmic bytes.
+//   hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench && build/membench [log2N]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e = (x);                                                       \
+    if (e != hipSuccess) {                                                    \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+template <int IPL>
+struct Vec;
+template <>
+struct Vec<1> {
+  using F = float;
+  using R = uint2;
+};
+template <>
+struct Vec<2> {
+  using F = float2;
+  using R = uint4;
+};
+
+template <int IPL>
+__global__ __launch_bounds__(256) void k_pattern(float *st, const float *yaw, const float *gz,
+                                                 const uint2 *rpm, uint64_t n, float sink) {
+  using F = typename Vec<IPL>::F;
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // vector index
+  const uint64_t nv = n / IPL;
+  if (v >= nv) return;
+  F s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = reinterpret_cast<const F *>(st + k * n)[v];
+  const F a = reinterpret_cast<const F *>(yaw)[v];
+  const F b = reinterpret_cast<const F *>(gz)[v];
+  uint2 r[IPL];
+#pragma unroll
+  for (int q = 0; q < IPL; q++) r[q] = rpm[v * IPL + q];
+  float m = sink;
+  if constexpr (IPL == 1) {
+    m = m * a * b * (float)(r[0].x & 1);
+  } else {
+    m = m * a.x * b.y * (float)(r[0].x & r[1].y & 1);
+  }
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    F t = s[k];
+    if constexpr (IPL == 1) t = t + m;
+    else {
+      t.x = t.x + m;
+      t.y = t.y + m;
+    }
+    reinterpret_cast<F *>(st + k * n)[v] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pattern4(float *st, const float *yaw, const float *gz,
+                                                  const uint4 *rpm, uint64_t n, float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n / 4) return;
+  float4 s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = reinterpret_cast<const float4 *>(st + k * n)[v];
+  const float4 a = reinterpret_cast<const float4 *>(yaw)[v];
+  const float4 b = reinterpret_cast<const float4 *>(gz)[v];
+  const uint4 r0 = rpm[2 * v], r1 = rpm[2 * v + 1];
+  const float m = sink * a.x * b.w * (float)(r0.x & r1.w & 1);
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    float4 t = s[k];
+    t.x += m;
+    t.y += m;
+    t.z += m;
+    t.w += m;
+    reinterpret_cast<float4 *>(st + k * n)[v] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
+    b[i] = a[i];
+}
+
+int main(int argc, char **argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 20;
+  const uint64_t n = 1ull << lg;
+  float *st, *yaw, *gz, *ca, *cb;
+  uint2 *rpm;
+  CK(hipMalloc(&st, 27 * n * 4));
+  CK(hipMalloc(&yaw, n * 4));
+  CK(hipMalloc(&gz, n * 4));
+  CK(hipMalloc(&rpm, n * 8));
+  CK(hipMemset(st, 0, 27 * n * 4));
+  CK(hipMemset(yaw, 0, n * 4));
+  CK(hipMemset(gz, 0, n * 4));
+  CK(hipMemset(rpm, 0, n * 8));
+  const uint64_t bytes = 232 * n;
+  CK(hipMalloc(&ca, bytes / 2));
+  CK(hipMalloc(&cb, bytes / 2));
+  CK(hipMemset(ca, 0, bytes / 2));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int iters = 100;
+  auto timeit = [&](const char *name, auto launch) {
+    for (int w = 0; w < 5; w++) launch();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int it = 0; it < iters; it++) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / iters;
+    printf("{\"n\": %llu, \"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n", (unsigned long long)n,
+           name, us, bytes / (us * 1e-6) / 1e9);
+  };
+  timeit("pattern_ipl1_dword", [&] {
+    k_pattern<1><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
+  });
+  timeit("pattern_ipl2_dwordx2", [&] {
+    k_pattern<2><<<(unsigned)((n / 2 + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
+  });
+  timeit("pattern_ipl4_dwordx4", [&] {
+    k_pattern4<<<(unsigned)((n / 4 + 255) / 256), 256>>>(st, yaw, gz, (const uint4 *)rpm, n, 0.f);
+  });
+  timeit("copy_float4_same_bytes", [&] {
+    k_copy4<<<2048, 256>>>((const float4 *)ca, (float4 *)cb, bytes / 2 / 16);
+  });
+  return 0;
+}
