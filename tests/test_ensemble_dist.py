@@ -1,0 +1,77 @@
+"""N > 1 path on CPU: world-size-2 gloo.
+
+Each rank owns a contiguous shard of the robots (the bench's sharding), reduces it to the
+{count, mean, M2} record (here with the oracle: no GPU on this host), the ranks all-gather
+the records, and every rank folds them in rank order with the library's host routine
+fmskf_ensemble_combine.  The result must equal the statistics of the unsharded data and be
+bitwise identical on both ranks.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard(n, world, rank):
+    per = n // world
+    lo = rank * per
+    hi = n if rank == world - 1 else lo + per
+    return lo, hi
+
+
+def _worker(rank, world, port, n, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "roboken-fmskf-robot-controller_amd")]
+    import torch.distributed as dist
+    import torch
+    import fmskf
+    from oracle import oracle as orc
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(1234)  # same global data on every rank
+    x = (rng.normal(size=(6, n)) * np.arange(1, 7)[:, None] + 5.0).astype(np.float32)
+    lo, hi = _shard(n, world, rank)
+    rec = torch.from_numpy(orc.ens_partial(np.ascontiguousarray(x[:, lo:hi])))
+    gathered = [torch.zeros_like(rec) for _ in range(world)]
+    dist.all_gather(gathered, rec)
+    recs = torch.stack(gathered).numpy()
+    mean, cov = fmskf.ensemble_combine(6, recs)
+    np.save(os.path.join(out_dir, f"r{rank}_mean.npy"), mean)
+    np.save(os.path.join(out_dir, f"r{rank}_cov.npy"), cov)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [10001, 65536])
+def test_ensemble_gloo_world2(tmp_path, orc, n):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
+    m0, c0 = np.load(tmp_path / "r0_mean.npy"), np.load(tmp_path / "r0_cov.npy")
+    m1, c1 = np.load(tmp_path / "r1_mean.npy"), np.load(tmp_path / "r1_cov.npy")
+    assert np.array_equal(m0, m1) and np.array_equal(c0, c1), "ranks disagree"
+    rng = np.random.default_rng(1234)
+    x = (rng.normal(size=(6, n)) * np.arange(1, 7)[:, None] + 5.0).astype(np.float32)
+    ref = np.cov(x.astype(np.float64))
+    np.testing.assert_allclose(m0, x.astype(np.float64).mean(axis=1), rtol=1e-12)
+    packed = np.array([ref[i, j] for i in range(6) for j in range(i + 1)])
+    np.testing.assert_allclose(c0, packed, rtol=1e-10)
+
+
+def test_shard_covers_all():
+    for n in (1, 7, 1 << 20):
+        for world in (1, 2, 3, 8):
+            spans = [_shard(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))

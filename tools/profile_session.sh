@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# GPU-box profiling session for the headline kernel:
+#   1. bench.py (the driver's default command) -> gpurun_out/bench.log
+#   2. rocprofv3 --kernel-trace --stats of the same bench -> gpurun_out/prof/
+#   3. rocprofv3 --pmc FETCH_SIZE and (separate pass) WRITE_SIZE of the tick kernel at the bench
+#      shape and of tools/membench.hip's pattern kernel (same access pattern, known bytes:
+#      the calibration the MI355X guide asks for before trusting absolute counter values)
+# Each GPU step has its own limit; a crash/timeout (rc not in {0,1}) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT" build
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!!! stopping"; exit $rc; fi
+}
+[ -x build/membench ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench
+run bench 600 python bench.py
+run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+  python bench.py --steps 400 --warmup 40 --no-cpu-baseline --no-fused
+for c in FETCH_SIZE WRITE_SIZE; do
+  run pmc_kf6_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_kf6_$c" -o run -- \
+    python tools/kbench.py --ticks 30
+  run pmc_pat_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_pat_$c" -o run -- \
+    build/membench 20
+done
+echo "=== session done"
