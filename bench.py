@@ -102,11 +102,14 @@ def main():
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # a torch.distributed.run launch (RANK set) always builds the RCCL group, also at N=1,
+    # so the collective path is the one measured whenever the launcher is used
+    distributed = world > 1 or "RANK" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier(device_ids=[local])
 
     n = args.n_per_gpu
@@ -129,7 +132,7 @@ def main():
         if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
             eng.ensemble_partial(rec)
             slot = gathered[ev_count[0] % n_events]
-            if world > 1:
+            if distributed:
                 dist.all_gather_into_tensor(slot.view(-1), rec)
             else:
                 slot[0].copy_(rec)
@@ -153,7 +156,7 @@ def main():
     barrier()
     elapsed = t1 - t0
     region_ms = ev0.elapsed_time(ev1)
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed, region_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, region_ms = float(t[0].item()), float(t[1].item())
@@ -251,7 +254,7 @@ def main():
     eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -609,6 +609,18 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
     F[pos[a]][pos[a] + 3] = prm->dt;
     pat[pos[a]][pos[a] + 3] = 1;
   }
+  /* R without base/tip cross terms: the joint update is the base-group update followed by
+   * the tip-group update (innovation taken from the updated state); canonical order then */
+  int seq = 1;
+  for (int a = 4; a < 8; a++)
+    for (int b = 0; b < 4; b++)
+      if (prm->r[a * (a + 1) / 2 + b] != 0.0) seq = 0;
+  double r1[10], r2[10];
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b <= a; b++) {
+      r1[a * (a + 1) / 2 + b] = prm->r[a * (a + 1) / 2 + b];
+      r2[a * (a + 1) / 2 + b] = prm->r[(a + 4) * (a + 5) / 2 + (b + 4)];
+    }
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel for num_threads(nthreads) schedule(static)
@@ -620,9 +632,17 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
     for (int k = 0; k < 78; k++) Ps[k] = P[k * n + i];
     if (do_update && (!valid || valid[i])) {
       double y[8];
-      for (int a = 0; a < 8; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
-      y[0] = orc_wrap_innov_d(y[0]);
-      orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r);
+      if (seq) {
+        for (int a = 0; a < 4; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
+        y[0] = orc_wrap_innov_d(y[0]);
+        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1, k_kf12_h2, y, r1);
+        for (int a = 0; a < 4; a++) y[a] = z[(a + 4) * n + i] - xs[k_kf12_h1[a + 4]];
+        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1 + 4, k_kf12_h2 + 4, y, r2);
+      } else {
+        for (int a = 0; a < 8; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
+        y[0] = orc_wrap_innov_d(y[0]);
+        orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r);
+      }
     }
     if (do_predict) {
       for (int a = 0; a < 6; a++) xs[pos[a]] = fma(prm->dt, xs[pos[a] + 3], xs[pos[a]]);

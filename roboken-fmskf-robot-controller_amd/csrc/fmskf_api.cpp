@@ -262,6 +262,8 @@ void convert_params(fmskf_ctx *h) {
   h->kf12.dt = c.dt;
   for (int k = 0; k < 78; k++) h->kf12.q[k] = c.q[k];
   for (int k = 0; k < 36; k++) h->kf12.r[k] = c.r[k];
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b <= a; b++) h->kf12.r2[a * (a + 1) / 2 + b] = c.r[(a + 4) * (a + 5) / 2 + (b + 4)];
 }
 
 void do_reset(fmskf_ctx *h) {

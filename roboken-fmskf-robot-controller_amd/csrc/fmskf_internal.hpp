@@ -64,7 +64,19 @@ struct KfParams {
 };
 using Kf6Params = KfParams<float, 21, 10>;
 using Ekf9Params = KfParams<float, 45, 21>;
-using Kf12dParams = KfParams<double, 78, 36>;
+struct Kf12dParams {
+  double dt;
+  double q[78];
+  double r[36];   // full packed 8x8 R (joint update)
+  double r2[10];  // packed R of the arm-tip group (rows/cols 4..7), used by the sequential path
+};
+// true when R has no terms between the base group (0..3) and the tip group (4..7)
+inline bool kf12d_sequential(const double *r36) {
+  for (int i = 4; i < 8; i++)
+    for (int j = 0; j < 4; j++)
+      if (r36[i * (i + 1) / 2 + j] != 0.0) return false;
+  return true;
+}
 
 struct Wt901Cfg {
   uint32_t read_reg_index;

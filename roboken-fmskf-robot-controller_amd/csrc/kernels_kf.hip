@@ -92,7 +92,9 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   nan_guard(x, P, a.counters);
 }
 
-template <bool UPD, bool PRED>
+// SEQ: R has no base/tip cross terms -> group-sequential update (base group, then tip group
+// with the innovation of the updated state); otherwise the joint 8-measurement update.
+template <bool SEQ, bool UPD, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
   const uint64_t n = a.n;
@@ -108,11 +110,23 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
     const uint64_t base = (uint64_t)t * a.in.stride * M;
     if (UPD) {
       if (a.in.valid == nullptr || a.in.valid[(uint64_t)t * a.in.stride + i]) {
-        double y[M];
+        if (SEQ) {
+          double y[4];
 #pragma unroll
-        for (int q = 0; q < M; q++) y[q] = a.in.z[base + q * a.in.stride + i] - x[MdKF12D::h1(q)];
-        y[0] = wrap_innov(y[0]);
-        kf_update<MdKF12D>(x, P, y, a.prm.r);
+          for (int q = 0; q < 4; q++) y[q] = a.in.z[base + q * a.in.stride + i] - x[MdKF12D_G1::h1(q)];
+          y[0] = wrap_innov(y[0]);
+          kf_update<MdKF12D_G1>(x, P, y, a.prm.r);
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            y[q] = a.in.z[base + (4 + q) * a.in.stride + i] - x[MdKF12D_G2::h1(q)];
+          kf_update<MdKF12D_G2>(x, P, y, a.prm.r2);
+        } else {
+          double y[M];
+#pragma unroll
+          for (int q = 0; q < M; q++) y[q] = a.in.z[base + q * a.in.stride + i] - x[MdKF12D::h1(q)];
+          y[0] = wrap_innov(y[0]);
+          kf_update<MdKF12D>(x, P, y, a.prm.r);
+        }
       }
     }
     if (PRED) {
@@ -152,9 +166,15 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
                  hipStream_t st) {
   KfArgs<MdKF12D, Kf12dParams> a{s.n, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
-  if (upd && pred) k_kf12d<true, true><<<g, kBlock, 0, st>>>(a);
-  else if (upd) k_kf12d<true, false><<<g, kBlock, 0, st>>>(a);
-  else k_kf12d<false, true><<<g, kBlock, 0, st>>>(a);
+  if (kf12d_sequential(p.r)) {
+    if (upd && pred) k_kf12d<true, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_kf12d<true, true, false><<<g, kBlock, 0, st>>>(a);
+    else k_kf12d<true, false, true><<<g, kBlock, 0, st>>>(a);
+  } else {
+    if (upd && pred) k_kf12d<false, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_kf12d<false, true, false><<<g, kBlock, 0, st>>>(a);
+    else k_kf12d<false, false, true><<<g, kBlock, 0, st>>>(a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -49,6 +49,22 @@ struct MdKF12D {
   }
 };
 
+// KF12D measured in two groups: base (th, w, vx, vy) and arm tip (tx, ty, tz, tvz).  When R
+// has no cross-group terms the joint update equals the two group updates in sequence
+// (canonical order then: group 1, then group 2), which halves the live update matrices.
+struct MdKF12D_G1 {
+  using T = double;
+  static constexpr int N = 12, M = 4;
+  __host__ __device__ static constexpr int h1(int a) { return a == 0 ? 2 : a == 1 ? 5 : a == 2 ? 3 : 4; }
+  __host__ __device__ static constexpr int h2(int) { return -1; }
+};
+struct MdKF12D_G2 {
+  using T = double;
+  static constexpr int N = 12, M = 4;
+  __host__ __device__ static constexpr int h1(int a) { return a == 0 ? 6 : a == 1 ? 7 : a == 2 ? 8 : 11; }
+  __host__ __device__ static constexpr int h2(int) { return -1; }
+};
+
 template <class Md, typename Prm>
 struct KfArgs {
   uint64_t n;

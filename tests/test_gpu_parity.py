@@ -241,16 +241,21 @@ def test_ekf9_bitexact(orc):
     bits_equal(P, Po, "P")
 
 
-def test_kf12d_vs_oracle(orc):
+@pytest.mark.parametrize("cross", [False, True], ids=["blockdiag_R_sequential", "joint_R"])
+def test_kf12d_vs_oracle(orc, cross):
     n, T = 700, 20
     tr = Trajectory(n, T, seed=51)
     z = tr.kf12d_z()
     cfg = fmskf.default_config("kf12d", n)
-    with Engine("kf12d", n) as e:
+    r = np.array(cfg.r[:36])
+    if cross:  # base/tip measurement correlation -> the joint 8-measurement update
+        r[4 * 5 // 2 + 0] = 1e-5
+        r[7 * 8 // 2 + 3] = -2e-5
+    with Engine("kf12d", n, r=r) as e:
         for t in range(T):
             e.tick(z=z[t])
         x, P = e.get_state()
-    prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), np.array(cfg.r[:36]))
+    prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), r)
     xo = np.zeros((12, n))
     Po = np.repeat(np.array(cfg.p0[:78])[:, None], n, 1).copy()
     for t in range(T):

@@ -28,6 +28,12 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout 600 -rf ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    dist1) run dist1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+             --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --steps 200 \
+             --warmup 20 --no-cpu-baseline --no-fused ;;
+    kb)    i=0; IFS=';' read -ra KBL <<< "${KB_LIST:-}"; for a in "${KBL[@]}"; do
+             i=$((i+1)); run kb$i 240 python tools/kbench.py $a
+           done ;;
     sweep) for v in ${VARIANTS:-0 2 3 4}; do
              export FMSKF_KF6_VARIANT=$v
              run kb_v$v 180 python tools/kbench.py ${KB_ARGS:-}
