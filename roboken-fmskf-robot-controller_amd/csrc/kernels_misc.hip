@@ -1,12 +1,13 @@
 // kernels_misc.hip -- sin/cos policy evaluation and the ensemble statistics reduction.
 //
 // Ensemble: mean and covariance of the state x across all instances of a rank, in fp64.
-// Each thread accumulates shifted moment sums of its grid-stride instances (no division
-// in the streaming loop), waves sum by a fixed xor butterfly, the 4 waves of a block
-// through LDS in wave order, and one block folds the per-block sums in block order and
-// converts them to the Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]}
-// that ranks all-gather and combine in rank order.  No atomics anywhere: the result is
-// bitwise reproducible run to run.
+// Each thread accumulates shifted moment sums of its grid-stride instances (no division in
+// the streaming loop), each block sums its threads through an LDS transpose in a fixed
+// order, and a one-block fold sums the per-block records in block order and converts them
+// to the Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]} that ranks
+// all-gather and combine in rank order.  No atomics: bitwise reproducible run to run.
+// (A single-launch "last block folds" variant measured slower: the agent-scope release
+// fence each block needs writes back the XCD's whole L2.)
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
 
@@ -39,115 +40,148 @@ template <int NX>
 struct EnsRec {
   static constexpr int NP = NX * (NX + 1) / 2;
   static constexpr int LEN = 1 + NX + NP;
-  double v[LEN];
 };
 
-// Plain sums of a record {count, S1[n], S2 packed} over the block: butterfly over the wave
-// (fixed xor order), then the 4 waves through LDS in wave order.  Deterministic.
+constexpr int kEnsPerThread = 8;  // instances per thread at full grid (n = 2^20: 512 blocks)
+constexpr int kEnsCh = 16;        // record elements reduced per LDS pass
+
+// Sum v[LEN] over the 256 threads of the block into tot[LEN] (LDS, visible to all threads
+// after return).  Transpose through LDS in chunks of 16 elements: thread t writes column t;
+// then 16 threads per element sum 16 columns each (column j*16+seg, j ascending), then one
+// thread per element sums the 16 segment partials in order.  Fixed order -> deterministic;
+// no cross-lane shuffles (the LDS bandwidth of a shuffle butterfly is ~6x this).
 template <int LEN>
-__device__ __forceinline__ void sum_block(double (&v)[LEN], double *lds) {
+__device__ __forceinline__ void block_sum(const double (&v)[LEN], double (*red)[kBlock],
+                                          double (*part)[kEnsCh], double *tot) {
+  const int t = threadIdx.x;
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
+  for (int c = 0; c < LEN; c += kEnsCh) {
 #pragma unroll
-    for (int k = 0; k < LEN; k++) v[k] = v[k] + __shfl_xor(v[k], off, 64);
-  }
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
+    for (int e = 0; e < kEnsCh; e++)
+      if (c + e < LEN) red[e][t] = v[c + e];
+    __syncthreads();
+    {
+      const int e = t >> 4, seg = t & 15;
+      if (c + e < LEN) {
+        double s = red[e][seg];
 #pragma unroll
-    for (int k = 0; k < LEN; k++) lds[wave * LEN + k] = v[k];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < LEN; k++) {
-      double s = lds[k];
-      for (int w = 1; w < kBlock / 64; w++) s = s + lds[w * LEN + k];
-      v[k] = s;
+        for (int j = 1; j < kBlock / kEnsCh; j++) s = s + red[e][j * kEnsCh + seg];
+        part[e][seg] = s;
+      }
     }
+    __syncthreads();
+    if (t < kEnsCh && c + t < LEN) {
+      double s = part[t][0];
+#pragma unroll
+      for (int j = 1; j < kEnsCh; j++) s = s + part[t][j];
+      tot[c + t] = s;
+    }
+    __syncthreads();
   }
 }
 
-// Shifted moment sums: S1 = sum(x - x0), S2 = sum((x - x0)(x - x0)^T) with the shift x0 =
-// instance 0's state (the same for every block), fp64, no division in the streaming loop.
+// Partial: every block accumulates shifted moment sums S1 = sum(x - x0),
+// S2 = sum((x - x0)(x - x0)^T) (x0 = instance 0's state, fp64, no division in the streaming
+// loop) of its grid-stride instances and writes its record.
 template <int NX, typename T>
-__global__ __launch_bounds__(kBlock) void k_ens_partial(const T *x, uint64_t n, double *blocks) {
+__global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
+                                                        double *blocks) {
   constexpr int LEN = EnsRec<NX>::LEN;
-  __shared__ double lds[(kBlock / 64) * LEN];
+  constexpr int U = 4;
+  __shared__ double red[kEnsCh][kBlock];
+  __shared__ double part[kEnsCh][kEnsCh];
+  __shared__ double tot[LEN];
   double sh[NX], v[LEN];
 #pragma unroll
   for (int k = 0; k < NX; k++) sh[k] = (double)x[k * n];
 #pragma unroll
   for (int k = 0; k < LEN; k++) v[k] = 0.0;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    double d[NX];
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += U * stride) {
+    T xv[U][NX];
 #pragma unroll
-    for (int k = 0; k < NX; k++) {
-      d[k] = (double)x[k * n + i] - sh[k];
-      v[1 + k] = v[1 + k] + d[k];
+    for (int u = 0; u < U; u++) {
+      const uint64_t i = i0 + u * stride;
+#pragma unroll
+      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[k * n + i] : (T)0;
     }
 #pragma unroll
-    for (int p = 0; p < NX; p++)
+    for (int u = 0; u < U; u++) {
+      if (i0 + u * stride >= n) break;
+      double d[NX];
 #pragma unroll
-      for (int q = 0; q <= p; q++) v[1 + NX + p * (p + 1) / 2 + q] += d[p] * d[q];
-    v[0] = v[0] + 1.0;
-  }
-  sum_block<LEN>(v, lds);
-  if (threadIdx.x == 0) {
+      for (int k = 0; k < NX; k++) {
+        d[k] = (double)xv[u][k] - sh[k];
+        v[1 + k] = v[1 + k] + d[k];
+      }
 #pragma unroll
-    for (int k = 0; k < LEN; k++) blocks[(uint64_t)blockIdx.x * LEN + k] = v[k];
+      for (int p = 0; p < NX; p++)
+#pragma unroll
+        for (int q = 0; q <= p; q++) v[1 + NX + p * (p + 1) / 2 + q] += d[p] * d[q];
+      v[0] = v[0] + 1.0;
+    }
   }
+  block_sum<LEN>(v, red, part, tot);
+  for (int k = threadIdx.x; k < LEN; k += kBlock) blocks[(uint64_t)blockIdx.x * LEN + k] = tot[k];
 }
 
-// Sum the block records (thread t: blocks t, t+256, ... in order), then convert the
-// shifted sums to the {count, mean, M2} record: mean = x0 + S1/c, M2 = S2 - S1 S1^T / c.
+// Fold (one block): thread t sums block records t, t + 256, ... in order, then the block sum,
+// then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
 template <int NX, typename T>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *x, uint64_t n, const double *blocks,
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t n,
+                                                     const double *__restrict__ blocks,
                                                      int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
-  __shared__ double lds[(kBlock / 64) * LEN];
+  __shared__ double red[kEnsCh][kBlock];
+  __shared__ double part[kEnsCh][kEnsCh];
+  __shared__ double tot[LEN];
   double v[LEN];
 #pragma unroll
   for (int k = 0; k < LEN; k++) v[k] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+    const double *rb = blocks + (uint64_t)b * LEN;
 #pragma unroll
-    for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)b * LEN + k];
+    for (int k = 0; k < LEN; k++) v[k] = v[k] + rb[k];
   }
-  sum_block<LEN>(v, lds);
-  if (threadIdx.x == 0) {
-    const double c = v[0];
-    out[0] = c;
-#pragma unroll
-    for (int k = 0; k < NX; k++) out[1 + k] = (double)x[k * n] + (c > 0.0 ? v[1 + k] / c : 0.0);
-#pragma unroll
-    for (int p = 0; p < NX; p++)
-#pragma unroll
-      for (int q = 0; q <= p; q++) {
-        const int k = 1 + NX + p * (p + 1) / 2 + q;
-        out[k] = c > 0.0 ? v[k] - v[1 + p] * v[1 + q] / c : 0.0;
-      }
+  block_sum<LEN>(v, red, part, tot);
+  const double c = tot[0];
+  for (int k = threadIdx.x; k < LEN; k += kBlock) {
+    double r;
+    if (k == 0) {
+      r = c;
+    } else if (k <= NX) {
+      r = (double)x[(k - 1) * n] + (c > 0.0 ? tot[k] / c : 0.0);
+    } else {
+      int p = 0, q = k - 1 - NX;
+      while (q > p) q -= ++p;
+      r = c > 0.0 ? tot[k] - tot[1 + p] * tot[1 + q] / c : 0.0;
+    }
+    out[k] = r;
   }
 }
 
 int ensemble_nblocks(uint64_t n) {
-  uint64_t b = (n + kBlock - 1) / kBlock;
+  uint64_t b = (n + (uint64_t)kBlock * kEnsPerThread - 1) / ((uint64_t)kBlock * kEnsPerThread);
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;
   return (int)b;
 }
 
+template <int NX, typename T>
+static void ens_launch(const DevState &s, double *blocks, double *out, hipStream_t st) {
+  const int nb = ensemble_nblocks(s.n);
+  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, blocks);
+  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.n, blocks, nb, out);
+}
+
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
                     hipStream_t st) {
-  const int nb = ensemble_nblocks(s.n);
   if (nx == 6 && !f64) {
-    k_ens_partial<6, float><<<nb, kBlock, 0, st>>>((const float *)s.x, s.n, blocks);
-    k_ens_fold<6, float><<<1, kBlock, 0, st>>>((const float *)s.x, s.n, blocks, nb, out);
+    ens_launch<6, float>(s, blocks, out, st);
   } else if (nx == 9 && !f64) {
-    k_ens_partial<9, float><<<nb, kBlock, 0, st>>>((const float *)s.x, s.n, blocks);
-    k_ens_fold<9, float><<<1, kBlock, 0, st>>>((const float *)s.x, s.n, blocks, nb, out);
+    ens_launch<9, float>(s, blocks, out, st);
   } else if (nx == 12 && f64) {
-    k_ens_partial<12, double><<<nb, kBlock, 0, st>>>((const double *)s.x, s.n, blocks);
-    k_ens_fold<12, double><<<1, kBlock, 0, st>>>((const double *)s.x, s.n, blocks, nb, out);
+    ens_launch<12, double>(s, blocks, out, st);
   } else {
     return (int)hipErrorInvalidValue;
   }

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ticks", type=int, default=300)
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     args = ap.parse_args()
     import numpy as np
@@ -56,11 +56,24 @@ def main():
         z[:, 1] = -torch.deg2rad(gz.double())
         preps = [e.prepare(z=z[r]) for r in range(R)]
         many = dict(z=z)
-    tick = getattr(fmskf.load(), "fmskf_" + args.op)
+    tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op == "ensemble" else args.op))
     for k in range(20):
         e.tick_prepared(preps[k % R], tick)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if args.op == "ensemble":  # the ensemble record reduction alone (partial + fold)
+        rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
+        e.ensemble_partial(rec)
+        torch.cuda.synchronize()
+        ev0.record(st)
+        for _ in range(args.ticks):
+            e.ensemble_partial(rec)
+        ev1.record(st)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / args.ticks
+        print(json.dumps({"model": args.model, "n": n, "op": "ensemble", "ms_per_call": ms,
+                          "x_GBps": e.nx * e.elem * n / (ms * 1e-3) / 1e9}), flush=True)
+        return
     if args.many:
         reps = max(1, args.ticks // args.many)
         sub = {k: v[: args.many] for k, v in many.items()}
