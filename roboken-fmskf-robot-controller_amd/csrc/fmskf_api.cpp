@@ -272,9 +272,10 @@ void do_reset(fmskf_ctx *h) {
   const Dims d = h->d;
   const uint32_t np = d.nx * (d.nx + 1) / 2;
   hipStream_t st = h->stream;
-  hip_check(hipMemsetAsync(s.x, 0, (size_t)d.nx * n * d.elem, st), "reset x");
+  const uint64_t pp = s.pitch;
+  hip_check(hipMemsetAsync(s.x, 0, (size_t)d.nx * pp * d.elem, st), "reset x");
   if (d.m > 0) {
-    hip_check(hipMemsetAsync(s.P, 0, (size_t)np * n * d.elem, st), "reset P");
+    hip_check(hipMemsetAsync(s.P, 0, (size_t)np * pp * d.elem, st), "reset P");
     for (uint32_t i = 0; i < d.nx; i++) {
       for (uint32_t j = 0; j <= i; j++) {
         const double v = h->cfg.p0[i * (i + 1) / 2 + j];
@@ -284,16 +285,16 @@ void do_reset(fmskf_ctx *h) {
           float f = (float)v;
           uint32_t bits;
           memcpy(&bits, &f, 4);
-          hip_check(hipMemsetD32Async((hipDeviceptr_t)((float *)s.P + k * n), bits, n, st), "reset P0");
+          hip_check(hipMemsetD32Async((hipDeviceptr_t)((float *)s.P + k * pp), bits, n, st), "reset P0");
         } else {
           uint64_t bits;
           memcpy(&bits, &v, 8);
-          launch_check(launch_fill64((double *)s.P + k * n, bits, n, st), "reset P0");
+          launch_check(launch_fill64((double *)s.P + k * pp, bits, n, st), "reset P0");
         }
       }
     }
   }
-  if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * n * 8, st), "reset prev");
+  if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * pp * 8, st), "reset prev");
   hip_check(hipMemsetAsync(s.imu_reg, 0, 0x90 * n * 2, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_parser, 0, 3 * n * 4, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_cnt, 0, n, st), "reset imu");
@@ -409,6 +410,20 @@ void copy_out(fmskf_ctx *h, void *dst, const void *src, size_t bytes, uint32_t m
     fail(FMSKF_EINVAL, "bad mem flag");
   }
 }
+// `planes` planes of `row` bytes: device planes at `dev_pitch` bytes <-> dense user planes
+void copy_planes_out(fmskf_ctx *h, void *dst, const void *src, size_t row, size_t dev_pitch,
+                     size_t planes, uint32_t mem) {
+  if (!dst) return;
+  if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+  const hipMemcpyKind k = mem == FMSKF_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  hip_check(hipMemcpy2DAsync(dst, row, src, dev_pitch, row, planes, k, h->stream), "copy planes");
+}
+void copy_planes_in(fmskf_ctx *h, void *dst, const void *src, size_t row, size_t dev_pitch,
+                    size_t planes, uint32_t mem) {
+  if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+  const hipMemcpyKind k = mem == FMSKF_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  hip_check(hipMemcpy2DAsync(dst, dev_pitch, src, row, row, planes, k, h->stream), "copy planes");
+}
 void finish_out(fmskf_ctx *h, uint32_t mem) {
   if (mem == FMSKF_MEM_HOST) hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
 }
@@ -479,9 +494,10 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.n = n;
       s.model = cfg->model;
       const uint32_t np = d.nx * (d.nx + 1) / 2;
-      s.x = h->alloc<char>((size_t)d.nx * n * d.elem);
-      s.P = d.m ? h->alloc<char>((size_t)np * n * d.elem) : nullptr;
-      s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * n) : nullptr;
+      s.pitch = plane_pitch(n);
+      s.x = h->alloc<char>((size_t)d.nx * s.pitch * d.elem);
+      s.P = d.m ? h->alloc<char>((size_t)np * s.pitch * d.elem) : nullptr;
+      s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
       s.imu_reg = h->alloc<int16_t>(0x90 * n);
       s.imu_parser = h->alloc<uint32_t>(3 * n);
       s.imu_cnt = h->alloc<uint8_t>(n);
@@ -649,10 +665,11 @@ int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem) {
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
     const Dims d = h->d;
-    copy_out(h, x, h->s.x, (size_t)d.nx * n * d.elem, mem);
+    const size_t row = (size_t)n * d.elem, pb = (size_t)h->s.pitch * d.elem;
+    copy_planes_out(h, x, h->s.x, row, pb, d.nx, mem);
     if (p_packed) {
       if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
-      copy_out(h, p_packed, h->s.P, (size_t)(d.nx * (d.nx + 1) / 2) * n * d.elem, mem);
+      copy_planes_out(h, p_packed, h->s.P, row, pb, d.nx * (d.nx + 1) / 2, mem);
     }
     finish_out(h, mem);
   });
@@ -664,14 +681,12 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
     const Dims d = h->d;
-    const hipMemcpyKind k = mem == FMSKF_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
     if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
-    if (x) hip_check(hipMemcpyAsync(h->s.x, x, (size_t)d.nx * n * d.elem, k, h->stream), "set x");
+    const size_t row = (size_t)n * d.elem, pb = (size_t)h->s.pitch * d.elem;
+    if (x) copy_planes_in(h, h->s.x, x, row, pb, d.nx, mem);
     if (p_packed) {
       if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
-      hip_check(hipMemcpyAsync(h->s.P, p_packed, (size_t)(d.nx * (d.nx + 1) / 2) * n * d.elem, k,
-                               h->stream),
-                "set P");
+      copy_planes_in(h, h->s.P, p_packed, row, pb, d.nx * (d.nx + 1) / 2, mem);
     }
     finish_out(h, mem);
   });
@@ -682,7 +697,7 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem) {
     check_handle(h);
     if (!h->s.prev_sum) fail(FMSKF_ENOTSUP, "prev_sum exists in the RS model only");
     DeviceGuard g(h->cfg.device);
-    copy_out(h, prev, h->s.prev_sum, 4 * h->s.n * 8, mem);
+    copy_planes_out(h, prev, h->s.prev_sum, h->s.n * 8, h->s.pitch * 8, 4, mem);
     finish_out(h, mem);
   });
 }

@@ -12,8 +12,12 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // instance i lives at [k * N + i] unless the comment says [N][k].
 struct DevState {
   uint64_t n = 0;
+  // plane pitch (elements) of x and P: plane k of instance i at [k * pitch + i].  Never a
+  // large power of two (see plane_pitch): power-of-two plane strides alias in the
+  // memory-side cache / channel hash and cost ~20% of bandwidth at N = 2^20 (membench).
+  uint64_t pitch = 0;
   uint32_t model = 0;
-  // estimator state: x [nx][N], P [np][N] (element type float, or double for KF12D);
+  // estimator state: x [nx][pitch], P [np][pitch] (element type float, or double for KF12D);
   // RS: x = (px, py, th, vx, vy, vth) floats
   void *x = nullptr;
   void *P = nullptr;
@@ -77,6 +81,10 @@ inline bool kf12d_sequential(const double *r36) {
       if (r36[i * (i + 1) / 2 + j] != 0.0) return false;
   return true;
 }
+
+// x / P plane pitch for N instances: N rounded up to 512, plus 256 -> an odd multiple of
+// 1 KiB (fp32) between planes
+inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; }
 
 struct Wt901Cfg {
   uint32_t read_reg_index;

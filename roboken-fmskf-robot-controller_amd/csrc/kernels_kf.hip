@@ -45,14 +45,14 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
     for (int k = threadIdx.x; k < 513; k += kBlock) stab[k] = a.in.sintab[k];
     __syncthreads();
   }
-  const uint64_t n = a.n;
+  const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   float x[N], P[NP];
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * n + i];
+  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + i];
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * n + i];
+  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + i];
   const float dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t j = (uint64_t)t * a.in.stride + i;
@@ -86,9 +86,9 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
     }
   }
 #pragma unroll
-  for (int k = 0; k < N; k++) a.x[k * n + i] = x[k];
+  for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
 #pragma unroll
-  for (int k = 0; k < NP; k++) a.P[k * n + i] = P[k];
+  for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
   nan_guard(x, P, a.counters);
 }
 
@@ -97,14 +97,14 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 template <bool SEQ, bool UPD, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
-  const uint64_t n = a.n;
+  const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   double x[N], P[NP];
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * n + i];
+  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + i];
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * n + i];
+  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + i];
   const double dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t base = (uint64_t)t * a.in.stride * M;
@@ -140,15 +140,15 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
     }
   }
 #pragma unroll
-  for (int k = 0; k < N; k++) a.x[k * n + i] = x[k];
+  for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
 #pragma unroll
-  for (int k = 0; k < NP; k++) a.P[k * n + i] = P[k];
+  for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
   nan_guard(x, P, a.counters);
 }
 
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
                 bool pred, hipStream_t st) {
-  KfArgs<MdEKF9, Ekf9Params> a{s.n, (float *)s.x, (float *)s.P, in, s.counters, p};
+  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   if (libm) {
     if (upd && pred) k_ekf9<true, true, true><<<g, kBlock, 0, st>>>(a);
@@ -164,7 +164,7 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,
                  hipStream_t st) {
-  KfArgs<MdKF12D, Kf12dParams> a{s.n, (double *)s.x, (double *)s.P, in, s.counters, p};
+  KfArgs<MdKF12D, Kf12dParams> a{s.n, s.pitch, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   if (kf12d_sequential(p.r)) {
     if (upd && pred) k_kf12d<true, true, true><<<g, kBlock, 0, st>>>(a);

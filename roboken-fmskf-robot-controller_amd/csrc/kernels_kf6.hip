@@ -64,38 +64,38 @@ __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint6
 }
 
 template <class O>
-__device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg, uint64_t n,
+__device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg, uint64_t pp,
                                                uint32_t i, float (&x)[6], float (&P)[21]) {
   if constexpr (O::SMALL) {
-    const auto rx = rsrc(xg, n * 24), rp = rsrc(Pg, n * 84);
-    const uint32_t ps = (uint32_t)n * 4u;
+    const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
+    const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
     for (int k = 0; k < 6; k++) x[k] = ld_f32(rx, i * 4u, k * ps);
 #pragma unroll
     for (int k = 0; k < 21; k++) P[k] = ld_f32(rp, i * 4u, k * ps);
   } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = ld_f32(rsrc(xg + k * n, n * 4), i * 4u, 0);
+    for (int k = 0; k < 6; k++) x[k] = ld_f32(rsrc(xg + k * pp, pp * 4), i * 4u, 0);
 #pragma unroll
-    for (int k = 0; k < 21; k++) P[k] = ld_f32(rsrc(Pg + k * n, n * 4), i * 4u, 0);
+    for (int k = 0; k < 21; k++) P[k] = ld_f32(rsrc(Pg + k * pp, pp * 4), i * 4u, 0);
   }
 }
 
 template <class O>
-__device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t n, uint32_t i,
+__device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t pp, uint32_t i,
                                                 const float (&x)[6], const float (&P)[21]) {
   if constexpr (O::SMALL) {
-    const auto rx = rsrc(xg, n * 24), rp = rsrc(Pg, n * 84);
-    const uint32_t ps = (uint32_t)n * 4u;
+    const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
+    const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
     for (int k = 0; k < 6; k++) st_f32(rx, i * 4u, k * ps, x[k]);
 #pragma unroll
     for (int k = 0; k < 21; k++) st_f32(rp, i * 4u, k * ps, P[k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_f32(rsrc(xg + k * n, n * 4), i * 4u, 0, x[k]);
+    for (int k = 0; k < 6; k++) st_f32(rsrc(xg + k * pp, pp * 4), i * 4u, 0, x[k]);
 #pragma unroll
-    for (int k = 0; k < 21; k++) st_f32(rsrc(Pg + k * n, n * 4), i * 4u, 0, P[k]);
+    for (int k = 0; k < 21; k++) st_f32(rsrc(Pg + k * pp, pp * 4), i * 4u, 0, P[k]);
   }
 }
 
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   float x[6], P[21];
   Kf6In m;
   if (live) {
-    kf6_load_state<O>(a.x, a.P, n, i, x, P);
+    kf6_load_state<O>(a.x, a.P, a.pitch, i, x, P);
     if (O::UPD) m = kf6_load_in<O>(a.in, n, 0, i);
   }
   stage_table<O::LIBM>(stab, a.in.sintab);
@@ -176,53 +176,83 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     kf6_tick1<O>(m, stab, a.prm, x, P);
     m = mn;
   }
-  kf6_store_state<O>(a.x, a.P, n, i, x, P);
+  kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
   nan_guard(x, P, a.counters);
 }
 
+// Single tick, straight line: no tick loop (so no loop-carried register copies) and no
+// live/dead branch around the loads: lanes past N load instance N-1 (a clamped index, always
+// in bounds), compute on it, and only their stores and NaN count are masked off.
+template <int WPE, class O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6t(
+    KfArgs<MdKF6, Kf6Params> a) {
+  __shared__ float stab[O::LIBM ? 1 : 513];
+  const uint64_t n = a.n;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i < (uint32_t)n;
+  const uint32_t ic = live ? i : (uint32_t)n - 1u;
+  float x[6], P[21];
+  Kf6In m;
+  kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
+  if (O::UPD) m = kf6_load_in<O>(a.in, n, 0, ic);
+  stage_table<O::LIBM>(stab, a.in.sintab);
+  kf6_tick1<O>(m, stab, a.prm, x, P);
+  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  nan_guard(x, P, a.counters, live);
+}
+
 // Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no
-// loop-carried copies); while set A is computed and stored, set B's loads are in flight.
+// loop-carried copies); while set A is computed and stored, set B's loads are in flight
+// (vmcnt is in-order: B's 30 loads + A's 27 stores stay within the 63-deep counter).
+// Loads use clamped indices (always in bounds); the loop condition is block-uniform.
 // Single-tick launches only.
 template <int WPE, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6db(
     KfArgs<MdKF6, Kf6Params> a) {
   __shared__ float stab[O::LIBM ? 1 : 513];
   const uint64_t n = a.n;
-  const uint32_t nn = (uint32_t)n;
+  const uint32_t nn = (uint32_t)n, last = nn - 1u;
   const uint32_t gs = gridDim.x * kBlock;
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t ba = blockIdx.x * kBlock;  // block base of set A
+  const uint32_t t = threadIdx.x;
   float xa[6], Pa[21], xb[6], Pb[21];
   Kf6In ma, mb;
-  if (i < nn) {
-    kf6_load_state<O>(a.x, a.P, n, i, xa, Pa);
+  {
+    const uint32_t i = min(ba + t, last);
+    kf6_load_state<O>(a.x, a.P, a.pitch, i, xa, Pa);
     if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, i);
   }
   stage_table<O::LIBM>(stab, a.in.sintab);
-  while (i < nn) {
-    const uint32_t ib = i + gs;
-    if (ib < nn) {
-      kf6_load_state<O>(a.x, a.P, n, ib, xb, Pb);
-      if (O::UPD) mb = kf6_load_in<O>(a.in, n, 0, ib);
+  for (;;) {
+    const uint32_t bb = ba + gs;
+    if (bb < nn) {
+      const uint32_t i = min(bb + t, last);
+      kf6_load_state<O>(a.x, a.P, a.pitch, i, xb, Pb);
+      if (O::UPD) mb = kf6_load_in<O>(a.in, n, 0, i);
     }
     kf6_tick1<O>(ma, stab, a.prm, xa, Pa);
-    kf6_store_state<O>(a.x, a.P, n, i, xa, Pa);
-    nan_guard(xa, Pa, a.counters);
-    if (ib >= nn) break;
-    const uint32_t ia = ib + gs;
-    if (ia < nn) {
-      kf6_load_state<O>(a.x, a.P, n, ia, xa, Pa);
-      if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, ia);
+    if (ba + t < nn) kf6_store_state<O>(a.x, a.P, a.pitch, ba + t, xa, Pa);
+    nan_guard(xa, Pa, a.counters, ba + t < nn);
+    if (bb >= nn) break;
+    const uint32_t bn = bb + gs;
+    if (bn < nn) {
+      const uint32_t i = min(bn + t, last);
+      kf6_load_state<O>(a.x, a.P, a.pitch, i, xa, Pa);
+      if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, i);
     }
     kf6_tick1<O>(mb, stab, a.prm, xb, Pb);
-    kf6_store_state<O>(a.x, a.P, n, ib, xb, Pb);
-    nan_guard(xb, Pb, a.counters);
-    i = ia;
+    if (bb + t < nn) kf6_store_state<O>(a.x, a.P, a.pitch, bb + t, xb, Pb);
+    nan_guard(xb, Pb, a.counters, bb + t < nn);
+    if (bn >= nn) break;
+    ba = bn;
   }
 }
 
 // Variant (FMSKF_KF6_VARIANT, read once) for single-tick launches; default 0:
-//   0: one instance per lane, grid = N/256 (4 waves/SIMD)
+//   0: one instance per lane, grid = N/256, straight-line single-tick kernel
+//   3: the same through the tick-loop kernel (k_kf6, as tick_many uses)
 //   1: double-buffered persistent, 2 blocks/CU   2: same, 3 blocks/CU
+//   4: same at <= 128 VGPRs, 4 blocks/CU          5: same, 8 blocks/CU
 static int kf6_variant() {
   static int v = [] {
     const char *e = getenv("FMSKF_KF6_VARIANT");
@@ -234,13 +264,17 @@ static int kf6_variant() {
 template <class O>
 static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   const int v = a.in.n_ticks == 1 ? kf6_variant() : 0;
-  if (v == 1 || v == 2) {
+  if (v == 1 || v == 2 || v == 4 || v == 5) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t g = (uint64_t)cus * (v == 1 ? 2 : 3);
+    const uint64_t g = (uint64_t)cus * (v == 1 ? 2 : v == 2 ? 3 : v == 4 ? 4 : 8);
     const uint64_t need = (a.n + kBlock - 1) / kBlock;
-    k_kf6db<2, O><<<(unsigned)(g < need ? g : need), kBlock, 0, st>>>(a);
+    const unsigned grid = (unsigned)(g < need ? g : need);
+    if (v <= 2) k_kf6db<2, O><<<grid, kBlock, 0, st>>>(a);
+    else k_kf6db<4, O><<<grid, kBlock, 0, st>>>(a);
+  } else if (a.in.n_ticks == 1 && v == 0) {
+    k_kf6t<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);
   } else {
     k_kf6<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);
   }
@@ -259,8 +293,8 @@ static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid
 
 int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool libm, bool upd,
                bool pred, hipStream_t st) {
-  KfArgs<MdKF6, Kf6Params> a{s.n, (float *)s.x, (float *)s.P, in, s.counters, p};
-  const bool small = s.n * 84 < 0xFFFFFFFFull;
+  KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
+  const bool small = s.pitch * 84 < 0xFFFFFFFFull;
   const bool valid = upd && in.valid != nullptr;
   if (libm) {
     if (upd && pred) launch_lup<true, true, true>(a, small, valid, st);

@@ -85,7 +85,7 @@ __device__ __forceinline__ void block_sum(const double (&v)[LEN], double (*red)[
 // loop) of its grid-stride instances and writes its record.
 template <int NX, typename T>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
-                                                        double *blocks) {
+                                                        uint64_t pp, double *blocks) {
   constexpr int LEN = EnsRec<NX>::LEN;
   constexpr int U = 4;
   __shared__ double red[kEnsCh][kBlock];
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
   __shared__ double tot[LEN];
   double sh[NX], v[LEN];
 #pragma unroll
-  for (int k = 0; k < NX; k++) sh[k] = (double)x[k * n];
+  for (int k = 0; k < NX; k++) sh[k] = (double)x[k * pp];
 #pragma unroll
   for (int k = 0; k < LEN; k++) v[k] = 0.0;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
     for (int u = 0; u < U; u++) {
       const uint64_t i = i0 + u * stride;
 #pragma unroll
-      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[k * n + i] : (T)0;
+      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[k * pp + i] : (T)0;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
 // Fold (one block): thread t sums block records t, t + 256, ... in order, then the block sum,
 // then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
 template <int NX, typename T>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t n,
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp,
                                                      const double *__restrict__ blocks,
                                                      int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, ui
     if (k == 0) {
       r = c;
     } else if (k <= NX) {
-      r = (double)x[(k - 1) * n] + (c > 0.0 ? tot[k] / c : 0.0);
+      r = (double)x[(k - 1) * pp] + (c > 0.0 ? tot[k] / c : 0.0);
     } else {
       int p = 0, q = k - 1 - NX;
       while (q > p) q -= ++p;
@@ -170,8 +170,8 @@ int ensemble_nblocks(uint64_t n) {
 template <int NX, typename T>
 static void ens_launch(const DevState &s, double *blocks, double *out, hipStream_t st) {
   const int nb = ensemble_nblocks(s.n);
-  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, blocks);
-  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.n, blocks, nb, out);
+  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
+  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.pitch, blocks, nb, out);
 }
 
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
@@ -208,21 +208,21 @@ int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st) {
 // get_vehicle_vel_mmps_latest (body frame mm/s, mm/s, rad/s).  The KF6 / KF12D state
 // carries world-frame velocity in m/s: rotate by -theta (libm sin/cos, readout only).
 template <int MODEL>
-__global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, float *out) {
+__global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, uint64_t pp, float *out) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   if constexpr (MODEL == 0) {  // RS: x = px, py, th, vx, vy, vth (already reference units)
     const float *x = (const float *)xv;
 #pragma unroll
-    for (int k = 0; k < 6; k++) out[k * n + i] = x[k * n + i];
+    for (int k = 0; k < 6; k++) out[k * n + i] = x[k * pp + i];
   } else if constexpr (MODEL == 1 || MODEL == 3) {  // KF6 / KF12D base
     double px, py, th, vx, vy, w;
     if constexpr (MODEL == 1) {
       const float *x = (const float *)xv;
-      px = x[i]; py = x[n + i]; th = x[2 * n + i]; vx = x[3 * n + i]; vy = x[4 * n + i]; w = x[5 * n + i];
+      px = x[i]; py = x[pp + i]; th = x[2 * pp + i]; vx = x[3 * pp + i]; vy = x[4 * pp + i]; w = x[5 * pp + i];
     } else {
       const double *x = (const double *)xv;
-      px = x[i]; py = x[n + i]; th = x[2 * n + i]; vx = x[3 * n + i]; vy = x[4 * n + i]; w = x[5 * n + i];
+      px = x[i]; py = x[pp + i]; th = x[2 * pp + i]; vx = x[3 * pp + i]; vy = x[4 * pp + i]; w = x[5 * pp + i];
     }
     const double c = cos(th), s = sin(th);
     out[i] = (float)px;
@@ -234,21 +234,21 @@ __global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, 
   } else {  // EKF9: body-frame velocity already
     const float *x = (const float *)xv;
     out[i] = x[i];
-    out[n + i] = x[n + i];
-    out[2 * n + i] = x[2 * n + i];
-    out[3 * n + i] = x[3 * n + i] * 1000.0f;
-    out[4 * n + i] = x[4 * n + i] * 1000.0f;
-    out[5 * n + i] = x[5 * n + i];
+    out[n + i] = x[pp + i];
+    out[2 * n + i] = x[2 * pp + i];
+    out[3 * n + i] = x[3 * pp + i] * 1000.0f;
+    out[4 * n + i] = x[4 * pp + i] * 1000.0f;
+    out[5 * n + i] = x[5 * pp + i];
   }
 }
 
 int launch_readout(const DevState &s, float *out, hipStream_t st) {
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   switch (s.model) {
-    case 0: k_readout<0><<<g, kBlock, 0, st>>>(s.x, s.n, out); break;
-    case 1: k_readout<1><<<g, kBlock, 0, st>>>(s.x, s.n, out); break;
-    case 2: k_readout<2><<<g, kBlock, 0, st>>>(s.x, s.n, out); break;
-    case 3: k_readout<3><<<g, kBlock, 0, st>>>(s.x, s.n, out); break;
+    case 0: k_readout<0><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
+    case 1: k_readout<1><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
+    case 2: k_readout<2><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
+    case 3: k_readout<3><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

@@ -18,22 +18,23 @@ namespace fmskf {
 
 struct RsArgs {
   uint64_t n;
-  float *x;          // [6][N]: px, py, th, vx, vy, vth
-  int64_t *prev;     // [4][N]
+  uint64_t pitch;    // plane pitch of x and prev (elements)
+  float *x;          // [6][pitch]: px, py, th, vx, vy, vth
+  int64_t *prev;     // [4][pitch]
   TickIn in;
 };
 
 template <bool LIBM, bool CORR, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
-  const uint64_t n = a.n;
+  const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  float px = a.x[i], py = a.x[n + i], th = a.x[2 * n + i];
+  float px = a.x[i], py = a.x[pp + i], th = a.x[2 * pp + i];
   float vx = 0.f, vy = 0.f, vth = 0.f;
   int64_t prev[4];
   if (PRED) {
 #pragma unroll
-    for (int w = 0; w < 4; w++) prev[w] = a.prev[w * n + i];
+    for (int w = 0; w < 4; w++) prev[w] = a.prev[w * pp + i];
   }
   const uint64_t st = a.in.stride;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
@@ -64,19 +65,19 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   }
   if (PRED) {
     a.x[i] = px;
-    a.x[n + i] = py;
-    a.x[3 * n + i] = vx;
-    a.x[4 * n + i] = vy;
-    a.x[5 * n + i] = vth;
+    a.x[pp + i] = py;
+    a.x[3 * pp + i] = vx;
+    a.x[4 * pp + i] = vy;
+    a.x[5 * pp + i] = vth;
 #pragma unroll
-    for (int w = 0; w < 4; w++) a.prev[w * n + i] = prev[w];
+    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = prev[w];
   }
-  if (CORR) a.x[2 * n + i] = th;
+  if (CORR) a.x[2 * pp + i] = th;
 }
 
 int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool predict,
               hipStream_t st) {
-  RsArgs a{s.n, (float *)s.x, s.prev_sum, in};
+  RsArgs a{s.n, s.pitch, (float *)s.x, s.prev_sum, in};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   if (libm) {
     if (correct && predict) k_rs<true, true, true><<<g, kBlock, 0, st>>>(a);

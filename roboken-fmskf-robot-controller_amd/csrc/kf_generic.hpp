@@ -68,6 +68,7 @@ struct MdKF12D_G2 {
 template <class Md, typename Prm>
 struct KfArgs {
   uint64_t n;
+  uint64_t pitch;  // x / P plane pitch (elements)
   typename Md::T *x;
   typename Md::T *P;
   TickIn in;
@@ -196,13 +197,13 @@ __device__ __forceinline__ void unpack4(uint2 r, int16_t (&o)[4]) {
 // Count instances whose state became non-finite (one atomic per wave, rare path).
 template <typename T, int N, int NP>
 __device__ __forceinline__ void nan_guard(const T (&x)[N], const T (&P)[NP],
-                                          unsigned long long *counters) {
+                                          unsigned long long *counters, bool live = true) {
   T acc = x[0];
 #pragma unroll
   for (int k = 1; k < N; k++) acc = acc + x[k];
 #pragma unroll
   for (int k = 0; k < NP; k++) acc = acc + P[k];
-  const bool bad = !__builtin_isfinite(acc);
+  const bool bad = live && !__builtin_isfinite(acc);
   const unsigned long long m = __ballot(bad);
   if (m && (threadIdx.x & 63) == __builtin_ctzll(m))
     atomicAdd(counters, (unsigned long long)__popcll(m));

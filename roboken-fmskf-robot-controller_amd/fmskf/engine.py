@@ -21,6 +21,10 @@ _DTYPES = {
 }
 
 
+# elements per instance-tick of each input (fmskf_tick_inputs, include/fmskf.h)
+_PER_TICK = {"yaw_deg": 1, "gyro_z_dps": 1, "rpm": 4, "angle_sum": 4, "raw": 8, "z": 8, "valid": 1}
+
+
 def _is_torch(a) -> bool:
     return type(a).__module__.startswith("torch")
 
@@ -155,11 +159,24 @@ class Engine:
         check(load().fmskf_ingest_can(self.h, pf, ps, pp, a.mem), "ingest_can")
 
     # ------------------------------------------------------------------ ticks
-    def _inputs(self, kw):
+    def _inputs(self, kw, n_ticks=1, stride=None):
         a = _Args()
         ti = TickInputs()
+        unknown = set(kw) - set(_PER_TICK)
+        if unknown:
+            raise TypeError(f"unknown tick inputs: {sorted(unknown)}")
+        stride = self.n if stride is None else stride
         for name in ("yaw_deg", "gyro_z_dps", "rpm", "angle_sum", "raw", "z", "valid"):
-            p = a.ptr(kw.get(name), _DTYPES[name])
+            v = kw.get(name)
+            if v is not None:
+                # the C ABI takes bare pointers: check extents here, before the kernel reads
+                need = ((int(n_ticks) - 1) * int(stride) + self.n) * _PER_TICK[name]
+                have = v.numel() if _is_torch(v) else np.size(v)
+                if have < need:
+                    raise ValueError(f"{name}: {have} elements, {n_ticks} tick(s) need {need}")
+                if _is_torch(v) and v.is_cuda and str(v.dtype) != "torch." + np.dtype(_DTYPES[name]).name:
+                    raise TypeError(f"{name}: dtype {v.dtype}, expected {np.dtype(_DTYPES[name]).name}")
+            p = a.ptr(v, _DTYPES[name])
             setattr(ti, name, p.value if p is not None else None)
         ti.mem = MEM_HOST if a.mem is None else a.mem
         return ti, a
@@ -188,8 +205,8 @@ class Engine:
             check(rc, "tick")
 
     def tick_many(self, n_ticks, tick_stride=None, **kw):
-        ti, _keep = self._inputs(kw)
         stride = self.n if tick_stride is None else int(tick_stride)
+        ti, _keep = self._inputs(kw, n_ticks, stride)
         check(load().fmskf_tick_many(self.h, C.byref(ti), int(n_ticks), stride), "tick_many")
 
     # ------------------------------------------------------------------ readout

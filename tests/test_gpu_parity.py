@@ -431,3 +431,12 @@ def test_bad_inputs_rejected():
             e.tick_many(2, yaw_deg=np.zeros((2, 64), np.float32))  # missing planes
         with pytest.raises(fmskf.FmskfError):
             e.get_prev_sum()  # RS only
+        # extents are checked before any kernel can read past a short buffer
+        with pytest.raises(ValueError):
+            e.tick_many(4, yaw_deg=np.zeros((2, 64), np.float32),
+                        gyro_z_dps=np.zeros((4, 64), np.float32), rpm=np.zeros((4, 64, 4), np.int16))
+        with pytest.raises(ValueError):
+            e.tick(yaw_deg=np.zeros(63, np.float32), gyro_z_dps=np.zeros(64, np.float32),
+                   rpm=np.zeros((64, 4), np.int16))
+        with pytest.raises(TypeError):
+            e.tick(yaw=np.zeros(64, np.float32))

@@ -32,7 +32,7 @@ def main():
     from fmskf.synth import kf6_ring_torch
 
     dev = torch.device("cuda", 0)
-    n, R = args.n, args.ring
+    n, R = args.n, max(args.ring, args.many)  # tick_many reads `many` ticks of the ring
     e = fmskf.Engine(args.model, n, trig=fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512)
     st = torch.cuda.current_stream()
     e.set_stream(st)

@@ -87,6 +87,35 @@ __global__ __launch_bounds__(256) void k_pattern4(float *st, const float *yaw, c
   }
 }
 
+// plane pitch != n (padding), and tiled SoA ("AoSoA": [N/T][27][T], a wave's 27 state
+// rows are one contiguous 27*T*4-byte span) variants of the ipl1 pattern
+__global__ __launch_bounds__(256) void k_pattern_pitch(float *st, const float *yaw, const float *gz,
+                                                       const uint2 *rpm, uint64_t n, uint64_t pitch,
+                                                       float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = st[k * pitch + v];
+  const float m = sink * yaw[v] * gz[v] * (float)(rpm[v].x & 1);
+#pragma unroll
+  for (int k = 0; k < 27; k++) st[k * pitch + v] = s[k] + m;
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_pattern_tiled(float *st, const float *yaw, const float *gz,
+                                                       const uint2 *rpm, uint64_t n, float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float *tile = st + (v / T) * (27 * T) + (v % T);
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = tile[k * T];
+  const float m = sink * yaw[v] * gz[v] * (float)(rpm[v].x & 1);
+#pragma unroll
+  for (int k = 0; k < 27; k++) tile[k * T] = s[k] + m;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -97,7 +126,8 @@ int main(int argc, char **argv) {
   const uint64_t n = 1ull << lg;
   float *st, *yaw, *gz, *ca, *cb;
   uint2 *rpm;
-  CK(hipMalloc(&st, 27 * n * 4));
+  const uint64_t pad = 4096;  // elements of padding per plane for the pitch variants
+  CK(hipMalloc(&st, 27 * (n + 4 * pad) * 4));
   CK(hipMalloc(&yaw, n * 4));
   CK(hipMalloc(&gz, n * 4));
   CK(hipMalloc(&rpm, n * 8));
@@ -134,6 +164,22 @@ int main(int argc, char **argv) {
   });
   timeit("pattern_ipl4_dwordx4", [&] {
     k_pattern4<<<(unsigned)((n / 4 + 255) / 256), 256>>>(st, yaw, gz, (const uint4 *)rpm, n, 0.f);
+  });
+  for (uint64_t pp : {(uint64_t)64, (uint64_t)256, (uint64_t)1024, (uint64_t)4096, (uint64_t)16384 / 4}) {
+    char name[64];
+    snprintf(name, sizeof(name), "pattern_pitch_n+%llu", (unsigned long long)pp);
+    timeit(name, [&] {
+      k_pattern_pitch<<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + pp, 0.f);
+    });
+  }
+  timeit("pattern_tiled64", [&] {
+    k_pattern_tiled<64><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
+  });
+  timeit("pattern_tiled256", [&] {
+    k_pattern_tiled<256><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
+  });
+  timeit("pattern_tiled1024", [&] {
+    k_pattern_tiled<1024><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
   });
   timeit("copy_float4_same_bytes", [&] {
     k_copy4<<<2048, 256>>>((const float4 *)ca, (float4 *)cb, bytes / 2 / 16);
