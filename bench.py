@@ -156,14 +156,23 @@ def main():
     barrier()
     elapsed = t1 - t0
     region_ms = ev0.elapsed_time(ev1)
+
+    # the tick kernel's own average launch duration (the roofline's denominator): K more
+    # back-to-back ticks on the same stream, without the ensemble kernels, HIP events around
+    # them (rocprofv3's per-kernel average for the same command: profiles/)
+    ek0 = torch.cuda.Event(enable_timing=True)
+    ek1 = torch.cuda.Event(enable_timing=True)
+    ek0.record(stream)
+    for k in range(args.steps):
+        eng.tick_prepared(prepared[k % R], tick_fn)
+    ek1.record(stream)
+    torch.cuda.synchronize()
+    tick_ms = ek0.elapsed_time(ek1)
     if distributed:
-        t = torch.tensor([elapsed, region_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, region_ms, tick_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, region_ms = float(t[0].item()), float(t[1].item())
-    # per-launch average from the event region: includes the ensemble reduction kernels
-    # (1 in --ensemble-every ticks) and inter-kernel gaps, so it bounds the tick kernel's
-    # own duration from above (rocprofv3 reports the kernel alone: profiles/)
-    kern_avg_ms = region_ms / args.steps
+        elapsed, region_ms, tick_ms = (float(v) for v in t.tolist())
+    kern_avg_ms = tick_ms / args.steps
 
     total_steps = n * world * args.steps
     value = total_steps / elapsed
@@ -239,7 +248,8 @@ def main():
             "traffic": traffic,
             "bytes_per_step": BYTES_PER_STEP["kf6"],
             "kernel_ms": kern_avg_ms,
-            "kernel": "k_kf6<false,true,true>",
+            "kernel": "k_kf6t<4, Opt<TABLE512, UPD, PRED, SMALL, !VALID>>",
+            "timed_region_ms_per_step": region_ms / args.steps,
         },
         "cpu_baseline": None,
         "fused_replay": fused,

@@ -50,14 +50,20 @@ __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
 }
 
+#ifndef FMSKF_IN_CPOL
+#define FMSKF_IN_CPOL 0
+#endif
 // inputs of one tick; planes of tick t start at t * stride elements
 template <class O>
 __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint64_t t, uint32_t i) {
   const uint64_t tb = t * in.stride;
   Kf6In m;
-  m.yaw = ld_f32(rsrc(in.yaw_deg + tb, n * 4), i * 4u, 0);
-  m.gz = ld_f32(rsrc(in.gyro_z + tb, n * 4), i * 4u, 0);
-  const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + tb * 4, n * 8), i * 8u, 0, 0);
+  m.yaw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                        rsrc(in.yaw_deg + tb, n * 4), i * 4u, 0, FMSKF_IN_CPOL));
+  m.gz = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                       rsrc(in.gyro_z + tb, n * 4), i * 4u, 0, FMSKF_IN_CPOL));
+  const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + tb * 4, n * 8), i * 8u, 0,
+                                                       FMSKF_IN_CPOL);
   m.rpm = make_uint2(rr[0], rr[1]);
   m.valid = O::VALID ? (uint32_t)in.valid[tb + i] : 1u;
   return m;
@@ -274,7 +280,11 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     if (v <= 2) k_kf6db<2, O><<<grid, kBlock, 0, st>>>(a);
     else k_kf6db<4, O><<<grid, kBlock, 0, st>>>(a);
   } else if (a.in.n_ticks == 1 && v == 0) {
-    k_kf6t<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);
+    static const unsigned lds = [] {  // occupancy experiment: dynamic LDS per block
+      const char *e = getenv("FMSKF_KF6_LDS");
+      return e ? (unsigned)atoi(e) : 0u;
+    }();
+    k_kf6t<4, O><<<grid_for(a.n), kBlock, lds, st>>>(a);
   } else {
     k_kf6<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);
   }

@@ -116,6 +116,26 @@ __global__ __launch_bounds__(256) void k_pattern_tiled(float *st, const float *y
   for (int k = 0; k < 27; k++) tile[k * T] = s[k] + m;
 }
 
+// the ipl1 pattern (pitched) with ITERS x 27 FMAs between the loads and the stores: how
+// much arithmetic the memory phases hide
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_pattern_delay(float *st, const float *yaw, const float *gz,
+                                                       const uint2 *rpm, uint64_t n, uint64_t pitch,
+                                                       float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = st[k * pitch + v];
+  const float a = yaw[v], b = gz[v] * (float)(rpm[v].x & 1);
+#pragma unroll
+  for (int it = 0; it < ITERS; it++)
+#pragma unroll
+    for (int k = 0; k < 27; k++) s[k] = __builtin_fmaf(s[k], a, b);
+#pragma unroll
+  for (int k = 0; k < 27; k++) st[k * pitch + v] = s[k] + sink;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -172,6 +192,21 @@ int main(int argc, char **argv) {
       k_pattern_pitch<<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + pp, 0.f);
     });
   }
+  timeit("pattern_delay_0", [&] {
+    k_pattern_delay<0><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_delay_108fma", [&] {
+    k_pattern_delay<4><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_delay_216fma", [&] {
+    k_pattern_delay<8><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_delay_432fma", [&] {
+    k_pattern_delay<16><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_delay_864fma", [&] {
+    k_pattern_delay<32><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
   timeit("pattern_tiled64", [&] {
     k_pattern_tiled<64><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
   });
