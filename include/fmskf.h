@@ -30,6 +30,12 @@
  *   VDT::VEHICLE_CTRL::update (odometry) src/VehicleDrive/VD_vehicle_controller.cpp:6-51
  *   VEHICLE_CTRL::get_vehicle_*_latest   src/VehicleDrive/VD_vehicle_controller.hpp:59-60
  *   VDT::get_status_now_vehicle_pos_world/vel  src/VehicleDrive/VD_task_main.cpp:374-395
+ *   VEHICLE_CTRL::update (control part)  src/VehicleDrive/VD_vehicle_controller.cpp:53-98
+ *   VEHICLE_CTRL::set_target_vel/start/stop  VD_vehicle_controller.cpp:100-104, .hpp:54-55
+ *   UTIL::VelInterpConstJerk / FF_PI_D   src/Utility/util_vel_interp.hpp:25-157,
+ *                                        util_controller.hpp:92-186, util_iir.hpp:13-57
+ *   CAN_CTRL::tx_routine                 src/VehicleDrive/VD_can_controller.hpp:43-55
+ *   VehicleInfo publish                  src/RobotManager/RM_task_main.cpp:772-823
  */
 #ifndef FMSKF_H_
 #define FMSKF_H_
@@ -188,6 +194,69 @@ int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
 /* host-side: records [n_records][len] -> mean [n], cov packed [n(n+1)/2] (unbiased) */
 int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
                            double *mean, double *cov_packed);
+
+/* ---- vehicle control step -------------------------- */
+/* Per-robot control state is allocated on the first call of any entry point below
+ * (~250 B per robot); zero-initialised like the firmware's static objects, power off. */
+typedef struct fmskf_ctrl_params {
+  /* FF_PI_D construction (VD_task_main.cpp:86-89): built for 100 Hz (U32_VD_TASK_CTRL_FREQ_HZ)
+   * although stepped by the 1 kHz ISR -- the reference's quirk, kept as the default */
+  float ctrl_freq_hz;  /* 100 */
+  float ff_gain;       /* 0.0075 */
+  float p_gain;        /* 0.02 */
+  float i_gain;        /* 0.01 */
+  float d_gain;        /* 0.0 */
+  float i_limit;       /* 0.5 */
+  float lpf_freq_hz;   /* 10 (velocity LPF of PI_D, util_controller.hpp:99-101) */
+  float ff_limit;      /* 1.0 (set_FF_limit, VD_task_main.cpp:157-160) */
+  float interp_ts;     /* VelInterpConstJerk sample time 1/1000 s (VD_task_main.cpp:95-97) */
+  int16_t curr_limit_raw; /* MOTOR_IF_M2006::s16_rawCurr_lim 3000 (VD_motor_if_m2006.hpp:62) */
+  int16_t reserved;
+} fmskf_ctrl_params;
+
+int fmskf_ctrl_params_init(fmskf_ctrl_params *p);
+/* takes effect from the next control step; controller state is kept */
+int fmskf_set_ctrl_params(fmskf_handle h, const fmskf_ctrl_params *p);
+/* VEHICLE_CTRL::start / stop: on [N] (nonzero = on); NULL = all on */
+int fmskf_set_power(fmskf_handle h, const uint8_t *on, uint32_t mem);
+/* VEHICLE_CTRL::set_target_vel -> VelInterpConstJerk::set_target_params per axis.
+ * vel, acl, jrk: [3][N] planes (x mm/s, y mm/s, th rad/s); mask [N] (NULL = every robot). */
+int fmskf_set_target_vel(fmskf_handle h, const float *vel, const float *acl, const float *jrk,
+                         const uint8_t *mask, uint32_t mem);
+/* The control half of VEHICLE_CTRL::update, one tick: interpolators, conv_Vdir_to_Mdir, the
+ * four FF_PI_D loops on the measured wheel speed, set_CurrA_tgt.  rpm [N][4] (FL,BL,BR,FR
+ * s16_rawSpeedRpm); NULL = the device motor state fmskf_ingest_can keeps. */
+int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem);
+/* CAN_CTRL::tx_routine: frames [N][8] = the 0x200 payload (big-endian raw currents) */
+int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem);
+/* readout: vel_tgt [3][N] (get_vehicle_vel_tgt_mmps_latest), curr_raw [N][4]
+ * (get_rawCurr_tgt), wheel_tgt / wheel_ctrl [4][N] (FF_PI_D get_target / last output).
+ * Any pointer may be NULL. */
+int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *wheel_tgt,
+                   float *wheel_ctrl, uint32_t mem);
+
+/* ---- VehicleInfo export -------------------------------- */
+/* The ROS VehicleInfo message as RM_task_main.cpp:772-823 fills it (VehicleInfo.msg,
+ * VehiclePosition.msg, ImuInfo.msg, FloorDetection.msg), natural C alignment, 84 bytes. */
+typedef struct fmskf_vehicle_info {
+  int32_t pos_x, pos_y;   /* (int32_t)(x_m * 1000.0f): truncation, ARM saturation */
+  float pos_theta;        /* rad */
+  int32_t vel_x, vel_y;   /* (int32_t)(mm/s) */
+  float vel_theta;        /* rad/s */
+  uint8_t imu_fault;      /* 0xFF when IMU_IF::isError (every imu field 0), else 0 */
+  uint8_t pad_[3];
+  float imu_q[4];         /* qx qy qz qw = Data.qut[0..3] */
+  float imu_g[3];         /* Data.gyro */
+  float imu_a[3];         /* Data.accel */
+  uint8_t floor[8];       /* right left forward back rightforward leftforward rightback leftback */
+  float cam_pitch;
+  uint32_t fault;
+} fmskf_vehicle_info;
+
+/* out [N] records; floor [N][8], cam_pitch [N], fault [N] come from subsystems outside the
+ * path and may be NULL (zero). */
+int fmskf_export_vehicle_info(fmskf_handle h, fmskf_vehicle_info *out, const uint8_t *floor,
+                              const float *cam_pitch, const uint32_t *fault, uint32_t mem);
 
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Evaluate the device sin/cos policy on x[n] (device pointers when mem = DEVICE). */

@@ -715,6 +715,190 @@ void orc_ens_finalize(int nx, const double *rec, double *mean, double *cov_packe
   for (int k = 0; k < np; k++) cov_packed[k] = cnt > 1.0 ? rec[1 + nx + k] / (cnt - 1.0) : 0.0;
 }
 
+/* ------------------------------------------------------------------------- */
+/* Vehicle control step                            */
+/* ------------------------------------------------------------------------- */
+/* UTIL::controller / PI_D / FF_PI_D constructors, util_controller.hpp:10,96-101,167-169 */
+void orc_ctrl_params_make(orc_ctrl_params *p, float c_freq, float ff, float pg, float ig, float dg,
+                          float ilim, float lpf_freq, float ff_limit, float ts, int16_t clim) {
+  p->freq = c_freq;
+  p->dt = 1.0f / c_freq;
+  p->ff_gain = ff;
+  p->p_gain = pg;
+  p->i_gain = ig;
+  p->d_gain = dg;
+  p->i_limit = ilim;
+  p->ff_limit = ff_limit;
+  p->a1 = (2.0f * c_freq - lpf_freq) / (2.0f * c_freq + lpf_freq);
+  p->b0 = lpf_freq / (2.0f * c_freq + lpf_freq);
+  p->b1 = lpf_freq / (2.0f * c_freq + lpf_freq);
+  p->ts = ts;
+  p->curr_limit_raw = clim;
+}
+
+/* VelInterpConstJerk::reset, util_vel_interp.hpp:135-141 */
+void orc_interp_reset(orc_interp *s) { memset(s, 0, sizeof(*s)); }
+
+/* CMSIS-DSP arm_sqrt_f32 (third-party): sqrt for in >= 0, else 0 (parity unpinned) */
+static float orc_arm_sqrt(float in) { return in >= 0.0f ? sqrtf(in) : 0.0f; }
+
+/* VelInterpConstJerk::set_target_params, util_vel_interp.hpp:55-104 */
+void orc_interp_set(orc_interp *s, float v_t, float a_m, float jrk) {
+  s->vel_tgt = v_t;
+  s->acl_max = a_m;
+  s->vel_ini = s->vel_now;
+  s->acl_ini = s->acl_now;
+  if ((s->vel_tgt - s->vel_ini) < 0) s->acl_max = -a_m;
+  s->jerk_m = (s->acl_max >= 0) ? -jrk : jrk;
+  const float jm_inv = 1.0f / s->jerk_m;
+  s->jerk_p = (s->acl_max - s->acl_ini >= 0) ? jrk : -jrk;
+  const float jp_inv = 1.0f / s->jerk_p;
+  s->dt1 = (s->acl_max - s->acl_ini) * jp_inv;
+  s->dt3 = s->acl_max * (-jm_inv);
+  s->dt2 = 1.0f / s->acl_max *
+           (s->vel_tgt - s->vel_ini - s->acl_ini * s->dt1 * 0.5f - s->acl_max * (s->dt1 + s->dt3) * 0.5f);
+  if (s->dt2 < 0.0f) {
+    const float sq_in = (s->acl_ini * jp_inv) * (s->acl_ini * jp_inv) * 0.5f + (s->vel_tgt - s->vel_ini) * jp_inv;
+    const float sq = orc_arm_sqrt(sq_in);
+    s->dt1 = sq - s->acl_ini * jp_inv;
+    s->acl_max = s->acl_ini + s->jerk_p * s->dt1;
+    s->dt2 = 0.0f;
+    s->dt3 = s->acl_max * (-jm_inv);
+  }
+  s->dt1 = (s->dt1 < 0.0f) ? 0.0f : s->dt1;
+  s->dt3 = (s->dt3 < 0.0f) ? 0.0f : s->dt3;
+  s->dt = 0.0f;
+}
+
+/* VelInterpConstJerk::update, util_vel_interp.hpp:106-133 */
+float orc_interp_update(orc_interp *s, float ts) {
+  if (s->dt <= s->dt1 + ts) {
+    s->acl_now = s->acl_ini + s->jerk_p * s->dt;
+    s->vel_now = s->vel_ini + (s->acl_ini + s->acl_now) * s->dt * 0.5f;
+    s->dt = s->dt + ts;
+  } else if (s->dt <= s->dt1 + s->dt2 + ts) {
+    s->acl_now = s->acl_max;
+    s->vel_now = s->vel_now + s->acl_now * ts;
+    s->dt = s->dt + ts;
+  } else if (s->dt <= s->dt1 + s->dt2 + s->dt3 + ts) {
+    s->acl_now = s->acl_max + s->jerk_m * (s->dt - s->dt1 - s->dt2);
+    s->vel_now = s->vel_now + s->acl_now * ts;
+    s->dt = s->dt + ts;
+  } else {
+    s->acl_now = 0.0f;
+    s->vel_now = s->vel_tgt;
+  }
+  return s->vel_now;
+}
+
+/* PI_D::reset, util_controller.hpp:122-134 */
+void orc_pid_reset(orc_pid *c) { memset(c, 0, sizeof(*c)); }
+
+/* FF_PI_D::update = PI_D::update (util_controller.hpp:104-120) + FF (:171-177);
+ * velLpf_ = IIR1::update (util_iir.hpp:39-45) */
+float orc_pid_update(orc_pid *c, const orc_ctrl_params *p, float nowval) {
+  const float prev_val = c->val;
+  const float err = c->tgt - nowval;
+  const float lx = (nowval - prev_val) * p->freq;
+  const float ly = p->a1 * c->lpf_y + p->b0 * lx + p->b1 * c->lpf_x;
+  c->lpf_y = ly;
+  c->lpf_x = lx;
+  float integ = c->integ + p->i_gain * p->dt * err;
+  integ = (integ >= p->i_limit) ? p->i_limit : ((integ <= -p->i_limit) ? -p->i_limit : integ);
+  c->integ = integ;
+  float ctrl = p->p_gain * err + integ - p->d_gain * ly;
+  c->val = nowval;
+  float ff = c->tgt * p->ff_gain;
+  ff = (ff >= p->ff_limit) ? p->ff_limit : ((ff <= -p->ff_limit) ? -p->ff_limit : ff);
+  ctrl = ctrl + ff;
+  c->ctrl = ctrl;
+  return ctrl;
+}
+
+/* ARM VCVT.S32.F32 semantics: truncate, saturate to int32, NaN -> 0 */
+int32_t orc_f2i32_arm(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return INT32_MAX;
+  if (f <= -2147483648.0f) return INT32_MIN;
+  return (int32_t)f;
+}
+
+/* set_CurrA_tgt: (int16_t)(A * AMPERE_TO_RAW_CURR) -- Cortex-M7: VCVT to int32 then the low
+ * 16 bits; set_rawCurr_tgt: sat_curr(_tgt_cur * dir) with the int product narrowed to the
+ * int16_t parameter (VD_motor_if_m2006.hpp:36-37,59-60,76-79) */
+int16_t orc_curr_to_raw(float amp, int dir, int16_t lim) {
+  const int16_t raw = (int16_t)(uint16_t)(uint32_t)orc_f2i32_arm(amp * 1000.0f);
+  const int16_t t = (int16_t)(uint16_t)(uint32_t)((int)raw * dir);
+  return (t > lim) ? lim : ((t < -lim) ? (int16_t)-lim : t);
+}
+
+/* CAN_CTRL::tx_routine, VD_can_controller.hpp:43-55 */
+void orc_can_tx(const int16_t cur[4], uint8_t out[8]) {
+  for (int w = 0; w < 4; w++) {
+    out[2 * w] = (uint8_t)(cur[w] >> 8);
+    out[2 * w + 1] = (uint8_t)(cur[w] & 0x00FF);
+  }
+}
+
+void orc_ctrl_reset(orc_ctrl *c) { memset(c, 0, sizeof(*c)); }
+
+/* VEHICLE_CTRL::update, control part (VD_vehicle_controller.cpp:53-98): the interpolators
+ * run every tick; then either the four FF_PI_D loops drive the current targets (power on)
+ * or interpolators + controllers reset and the targets go to 0 (power off). */
+void orc_ctrl_step(orc_ctrl *c, const orc_ctrl_params *p, const int16_t rpm[4], const int8_t dir[4]) {
+  float v[3], mt[4];
+  for (int a = 0; a < 3; a++) v[a] = orc_interp_update(&c->ax[a], p->ts);
+  for (int a = 0; a < 3; a++) c->vel_tgt[a] = v[a];
+  orc_vdir_to_mdir(v, mt);
+  if (c->power) {
+    for (int w = 0; w < 4; w++) {
+      c->pid[w].tgt = mt[w] * 36.0f;
+      const float amp = orc_pid_update(&c->pid[w], p, orc_rpm_to_mvel(rpm[w]) * 36.0f);
+      c->curr[w] = orc_curr_to_raw(amp, dir[w], p->curr_limit_raw);
+    }
+  } else {
+    for (int a = 0; a < 3; a++) orc_interp_reset(&c->ax[a]);
+    for (int w = 0; w < 4; w++) {
+      orc_pid_reset(&c->pid[w]);
+      c->curr[w] = orc_curr_to_raw(0.0f, dir[w], p->curr_limit_raw);
+    }
+  }
+}
+
+void orc_ctrl_step_batch(size_t n, orc_ctrl *c, const orc_ctrl_params *p, const int16_t *rpm,
+                         const int8_t dir[4]) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (long long i = 0; i < (long long)n; i++) orc_ctrl_step(&c[i], p, rpm + 4 * i, dir);
+}
+
+/* ------------------------------------------------------------------------- */
+/* VehicleInfo export, RM_task_main.cpp:772-823                               */
+/* ------------------------------------------------------------------------- */
+void orc_vehicle_info_fill(orc_vehicle_info *o, float px, float py, float pth, float vx, float vy,
+                           float vth, const float d[16], uint8_t is_error,
+                           const uint8_t floor[8], float cam_pitch, uint32_t fault) {
+  memset(o, 0, sizeof(*o));
+  o->pos_x = orc_f2i32_arm(px * 1000.0f);
+  o->pos_y = orc_f2i32_arm(py * 1000.0f);
+  o->pos_theta = pth;
+  o->vel_x = orc_f2i32_arm(vx);
+  o->vel_y = orc_f2i32_arm(vy);
+  o->vel_theta = vth;
+  if (is_error) {
+    o->imu_fault = 0xFF;
+  } else {
+    o->imu_fault = 0;
+    for (int k = 0; k < 4; k++) o->imu_q[k] = d[12 + k];
+    for (int k = 0; k < 3; k++) o->imu_g[k] = d[3 + k];
+    for (int k = 0; k < 3; k++) o->imu_a[k] = d[k];
+  }
+  if (floor) memcpy(o->floor, floor, 8);
+  o->cam_pitch = cam_pitch;
+  o->fault = fault;
+}
+
 int orc_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -148,6 +148,80 @@ void orc_ens_partial_f64(size_t n, int nx, const double *x, size_t lo, size_t hi
 void orc_ens_combine(int nx, const double *a, const double *b, double *out);
 void orc_ens_finalize(int nx, const double *rec, double *mean, double *cov_packed);
 
+/* ---------------- vehicle control step ---------- */
+/* UTIL::VelInterpConstJerk (src/Utility/util_vel_interp.hpp:25-157): one active
+ * StatusBuf page + the current velocity / acceleration.  The reference's two pages only
+ * separate the ISR from the task on the MCU; set_target_params rewrites every field
+ * of the inactive page and flips, so one page carries identical semantics. */
+typedef struct {
+  float vel_tgt, acl_max, jerk_p, jerk_m, dt1, dt2, dt3, vel_ini, acl_ini, dt;
+  float vel_now, acl_now;
+} orc_interp;
+/* UTIL::FF_PI_D state (util_controller.hpp:28-37, 139-149, 170-186); prev_val == now_val
+ * after every update, the IIR1's now_Y == prev_Y (util_iir.hpp:39-45) */
+typedef struct {
+  float val, integ, lpf_y, lpf_x, tgt, ctrl;
+} orc_pid;
+typedef struct {
+  float freq, dt;                /* controller(_c_freq): freq_, dt_ = 1.0f / freq (:10) */
+  float ff_gain, p_gain, i_gain, d_gain, i_limit, ff_limit;
+  float a1, b0, b1;              /* velLpf_ coefficients (:99-101) */
+  float ts;                      /* VelInterpConstJerk sample time */
+  int16_t curr_limit_raw;        /* MOTOR_IF_M2006::s16_rawCurr_lim */
+} orc_ctrl_params;
+
+/* params from the construction arguments of VD_task_main.cpp:86-97,157-160 (freq 100 Hz,
+ * FF 0.0075, P 0.02, I 0.01, D 0, I-limit 0.5, LPF 10 Hz, FF-limit 1, ts 1/1000 s) or any other */
+void orc_ctrl_params_make(orc_ctrl_params *p, float c_freq, float ff, float pg, float ig, float dg,
+                          float ilim, float lpf_freq, float ff_limit, float ts, int16_t clim);
+void  orc_interp_reset(orc_interp *s);
+void  orc_interp_set(orc_interp *s, float v_t, float a_m, float jrk);  /* set_target_params */
+float orc_interp_update(orc_interp *s, float ts);                     /* update */
+void  orc_pid_reset(orc_pid *c);
+float orc_pid_update(orc_pid *c, const orc_ctrl_params *p, float nowval);  /* FF_PI_D::update */
+/* MOTOR_IF_M2006::set_CurrA_tgt -> set_rawCurr_tgt -> sat_curr (VD_motor_if_m2006.hpp:36-37,59-60) */
+int16_t orc_curr_to_raw(float amp, int dir, int16_t lim);
+/* CAN_CTRL::tx_routine (VD_can_controller.hpp:43-55): 0x200 payload from 4 raw currents */
+void orc_can_tx(const int16_t cur[4], uint8_t out[8]);
+
+/* One robot's control state (VEHICLE_CTRL parts: 3 interpolators, 4 controllers, 4 motor
+ * current targets, isPowerOn) and the per-tick step (VD_vehicle_controller.cpp:53-98). */
+typedef struct {
+  orc_interp ax[3];
+  orc_pid    pid[4];
+  int16_t    curr[4];
+  float      vel_tgt[3];   /* now_vhcl_vel_tgt_mmps */
+  uint8_t    power;        /* isPowerOn */
+} orc_ctrl;
+void orc_ctrl_reset(orc_ctrl *c);
+void orc_ctrl_step(orc_ctrl *c, const orc_ctrl_params *p, const int16_t rpm[4], const int8_t dir[4]);
+/* batched: ctrl [n], rpm [n][4] */
+void orc_ctrl_step_batch(size_t n, orc_ctrl *c, const orc_ctrl_params *p, const int16_t *rpm,
+                         const int8_t dir[4]);
+
+/* ---------------- VehicleInfo export ---------------- */
+/* RM_task_main.cpp:772-823 -> VehicleInfo.msg / VehiclePosition.msg / ImuInfo.msg /
+ * FloorDetection.msg; natural C alignment, 84 bytes */
+typedef struct {
+  int32_t pos_x, pos_y;    /* (int32_t)(px*1000.0f) [mm] */
+  float   pos_theta;       /* [rad] */
+  int32_t vel_x, vel_y;    /* (int32_t)vx [mm/s] */
+  float   vel_theta;       /* [rad/s] */
+  uint8_t imu_fault;       /* 0xFF when is_error (all imu floats 0), else 0 */
+  uint8_t pad_[3];
+  float   imu_q[4];        /* qx qy qz qw = Data.qut[0..3] */
+  float   imu_g[3];        /* Data.gyro */
+  float   imu_a[3];        /* Data.accel */
+  uint8_t floor[8];        /* right left forward back rightforward leftforward rightback leftback */
+  float   cam_pitch;
+  uint32_t fault;
+} orc_vehicle_info;
+/* ARM float -> int32 conversion (VCVT: round toward zero, saturating, NaN -> 0) */
+int32_t orc_f2i32_arm(float f);
+void orc_vehicle_info_fill(orc_vehicle_info *o, float px, float py, float pth, float vx, float vy,
+                           float vth, const float imu_data[16], uint8_t is_error,
+                           const uint8_t floor[8], float cam_pitch, uint32_t fault);
+
 /* ---------------- timing helper for the CPU baseline --------------------- */
 int orc_max_threads(void);
 

@@ -15,6 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libwit_ref.so")
+REF_CTRL_PATH = os.path.join(HERE, "_ref", "libctrl_ref.so")
 
 TRIG_TABLE512 = 0
 TRIG_LIBM = 1
@@ -86,6 +87,34 @@ class Kf12dParams(C.Structure):
                 ("r", C.c_double * 36)]
 
 
+class Interp(C.Structure):  # orc_interp (util_vel_interp.hpp:25-157)
+    _fields_ = [(f, C.c_float) for f in ("vel_tgt", "acl_max", "jerk_p", "jerk_m", "dt1", "dt2",
+                                          "dt3", "vel_ini", "acl_ini", "dt", "vel_now", "acl_now")]
+
+
+class Pid(C.Structure):  # orc_pid (util_controller.hpp FF_PI_D state)
+    _fields_ = [(f, C.c_float) for f in ("val", "integ", "lpf_y", "lpf_x", "tgt", "ctrl")]
+
+
+class CtrlParams(C.Structure):
+    _fields_ = [(f, C.c_float) for f in ("freq", "dt", "ff_gain", "p_gain", "i_gain", "d_gain",
+                                          "i_limit", "ff_limit", "a1", "b0", "b1", "ts")] + \
+               [("curr_limit_raw", C.c_int16)]
+
+
+class Ctrl(C.Structure):  # orc_ctrl: one robot's control state
+    _fields_ = [("ax", Interp * 3), ("pid", Pid * 4), ("curr", C.c_int16 * 4),
+                ("vel_tgt", C.c_float * 3), ("power", C.c_uint8)]
+
+
+class VehicleInfo(C.Structure):  # orc_vehicle_info (VehicleInfo.msg layout, 84 B)
+    _fields_ = [("pos_x", C.c_int32), ("pos_y", C.c_int32), ("pos_theta", C.c_float),
+                ("vel_x", C.c_int32), ("vel_y", C.c_int32), ("vel_theta", C.c_float),
+                ("imu_fault", C.c_uint8), ("pad_", C.c_uint8 * 3), ("imu_q", C.c_float * 4),
+                ("imu_g", C.c_float * 3), ("imu_a", C.c_float * 3), ("floor", C.c_uint8 * 8),
+                ("cam_pitch", C.c_float), ("fault", C.c_uint32)]
+
+
 _lib = None
 
 
@@ -132,6 +161,23 @@ def lib():
         L.orc_ens_combine.argtypes = [C.c_int, _f64p, _f64p, _f64p]
         L.orc_ens_finalize.argtypes = [C.c_int, _f64p, _f64p, _f64p]
         L.orc_max_threads.restype = C.c_int
+        L.orc_ctrl_params_make.argtypes = [C.POINTER(CtrlParams)] + [C.c_float] * 9 + [C.c_int16]
+        L.orc_interp_reset.argtypes = [C.POINTER(Interp)]
+        L.orc_interp_set.argtypes = [C.POINTER(Interp), C.c_float, C.c_float, C.c_float]
+        L.orc_interp_update.argtypes = [C.POINTER(Interp), C.c_float]
+        L.orc_interp_update.restype = C.c_float
+        L.orc_pid_reset.argtypes = [C.POINTER(Pid)]
+        L.orc_pid_update.argtypes = [C.POINTER(Pid), C.POINTER(CtrlParams), C.c_float]
+        L.orc_pid_update.restype = C.c_float
+        L.orc_curr_to_raw.argtypes = [C.c_float, C.c_int, C.c_int16]
+        L.orc_curr_to_raw.restype = C.c_int16
+        L.orc_can_tx.argtypes = [_i16p, _u8p]
+        L.orc_ctrl_reset.argtypes = [C.POINTER(Ctrl)]
+        L.orc_ctrl_step_batch.argtypes = [C.c_size_t, _vp, C.POINTER(CtrlParams), _i16p, _vp]
+        L.orc_f2i32_arm.argtypes = [C.c_float]
+        L.orc_f2i32_arm.restype = C.c_int32
+        L.orc_vehicle_info_fill.argtypes = [C.POINTER(VehicleInfo)] + [C.c_float] * 6 + \
+            [_f32p, C.c_uint8, _vp, C.c_float, C.c_uint32]
         _lib = L
     return _lib
 
@@ -333,6 +379,102 @@ def ens_finalize(nx, rec):
     return mean, cov
 
 
+# ----------------------------------------------------------------------------- control step
+# VD_task_main.cpp:86-89 (FF_PI_D(100 Hz, FF 0.0075, P 0.02, I 0.01, D 0, I-lim 0.5, LPF 10 Hz)),
+# :157-160 (FF limit 1), :95-97 (interpolators at 1/1000 s), VD_motor_if_m2006.hpp:62 (3000)
+CTRL_DEFAULTS = dict(c_freq=100.0, ff=0.0075, pg=0.02, ig=0.01, dg=0.0, ilim=0.5, lpf=10.0,
+                     fflim=1.0, ts=np.float32(1.0) / np.float32(1000.0), clim=3000)
+
+
+def ctrl_params(**kw):
+    a = dict(CTRL_DEFAULTS)
+    a.update(kw)
+    p = CtrlParams()
+    lib().orc_ctrl_params_make(C.byref(p), a["c_freq"], a["ff"], a["pg"], a["ig"], a["dg"],
+                               a["ilim"], a["lpf"], a["fflim"], float(a["ts"]), int(a["clim"]))
+    return p
+
+
+class CtrlBatch:
+    """n robots' VEHICLE_CTRL control state (orc_ctrl array)."""
+
+    def __init__(self, n, prm=None, motor_dir=(1, 1, -1, -1)):
+        self.n = n
+        self.c = (Ctrl * n)()
+        for i in range(n):
+            lib().orc_ctrl_reset(C.byref(self.c[i]))
+        self.p = prm if prm is not None else ctrl_params()
+        self.dir = np.ascontiguousarray(np.asarray(motor_dir, np.int8))
+
+    def set_power(self, on):
+        on = np.broadcast_to(np.asarray(on, np.uint8), (self.n,))
+        for i in range(self.n):
+            self.c[i].power = int(on[i])
+
+    def set_target_vel(self, vel, acl, jrk, mask=None):
+        """vel/acl/jrk [3][n] (x, y, th) -> VelInterpConstJerk::set_target_params per axis"""
+        vel, acl, jrk = (np.asarray(a, np.float32) for a in (vel, acl, jrk))
+        for i in range(self.n):
+            if mask is not None and not mask[i]:
+                continue
+            for a in range(3):
+                lib().orc_interp_set(C.byref(self.c[i].ax[a]), float(vel[a, i]), float(acl[a, i]),
+                                     float(jrk[a, i]))
+
+    def step(self, rpm):
+        rpm = np.ascontiguousarray(rpm, np.int16)
+        lib().orc_ctrl_step_batch(self.n, C.cast(self.c, C.c_void_p), C.byref(self.p), rpm,
+                                  self.dir.ctypes.data_as(C.c_void_p))
+
+    def curr(self):
+        return np.array([[self.c[i].curr[w] for w in range(4)] for i in range(self.n)], np.int16)
+
+    def vel_tgt(self):
+        return np.array([[self.c[i].vel_tgt[a] for i in range(self.n)] for a in range(3)], np.float32)
+
+    def wheel(self, field):
+        """FF_PI_D field ('tgt', 'ctrl', 'val', 'integ', ...) as [4][n]"""
+        return np.array([[getattr(self.c[i].pid[w], field) for i in range(self.n)]
+                         for w in range(4)], np.float32)
+
+
+def can_tx(cur):
+    cur = np.ascontiguousarray(cur, np.int16).reshape(-1, 4)
+    out = np.zeros((cur.shape[0], 8), np.uint8)
+    for i in range(cur.shape[0]):
+        row = np.ascontiguousarray(out[i])
+        lib().orc_can_tx(np.ascontiguousarray(cur[i]), row)
+        out[i] = row
+    return out
+
+
+def f2i32_arm(f) -> int:
+    return lib().orc_f2i32_arm(float(np.float32(f)))
+
+
+def vehicle_info(px, py, pth, vx, vy, vth, imu_data, is_error, floor=None, cam_pitch=0.0,
+                 fault=0):
+    """[n] VehicleInfo records (RM_task_main.cpp:772-823) as a structured numpy array"""
+    n = len(px)
+    out = (VehicleInfo * n)()
+    for i in range(n):
+        fl = None if floor is None else np.ascontiguousarray(floor[i], np.uint8)
+        lib().orc_vehicle_info_fill(C.byref(out[i]), float(px[i]), float(py[i]), float(pth[i]),
+                                    float(vx[i]), float(vy[i]), float(vth[i]),
+                                    np.ascontiguousarray(imu_data[:, i], np.float32),
+                                    int(is_error[i]), _ptr(fl),
+                                    float(np.broadcast_to(cam_pitch, (n,))[i]),
+                                    int(np.broadcast_to(fault, (n,))[i]))
+    return np.frombuffer(bytes(out), dtype=VEHICLE_INFO_DTYPE).copy()
+
+
+VEHICLE_INFO_DTYPE = np.dtype([("pos_x", "<i4"), ("pos_y", "<i4"), ("pos_theta", "<f4"),
+                               ("vel_x", "<i4"), ("vel_y", "<i4"), ("vel_theta", "<f4"),
+                               ("imu_fault", "u1"), ("pad_", "u1", 3), ("imu_q", "<f4", 4),
+                               ("imu_g", "<f4", 3), ("imu_a", "<f4", 3), ("floor", "u1", 8),
+                               ("cam_pitch", "<f4"), ("fault", "<u4")])
+
+
 def max_threads() -> int:
     return lib().orc_max_threads()
 
@@ -377,3 +519,35 @@ class RefWt901:
         m = np.zeros(4096, np.uint16)
         n = RefWt901._l.ref_wt901_take_cb(r, m, 4096)
         return list(zip(r[:n].tolist(), m[:n].tolist()))
+
+
+# ----------------------------------------------------------------------------- reference FF_PI_D
+class RefFfPiD:
+    """The reference's own UTIL::FF_PI_D (src/Utility/util_controller.hpp), compiled from
+    /root/reference into oracle/_ref/libctrl_ref.so.  Only where the reference existed at build
+    time; the fixtures it produced are committed under tests/golden/."""
+
+    _l = None
+
+    @classmethod
+    def lib(cls):
+        if cls._l is None:
+            if not os.path.exists(REF_CTRL_PATH):
+                raise FileNotFoundError(REF_CTRL_PATH)
+            L = C.CDLL(REF_CTRL_PATH)
+            L.ref_ffpid_run.argtypes = [C.c_float] * 8 + [C.c_int, _f32p, _f32p, _vp, _f32p, _f32p, _f32p]
+            L.ref_iir1_run.argtypes = [C.c_float] * 3 + [C.c_int, _f32p, _f32p]
+            cls._l = L
+        return cls._l
+
+    @classmethod
+    def run(cls, tgt, val, reset=None, c_freq=100.0, ff=0.0075, pg=0.02, ig=0.01, dg=0.0, ilim=0.5,
+            lpf=10.0, fflim=1.0):
+        tgt = np.ascontiguousarray(tgt, np.float32)
+        val = np.ascontiguousarray(val, np.float32)
+        n = tgt.size
+        ctrl, now_val, target = (np.zeros(n, np.float32) for _ in range(3))
+        rs = None if reset is None else np.ascontiguousarray(reset, np.uint8)
+        cls.lib().ref_ffpid_run(c_freq, ff, pg, ig, dg, ilim, lpf, fflim, n, tgt, val, _ptr(rs),
+                                ctrl, now_val, target)
+        return ctrl, now_val, target

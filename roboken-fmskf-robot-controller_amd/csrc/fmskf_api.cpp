@@ -94,6 +94,13 @@ struct fmskf_ctx {
   double *ens_out = nullptr;
   // readout scratch [6][N] float
   float *readout = nullptr;
+  // output scratch for host-destined results of the control / export entry points
+  void *oscratch = nullptr;
+  size_t oscratch_bytes = 0;
+  // vehicle control state (allocated on first use) and its parameters
+  CtrlDev ctrl{};
+  fmskf_ctrl_params cprm{};
+  bool ctrl_ready = false;
   // model parameters (fp32 / fp64 copies of cfg)
   Kf6Params kf6{};
   Ekf9Params ekf9{};
@@ -148,11 +155,25 @@ struct fmskf_ctx {
     }
     return stage;
   }
+  void *out_for(size_t bytes) {
+    if (bytes > oscratch_bytes) {
+      if (oscratch) {
+        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        hip_check(hipFree(oscratch), "hipFree");
+        oscratch = nullptr;
+      }
+      hipError_t e = hipMalloc(&oscratch, bytes);
+      if (e != hipSuccess) fail(FMSKF_ENOMEM, "output scratch hipMalloc failed");
+      oscratch_bytes = bytes;
+    }
+    return oscratch;
+  }
   ~fmskf_ctx() {
     if (stream) (void)hipStreamSynchronize(stream);
     else (void)hipDeviceSynchronize();
     for (void *p : allocs) (void)hipFree(p);
     if (stage) (void)hipFree(stage);
+    if (oscratch) (void)hipFree(oscratch);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     for (hipEvent_t e : tpool) (void)hipEventDestroy(e);
@@ -807,6 +828,204 @@ int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_r
       for (uint32_t k = 0; k < nx; k++) mean[k] = acc[1 + k];
     if (cov_packed)
       for (uint32_t k = 0; k < np; k++) cov_packed[k] = acc[0] > 1.0 ? acc[1 + nx + k] / (acc[0] - 1.0) : 0.0;
+  });
+}
+
+// ============================================================================
+// vehicle control step, CAN TX, VehicleInfo export
+// ============================================================================
+namespace {
+
+void ctrl_params_defaults(fmskf_ctrl_params *p) {
+  memset(p, 0, sizeof(*p));
+  p->ctrl_freq_hz = 100.0f;  // U32_VD_TASK_CTRL_FREQ_HZ (VD_task_main.cpp:23,86-89)
+  p->ff_gain = 0.0075f;
+  p->p_gain = 0.02f;
+  p->i_gain = 0.01f;
+  p->d_gain = 0.0f;
+  p->i_limit = 0.5f;
+  p->lpf_freq_hz = 10.0f;
+  p->ff_limit = 1.0f;                            // VD_task_main.cpp:157-160
+  p->interp_ts = 1.0f / (float)1000;             // VD_task_main.cpp:95-97
+  p->curr_limit_raw = 3000;                      // VD_motor_if_m2006.hpp:62
+}
+
+// the device parameter block, computed like the reference's constructors
+// (util_controller.hpp:10,96-101: dt_ = 1.0f / freq, the IIR1 coefficients in float)
+CtrlPrm make_ctrl_prm(const fmskf_ctx *h) {
+  const fmskf_ctrl_params &c = h->cprm;
+  CtrlPrm p{};
+  p.freq = c.ctrl_freq_hz;
+  p.dt = 1.0f / c.ctrl_freq_hz;
+  p.ff_gain = c.ff_gain;
+  p.p_gain = c.p_gain;
+  p.i_gain = c.i_gain;
+  p.d_gain = c.d_gain;
+  p.i_limit = c.i_limit;
+  p.ff_limit = c.ff_limit;
+  p.a1 = (2.0f * c.ctrl_freq_hz - c.lpf_freq_hz) / (2.0f * c.ctrl_freq_hz + c.lpf_freq_hz);
+  p.b0 = c.lpf_freq_hz / (2.0f * c.ctrl_freq_hz + c.lpf_freq_hz);
+  p.b1 = c.lpf_freq_hz / (2.0f * c.ctrl_freq_hz + c.lpf_freq_hz);
+  p.ts = c.interp_ts;
+  p.curr_limit = c.curr_limit_raw;
+  for (int w = 0; w < 4; w++) p.dir[w] = h->cfg.motor_dir[w];
+  return p;
+}
+
+void ensure_ctrl(fmskf_ctx *h) {
+  if (h->ctrl_ready) return;
+  CtrlDev &c = h->ctrl;
+  c.n = h->s.n;
+  c.pitch = h->s.pitch;
+  c.ax = h->alloc<float>((size_t)3 * kAxF * c.pitch);
+  c.pid = h->alloc<float>((size_t)4 * kPidF * c.pitch);
+  c.vel_tgt = h->alloc<float>((size_t)3 * c.pitch);
+  c.curr = h->alloc<int16_t>((size_t)4 * c.n);
+  c.power = h->alloc<uint8_t>((size_t)c.n);
+  hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, h->stream), "ctrl init");
+  ctrl_params_defaults(&h->cprm);
+  h->ctrl_ready = true;
+}
+
+}  // namespace
+
+int fmskf_ctrl_params_init(fmskf_ctrl_params *p) {
+  return guarded([&] {
+    if (!p) fail(FMSKF_EINVAL, "null params");
+    ctrl_params_defaults(p);
+  });
+}
+
+int fmskf_set_ctrl_params(fmskf_handle h, const fmskf_ctrl_params *p) {
+  return guarded([&] {
+    check_handle(h);
+    if (!p) fail(FMSKF_EINVAL, "null params");
+    if (!(p->ctrl_freq_hz > 0.0f) || !(p->interp_ts > 0.0f) || p->curr_limit_raw < 0)
+      fail(FMSKF_EINVAL, "ctrl params: freq and ts must be > 0, current limit >= 0");
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    h->cprm = *p;
+  });
+}
+
+int fmskf_set_power(fmskf_handle h, const uint8_t *on, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const uint64_t n = h->s.n;
+    if (!on) {
+      hip_check(hipMemsetAsync(h->ctrl.power, 1, n, h->stream), "power");
+      return;
+    }
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    hip_check(hipMemcpyAsync(h->ctrl.power, on, n,
+                             mem == FMSKF_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                             h->stream),
+              "power");
+    finish_out(h, mem);  // the caller's host buffer may be reused on return
+  });
+}
+
+int fmskf_set_target_vel(fmskf_handle h, const float *vel, const float *acl, const float *jrk,
+                         const uint8_t *mask, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!vel || !acl || !jrk) fail(FMSKF_EINVAL, "null vel/acl/jrk");
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const uint64_t n = h->s.n;
+    Stager sg(h, mem);
+    const void *v = vel, *a = acl, *j = jrk, *m = mask;
+    sg.add(&v, 3 * n * 4);
+    sg.add(&a, 3 * n * 4);
+    sg.add(&j, 3 * n * 4);
+    sg.add(&m, n);
+    sg.run();
+    launch_check(launch_ctrl_set_target(h->ctrl, (const float *)v, (const float *)a,
+                                        (const float *)j, (const uint8_t *)m, h->stream),
+                 "set_target_vel launch");
+  });
+}
+
+int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const void *r = rpm;
+    if (r) {
+      Stager sg(h, mem);
+      sg.add(&r, h->s.n * 8);
+      sg.run();
+    } else {
+      r = h->s.m_rpm;
+    }
+    h->time_begin();
+    launch_check(launch_ctrl_step(h->ctrl, make_ctrl_prm(h), (const int16_t *)r, h->stream),
+                 "control launch");
+    h->time_end();
+  });
+}
+
+int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!frames) fail(FMSKF_EINVAL, "null frames");
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const size_t bytes = h->s.n * 8;
+    uint8_t *dst = mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)h->out_for(bytes);
+    launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
+    if (mem == FMSKF_MEM_HOST) copy_out(h, frames, dst, bytes, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *wheel_tgt,
+                   float *wheel_ctrl, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const CtrlDev &c = h->ctrl;
+    const size_t row = c.n * 4, pb = c.pitch * 4;
+    copy_planes_out(h, vel_tgt, c.vel_tgt, row, pb, 3, mem);
+    copy_out(h, curr_raw, c.curr, c.n * 8, mem);
+    // wheel w's field k is plane w*kPidF + k: planes of one field are kPidF planes apart
+    copy_planes_out(h, wheel_tgt, c.pid + 4 * c.pitch, row, pb * kPidF, 4, mem);
+    copy_planes_out(h, wheel_ctrl, c.pid + 5 * c.pitch, row, pb * kPidF, 4, mem);
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_export_vehicle_info(fmskf_handle h, fmskf_vehicle_info *out, const uint8_t *floor,
+                              const float *cam_pitch, const uint32_t *fault, uint32_t mem) {
+  static_assert(sizeof(fmskf_vehicle_info) == 84, "VehicleInfo record layout");
+  return guarded([&] {
+    check_handle(h);
+    if (!out) fail(FMSKF_EINVAL, "null out");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    Stager sg(h, mem);
+    const void *f = floor, *c = cam_pitch, *u = fault;
+    sg.add(&f, n * 8);
+    sg.add(&c, n * 4);
+    sg.add(&u, n * 4);
+    sg.run();
+    launch_check(launch_readout(h->s, h->readout, h->stream), "readout");
+    const size_t bytes = n * sizeof(fmskf_vehicle_info);
+    void *dst = mem == FMSKF_MEM_DEVICE ? (void *)out : h->out_for(bytes);
+    launch_check(launch_vehicle_info(h->s, h->readout, dst, (const uint8_t *)f, (const float *)c,
+                                     (const uint32_t *)u, h->stream),
+                 "vehicle_info launch");
+    if (mem == FMSKF_MEM_HOST) copy_out(h, out, dst, bytes, mem);
+    finish_out(h, mem);
   });
 }
 

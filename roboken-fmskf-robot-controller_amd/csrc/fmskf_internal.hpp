@@ -82,6 +82,31 @@ inline bool kf12d_sequential(const double *r36) {
   return true;
 }
 
+// Vehicle control state, allocated on first use of the control entry
+// points.  Planes at the state pitch:
+//   ax  [3 axes][12][pitch]: VelInterpConstJerk page (vel_tgt, acl_max, jerk_p, jerk_m, dt1,
+//                            dt2, dt3, vel_ini, acl_ini, dt) + vel_now, acl_now
+//   pid [4 wheels][6][pitch]: FF_PI_D (now_val == prev_val, Integ, LPF now_Y, LPF prev_X,
+//                            now_tgt, now_ctrl)
+//   vel_tgt [3][pitch]       : now_vhcl_vel_tgt_mmps
+//   curr [N][4] int16        : MOTOR_IF_M2006::s16_rawCurr_tgt (one 8-byte access per robot)
+//   power [N] u8             : isPowerOn
+struct CtrlDev {
+  uint64_t n = 0, pitch = 0;
+  float *ax = nullptr;
+  float *pid = nullptr;
+  float *vel_tgt = nullptr;
+  int16_t *curr = nullptr;
+  uint8_t *power = nullptr;
+};
+constexpr int kAxF = 12, kPidF = 6;
+// FF_PI_D / interpolator / current-limit parameters as the device uses them
+struct CtrlPrm {
+  float freq, dt, ff_gain, p_gain, i_gain, d_gain, i_limit, ff_limit, a1, b0, b1, ts;
+  int32_t curr_limit;
+  int32_t dir[4];
+};
+
 // x / P plane pitch for N instances: N rounded up to 512, plus 256 -> an odd multiple of
 // 1 KiB (fp32) between planes
 inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; }
@@ -109,6 +134,13 @@ int launch_trig(const float *x, float *sv, float *cv, uint64_t n, bool libm, con
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
                     hipStream_t st);
 int ensemble_nblocks(uint64_t n);
+// vehicle control step, TX frames, VehicleInfo export (kernels_ctrl.hip)
+int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
+                           const uint8_t *mask, hipStream_t st);
+int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hipStream_t st);
+int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st);
+int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
+                        const float *cam_pitch, const uint32_t *fault, hipStream_t st);
 // readout helpers
 int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st);
 // pose / body velocity readout as float planes: out [6][N] = x, y, th, vx_body_mmps, vy_body_mmps, w

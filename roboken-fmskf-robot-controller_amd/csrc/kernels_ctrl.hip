@@ -1,0 +1,340 @@
+// kernels_ctrl.hip -- the vehicle control step for gfx950:
+// velocity interpolation, inverse kinematics, the four FF_PI_D wheel loops, the C610 current
+// frame, and the VehicleInfo export.
+//
+// One robot per lane over plane-major state (fmskf_internal.hpp CtrlDev).  The control step
+// is the control half of VEHICLE_CTRL::update (VD_vehicle_controller.cpp:53-98): every tick
+// the three VelInterpConstJerk interpolators advance (util_vel_interp.hpp:106-133) and their
+// output goes through conv_Vdir_to_Mdir (:113-118); with the power on each wheel's FF_PI_D
+// (util_controller.hpp:104-120,171-177, IIR1 util_iir.hpp:39-45) turns target and measured
+// motor speed into a current, narrowed like MOTOR_IF_M2006::set_CurrA_tgt (hpp:36-37,59-60);
+// with the power off interpolators and controllers reset and the current is 0.  Every float
+// expression keeps the reference's operation order (library built with -ffp-contract=off), so
+// results are bit-identical to oracle/fmskf_oracle.c, itself pinned to the reference's own
+// FF_PI_D (tests/golden/ctrl_ref.npz).  HBM-bound: ~370 B per robot-tick, no reuse.
+#include "fmskf_device.hpp"
+#include "fmskf_internal.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+namespace {
+
+enum { IV_TGT, IV_AMAX, IV_JP, IV_JM, IV_DT1, IV_DT2, IV_DT3, IV_VINI, IV_AINI, IV_DT, IV_V, IV_A };
+enum { PD_VAL, PD_INTEG, PD_LY, PD_LX, PD_TGT, PD_CTRL };
+
+struct Interp {
+  float f[kAxF];
+};
+
+// VelInterpConstJerk::set_target_params, util_vel_interp.hpp:55-104 (one active page:
+// the reference rewrites every field of the inactive page, then flips)
+__device__ __forceinline__ void interp_set(Interp &s, float v_t, float a_m, float jrk) {
+  float *f = s.f;
+  f[IV_TGT] = v_t;
+  f[IV_AMAX] = a_m;
+  f[IV_VINI] = f[IV_V];
+  f[IV_AINI] = f[IV_A];
+  if ((f[IV_TGT] - f[IV_VINI]) < 0) f[IV_AMAX] = -a_m;
+  f[IV_JM] = (f[IV_AMAX] >= 0) ? -jrk : jrk;
+  const float jm_inv = 1.0f / f[IV_JM];
+  f[IV_JP] = (f[IV_AMAX] - f[IV_AINI] >= 0) ? jrk : -jrk;
+  const float jp_inv = 1.0f / f[IV_JP];
+  f[IV_DT1] = (f[IV_AMAX] - f[IV_AINI]) * jp_inv;
+  f[IV_DT3] = f[IV_AMAX] * (-jm_inv);
+  f[IV_DT2] = 1.0f / f[IV_AMAX] *
+              (f[IV_TGT] - f[IV_VINI] - f[IV_AINI] * f[IV_DT1] * 0.5f -
+               f[IV_AMAX] * (f[IV_DT1] + f[IV_DT3]) * 0.5f);
+  if (f[IV_DT2] < 0.0f) {
+    const float sq_in = (f[IV_AINI] * jp_inv) * (f[IV_AINI] * jp_inv) * 0.5f +
+                        (f[IV_TGT] - f[IV_VINI]) * jp_inv;
+    const float sq = sq_in >= 0.0f ? __builtin_sqrtf(sq_in) : 0.0f;  // arm_sqrt_f32
+    f[IV_DT1] = sq - f[IV_AINI] * jp_inv;
+    f[IV_AMAX] = f[IV_AINI] + f[IV_JP] * f[IV_DT1];
+    f[IV_DT2] = 0.0f;
+    f[IV_DT3] = f[IV_AMAX] * (-jm_inv);
+  }
+  f[IV_DT1] = (f[IV_DT1] < 0.0f) ? 0.0f : f[IV_DT1];
+  f[IV_DT3] = (f[IV_DT3] < 0.0f) ? 0.0f : f[IV_DT3];
+  f[IV_DT] = 0.0f;
+}
+
+// VelInterpConstJerk::update, util_vel_interp.hpp:106-133
+__device__ __forceinline__ float interp_update(Interp &s, float ts) {
+  float *f = s.f;
+  if (f[IV_DT] <= f[IV_DT1] + ts) {
+    f[IV_A] = f[IV_AINI] + f[IV_JP] * f[IV_DT];
+    f[IV_V] = f[IV_VINI] + (f[IV_AINI] + f[IV_A]) * f[IV_DT] * 0.5f;
+    f[IV_DT] = f[IV_DT] + ts;
+  } else if (f[IV_DT] <= f[IV_DT1] + f[IV_DT2] + ts) {
+    f[IV_A] = f[IV_AMAX];
+    f[IV_V] = f[IV_V] + f[IV_A] * ts;
+    f[IV_DT] = f[IV_DT] + ts;
+  } else if (f[IV_DT] <= f[IV_DT1] + f[IV_DT2] + f[IV_DT3] + ts) {
+    f[IV_A] = f[IV_AMAX] + f[IV_JM] * (f[IV_DT] - f[IV_DT1] - f[IV_DT2]);
+    f[IV_V] = f[IV_V] + f[IV_A] * ts;
+    f[IV_DT] = f[IV_DT] + ts;
+  } else {
+    f[IV_A] = 0.0f;
+    f[IV_V] = f[IV_TGT];
+  }
+  return f[IV_V];
+}
+
+// ARM VCVT.S32.F32: truncate, saturate, NaN -> 0
+__device__ __forceinline__ int32_t f2i32_arm(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return 2147483647;
+  if (f <= -2147483648.0f) return (int32_t)0x80000000u;
+  return (int32_t)f;
+}
+
+// set_CurrA_tgt -> set_rawCurr_tgt -> sat_curr (VD_motor_if_m2006.hpp:36-37,59-60)
+__device__ __forceinline__ int16_t curr_to_raw(float amp, int dir, int lim) {
+  const int16_t raw = (int16_t)(uint16_t)(uint32_t)f2i32_arm(amp * 1000.0f);
+  const int16_t t = (int16_t)(uint16_t)(uint32_t)((int)raw * dir);
+  return (t > lim) ? (int16_t)lim : ((t < -lim) ? (int16_t)-lim : t);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(base), 0, (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes),
+      0x00020000);
+}
+
+}  // namespace
+
+// set_target_vel: VEHICLE_CTRL::set_target_vel (VD_vehicle_controller.cpp:100-104) per robot
+// with mask[i] != 0 (or all); vel/acl/jrk [3][N] (x mm/s, y mm/s, th rad/s)
+__global__ __launch_bounds__(kBlock) void k_ctrl_set_target(CtrlDev c, const float *vel,
+                                                            const float *acl, const float *jrk,
+                                                            const uint8_t *mask) {
+  const uint64_t n = c.n, pp = c.pitch;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if (mask && !mask[i]) return;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    Interp s;
+    float *base = c.ax + (uint64_t)a * kAxF * pp;
+#pragma unroll
+    for (int k = 0; k < kAxF; k++) s.f[k] = base[k * pp + i];
+    interp_set(s, vel[a * n + i], acl[a * n + i], jrk[a * n + i]);
+#pragma unroll
+    for (int k = 0; k < kAxF; k++) base[k * pp + i] = s.f[k];
+  }
+}
+
+// Plane access for the control state: SMALL (every array within a 4 GiB buffer window) uses
+// buffer descriptors with a 32-bit lane offset and a scalar per-plane offset; otherwise plain
+// 64-bit global addressing.
+template <bool SMALL>
+struct Planes {
+  __amdgpu_buffer_rsrc_t r;
+  float *base;
+  uint64_t pp;
+  __device__ __forceinline__ Planes(float *b, uint64_t pitch, int nplanes) : base(b), pp(pitch) {
+    if constexpr (SMALL) r = rsrc(b, pitch * 4 * nplanes);
+  }
+  __device__ __forceinline__ float ld(int plane, uint32_t i) const {
+    if constexpr (SMALL)
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           r, i * 4u, (uint32_t)(plane * pp * 4), 0));
+    else
+      return base[plane * pp + i];
+  }
+  __device__ __forceinline__ void st(int plane, uint32_t i, float v) const {
+    if constexpr (SMALL)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u,
+                                            (uint32_t)(plane * pp * 4), 0);
+    else
+      base[plane * pp + i] = v;
+  }
+};
+
+// The per-tick control step.  rpm [N][4] int16 (MOTOR_IF_M2006::Status.s16_rawSpeedRpm).
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, const int16_t *rpm) {
+  const uint64_t n = c.n, pp = c.pitch;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (uint32_t)n) return;
+  const Planes<SMALL> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
+  // issue every load up front (vmcnt retires in order), then compute
+  const uint8_t on = c.power[i];
+  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[i];
+  Interp ax[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int k = 0; k < kAxF; k++) ax[a].f[k] = AX.ld(a * kAxF + k, i);
+  float pv[4][4];
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+#pragma unroll
+    for (int k = 0; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
+
+  float v[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
+  // conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
+  float mt[4];
+  mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  const int16_t r[4] = {(int16_t)(rw.x & 0xFFFFu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xFFFFu),
+                        (int16_t)(rw.y >> 16)};
+  float po[4][kPidF];
+  int16_t cur[4];
+  if (on) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      // FF_PI_D::update with now_tgt_ = Mvel_tgt * GEAR_RATIO, _nowval = Mvel * GEAR_RATIO
+      const float tgt = mt[w] * 36.0f;
+      const float val = rpm_to_mvel(r[w]) * 36.0f;
+      const float err = tgt - val;
+      const float lx = (val - pv[w][PD_VAL]) * p.freq;
+      const float ly = p.a1 * pv[w][PD_LY] + p.b0 * lx + p.b1 * pv[w][PD_LX];
+      float integ = pv[w][PD_INTEG] + p.i_gain * p.dt * err;
+      integ = (integ >= p.i_limit) ? p.i_limit : ((integ <= -p.i_limit) ? -p.i_limit : integ);
+      float ctrl = p.p_gain * err + integ - p.d_gain * ly;
+      float ff = tgt * p.ff_gain;
+      ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
+      ctrl = ctrl + ff;
+      po[w][PD_VAL] = val;
+      po[w][PD_INTEG] = integ;
+      po[w][PD_LY] = ly;
+      po[w][PD_LX] = lx;
+      po[w][PD_TGT] = tgt;
+      po[w][PD_CTRL] = ctrl;
+      cur[w] = curr_to_raw(ctrl, p.dir[w], p.curr_limit);
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int k = 0; k < kAxF; k++) ax[a].f[k] = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+#pragma unroll
+      for (int k = 0; k < kPidF; k++) po[w][k] = 0.0f;
+      cur[w] = curr_to_raw(0.0f, p.dir[w], p.curr_limit);
+    }
+  }
+  // the interpolator fields update() changes; after a reset (power off) all of them
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    AX.st(a * kAxF + IV_DT, i, ax[a].f[IV_DT]);
+    AX.st(a * kAxF + IV_V, i, ax[a].f[IV_V]);
+    AX.st(a * kAxF + IV_A, i, ax[a].f[IV_A]);
+  }
+  if (!on) {
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int k = 0; k < IV_DT; k++) AX.st(a * kAxF + k, i, 0.0f);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+#pragma unroll
+    for (int k = 0; k < kPidF; k++) PD.st(w * kPidF + k, i, po[w][k]);
+#pragma unroll
+  for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
+  reinterpret_cast<uint2 *>(c.curr)[i] =
+      make_uint2((uint32_t)(uint16_t)cur[0] | ((uint32_t)(uint16_t)cur[1] << 16),
+                 (uint32_t)(uint16_t)cur[2] | ((uint32_t)(uint16_t)cur[3] << 16));
+}
+
+// CAN_CTRL::tx_routine, VD_can_controller.hpp:43-55: frames [N][8], big-endian raw currents
+__global__ __launch_bounds__(kBlock) void k_can_tx(const int16_t *curr, uint64_t n, uint8_t *frames) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint2 c = reinterpret_cast<const uint2 *>(curr)[i];
+  // bytes (hi, lo) per wheel: swap the bytes of every 16-bit half
+  auto sw = [](uint32_t v) { return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu); };
+  reinterpret_cast<uint2 *>(frames)[i] = make_uint2(sw(c.x), sw(c.y));
+}
+
+// VehicleInfo export (RM_task_main.cpp:772-823), 84-byte records (fmskf_vehicle_info).  Each
+// lane builds its record in LDS, then the block writes its 256 records as one contiguous
+// run of dwords (coalesced), instead of 21 strided stores per lane.
+constexpr int kViWords = 21;
+__global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, const float *imu_data,
+                                                         const uint8_t *imu_err, uint64_t n,
+                                                         uint64_t ipitch, uint32_t *out,
+                                                         const uint8_t *floor,
+                                                         const float *cam_pitch,
+                                                         const uint32_t *fault) {
+  __shared__ uint32_t rec[kBlock * kViWords];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock;
+  const uint64_t i = b0 + threadIdx.x;
+  if (i < n) {
+    uint32_t *r = rec + threadIdx.x * kViWords;
+    const float px = ro[i], py = ro[n + i], pth = ro[2 * n + i];
+    const float vx = ro[3 * n + i], vy = ro[4 * n + i], vth = ro[5 * n + i];
+    r[0] = (uint32_t)f2i32_arm(px * 1000.0f);
+    r[1] = (uint32_t)f2i32_arm(py * 1000.0f);
+    r[2] = __builtin_bit_cast(uint32_t, pth);
+    r[3] = (uint32_t)f2i32_arm(vx);
+    r[4] = (uint32_t)f2i32_arm(vy);
+    r[5] = __builtin_bit_cast(uint32_t, vth);
+    const bool err = imu_err[i] != 0;
+    r[6] = err ? 0xFFu : 0u;
+    // Data page [16][N]: accel 0-2, gyro 3-5, mag 6-8, angle 9-11, qut 12-15
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[7 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[(12 + k) * ipitch + i]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) r[11 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[(3 + k) * ipitch + i]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) r[14 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[k * ipitch + i]);
+    if (floor) {
+      const uint2 f = reinterpret_cast<const uint2 *>(floor)[i];
+      r[17] = f.x;
+      r[18] = f.y;
+    } else {
+      r[17] = r[18] = 0u;
+    }
+    r[19] = cam_pitch ? __builtin_bit_cast(uint32_t, cam_pitch[i]) : 0u;
+    r[20] = fault ? fault[i] : 0u;
+  }
+  __syncthreads();
+  const uint64_t valid = (n - b0) < (uint64_t)kBlock ? (n - b0) : (uint64_t)kBlock;
+  const uint32_t words = (uint32_t)valid * kViWords;
+  uint32_t *dst = out + b0 * kViWords;
+  for (uint32_t k = threadIdx.x; k < words; k += kBlock) dst[k] = rec[k];
+}
+
+static inline dim3 grid1(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
+                           const uint8_t *mask, hipStream_t st) {
+  if (c.n == 0) return 0;
+  k_ctrl_set_target<<<grid1(c.n), kBlock, 0, st>>>(c, vel, acl, jrk, mask);
+  return (int)hipGetLastError();
+}
+
+int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hipStream_t st) {
+  if (c.n == 0) return 0;
+  if (c.pitch * 4 * 4 * kPidF < 0xFFFFFFFFull)
+    k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
+  else
+    k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
+  return (int)hipGetLastError();
+}
+
+int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {
+  if (c.n == 0) return 0;
+  k_can_tx<<<grid1(c.n), kBlock, 0, st>>>(c.curr, c.n, frames);
+  return (int)hipGetLastError();
+}
+
+int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
+                        const float *cam_pitch, const uint32_t *fault, hipStream_t st) {
+  if (s.n == 0) return 0;
+  k_vehicle_info<<<grid1(s.n), kBlock, 0, st>>>(readout, s.imu_data, s.imu_err, s.n, s.n,
+                                                (uint32_t *)out, floor, cam_pitch, fault);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fmskf

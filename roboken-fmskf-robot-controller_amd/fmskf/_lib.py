@@ -67,6 +67,20 @@ class TickInputs(C.Structure):
     ]
 
 
+class CtrlParams(C.Structure):
+    _fields_ = [(f, C.c_float) for f in ("ctrl_freq_hz", "ff_gain", "p_gain", "i_gain", "d_gain",
+                                          "i_limit", "lpf_freq_hz", "ff_limit", "interp_ts")] + \
+               [("curr_limit_raw", C.c_int16), ("reserved", C.c_int16)]
+
+
+class VehicleInfo(C.Structure):
+    _fields_ = [("pos_x", C.c_int32), ("pos_y", C.c_int32), ("pos_theta", C.c_float),
+                ("vel_x", C.c_int32), ("vel_y", C.c_int32), ("vel_theta", C.c_float),
+                ("imu_fault", C.c_uint8), ("pad_", C.c_uint8 * 3), ("imu_q", C.c_float * 4),
+                ("imu_g", C.c_float * 3), ("imu_a", C.c_float * 3), ("floor", C.c_uint8 * 8),
+                ("cam_pitch", C.c_float), ("fault", C.c_uint32)]
+
+
 # every symbol include/fmskf.h declares, with its ctypes signature
 _H = C.c_void_p
 _P = C.c_void_p
@@ -101,6 +115,14 @@ SIGNATURES = {
     "fmskf_ensemble_record_len": (C.c_int, [_H, C.POINTER(C.c_uint32)]),
     "fmskf_ensemble_partial": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_ensemble_combine": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
+    "fmskf_ctrl_params_init": (C.c_int, [C.POINTER(CtrlParams)]),
+    "fmskf_set_ctrl_params": (C.c_int, [_H, C.POINTER(CtrlParams)]),
+    "fmskf_set_power": (C.c_int, [_H, _P, C.c_uint32]),
+    "fmskf_set_target_vel": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
+    "fmskf_control": (C.c_int, [_H, _P, C.c_uint32]),
+    "fmskf_can_tx": (C.c_int, [_H, _P, C.c_uint32]),
+    "fmskf_get_ctrl": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
+    "fmskf_export_vehicle_info": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
     "fmskf_eval_trig": (C.c_int, [_H, _P, _P, _P, C.c_uint64, C.c_uint32]),
     "fmskf_set_timing": (C.c_int, [_H, C.c_int]),
     "fmskf_last_kernel_ms": (C.c_int, [_H, C.POINTER(C.c_float)]),

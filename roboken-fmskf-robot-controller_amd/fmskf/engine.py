@@ -13,7 +13,15 @@ import numpy as np
 
 from . import _lib
 from ._lib import (MEM_DEVICE, MEM_HOST, MODEL_EKF9, MODEL_KF6, MODEL_KF12D, MODEL_NAMES,
-                   MODEL_RS, TRIG_LIBM, TRIG_TABLE512, Config, TickInputs, check, load)
+                   MODEL_RS, TRIG_LIBM, TRIG_TABLE512, Config, CtrlParams, TickInputs, check,
+                   load)
+
+# fmskf_vehicle_info (include/fmskf.h): the VehicleInfo message layout, 84 bytes
+VEHICLE_INFO_DTYPE = np.dtype([("pos_x", "<i4"), ("pos_y", "<i4"), ("pos_theta", "<f4"),
+                               ("vel_x", "<i4"), ("vel_y", "<i4"), ("vel_theta", "<f4"),
+                               ("imu_fault", "u1"), ("pad_", "u1", 3), ("imu_q", "<f4", 4),
+                               ("imu_g", "<f4", 3), ("imu_a", "<f4", 3), ("floor", "u1", 8),
+                               ("cam_pitch", "<f4"), ("fault", "<u4")])
 
 _DTYPES = {
     "yaw_deg": np.float32, "gyro_z_dps": np.float32, "rpm": np.int16, "angle_sum": np.int64,
@@ -267,6 +275,75 @@ class Engine:
               "get_motors")
         return dict(angle=ang, rpm=rpm, curr=cur, angle_sum=s, speed_radps=spd)
 
+    # ------------------------------------------------------------------ control step
+    def set_ctrl_params(self, **kw):
+        """FF_PI_D / interpolator / current-limit parameters (fmskf_ctrl_params); unspecified
+        fields keep the firmware defaults (VD_task_main.cpp:86-97,157-160)."""
+        p = CtrlParams()
+        check(load().fmskf_ctrl_params_init(C.byref(p)), "ctrl_params_init")
+        for k, v in kw.items():
+            setattr(p, k, v)
+        check(load().fmskf_set_ctrl_params(self.h, C.byref(p)), "set_ctrl_params")
+
+    def set_power(self, on=None):
+        a = _Args()
+        p = a.ptr(None if on is None else np.broadcast_to(np.asarray(on, np.uint8), (self.n,)),
+                  np.uint8)
+        check(load().fmskf_set_power(self.h, p, MEM_HOST if a.mem is None else a.mem), "set_power")
+
+    def set_target_vel(self, vel, acl, jrk, mask=None):
+        """vel/acl/jrk [3][N] (x mm/s, y mm/s, th rad/s)"""
+        a = _Args()
+        ps = [a.ptr(v, np.float32) for v in (vel, acl, jrk)]
+        for name, v in zip(("vel", "acl", "jrk"), (vel, acl, jrk)):
+            have = v.numel() if _is_torch(v) else np.size(v)
+            if have < 3 * self.n:
+                raise ValueError(f"{name}: {have} elements, need 3*N = {3 * self.n}")
+        pm = a.ptr(mask, np.uint8)
+        check(load().fmskf_set_target_vel(self.h, *ps, pm, MEM_HOST if a.mem is None else a.mem),
+              "set_target_vel")
+
+    def control(self, rpm=None):
+        a = _Args()
+        if rpm is not None:
+            have = rpm.numel() if _is_torch(rpm) else np.size(rpm)
+            if have < 4 * self.n:
+                raise ValueError(f"rpm: {have} elements, need 4*N = {4 * self.n}")
+        p = a.ptr(rpm, np.int16)
+        check(load().fmskf_control(self.h, p, MEM_HOST if a.mem is None else a.mem), "control")
+
+    def can_tx(self, out=None):
+        """CAN_CTRL::tx_routine payloads [N][8] (host numpy, or into a device tensor `out`)"""
+        if out is not None and _is_torch(out) and out.is_cuda:
+            check(load().fmskf_can_tx(self.h, C.c_void_p(out.data_ptr()), MEM_DEVICE), "can_tx")
+            return out
+        f = np.empty((self.n, 8), np.uint8)
+        check(load().fmskf_can_tx(self.h, f.ctypes.data_as(C.c_void_p), MEM_HOST), "can_tx")
+        return f
+
+    def get_ctrl(self):
+        vt = np.empty((3, self.n), np.float32)
+        cur = np.empty((self.n, 4), np.int16)
+        wt = np.empty((4, self.n), np.float32)
+        wc = np.empty((4, self.n), np.float32)
+        check(load().fmskf_get_ctrl(self.h, *(x.ctypes.data_as(C.c_void_p) for x in (vt, cur, wt, wc)),
+                                    MEM_HOST), "get_ctrl")
+        return dict(vel_tgt=vt, curr=cur, wheel_tgt=wt, wheel_ctrl=wc)
+
+    def export_vehicle_info(self, floor=None, cam_pitch=None, fault=None):
+        """[N] VehicleInfo records (structured numpy array, VEHICLE_INFO_DTYPE)"""
+        a = _Args()
+        pf = a.ptr(floor, np.uint8)
+        pc = a.ptr(cam_pitch, np.float32)
+        pu = a.ptr(fault, np.uint32)
+        mem = MEM_HOST if a.mem is None else a.mem
+        if mem != MEM_HOST:
+            raise ValueError("export_vehicle_info: host inputs only from Python")
+        out = np.empty(self.n, VEHICLE_INFO_DTYPE)
+        check(load().fmskf_export_vehicle_info(self.h, out.ctypes.data_as(C.c_void_p), pf, pc, pu,
+                                               MEM_HOST), "export_vehicle_info")
+        return out
+
     def get_counters(self):
         out = (C.c_uint64 * 8)()
         check(load().fmskf_get_counters(self.h, out, 8), "get_counters")
@@ -320,5 +397,5 @@ def default_config(model="kf6", n=1) -> Config:
     return cfg
 
 
-__all__ = ["Engine", "ensemble_combine", "default_config", "MODEL_RS", "MODEL_KF6", "MODEL_EKF9",
+__all__ = ["Engine", "ensemble_combine", "default_config", "VEHICLE_INFO_DTYPE", "MODEL_RS", "MODEL_KF6", "MODEL_EKF9",
            "MODEL_KF12D", "TRIG_TABLE512", "TRIG_LIBM", "_lib"]

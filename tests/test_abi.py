@@ -62,6 +62,25 @@ def test_config_defaults_without_gpu():
         assert (a.value, b.value, c.value) == (n, mm, eb)
 
 
+def test_ctrl_params_defaults_and_record_layouts(lib):
+    """fmskf_ctrl_params_init = the firmware's construction (VD_task_main.cpp:86-97,157-160,
+    VD_motor_if_m2006.hpp:62); the VehicleInfo record is 84 bytes with the message's field
+    order (RM_task_main.cpp:772-823)."""
+    import fmskf
+    from fmskf import _lib
+    from fmskf.engine import VEHICLE_INFO_DTYPE
+    p = _lib.CtrlParams()
+    assert lib.fmskf_ctrl_params_init(C.byref(p)) == 0
+    assert (p.ctrl_freq_hz, p.p_gain, p.d_gain, p.i_limit, p.lpf_freq_hz, p.ff_limit) == \
+        (100.0, np.float32(0.02), 0.0, 0.5, 10.0, 1.0)
+    assert p.ff_gain == np.float32(0.0075) and p.i_gain == np.float32(0.01)
+    assert p.interp_ts == np.float32(1.0) / np.float32(1000.0) and p.curr_limit_raw == 3000
+    assert C.sizeof(_lib.VehicleInfo) == 84 == VEHICLE_INFO_DTYPE.itemsize
+    assert VEHICLE_INFO_DTYPE.names[:3] == ("pos_x", "pos_y", "pos_theta")
+    assert lib.fmskf_ctrl_params_init(None) == fmskf._lib.EINVAL
+    assert lib.fmskf_control(None, None, 0) == fmskf._lib.EINVAL
+
+
 def test_invalid_arguments_are_rejected(lib):
     import fmskf
     cfg = fmskf.default_config("kf6", 16)

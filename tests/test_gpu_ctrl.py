@@ -1,0 +1,168 @@
+"""GPU parity for SURVEY.md 8(f) rows 2-4: the vehicle control step, the C610 TX frame and
+the VehicleInfo export, through the C ABI, against the oracle (itself pinned to the
+reference's own FF_PI_D by tests/golden/ctrl_ref.npz, tests/test_oracle_ctrl.py).
+Bar: bit-exact (float results compared as bit patterns, integers exactly)."""
+import numpy as np
+import pytest
+
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+def _schedule(rng, n, T):
+    """random set_target / power events: list per tick of (kind, payload)"""
+    ev = {}
+    for t in range(T):
+        if t == 0 or rng.random() < 0.05:
+            vel = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                            rng.uniform(-6 * np.pi, 6 * np.pi, n)]).astype(np.float32)
+            big = rng.random() < 0.5  # C_ACCEL/JERK_MAX_MOVE vs _STOP (VD_task_main.cpp:29-48)
+            acl = np.array([[2000.0 if big else 1000.0], [2000.0 if big else 1000.0],
+                            [70.0 if big else 30.0]], np.float32).repeat(n, 1)
+            jrk = np.array([[30000.0 if big else 10000.0], [30000.0 if big else 10000.0],
+                            [1000.0 if big else 300.0]], np.float32).repeat(n, 1)
+            mask = (rng.random(n) < 0.7).astype(np.uint8)
+            ev.setdefault(t, []).append(("target", (vel, acl, jrk, mask)))
+        if t == 0 or rng.random() < 0.03:
+            ev.setdefault(t, []).append(("power", (rng.random(n) < 0.85).astype(np.uint8)))
+    return ev
+
+
+@pytest.mark.parametrize("n,T", [(1, 50), (3001, 300)])
+def test_control_step_bitexact(orc, n, T):
+    rng = np.random.default_rng(1234 + n)
+    ev = _schedule(rng, n, T)
+    ref = orc.CtrlBatch(n)
+    with Engine("kf6", n) as e:
+        for t in range(T):
+            for kind, pl in ev.get(t, []):
+                if kind == "target":
+                    e.set_target_vel(*pl)
+                    ref.set_target_vel(*pl)
+                else:
+                    e.set_power(pl)
+                    ref.set_power(pl)
+            rpm = rng.integers(-9000, 9000, (n, 4)).astype(np.int16)
+            e.control(rpm)
+            ref.step(rpm)
+        got = e.get_ctrl()
+        frames = e.can_tx()
+    np.testing.assert_array_equal(got["curr"], ref.curr())
+    np.testing.assert_array_equal(bits(got["vel_tgt"]), bits(ref.vel_tgt()))
+    np.testing.assert_array_equal(bits(got["wheel_tgt"]), bits(ref.wheel("tgt")))
+    np.testing.assert_array_equal(bits(got["wheel_ctrl"]), bits(ref.wheel("ctrl")))
+    np.testing.assert_array_equal(frames, orc.can_tx(ref.curr()))
+
+
+def test_control_custom_params_and_d_term(orc):
+    n, T = 777, 120
+    rng = np.random.default_rng(5)
+    kw = dict(ctrl_freq_hz=1000.0, ff_gain=0.01, p_gain=0.05, i_gain=0.2, d_gain=0.004,
+              i_limit=0.8, lpf_freq_hz=25.0, ff_limit=0.7, interp_ts=np.float32(0.001),
+              curr_limit_raw=2500)
+    prm = orc.ctrl_params(c_freq=1000.0, ff=0.01, pg=0.05, ig=0.2, dg=0.004, ilim=0.8, lpf=25.0,
+                          fflim=0.7, ts=np.float32(0.001), clim=2500)
+    ref = orc.CtrlBatch(n, prm)
+    vel = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                    rng.uniform(-3, 3, n)]).astype(np.float32)
+    acl = np.array([[1000.0], [1000.0], [30.0]], np.float32).repeat(n, 1)
+    jrk = np.array([[10000.0], [10000.0], [300.0]], np.float32).repeat(n, 1)
+    with Engine("rs", n) as e:
+        e.set_ctrl_params(**kw)
+        e.set_power(None)
+        ref.set_power(np.ones(n, np.uint8))
+        e.set_target_vel(vel, acl, jrk)
+        ref.set_target_vel(vel, acl, jrk)
+        for t in range(T):
+            rpm = rng.integers(-300, 300, (n, 4)).astype(np.int16)
+            e.control(rpm)
+            ref.step(rpm)
+        got = e.get_ctrl()
+    np.testing.assert_array_equal(got["curr"], ref.curr())
+    np.testing.assert_array_equal(bits(got["wheel_ctrl"]), bits(ref.wheel("ctrl")))
+
+
+def test_control_reads_ingested_motor_state():
+    n = 513
+    T = 6
+    tr = Trajectory(n, T, seed=17)
+    vel = np.zeros((3, n), np.float32)
+    vel[0] = 150.0
+    acl = np.full((3, n), 1000.0, np.float32)
+    jrk = np.full((3, n), 10000.0, np.float32)
+    with Engine("kf6", n) as a, Engine("kf6", n) as b:
+        for e in (a, b):
+            e.set_power(None)
+            e.set_target_vel(vel, acl, jrk)
+        for t in range(T):
+            fr, st = tr.can_frames(t)
+            a.ingest_can(fr, st)
+            rpm = a.get_motors()["rpm"]
+            a.control()          # NULL rpm: the device-resident motor state
+            b.control(rpm)
+        np.testing.assert_array_equal(a.get_ctrl()["curr"], b.get_ctrl()["curr"])
+
+
+def test_vehicle_info_export_bitexact(orc):
+    n, T = 2049, 20
+    tr = Trajectory(n, T, seed=23)
+    yaw, gz, rpm = tr.kf6_inputs()
+    buf = np.zeros((n, 48), np.uint8)
+    lens = np.zeros(n, np.uint32)
+    for i in range(n):
+        b = np.frombuffer(tr.wt901_poll_bytes(0, i), np.uint8)
+        buf[i, :b.size] = b
+        lens[i] = b.size
+    lens[::7] = 0  # no bytes this poll -> is_error, exported as imu.fault 0xFF
+    rng = np.random.default_rng(3)
+    floor = rng.integers(0, 2, (n, 8)).astype(np.uint8)
+    cam = rng.uniform(-30, 30, n).astype(np.float32)
+    fault = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    for model in ("rs", "kf6"):
+        with Engine(model, n) as e:
+            e.ingest_wt901(buf, lens, latch_qinit=True)
+            for t in range(T):
+                if model == "rs":
+                    e.tick(yaw_deg=yaw[t], angle_sum=np.zeros((4, n), np.int64), rpm=rpm[t])
+                else:
+                    e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])
+            rec = e.export_vehicle_info(floor, cam, fault)
+            px, py, pth = e.get_pose()
+            vx, vy, vth = e.get_vel()
+            data, err = e.get_imu()
+        ref = orc.vehicle_info(px, py, pth, vx, vy, vth, data, err, floor=floor, cam_pitch=cam,
+                               fault=fault)
+        assert rec.tobytes() == ref.tobytes(), model
+    assert set(np.unique(rec["imu_fault"])) <= {0, 0xFF}
+
+
+def test_control_large_n_properties():
+    """N = 2^20 robots, all powered, one target: every robot's interpolator reaches the
+    target; currents stay within the limit; TX frames decode back to the currents."""
+    import torch
+    n = 1 << 20
+    with Engine("kf6", n) as e:
+        e.set_power(None)
+        vel = np.zeros((3, n), np.float32)
+        vel[0] = 200.0
+        vel[2] = -1.0
+        e.set_target_vel(vel, np.full((3, n), 1000.0, np.float32) * np.float32([[1], [1], [0.03]]),
+                         np.full((3, n), 10000.0, np.float32) * np.float32([[1], [1], [0.03]]))
+        rpm = torch.zeros((n, 4), dtype=torch.int16, device="cuda")
+        for _ in range(400):
+            e.control(rpm)
+        got = e.get_ctrl()
+        fr = e.can_tx()
+    assert (got["vel_tgt"][0] == np.float32(200.0)).all()
+    assert (got["vel_tgt"][2] == np.float32(-1.0)).all()
+    assert np.abs(got["curr"]).max() <= 3000
+    dec = ((fr[:, 0::2].astype(np.int32) << 8) | fr[:, 1::2]).astype(np.uint16).view(np.int16)
+    np.testing.assert_array_equal(dec, got["curr"])
