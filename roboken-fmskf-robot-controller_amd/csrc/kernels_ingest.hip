@@ -54,19 +54,15 @@ struct Wt901Args {
   float *data;
 };
 
-__global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
-  const uint64_t n = a.n;
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  uint64_t lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
-  uint64_t hi = (uint64_t)a.parser[2 * n + i];
-  uint32_t cnt = a.cnt[i];
-  uint32_t flags = a.flags[i];
-  int16_t *reg = a.reg;
-  const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
-  const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
-  for (uint32_t b = 0; b < len; b++) {
-    const uint64_t byte = p[b];
+// One byte through WitSerialDataIn (wit_c_sdk.c:132-198): append to the window, resync by
+// one byte on a bad header or checksum, dispatch a complete 11-byte frame to CopeWitData.
+struct Wt901Parser {
+  uint64_t lo, hi;
+  uint32_t cnt, flags;
+  __device__ __forceinline__ void byte(uint32_t bv, const Wt901Args &a, uint64_t i) {
+    const uint64_t n = a.n;
+    int16_t *reg = a.reg;
+    const uint64_t byte = bv;
     // s_ucWitDataBuff[s_uiWitDataCnt++] = ucData  (bytes >= cnt are kept zero)
     if (cnt < 8) lo |= byte << (8 * cnt);
     else hi |= byte << (8 * (cnt - 8));
@@ -112,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
         cnt = 0;
         lo = 0;
         hi = 0;
-        continue;
+        return;
       }
     }
     if (drop) {
@@ -122,6 +118,53 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
       hi >>= 8;
     }
   }
+};
+
+// VEC: the poll buffer rows are 16-byte aligned and at most 64 bytes (the 44-byte standard
+// poll in a 48-byte row): the lane's whole row is fetched with up to four 16-byte loads
+// issued before any byte is parsed, instead of one dependent byte load per parser step.
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
+  const uint64_t n = a.n;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Wt901Parser ps;
+  ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
+  ps.hi = (uint64_t)a.parser[2 * n + i];
+  ps.cnt = a.cnt[i];
+  ps.flags = a.flags[i];
+  const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
+  const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
+  if constexpr (VEC) {
+    const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
+    uint4 ch[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
+    // one parser body: the next chunk's bytes are consumed from the bottom of a 128-bit
+    // shift register
+#pragma unroll 1
+    for (uint32_t c = 0; c * 16 < len; c++) {
+      uint4 cur = ch[0];  // chunks advance by register moves, never a dynamic index
+      ch[0] = ch[1];
+      ch[1] = ch[2];
+      ch[2] = ch[3];
+      const uint32_t lim = len - c * 16 < 16 ? len - c * 16 : 16;
+#pragma unroll 1
+      for (uint32_t j = 0; j < lim; j++) {
+        ps.byte(cur.x & 0xFFu, a, i);
+        cur.x = (cur.x >> 8) | (cur.y << 24);
+        cur.y = (cur.y >> 8) | (cur.z << 24);
+        cur.z = (cur.z >> 8) | (cur.w << 24);
+        cur.w >>= 8;
+      }
+    }
+  } else {
+    for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);
+  }
+  uint64_t lo = ps.lo, hi = ps.hi;
+  uint32_t cnt = ps.cnt, flags = ps.flags;
+  int16_t *reg = a.reg;
   // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
   const bool ok = (flags & F_QUAT) != 0;
   if (ok) flags = 0;
@@ -175,7 +218,9 @@ int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const
               read_reg_index, s.imu_reg,    s.imu_parser, s.imu_cnt,   s.imu_flags,
               s.imu_err,    s.imu_qinit,    s.imu_data};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
-  k_wt901<<<g, kBlock, 0, st>>>(a);
+  const bool vec = stride % 16 == 0 && stride <= 64 && ((uintptr_t)bytes & 15) == 0;
+  if (vec) k_wt901<true><<<g, kBlock, 0, st>>>(a);
+  else k_wt901<false><<<g, kBlock, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ticks", type=int, default=300)
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     args = ap.parse_args()
     import numpy as np
@@ -56,6 +56,8 @@ def main():
         z[:, 1] = -torch.deg2rad(gz.double())
         preps = [e.prepare(z=z[r]) for r in range(R)]
         many = dict(z=z)
+    if args.op in ("control", "can_tx", "wt901", "can"):
+        return bench_io(args, e, n, R, dev, rpm, st)
     tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op == "ensemble" else args.op))
     for k in range(20):
         e.tick_prepared(preps[k % R], tick)
@@ -99,6 +101,61 @@ def main():
                       "steps_per_s": n / (ms_tick * 1e-3),
                       "algo_GBps": BYTES[args.model] * n / (ms_tick * 1e-3) / 1e9, "finite": ok}),
           flush=True)
+
+
+def bench_io(args, e, n, R, dev, rpm, st):
+    """The rows either side of the tick: control step (+TX frame), WT901 and CAN ingest."""
+    import numpy as np
+    import torch
+    from fmskf.synth import wt901_frame
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    if args.op in ("control", "can_tx"):
+        e.set_power(None)
+        vel = torch.stack([torch.rand(n, generator=g) * 800 - 400, torch.rand(n, generator=g) * 800 - 400,
+                           torch.rand(n, generator=g) * 6 - 3]).to(dev)
+        acl = torch.tensor([[1000.0], [1000.0], [30.0]], device=dev).expand(3, n).contiguous()
+        jrk = torch.tensor([[10000.0], [10000.0], [300.0]], device=dev).expand(3, n).contiguous()
+        e.set_target_vel(vel, acl, jrk)
+        frames = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+        run = (lambda k: e.control(rpm[k % R])) if args.op == "control" else (lambda k: e.can_tx(frames))
+        # control: power 1 + interpolators 3x12 + FF_PI_D 4x4 read, rpm 8 read; writes
+        # interpolator dt/v/a 3x3, FF_PI_D 4x6, vel_tgt 3, currents 8 (power on)
+        bpr = (1 + 4 * 36 + 4 * 16 + 8 + 4 * 9 + 4 * 24 + 4 * 3 + 8) if args.op == "control" else 16
+    elif args.op == "wt901":
+        # one 10 ms poll per robot: acc, gyro, angle, quaternion frames (44 B), ring of R polls
+        stride = 48
+        rng = np.random.default_rng(1)
+        polls = []
+        for r in range(min(R, 8)):
+            base = bytearray()
+            for t in (0x51, 0x52, 0x53, 0x59):
+                base += wt901_frame(t, rng.integers(0, 65536, 4))
+            row = np.zeros(stride, np.uint8)
+            row[:44] = np.frombuffer(bytes(base), np.uint8)
+            polls.append(torch.from_numpy(np.tile(row, (n, 1))).to(dev))
+        lens = torch.full((n,), 44, dtype=torch.int32, device=dev)
+        run = lambda k: e.ingest_wt901(polls[k % len(polls)], lens)  # noqa: E731
+        bpr = 44 + 4
+    else:  # can
+        rng = np.random.default_rng(2)
+        fr = [torch.from_numpy(rng.integers(0, 256, (n, 4, 8)).astype(np.uint8)).to(dev) for _ in range(4)]
+        stp = [torch.from_numpy((np.arange(4)[None, :] * 250 + k * 1000 + np.zeros((n, 1))).astype(np.int16)).to(dev)
+               for k in range(4)]
+        run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
+        bpr = 4 * (8 + 2)
+    for k in range(10):
+        run(k)
+    torch.cuda.synchronize()
+    ev0.record(st)
+    for k in range(args.ticks):
+        run(k)
+    ev1.record(st)
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / args.ticks
+    print(json.dumps({"model": args.model, "n": n, "op": args.op, "ms_per_call": ms,
+                      "robots_per_s": n / (ms * 1e-3), "bytes_per_robot": bpr,
+                      "algo_GBps": bpr * n / (ms * 1e-3) / 1e9}), flush=True)
 
 
 if __name__ == "__main__":
