@@ -3,9 +3,10 @@
 // Mirrors the task structure of the reference: the IMU task polls the WT901 every
 // 10 ms (IMT::main, imu_task_main.cpp:43-82), CAN RX delivers four C610 frames per
 // millisecond (VD_can_controller.hpp:65-95), the 1 kHz ISR corrects with the IMU yaw
-// and predicts from the wheels (VD_task_main.cpp:366-372), and the ROS task reads the
-// pose (RM_task_main.cpp:776-784).  Synthetic traffic: each robot drives its wheels at
-// a constant rpm.  Usage: fleet_loop [N] [ticks]
+// and predicts from the wheels, runs the wheel speed loops and sends the 0x200 current
+// frame (VD_task_main.cpp:366-372), and the ROS task publishes VehicleInfo at 60 Hz
+// (RM_task_main.cpp:772-823).  Synthetic traffic: each robot drives its wheels at a
+// constant rpm and is commanded forward at 200 mm/s.  Usage: fleet_loop [N] [ticks]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -42,7 +43,20 @@ int main(int argc, char **argv) {
     std::vector<int16_t> stamps(n * 4);
     std::vector<int64_t> enc(n * 4, 0);
     std::vector<float> px(n), py(n), pth(n);
+    std::vector<uint8_t> tx(n * 8);
+    std::vector<fmskf_vehicle_info> info(n);
     const int dir[4] = {1, 1, -1, -1};
+    // REQ_MOVE_DIR GO_FORWARD at 200 mm/s with C_ACCEL/JERK_MAX_MOVE (VD_task_main.cpp:29-38,191-198)
+    std::vector<float> vel(3 * n, 0.f), acl(3 * n), jrk(3 * n);
+    for (uint64_t i = 0; i < n; i++) {
+      vel[i] = 200.f;
+      acl[i] = acl[n + i] = 1000.f;
+      acl[2 * n + i] = 30.f;
+      jrk[i] = jrk[n + i] = 10000.f;
+      jrk[2 * n + i] = 300.f;
+    }
+    vehicle.start();
+    vehicle.set_target_vel(vel.data(), acl.data(), jrk.data());
 
     auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < ticks; t++) {
@@ -75,8 +89,9 @@ int main(int argc, char **argv) {
         if (t == 0) imu.init(bytes.data(), stride, len.data());
         else imu.update(bytes.data(), stride, len.data());
       }
-      robots.can_tx_routine();  // correct + predict, device-resident inputs
-      if (t % 60 == 59) vehicle.get_vehicle_pos_m_latest(px.data(), py.data(), pth.data());
+      // correct + predict + wheel loops + 0x200 frames, device-resident inputs
+      robots.can_tx_routine(tx.data());
+      if (t % 17 == 16) fmskf::publish_vehicle_info(robots, info.data());  // ~60 Hz
     }
     robots.sync();
     auto t1 = std::chrono::steady_clock::now();
@@ -86,6 +101,9 @@ int main(int argc, char **argv) {
            (unsigned long long)n, ticks, s, (double)n * ticks / s);
     printf("robot 0: x=%.6f m y=%.6f m th=%.6f rad   robot 4: x=%.6f m\n", px[0], py[0], pth[0],
            n > 4 ? px[4] : 0.f);
+    printf("robot 0: VehicleInfo pos=(%d, %d) mm imu.fault=%u  tx=[%02x %02x %02x %02x %02x %02x %02x %02x]\n",
+           info[0].pos_x, info[0].pos_y, info[0].imu_fault, tx[0], tx[1], tx[2], tx[3], tx[4], tx[5],
+           tx[6], tx[7]);
   } catch (const std::exception &e) {
     fprintf(stderr, "fleet_loop: %s\n", e.what());
     return 1;

@@ -12,12 +12,18 @@
 //     get_vehicle_pos_m_latest / get_vehicle_vel_mmps_latest
 //     (src/VehicleDrive/VD_vehicle_controller.hpp:52-61)
 //   VDT::can_tx_routine_intr (VD_task_main.cpp:366-372)      fmskf::Robots::can_tx_routine
+//   VEHICLE_CTRL::start / stop / set_target_vel /            fmskf::VehicleCtrl
+//     get_vehicle_vel_tgt_mmps_latest (VD_vehicle_controller.hpp:54-61)
+//   MOTOR_IF_M2006::get_rawCurr_tgt (VD_motor_if_m2006.hpp:52) MotorIfM2006::get_rawCurr_tgt
+//   CAN_CTRL::tx_routine (VD_can_controller.hpp:43-55)        Robots::can_tx_routine(frames)
+//   RM_task_main routine_ros VehicleInfo publish (:772-823)   fmskf::publish_vehicle_info
 //
 // Errors: the reference's calls are void; here a non-OK status throws fmskf::Error
 // (host side only -- nothing throws across the C ABI).
 #pragma once
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "fmskf.h"
 
@@ -58,12 +64,19 @@ class Robots {
   void set_stream(void *hip_stream) { check(fmskf_set_stream(h_, hip_stream), "fmskf_set_stream"); }
   void sync() { check(fmskf_sync(h_), "fmskf_sync"); }
 
-  // VDT::can_tx_routine_intr: correct with the IMU yaw, then predict from the wheels,
-  // reading the device-resident IMU / motor state the ingest calls produced.
-  void can_tx_routine() {
+  // VDT::can_tx_routine_intr: correct with the IMU yaw, then VEHICLE_CTRL::update (the
+  // odometry / estimator time update, then the control half: interpolators, IK, FF_PI_D),
+  // then M_CAN.tx_routine -- reading the device-resident IMU / motor state the ingest calls
+  // produced.  tx_frames [N][8] receives the 0x200 payloads; NULL skips control and TX
+  // (estimation only).
+  void can_tx_routine(uint8_t *tx_frames = nullptr, uint32_t mem = FMSKF_MEM_HOST) {
     fmskf_tick_inputs in{};
     in.mem = FMSKF_MEM_HOST;
     check(fmskf_tick(h_, &in), "fmskf_tick");
+    if (tx_frames) {
+      check(fmskf_control(h_, nullptr, FMSKF_MEM_HOST), "fmskf_control");
+      check(fmskf_can_tx(h_, tx_frames, mem), "fmskf_can_tx");
+    }
   }
 
  private:
@@ -105,6 +118,10 @@ class MotorIfM2006 {
   void get_rawAngleSum(int64_t *sum, uint32_t mem = FMSKF_MEM_HOST) {
     check(fmskf_get_motors(r_.handle(), nullptr, nullptr, nullptr, sum, nullptr, mem), "get_rawAngleSum");
   }
+  // get_rawCurr_tgt: [N][4] (FL, BL, BR, FR), what tx_routine packs
+  void get_rawCurr_tgt(int16_t *curr, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_get_ctrl(r_.handle(), nullptr, curr, nullptr, nullptr, mem), "get_rawCurr_tgt");
+  }
 
  private:
   Robots &r_;
@@ -133,9 +150,39 @@ class VehicleCtrl {
   void get_vehicle_vel_mmps_latest(float *vx, float *vy, float *vth, uint32_t mem = FMSKF_MEM_HOST) {
     check(fmskf_get_vel(r_.handle(), vx, vy, vth, mem), "get_vehicle_vel_mmps_latest");
   }
+  // start / stop (isPowerOn) for every robot, or per robot with on [N]
+  void start(const uint8_t *on = nullptr, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_set_power(r_.handle(), on, mem), "start");
+  }
+  void stop() {
+    // power off for all: a zero plane
+    std::vector<uint8_t> off(r_.size(), 0);
+    check(fmskf_set_power(r_.handle(), off.data(), FMSKF_MEM_HOST), "stop");
+  }
+  // set_target_vel(vel, acl, jrk): [3][N] planes each (x mm/s, y mm/s, th rad/s)
+  void set_target_vel(const float *vel, const float *acl, const float *jrk,
+                      const uint8_t *mask = nullptr, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_set_target_vel(r_.handle(), vel, acl, jrk, mask, mem), "set_target_vel");
+  }
+  // the control half of update() on explicit wheel speeds ([N][4] rpm) or, with NULL, on
+  // the device motor state
+  void control(const int16_t *rpm = nullptr, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_control(r_.handle(), rpm, mem), "control");
+  }
+  void get_vehicle_vel_tgt_mmps_latest(float *vel_tgt /*[3][N]*/, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_get_ctrl(r_.handle(), vel_tgt, nullptr, nullptr, nullptr, mem),
+          "get_vehicle_vel_tgt_mmps_latest");
+  }
 
  private:
   Robots &r_;
 };
+
+// routine_ros (RM_task_main.cpp:772-823): the VehicleInfo message of every robot
+inline void publish_vehicle_info(Robots &r, fmskf_vehicle_info *out, const uint8_t *floor = nullptr,
+                                 const float *cam_pitch = nullptr, const uint32_t *fault = nullptr,
+                                 uint32_t mem = FMSKF_MEM_HOST) {
+  check(fmskf_export_vehicle_info(r.handle(), out, floor, cam_pitch, fault, mem), "publish");
+}
 
 }  // namespace fmskf

@@ -166,3 +166,20 @@ def test_control_large_n_properties():
     assert np.abs(got["curr"]).max() <= 3000
     dec = ((fr[:, 0::2].astype(np.int32) << 8) | fr[:, 1::2]).astype(np.uint16).view(np.int16)
     np.testing.assert_array_equal(dec, got["curr"])
+
+
+def test_fleet_loop_cpp_host_program():
+    """examples/fleet_loop.cpp (C++ over the C ABI, the firmware's task structure incl. the
+    wheel loops, TX frames and the VehicleInfo publish) runs and prints sane values."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "fleet_loop")
+    assert os.path.exists(exe), "build() makes build/fleet_loop"
+    out = subprocess.run([exe, "4096", "200"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.strip().splitlines()
+    assert lines[0].startswith("robots=4096 ticks=200")
+    x0 = float(lines[1].split("x=")[1].split()[0])
+    assert 0.0 < x0 < 1.0          # driven forward for 0.2 s
+    assert "imu.fault=0" in lines[2]
