@@ -37,6 +37,40 @@ __device__ __forceinline__ void ekf9_innov(const TickIn &in, uint64_t j, const f
   y[5] = z5 - x[4];
 }
 
+// one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
+template <bool LIBM, bool UPD, bool PRED>
+__device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, uint64_t j,
+                                           bool have, const float *stab, float (&x)[9],
+                                           float (&P)[45]) {
+  const float dt = a.prm.dt;
+  if (UPD && have) {
+    float y[6];
+    ekf9_innov(a.in, j, x, y);
+    kf_update<MdEKF9>(x, P, y, a.prm.r);
+  }
+  if (PRED) {
+    // f(x): mecanum body velocity rotated into the world frame (the reference's
+    // odometry, VD_vehicle_controller.cpp:47-51, generalised) + its Jacobian
+    const float rr = normalize_rad_0to2pi(x[2]);
+    const float c = cos_p<LIBM>(rr, stab), s = sin_p<LIBM>(rr, stab);
+    const float vwx = x[3] * c - x[4] * s;
+    const float vwy = x[3] * s + x[4] * c;
+    const float f02 = -(vwy * dt), f03 = c * dt, f04 = -(s * dt);
+    const float f12 = vwx * dt, f13 = s * dt, f14 = c * dt;
+    x[0] = x[0] + vwx * dt;
+    x[1] = x[1] + vwy * dt;
+    x[2] = wrap_pi(x[2] + x[5] * dt);
+    x[3] = x[3] + x[7] * dt;
+    x[4] = x[4] + x[8] * dt;
+    auto fv = [&](int r, int k) -> float {
+      if (r == 0) return k == 2 ? f02 : k == 3 ? f03 : f04;
+      if (r == 1) return k == 2 ? f12 : k == 3 ? f13 : f14;
+      return dt;
+    };
+    kf_predict_cov<MdEKF9>(P, fv, a.prm.q);
+  }
+}
+
 template <bool LIBM, bool UPD, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
@@ -53,43 +87,45 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   for (int k = 0; k < N; k++) x[k] = a.x[k * pp + i];
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + i];
-  const float dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t j = (uint64_t)t * a.in.stride + i;
-    if (UPD) {
-      if (a.in.valid == nullptr || a.in.valid[j]) {
-        float y[6];
-        ekf9_innov(a.in, j, x, y);
-        kf_update<MdEKF9>(x, P, y, a.prm.r);
-      }
-    }
-    if (PRED) {
-      // f(x): mecanum body velocity rotated into the world frame (the reference's
-      // odometry, VD_vehicle_controller.cpp:47-51, generalised) + its Jacobian
-      const float rr = normalize_rad_0to2pi(x[2]);
-      const float c = cos_p<LIBM>(rr, stab), s = sin_p<LIBM>(rr, stab);
-      const float vwx = x[3] * c - x[4] * s;
-      const float vwy = x[3] * s + x[4] * c;
-      const float f02 = -(vwy * dt), f03 = c * dt, f04 = -(s * dt);
-      const float f12 = vwx * dt, f13 = s * dt, f14 = c * dt;
-      x[0] = x[0] + vwx * dt;
-      x[1] = x[1] + vwy * dt;
-      x[2] = wrap_pi(x[2] + x[5] * dt);
-      x[3] = x[3] + x[7] * dt;
-      x[4] = x[4] + x[8] * dt;
-      auto fv = [&](int r, int k) -> float {
-        if (r == 0) return k == 2 ? f02 : k == 3 ? f03 : f04;
-        if (r == 1) return k == 2 ? f12 : k == 3 ? f13 : f14;
-        return dt;
-      };
-      kf_predict_cov<MdEKF9>(P, fv, a.prm.q);
-    }
+    ekf9_tick1<LIBM, UPD, PRED>(a, j, a.in.valid == nullptr || a.in.valid[j], stab, x, P);
   }
 #pragma unroll
   for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
 #pragma unroll
   for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
   nan_guard(x, P, a.counters);
+}
+
+// Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
+// their stores and NaN count are masked), every load issued before the table barrier.
+template <bool LIBM, bool UPD, bool PRED>
+__global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
+  constexpr int N = 9, NP = 45;
+  __shared__ float stab[LIBM ? 1 : 513];
+  const uint64_t n = a.n, pp = a.pitch;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i < n;
+  const uint64_t ic = live ? i : n - 1;
+  float x[N], P[NP];
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
+#pragma unroll
+  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+  const bool have = a.in.valid == nullptr || a.in.valid[ic];
+  if (!LIBM) {
+    for (int k = threadIdx.x; k < 513; k += kBlock) stab[k] = a.in.sintab[k];
+    __syncthreads();
+  }
+  ekf9_tick1<LIBM, UPD, PRED>(a, ic, have, stab, x, P);
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+#pragma unroll
+    for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+  }
+  nan_guard(x, P, a.counters, live);
 }
 
 // SEQ: R has no base/tip cross terms -> group-sequential update (base group, then tip group
@@ -150,7 +186,17 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
                 bool pred, hipStream_t st) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
-  if (libm) {
+  if (in.n_ticks == 1) {
+    if (libm) {
+      if (upd && pred) k_ekf9t<true, true, true><<<g, kBlock, 0, st>>>(a);
+      else if (upd) k_ekf9t<true, true, false><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<true, false, true><<<g, kBlock, 0, st>>>(a);
+    } else {
+      if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, 0, st>>>(a);
+      else if (upd) k_ekf9t<false, true, false><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<false, false, true><<<g, kBlock, 0, st>>>(a);
+    }
+  } else if (libm) {
     if (upd && pred) k_ekf9<true, true, true><<<g, kBlock, 0, st>>>(a);
     else if (upd) k_ekf9<true, true, false><<<g, kBlock, 0, st>>>(a);
     else k_ekf9<true, false, true><<<g, kBlock, 0, st>>>(a);
