@@ -50,8 +50,11 @@ __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
 }
 
+// The per-tick inputs are read exactly once: load them non-temporal (gfx950 `nt`, aux bit 1)
+// so the fresh 16 MB per tick at 2^20 displaces less of the state from the caches (measured
+// 43.6 -> 42.7 us per tick with a 64-tick input ring).
 #ifndef FMSKF_IN_CPOL
-#define FMSKF_IN_CPOL 0
+#define FMSKF_IN_CPOL 2
 #endif
 // inputs of one tick; planes of tick t start at t * stride elements
 template <class O>
