@@ -195,6 +195,20 @@ int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
 int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
                            double *mean, double *cov_packed);
 
+/* Native multi-GPU path: one process per GPU, an RCCL communicator owned by
+ * the handle, the ensemble record all-gathered over xGMI on the handle's stream.  RCCL
+ * (librccl.so.1) is resolved at run time, so the library has no link-time dependency on it;
+ * FMSKF_ERCCL when it cannot be loaded or a collective fails.
+ *   rank 0: fmskf_comm_unique_id(id); distribute the 128 bytes to every rank (any channel);
+ *   every rank: fmskf_comm_init(h, id, rank, world); then fmskf_ensemble_stats(h, ...). */
+#define FMSKF_COMM_ID_BYTES 128
+int fmskf_comm_unique_id(uint8_t id[FMSKF_COMM_ID_BYTES]);
+int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int rank, int world);
+/* mean [n], cov packed [n(n+1)/2] (unbiased) over every robot of every rank (the ranks of
+ * fmskf_comm_init; without a communicator, this handle's robots): device partial record,
+ * ncclAllGather, fold in rank order on the host -> identical on every rank, deterministic. */
+int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
+
 /* ---- vehicle control step -------------------------- */
 /* Per-robot control state is allocated on the first call of any entry point below
  * (~250 B per robot); zero-initialised like the firmware's static objects, power off. */

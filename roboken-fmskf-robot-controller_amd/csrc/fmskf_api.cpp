@@ -7,8 +7,10 @@
 // compute entry point launches a HIP kernel or fails with FMSKF_EDEVICE.
 #include "../../include/fmskf.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
 #include <string>
@@ -97,6 +99,10 @@ struct fmskf_ctx {
   // output scratch for host-destined results of the control / export entry points
   void *oscratch = nullptr;
   size_t oscratch_bytes = 0;
+  // RCCL communicator (fmskf_comm_init) and the all-gather buffer [world][record]
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+  double *ens_gather = nullptr;
   // vehicle control state (allocated on first use) and its parameters
   CtrlDev ctrl{};
   fmskf_ctrl_params cprm{};
@@ -155,6 +161,7 @@ struct fmskf_ctx {
     }
     return stage;
   }
+  void destroy_comm();
   void *out_for(size_t bytes) {
     if (bytes > oscratch_bytes) {
       if (oscratch) {
@@ -174,6 +181,7 @@ struct fmskf_ctx {
     for (void *p : allocs) (void)hipFree(p);
     if (stage) (void)hipFree(stage);
     if (oscratch) (void)hipFree(oscratch);
+    destroy_comm();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     for (hipEvent_t e : tpool) (void)hipEventDestroy(e);
@@ -831,6 +839,119 @@ int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_r
   });
 }
 
+}  // extern "C"
+
+// ============================================================================
+// native multi-GPU ensemble over RCCL
+// ============================================================================
+namespace {
+
+// RCCL entry points, resolved once from librccl.so.1 (the copy torch already loaded, if any)
+struct RcclApi {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+const RcclApi &rccl() {
+  static RcclApi api = [] {
+    RcclApi a;
+    void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) {
+      a.why = std::string("cannot load librccl.so.1: ") + dlerror();
+      return a;
+    }
+    a.get_unique_id = (decltype(a.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+    a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+    a.comm_destroy = (decltype(a.comm_destroy))dlsym(lib, "ncclCommDestroy");
+    a.all_gather = (decltype(a.all_gather))dlsym(lib, "ncclAllGather");
+    a.error_string = (decltype(a.error_string))dlsym(lib, "ncclGetErrorString");
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.error_string;
+    if (!a.ok) a.why = "librccl.so.1 lacks an entry point";
+    return a;
+  }();
+  return api;
+}
+
+const RcclApi &need_rccl() {
+  const RcclApi &a = rccl();
+  if (!a.ok) fail(FMSKF_ERCCL, a.why);
+  return a;
+}
+
+void nccl_check(ncclResult_t r, const char *what) {
+  if (r != ncclSuccess) fail(FMSKF_ERCCL, std::string(what) + ": " + rccl().error_string(r));
+}
+
+}  // namespace
+
+void fmskf_ctx::destroy_comm() {
+  if (comm) {
+    (void)rccl().comm_destroy(comm);
+    comm = nullptr;
+  }
+}
+
+extern "C" {
+
+int fmskf_comm_unique_id(uint8_t id[FMSKF_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == FMSKF_COMM_ID_BYTES, "RCCL unique id size");
+  return guarded([&] {
+    if (!id) fail(FMSKF_EINVAL, "null id");
+    ncclUniqueId u;
+    nccl_check(need_rccl().get_unique_id(&u), "ncclGetUniqueId");
+    memcpy(id, &u, sizeof(u));
+  });
+}
+
+int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int rank, int world) {
+  return guarded([&] {
+    check_handle(h);
+    if (!id || world < 1 || rank < 0 || rank >= world) fail(FMSKF_EINVAL, "bad rank / world / id");
+    const RcclApi &a = need_rccl();
+    DeviceGuard g(h->cfg.device);
+    h->destroy_comm();
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    nccl_check(a.comm_init_rank(&h->comm, world, u, rank), "ncclCommInitRank");
+    h->rank = rank;
+    h->world = world;
+    h->ens_gather = h->alloc<double>((size_t)world * 91);
+  });
+}
+
+int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed) {
+  return guarded([&] {
+    check_handle(h);
+    DeviceGuard g(h->cfg.device);
+    const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
+    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, h->ens_out, h->stream),
+                 "ensemble launch");
+    const double *src = h->ens_out;
+    int ranks = 1;
+    if (h->comm) {
+      nccl_check(need_rccl().all_gather(h->ens_out, h->ens_gather, len, ncclFloat64, h->comm,
+                                        h->stream),
+                 "ncclAllGather");
+      src = h->ens_gather;
+      ranks = h->world;
+    }
+    std::vector<double> recs((size_t)ranks * len);
+    hip_check(hipMemcpyAsync(recs.data(), src, recs.size() * 8, hipMemcpyDeviceToHost, h->stream),
+              "D2H");
+    hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    const int rc = fmskf_ensemble_combine(nx, recs.data(), (uint32_t)ranks, mean, cov_packed);
+    if (rc != FMSKF_OK) fail(rc, "ensemble combine");
+  });
+}
+
+}  // extern "C"
+
 // ============================================================================
 // vehicle control step, CAN TX, VehicleInfo export
 // ============================================================================
@@ -892,6 +1013,8 @@ void ensure_ctrl(fmskf_ctx *h) {
 }
 
 }  // namespace
+
+extern "C" {
 
 int fmskf_ctrl_params_init(fmskf_ctrl_params *p) {
   return guarded([&] {

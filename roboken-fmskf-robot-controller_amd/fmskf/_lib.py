@@ -115,6 +115,9 @@ SIGNATURES = {
     "fmskf_ensemble_record_len": (C.c_int, [_H, C.POINTER(C.c_uint32)]),
     "fmskf_ensemble_partial": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_ensemble_combine": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
+    "fmskf_comm_unique_id": (C.c_int, [_P]),
+    "fmskf_comm_init": (C.c_int, [_H, _P, C.c_int, C.c_int]),
+    "fmskf_ensemble_stats": (C.c_int, [_H, _P, _P]),
     "fmskf_ctrl_params_init": (C.c_int, [C.POINTER(CtrlParams)]),
     "fmskf_set_ctrl_params": (C.c_int, [_H, C.POINTER(CtrlParams)]),
     "fmskf_set_power": (C.c_int, [_H, _P, C.c_uint32]),

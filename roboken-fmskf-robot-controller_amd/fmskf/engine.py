@@ -275,6 +275,22 @@ class Engine:
               "get_motors")
         return dict(angle=ang, rpm=rpm, curr=cur, angle_sum=s, speed_radps=spd)
 
+    # ------------------------------------------------------------------ native RCCL path
+    def comm_init(self, unique_id: bytes, rank: int, world: int):
+        """fmskf_comm_init: an RCCL communicator owned by this handle (one process per GPU)"""
+        b = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        check(load().fmskf_comm_init(self.h, b, int(rank), int(world)), "comm_init")
+
+    def ensemble_stats(self):
+        """(mean [n], cov packed [n(n+1)/2]) over all ranks of the communicator (or this
+        handle alone): device record, ncclAllGather, rank-order fold"""
+        nx = self.nx
+        mean = np.empty(nx, np.float64)
+        cov = np.empty(nx * (nx + 1) // 2, np.float64)
+        check(load().fmskf_ensemble_stats(self.h, mean.ctypes.data_as(C.c_void_p),
+                                          cov.ctypes.data_as(C.c_void_p)), "ensemble_stats")
+        return mean, cov
+
     # ------------------------------------------------------------------ control step
     def set_ctrl_params(self, **kw):
         """FF_PI_D / interpolator / current-limit parameters (fmskf_ctrl_params); unspecified
@@ -389,6 +405,13 @@ def ensemble_combine(n_state: int, records) -> tuple[np.ndarray, np.ndarray]:
     return mean, cov
 
 
+def comm_unique_id() -> bytes:
+    """fmskf_comm_unique_id (rank 0): 128 bytes to hand to every rank's comm_init"""
+    b = (C.c_uint8 * 128)()
+    check(load().fmskf_comm_unique_id(b), "comm_unique_id")
+    return bytes(b)
+
+
 def default_config(model="kf6", n=1) -> Config:
     """Model defaults (pure host call, no GPU needed)."""
     cfg = Config()
@@ -397,5 +420,5 @@ def default_config(model="kf6", n=1) -> Config:
     return cfg
 
 
-__all__ = ["Engine", "ensemble_combine", "default_config", "VEHICLE_INFO_DTYPE", "MODEL_RS", "MODEL_KF6", "MODEL_EKF9",
+__all__ = ["Engine", "ensemble_combine", "default_config", "comm_unique_id", "VEHICLE_INFO_DTYPE", "MODEL_RS", "MODEL_KF6", "MODEL_EKF9",
            "MODEL_KF12D", "TRIG_TABLE512", "TRIG_LIBM", "_lib"]

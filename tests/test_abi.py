@@ -33,6 +33,16 @@ def test_library_exports_every_declared_symbol(lib):
     assert not missing, missing
 
 
+def test_library_exports_only_the_abi():
+    """libfmskf.so exports the C ABI and nothing else (csrc/fmskf.map)"""
+    import subprocess
+    from fmskf import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    names = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert names == set(_declared())
+
+
 def test_python_binding_covers_header():
     from fmskf import _lib
     assert set(_declared()) == set(_lib.SIGNATURES)
