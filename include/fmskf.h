@@ -272,6 +272,17 @@ typedef struct fmskf_vehicle_info {
 int fmskf_export_vehicle_info(fmskf_handle h, fmskf_vehicle_info *out, const uint8_t *floor,
                               const float *cam_pitch, const uint32_t *fault, uint32_t mem);
 
+/* ---- HIP graph of a per-tick call sequence ------------------------------------- */
+/* Record the device work of the entry points called between begin and end (on the handle's
+ * stream, which must be a stream set with fmskf_set_stream, not the null stream) into a HIP
+ * graph, then replay it: one launch per tick for launch-bound (small-N) fleets.  Only
+ * device-pointer calls (FMSKF_MEM_DEVICE, or NULL planes reading the device state) can be
+ * captured; a call that needs a host round trip fails during capture.  A new begin
+ * replaces the previous graph. */
+int fmskf_graph_begin(fmskf_handle h);
+int fmskf_graph_end(fmskf_handle h);
+int fmskf_graph_launch(fmskf_handle h, uint32_t times);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Evaluate the device sin/cos policy on x[n] (device pointers when mem = DEVICE). */
 int fmskf_eval_trig(fmskf_handle h, const float *x, float *s, float *c, uint64_t n, uint32_t mem);

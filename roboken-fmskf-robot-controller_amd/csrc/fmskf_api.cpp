@@ -99,6 +99,10 @@ struct fmskf_ctx {
   // output scratch for host-destined results of the control / export entry points
   void *oscratch = nullptr;
   size_t oscratch_bytes = 0;
+  // captured per-tick sequence (fmskf_graph_*)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  bool capturing = false;
   // RCCL communicator (fmskf_comm_init) and the all-gather buffer [world][record]
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
@@ -182,6 +186,8 @@ struct fmskf_ctx {
     if (stage) (void)hipFree(stage);
     if (oscratch) (void)hipFree(oscratch);
     destroy_comm();
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    if (graph) (void)hipGraphDestroy(graph);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     for (hipEvent_t e : tpool) (void)hipEventDestroy(e);
@@ -585,6 +591,47 @@ int fmskf_set_stream(fmskf_handle h, void *stream) {
   return guarded([&] {
     check_handle(h);
     h->stream = (hipStream_t)stream;
+  });
+}
+
+int fmskf_graph_begin(fmskf_handle h) {
+  return guarded([&] {
+    check_handle(h);
+    if (!h->stream) fail(FMSKF_EINVAL, "graph capture needs a stream (fmskf_set_stream)");
+    if (h->capturing) fail(FMSKF_EINVAL, "capture already open");
+    if (h->timing) fail(FMSKF_EINVAL, "disable per-launch timing before capturing");
+    DeviceGuard g(h->cfg.device);
+    hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
+              "hipStreamBeginCapture");
+    h->capturing = true;
+  });
+}
+
+int fmskf_graph_end(fmskf_handle h) {
+  return guarded([&] {
+    check_handle(h);
+    if (!h->capturing) fail(FMSKF_EINVAL, "no capture open");
+    DeviceGuard g(h->cfg.device);
+    h->capturing = false;
+    hipGraph_t gnew = nullptr;
+    hip_check(hipStreamEndCapture(h->stream, &gnew), "hipStreamEndCapture");
+    if (h->graph_exec) hip_check(hipGraphExecDestroy(h->graph_exec), "hipGraphExecDestroy");
+    if (h->graph) hip_check(hipGraphDestroy(h->graph), "hipGraphDestroy");
+    h->graph_exec = nullptr;
+    h->graph = gnew;
+    hip_check(hipGraphInstantiate(&h->graph_exec, h->graph, nullptr, nullptr, 0),
+              "hipGraphInstantiate");
+  });
+}
+
+int fmskf_graph_launch(fmskf_handle h, uint32_t times) {
+  return guarded([&] {
+    check_handle(h);
+    if (!h->graph_exec) fail(FMSKF_EINVAL, "no graph captured");
+    if (h->capturing) fail(FMSKF_EINVAL, "capture still open");
+    DeviceGuard g(h->cfg.device);
+    for (uint32_t k = 0; k < times; k++)
+      hip_check(hipGraphLaunch(h->graph_exec, h->stream), "hipGraphLaunch");
   });
 }
 

@@ -275,6 +275,16 @@ class Engine:
               "get_motors")
         return dict(angle=ang, rpm=rpm, curr=cur, angle_sum=s, speed_radps=spd)
 
+    # ------------------------------------------------------------------ HIP graph
+    def graph_begin(self):
+        check(load().fmskf_graph_begin(self.h), "graph_begin")
+
+    def graph_end(self):
+        check(load().fmskf_graph_end(self.h), "graph_end")
+
+    def graph_launch(self, times=1):
+        check(load().fmskf_graph_launch(self.h, int(times)), "graph_launch")
+
     # ------------------------------------------------------------------ native RCCL path
     def comm_init(self, unique_id: bytes, rank: int, world: int):
         """fmskf_comm_init: an RCCL communicator owned by this handle (one process per GPU)"""

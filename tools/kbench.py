@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ticks", type=int, default=300)
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     args = ap.parse_args()
     import numpy as np
@@ -56,6 +56,8 @@ def main():
         z[:, 1] = -torch.deg2rad(gz.double())
         preps = [e.prepare(z=z[r]) for r in range(R)]
         many = dict(z=z)
+    if args.op in ("pipeline", "pipeline_graph"):
+        return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
     tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op == "ensemble" else args.op))
@@ -101,6 +103,47 @@ def main():
                       "steps_per_s": n / (ms_tick * 1e-3),
                       "algo_GBps": BYTES[args.model] * n / (ms_tick * 1e-3) / 1e9, "finite": ok}),
           flush=True)
+
+
+def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
+    """The firmware ISR per tick -- estimator tick, wheel loops, 0x200 frames -- as three
+    launches, or replayed as one HIP graph (fmskf_graph_*); launch-bound at small N."""
+    import torch
+    st = torch.cuda.Stream()  # graph capture needs a real stream, not the null stream
+    torch.cuda.set_stream(st)
+    e.set_stream(st)
+    e.set_power(None)
+    vel = torch.zeros((3, n), device=dev)
+    vel[0] = 150.0
+    e.set_target_vel(vel, torch.full((3, n), 1000.0, device=dev), torch.full((3, n), 10000.0, device=dev))
+    dy, dg, dr = yaw[0].clone(), gz[0].clone(), rpm[0].clone()
+    fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+
+    def direct():
+        e.tick(yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+        e.control(dr)
+        e.can_tx(fr)
+    if args.op == "pipeline_graph":
+        e.graph_begin()
+        direct()
+        e.graph_end()
+        run = lambda: e.graph_launch(1)  # noqa: E731
+    else:
+        run = direct
+    for _ in range(20):
+        run()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(st)
+    for _ in range(args.ticks):
+        run()
+    ev1.record(st)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / args.ticks
+    ms = ev0.elapsed_time(ev1) / args.ticks
+    print(json.dumps({"model": args.model, "n": n, "op": args.op, "ms_per_tick": ms,
+                      "host_ms_per_tick": wall * 1e3, "robot_ticks_per_s": n / (ms * 1e-3)}), flush=True)
 
 
 def bench_io(args, e, n, R, dev, rpm, st):
