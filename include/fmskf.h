@@ -105,7 +105,8 @@ int fmskf_config_init(fmskf_config *cfg, uint32_t model, uint64_t n);
 int fmskf_create(const fmskf_config *cfg, fmskf_handle *out);
 int fmskf_destroy(fmskf_handle h);
 /* Zero-initialised state, as the firmware's static objects at boot
- * (VD_vehicle_controller.hpp:73-77), P = P0 for KF models. */
+ * (VD_vehicle_controller.hpp:73-77), P = P0 for KF models; the
+ * control state too (power off), keeping the control parameters. */
 int fmskf_reset(fmskf_handle h);
 int fmskf_set_stream(fmskf_handle h, void *hip_stream); /* hipStream_t; NULL = default */
 int fmskf_sync(fmskf_handle h);

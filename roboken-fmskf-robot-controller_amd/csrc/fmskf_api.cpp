@@ -347,6 +347,14 @@ void do_reset(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
+  if (h->ctrl_ready) {  // the control objects are static in the firmware too: zero, power off
+    const CtrlDev &c = h->ctrl;
+    hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, st), "reset ctrl");
+    hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, st), "reset ctrl");
+    hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, st), "reset ctrl");
+    hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, st), "reset ctrl");
+    hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, st), "reset ctrl");
+  }
   hip_check(hipMemsetAsync(s.counters, 0, 8 * 8, st), "reset counters");
 }
 

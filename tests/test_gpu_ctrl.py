@@ -183,3 +183,19 @@ def test_fleet_loop_cpp_host_program():
     x0 = float(lines[1].split("x=")[1].split()[0])
     assert 0.0 < x0 < 1.0          # driven forward for 0.2 s
     assert "imu.fault=0" in lines[2]
+
+
+def test_reset_zeroes_control_state():
+    n = 300
+    with Engine("rs", n) as e:
+        e.set_power(None)
+        vel = np.full((3, n), 100.0, np.float32)
+        e.set_target_vel(vel, np.full((3, n), 1000.0, np.float32), np.full((3, n), 10000.0, np.float32))
+        for _ in range(20):
+            e.control(np.full((n, 4), 50, np.int16))
+        assert np.abs(e.get_ctrl()["curr"]).max() > 0
+        e.reset()
+        g = e.get_ctrl()
+        assert not g["curr"].any() and not g["vel_tgt"].any() and not g["wheel_ctrl"].any()
+        e.control(np.full((n, 4), 50, np.int16))   # power is off after reset
+        assert not e.get_ctrl()["curr"].any()
