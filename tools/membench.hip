@@ -4,7 +4,7 @@
 // yaw/gyro planes and the [N][4] int16 rpm plane read = 232 B per instance) with no
 // arithmetic, at 1, 2 and 4 instances per lane (dword / dwordx2 / dwordx4 accesses),
 // plus a plain float4 copy of the same byte count.  Prints GB/s of algorithmic bytes.
-//   hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench && build/membench [log2N]
+//   hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench && build/membench [log2N] [0=zeros]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -136,9 +136,39 @@ __global__ __launch_bounds__(256) void k_pattern_delay(float *st, const float *y
   for (int k = 0; k < 27; k++) st[k * pitch + v] = s[k] + sink;
 }
 
+// the same with ONE dependent chain of ITERS FMAs (the KF update's shape: serial, low ILP)
+template <int ITERS>
+__global__ __launch_bounds__(256) void k_pattern_chain(float *st, const float *yaw, const float *gz,
+                                                       const uint2 *rpm, uint64_t n, uint64_t pitch,
+                                                       float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) s[k] = st[k * pitch + v];
+  const float a = yaw[v], b = gz[v] * (float)(rpm[v].x & 1);
+  float t = b;
+#pragma unroll
+  for (int it = 0; it < ITERS; it++) t = __builtin_fmaf(t, a, s[it % 27]);
+#pragma unroll
+  for (int k = 0; k < 27; k++) st[k * pitch + v] = s[k] + t * sink;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
+}
+
+// fill with nonzero pseudo-random floats in [1, 2): memory traffic of all-zero buffers is
+// measurably cheaper on MI355X (tools/mallbench.hip), so ceilings are measured on real-looking data
+__global__ void k_fill_rand(uint32_t *p, uint64_t words, uint32_t seed) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    p[i] = (x & 0x007FFFFFu) | 0x3F800000u;
+  }
 }
 
 int main(int argc, char **argv) {
@@ -159,6 +189,16 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&ca, bytes / 2));
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
+  const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (!zeros) {
+    k_fill_rand<<<4096, 256>>>((uint32_t *)st, 27 * (n + 4 * pad), 1);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)yaw, n, 2);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)gz, n, 3);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)rpm, 2 * n, 4);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ca, bytes / 8, 5);
+    CK(hipDeviceSynchronize());
+  }
+  printf("{\"data\": \"%s\"}\n", zeros ? "zeros" : "random");
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -206,6 +246,18 @@ int main(int argc, char **argv) {
   });
   timeit("pattern_delay_864fma", [&] {
     k_pattern_delay<32><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_chain_0", [&] {
+    k_pattern_chain<0><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_chain_200", [&] {
+    k_pattern_chain<200><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_chain_400", [&] {
+    k_pattern_chain<400><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
+  });
+  timeit("pattern_chain_800", [&] {
+    k_pattern_chain<800><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, n + 256, 0.f);
   });
   timeit("pattern_tiled64", [&] {
     k_pattern_tiled<64><<<(unsigned)((n + 255) / 256), 256>>>(st, yaw, gz, rpm, n, 0.f);
