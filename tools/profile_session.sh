@@ -31,3 +31,17 @@ for c in FETCH_SIZE WRITE_SIZE; do
     build/membench 20
 done
 echo "=== session done"
+# secondary rows: every tick model and the rows either side of the tick, one rocprofv3 kernel
+# trace each (PROF_ALL=1)
+if [ "${PROF_ALL:-0}" = 1 ]; then
+  for spec in "kf6_2p24:--model kf6 --n 16777216 --ticks 20" "ekf9:--model ekf9 --ticks 100" \
+              "ekf9_2p22:--model ekf9 --n 4194304 --ticks 30" "kf12d:--model kf12d --ticks 30" \
+              "rs:--model rs --ticks 200" "control:--op control --ticks 100" \
+              "wt901:--op wt901 --ticks 50" "can:--op can --ticks 100" "ensemble:--op ensemble --ticks 100" \
+              "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000"; do
+    name=${spec%%:*}; args=${spec#*:}
+    run prof_$name 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
+      python tools/kbench.py $args
+  done
+fi
+echo "=== session done (all)"
