@@ -192,6 +192,10 @@ int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
  * rank order -> deterministic.  `out` may be host or device per mem. */
 int fmskf_ensemble_record_len(fmskf_handle h, uint32_t *len);
 int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
+/* fmskf_tick, then this rank's record of the post-tick state (fmskf_ensemble_partial) in one
+ * call.  (A single fused kernel reducing x from registers was measured slower: each robot
+ * feeds 28 fp64 products through the block reduction, ~10x the bytes of re-reading x.) */
+int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out, uint32_t mem);
 /* host-side: records [n_records][len] -> mean [n], cov packed [n(n+1)/2] (unbiased) */
 int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
                            double *mean, double *cov_packed);

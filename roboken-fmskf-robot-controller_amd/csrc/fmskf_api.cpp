@@ -861,6 +861,25 @@ int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem) {
   });
 }
 
+int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!out) fail(FMSKF_EINVAL, "null out");
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    const uint32_t nx = h->d.nx;
+    const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
+    double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
+    run_tick(h, in, true, true, 1, h->s.n);
+    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, dst, h->stream),
+                 "ensemble launch");
+    if (mem == FMSKF_MEM_HOST) {
+      copy_out(h, out, h->ens_out, len * 8, mem);
+      finish_out(h, mem);
+    }
+  });
+}
+
 int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_records,
                            double *mean, double *cov_packed) {
   return guarded([&] {

@@ -115,6 +115,7 @@ SIGNATURES = {
     "fmskf_ensemble_record_len": (C.c_int, [_H, C.POINTER(C.c_uint32)]),
     "fmskf_ensemble_partial": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_ensemble_combine": (C.c_int, [C.c_uint32, _P, C.c_uint32, _P, _P]),
+    "fmskf_tick_ensemble": (C.c_int, [_H, C.POINTER(TickInputs), _P, C.c_uint32]),
     "fmskf_graph_begin": (C.c_int, [_H]),
     "fmskf_graph_end": (C.c_int, [_H]),
     "fmskf_graph_launch": (C.c_int, [_H, C.c_uint32]),

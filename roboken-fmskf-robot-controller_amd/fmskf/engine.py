@@ -392,6 +392,24 @@ class Engine:
               "ensemble_partial")
         return rec
 
+    def tick_ensemble(self, out=None, **kw):
+        """fmskf_tick_ensemble: one tick plus this rank's record of the post-tick state"""
+        ti, _keep = self._inputs(kw)
+        return self._tick_ens(C.byref(ti), out)
+
+    def tick_ensemble_prepared(self, prepared, out=None):
+        return self._tick_ens(prepared[2], out)
+
+    def _tick_ens(self, ti_ref, out):
+        if out is not None and _is_torch(out) and out.is_cuda:
+            check(load().fmskf_tick_ensemble(self.h, ti_ref, C.c_void_p(out.data_ptr()), MEM_DEVICE),
+                  "tick_ensemble")
+            return out
+        rec = np.empty(self.ensemble_record_len(), np.float64)
+        check(load().fmskf_tick_ensemble(self.h, ti_ref, rec.ctypes.data_as(C.c_void_p), MEM_HOST),
+              "tick_ensemble")
+        return rec
+
     # ------------------------------------------------------------------ diagnostics
     def eval_trig(self, x):
         x = np.ascontiguousarray(x, np.float32)

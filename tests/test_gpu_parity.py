@@ -440,3 +440,41 @@ def test_bad_inputs_rejected():
                    rpm=np.zeros((64, 4), np.int16))
         with pytest.raises(TypeError):
             e.tick(yaw=np.zeros(64, np.float32))
+
+
+# ----------------------------------------------------------------------------- fused ensemble
+@pytest.mark.parametrize("model,n", [("kf6", 100003), ("kf6", 1), ("kf6", 70000), ("ekf9", 3000)])
+def test_tick_ensemble_fused(orc, model, n):
+    """fmskf_tick_ensemble = fmskf_tick + the record of the post-tick state: state bit-exact
+    vs a plain tick, record vs the oracle's two-pass moments of that state, and bitwise
+    reproducible."""
+    T = 6
+    tr = Trajectory(n, T, seed=88)
+    if model == "kf6":
+        yaw, gz, rpm = tr.kf6_inputs()
+        kw = lambda t: dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])  # noqa: E731
+    else:
+        raw = tr.ekf9_raw()
+        kw = lambda t: dict(raw=raw[t])  # noqa: E731
+    with Engine(model, n) as a, Engine(model, n) as b, Engine(model, n) as c:
+        for t in range(T - 1):
+            for e in (a, b, c):
+                e.tick(**kw(t))
+        a.tick(**kw(T - 1))
+        rb = b.tick_ensemble(**kw(T - 1))
+        rc = c.tick_ensemble(**kw(T - 1))
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        rp = b.ensemble_partial()
+    bits_equal(xa, xb, "x")
+    bits_equal(Pa, Pb, "P")
+    bits_equal(rb, rc, "deterministic")
+    assert rb[0] == n
+    mo, co = orc.ens_finalize(xb.shape[0], orc.ens_partial(xb))
+    mf, cf = fmskf.ensemble_combine(xb.shape[0], rb[None, :])
+    np.testing.assert_allclose(mf, mo, rtol=1e-12, atol=1e-12)
+    if n > 1:
+        np.testing.assert_allclose(cf, co, rtol=1e-9, atol=1e-15)
+    # same statistics as the stand-alone partial record of the same state
+    mp, cp = fmskf.ensemble_combine(xb.shape[0], rp[None, :])
+    np.testing.assert_allclose(mf, mp, rtol=1e-12, atol=1e-12)
