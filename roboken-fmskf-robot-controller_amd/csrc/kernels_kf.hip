@@ -103,21 +103,20 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 template <bool LIBM, bool UPD, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
-  __shared__ float stab[LIBM ? 1 : 513];
+  __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
+  float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
+  WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
-  if (!LIBM) {
-    for (int k = threadIdx.x; k < 513; k += kBlock) stab[k] = a.in.sintab[k];
-    __syncthreads();
-  }
+  tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED>(a, ic, have, stab, x, P);
   if (live) {
 #pragma unroll

@@ -209,6 +209,30 @@ __device__ __forceinline__ void nan_guard(const T (&x)[N], const T (&P)[NP],
     atomicAdd(counters, (unsigned long long)__popcll(m));
 }
 
+// Per-wave copy of the 513-entry table: the constructor issues the lane's 9 loads, store()
+// writes them to the wave's LDS slice (waits only on those loads, the oldest in flight)
+constexpr int kWaveTab = 520;
+template <bool LIBM>
+struct WaveTable {
+  float v[LIBM ? 1 : 9];
+  __device__ __forceinline__ explicit WaveTable(const float *g) {
+    if constexpr (!LIBM) {
+      const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+      for (int k = 0; k < 9; k++) v[k] = (lane + 64 * k) < 513 ? g[lane + 64 * k] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float *stab) const {
+    if constexpr (!LIBM) {
+      const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+      for (int k = 0; k < 9; k++)
+        if (lane + 64 * k < 513) stab[lane + 64 * k] = v[k];
+      __builtin_amdgcn_wave_barrier();  // same-wave LDS ops retire in order
+    }
+  }
+};
+
 static inline dim3 grid_for(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
 }  // namespace fmskf

@@ -50,6 +50,7 @@ __global__ __launch_bounds__(256) void k_pat(float *st, const float *yaw, const 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void *base, uint64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)(uint32_t)bytes, 0x00020000);
 }
+// MODE 4: the three input streams interleaved into one 16-byte record per robot
 template <int MODE>
 __global__ __launch_bounds__(256) void k_pat2(float *st, const float *yaw, const float *gz,
                                               const uint2 *rpm, const float *tab, uint64_t n,
@@ -62,7 +63,11 @@ __global__ __launch_bounds__(256) void k_pat2(float *st, const float *yaw, const
 #pragma unroll
   for (int k = 0; k < 27; k++) s[k] = st[k * pitch + vc];
   float m = sink;
-  if constexpr (MODE == 1) {
+  if constexpr (MODE == 4) {
+    const uint32_t i = (uint32_t)vc;
+    const auto r = __builtin_amdgcn_raw_buffer_load_b128(mk_rsrc(yaw, n * 16), i * 16u, 0, 2);
+    m = m * __builtin_bit_cast(float, r[0]) * __builtin_bit_cast(float, r[1]) * (float)(r[2] & 1);
+  } else if constexpr (MODE == 1) {
     m = m * yaw[vc] * gz[vc] * (float)(rpm[vc].x & 1);
   } else if constexpr (MODE >= 2) {
     const uint32_t i = (uint32_t)vc;
@@ -107,7 +112,7 @@ int main(int argc, char **argv) {
     const int R = argc > 2 ? atoi(argv[2]) : 64;
     float *yaw, *gz, *tab;
     uint2 *rpm;
-    CK(hipMalloc(&yaw, R * n * 4));
+    CK(hipMalloc(&yaw, R * n * 16));
     CK(hipMalloc(&gz, R * n * 4));
     CK(hipMalloc(&rpm, R * n * 8));
     CK(hipMalloc(&tab, 513 * 4));
@@ -116,14 +121,15 @@ int main(int argc, char **argv) {
     CK(hipMemset(rpm, 0, R * n * 8));
     CK(hipMemset(tab, 0, 513 * 4));
     if (argc > 4) {  // random (nonzero) contents for inputs and state
-      k_fill_rand<<<4096, 256>>>((uint32_t *)yaw, R * n, 1);
+      k_fill_rand<<<4096, 256>>>((uint32_t *)yaw, R * n * 4, 1);
       k_fill_rand<<<4096, 256>>>((uint32_t *)gz, R * n, 2);
       k_fill_rand<<<4096, 256>>>((uint32_t *)rpm, R * n * 2, 3);
       k_fill_rand<<<4096, 256>>>((uint32_t *)st, 27 * pitch, 4);
       CK(hipDeviceSynchronize());
     }
-    const char *names[] = {"no_inputs", "inputs_global", "inputs_buffer_nt", "inputs_buffer_nt+lds_table"};
-    for (int mode = 0; mode < 4; mode++) {
+    const char *names[] = {"no_inputs", "inputs_global", "inputs_buffer_nt", "inputs_buffer_nt+lds_table",
+                           "inputs_packed16_nt"};
+    for (int mode = 0; mode < 5; mode++) {
       auto launch = [&](int it) {
         const uint64_t o = (uint64_t)(it % R) * n;
         const dim3 g((unsigned)((n + 255) / 256));
@@ -131,6 +137,7 @@ int main(int argc, char **argv) {
         if (mode == 1) k_pat2<1><<<g, 256>>>(st, yaw + o, gz + o, rpm + o, tab, n, pitch, 0.f);
         if (mode == 2) k_pat2<2><<<g, 256>>>(st, yaw + o, gz + o, rpm + o, tab, n, pitch, 0.f);
         if (mode == 3) k_pat2<3><<<g, 256>>>(st, yaw + o, gz + o, rpm + o, tab, n, pitch, 0.f);
+        if (mode == 4) k_pat2<4><<<g, 256>>>(st, yaw + 4 * o, gz + o, rpm + o, tab, n, pitch, 0.f);
       };
       for (int w = 0; w < 2 * R; w++) launch(w);
       CK(hipDeviceSynchronize());
