@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
     ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
+    ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
+                    help="KF6 tick with host-resident inputs staged over PCIe per call")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -56,6 +58,8 @@ def main():
         z[:, 1] = -torch.deg2rad(gz.double())
         preps = [e.prepare(z=z[r]) for r in range(R)]
         many = dict(z=z)
+    if args.host:
+        return bench_host(args, e, n, yaw, gz, rpm)
     if args.op in ("pipeline", "pipeline_graph"):
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
@@ -103,6 +107,26 @@ def main():
                       "steps_per_s": n / (ms_tick * 1e-3),
                       "algo_GBps": BYTES[args.model] * n / (ms_tick * 1e-3) / 1e9, "finite": ok}),
           flush=True)
+
+
+def bench_host(args, e, n, yaw, gz, rpm):
+    """PCIe-inclusive rate: every tick's 16 B/robot of inputs start in host memory."""
+    import torch
+    R = yaw.shape[0]
+    pin = args.host == "pinned"
+    hy, hg, hr = (t.cpu().pin_memory() if pin else t.cpu() for t in (yaw, gz, rpm))
+    hy, hg, hr = (t.numpy() for t in (hy, hg, hr))
+    for k in range(5):
+        e.tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.ticks):
+        e.tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.ticks
+    print(json.dumps({"model": args.model, "n": n, "op": "tick", "host_inputs": args.host,
+                      "ms_per_tick": dt * 1e3, "steps_per_s": n / dt,
+                      "pcie_GBps": 16 * n / dt / 1e9}), flush=True)
 
 
 def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
