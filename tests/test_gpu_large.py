@@ -74,3 +74,68 @@ def test_control_past_the_buffer_window(orc):
 
 def fmskf_pitch(n):
     return ((n + 511) // 512) * 512 + 256
+
+
+def test_ekf9_2p20_sampled_with_mask(orc):
+    """cfg 3's model at 2^20 robots with a random validity mask: a sample bit for bit."""
+    from fmskf.synth import Trajectory
+    n, T = 1 << 20, 4
+    tr = Trajectory(n, T, seed=12)
+    raw = tr.ekf9_raw()
+    valid = (np.random.default_rng(5).random((T, n)) > 0.2).astype(np.uint8)
+    with Engine("ekf9", n) as e:
+        for t in range(T):
+            e.tick(raw=raw[t], valid=valid[t])
+        x, P = e.get_state()
+    idx = _sample(n, seed=2)
+    cfg = fmskf.default_config("ekf9", idx.size)
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((9, idx.size), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], idx.size, 1).copy()
+    for t in range(T):
+        orc.ekf9_tick(xo, Po, np.ascontiguousarray(raw[t][idx]), np.ascontiguousarray(valid[t][idx]),
+                      prm, nthreads=0)
+    np.testing.assert_array_equal(x[:, idx].view(np.uint32), xo.view(np.uint32))
+    np.testing.assert_array_equal(P[:, idx].view(np.uint32), Po.view(np.uint32))
+
+
+def test_rs_2p20_sampled(orc):
+    from fmskf.synth import Trajectory
+    n, T = 1 << 20, 5
+    tr = Trajectory(n, T, seed=13)
+    yaw, sums, rpm = tr.rs_inputs()
+    with Engine("rs", n) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t])
+        pose = e.get_pose()
+        prev = e.get_prev_sum()
+    idx = _sample(n, seed=3)
+    pos = np.zeros((3, idx.size), np.float32)
+    vel = np.zeros((3, idx.size), np.float32)
+    pv = np.zeros((4, idx.size), np.int64)
+    for t in range(T):
+        orc.rs_tick(pos, vel, pv, np.ascontiguousarray(yaw[t][idx]),
+                    np.ascontiguousarray(sums[t][:, idx]), np.ascontiguousarray(rpm[t][idx]))
+    np.testing.assert_array_equal(np.stack(pose)[:, idx].view(np.uint32), pos.view(np.uint32))
+    np.testing.assert_array_equal(prev[:, idx], pv)
+
+
+def test_kf12d_2p18_sampled(orc):
+    from fmskf.synth import Trajectory
+    n, T = 1 << 18, 4
+    tr = Trajectory(n, T, seed=14)
+    z = tr.kf12d_z()
+    with Engine("kf12d", n) as e:
+        for t in range(T):
+            e.tick(z=z[t])
+        x, P = e.get_state()
+    idx = _sample(n, seed=4)
+    cfg = fmskf.default_config("kf12d", idx.size)
+    prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), np.array(cfg.r[:36]))
+    xo = np.zeros((12, idx.size))
+    Po = np.repeat(np.array(cfg.p0[:78])[:, None], idx.size, 1).copy()
+    for t in range(T):
+        orc.kf12d_tick(xo, Po, np.ascontiguousarray(z[t][:, idx]), None, prm, nthreads=0)
+    scale = np.maximum(np.abs(xo).max(axis=1, keepdims=True), 1e-3)
+    assert (np.abs(x[:, idx] - xo) / scale).max() <= 1e-12
+    assert (np.abs(P[:, idx] - Po) / max(np.abs(Po).max(), 1e-3)).max() <= 1e-12
