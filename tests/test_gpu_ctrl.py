@@ -5,7 +5,6 @@ Bar: bit-exact (float results compared as bit patterns, integers exactly)."""
 import numpy as np
 import pytest
 
-import fmskf
 from fmskf import Engine
 from fmskf.synth import Trajectory
 
