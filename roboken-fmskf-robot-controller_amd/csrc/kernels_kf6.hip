@@ -165,7 +165,9 @@ __device__ __forceinline__ void stage_table(float *stab, const float *g) {
 static_assert(2 * kBlock + 1 == 513, "table staging assumes 256-thread blocks");
 
 
-// one instance per lane, grid = ceil(N / 256)
+// tick_many: T ticks per launch, state in VGPRs throughout; the inputs of the next tick are
+// loaded while the current one computes.  Unrolled by two with ping-pong input registers
+// (ma / mb) so no input record is copied around the loop; clamped index, no live branch.
 template <int WPE, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6(
     KfArgs<MdKF6, Kf6Params> a) {
@@ -173,22 +175,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   const uint64_t n = a.n;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
+  const uint32_t ic = live ? i : (uint32_t)n - 1u;
+  const uint32_t T = a.in.n_ticks;
   float x[6], P[21];
-  Kf6In m;
-  if (live) {
-    kf6_load_state<O>(a.x, a.P, a.pitch, i, x, P);
-    if (O::UPD) m = kf6_load_in<O>(a.in, n, 0, i);
-  }
+  Kf6In ma, mb;
+  kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
+  if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, ic);
   stage_table<O::LIBM>(stab, a.in.sintab);
-  if (!live) return;
-  for (uint32_t t = 0; t < a.in.n_ticks; t++) {
-    Kf6In mn;
-    if (O::UPD && t + 1 < a.in.n_ticks) mn = kf6_load_in<O>(a.in, n, t + 1, i);
-    kf6_tick1<O>(m, stab, a.prm, x, P);
-    m = mn;
+  for (uint32_t t = 0; t < T; t += 2) {
+    if (O::UPD && t + 1 < T) mb = kf6_load_in<O>(a.in, n, t + 1, ic);
+    kf6_tick1<O>(ma, stab, a.prm, x, P);
+    if (t + 1 >= T) break;
+    if (O::UPD && t + 2 < T) ma = kf6_load_in<O>(a.in, n, t + 2, ic);
+    kf6_tick1<O>(mb, stab, a.prm, x, P);
   }
-  kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
-  nan_guard(x, P, a.counters);
+  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  nan_guard(x, P, a.counters, live);
 }
 
 // Single tick, straight line: no tick loop (so no loop-carried register copies) and no

@@ -16,7 +16,7 @@ args = [a for a in sys.argv[2:] if not a.startswith("--")]
 flt = args[0] if args else ""
 dump = "--dump" in sys.argv
 asm = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                      "-ffp-contract=off", "-x", "hip", "--cuda-device-only", "-S", src, "-o", "-"],
+                      "-ffp-contract=off", "-fno-slp-vectorize", "-x", "hip", "--cuda-device-only", "-S", src, "-o", "-"],
                      capture_output=True, text=True, check=True).stdout
 
 funcs = {}
