@@ -14,9 +14,7 @@
 namespace fmskf {
 
 // EKF9 z from raw WT901 registers (imu_if_wt901c.cpp:96-99,107-113) + wheel rpm
-__device__ __forceinline__ void ekf9_innov(const TickIn &in, uint64_t j, const float (&x)[9],
-                                           float (&y)[6]) {
-  const uint4 w = reinterpret_cast<const uint4 *>(in.raw)[j];
+__device__ __forceinline__ void ekf9_innov(const uint4 w, const float (&x)[9], float (&y)[6]) {
   int16_t a[4], r[4];
   unpack4(make_uint2(w.x, w.y), a);
   unpack4(make_uint2(w.z, w.w), r);
@@ -39,13 +37,13 @@ __device__ __forceinline__ void ekf9_innov(const TickIn &in, uint64_t j, const f
 
 // one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
 template <bool LIBM, bool UPD, bool PRED>
-__device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, uint64_t j,
+__device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, const uint4 raw,
                                            bool have, const float *stab, float (&x)[9],
                                            float (&P)[45]) {
   const float dt = a.prm.dt;
   if (UPD && have) {
     float y[6];
-    ekf9_innov(a.in, j, x, y);
+    ekf9_innov(raw, x, y);
     kf_update<MdEKF9>(x, P, y, a.prm.r);
   }
   if (PRED) {
@@ -71,6 +69,8 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
   }
 }
 
+// tick_many: T ticks per launch, state in VGPRs; the next tick's raw record (16 B) and validity
+// byte are loaded while the current tick computes (ping-pong registers, loop unrolled by two)
 template <bool LIBM, bool UPD, bool PRED>
 __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
@@ -81,21 +81,43 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   }
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+  const bool live = i < n;
+  const uint64_t ic = live ? i : n - 1;
+  const uint32_t T = a.in.n_ticks;
+  const uint64_t st = a.in.stride;
+  auto raw_at = [&](uint32_t t) -> uint4 {
+    return UPD ? reinterpret_cast<const uint4 *>(a.in.raw)[(uint64_t)t * st + ic] : make_uint4(0, 0, 0, 0);
+  };
+  auto have_at = [&](uint32_t t) -> bool {
+    return a.in.valid == nullptr || a.in.valid[(uint64_t)t * st + ic];
+  };
   float x[N], P[NP];
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + i];
+  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + i];
-  for (uint32_t t = 0; t < a.in.n_ticks; t++) {
-    const uint64_t j = (uint64_t)t * a.in.stride + i;
-    ekf9_tick1<LIBM, UPD, PRED>(a, j, a.in.valid == nullptr || a.in.valid[j], stab, x, P);
+  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+  uint4 ra = raw_at(0), rb;
+  bool ha = have_at(0), hb;
+  for (uint32_t t = 0; t < T; t += 2) {
+    if (t + 1 < T) {
+      rb = raw_at(t + 1);
+      hb = have_at(t + 1);
+    }
+    ekf9_tick1<LIBM, UPD, PRED>(a, ra, ha, stab, x, P);
+    if (t + 1 >= T) break;
+    if (t + 2 < T) {
+      ra = raw_at(t + 2);
+      ha = have_at(t + 2);
+    }
+    ekf9_tick1<LIBM, UPD, PRED>(a, rb, hb, stab, x, P);
   }
+  if (live) {
 #pragma unroll
-  for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+    for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
 #pragma unroll
-  for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
-  nan_guard(x, P, a.counters);
+    for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+  }
+  nan_guard(x, P, a.counters, live);
 }
 
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
@@ -116,8 +138,9 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
+  const uint4 raw = UPD ? reinterpret_cast<const uint4 *>(a.in.raw)[ic] : make_uint4(0, 0, 0, 0);
   tv.store(stab);
-  ekf9_tick1<LIBM, UPD, PRED>(a, ic, have, stab, x, P);
+  ekf9_tick1<LIBM, UPD, PRED>(a, raw, have, stab, x, P);
   if (live) {
 #pragma unroll
     for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
