@@ -124,22 +124,33 @@ def main():
     rec_len = eng.ensemble_record_len()
     rec = torch.empty(rec_len, dtype=torch.float64, device=dev)
     n_events = max(1, (args.steps + args.warmup) // max(1, args.ensemble_every) + 1)
+    # one record and one gather slot per ensemble event: the all-gather runs asynchronously
+    # on RCCL's stream (ordered after the record by RCCL's stream dependency) while the next
+    # ticks proceed; pending gathers are joined before the timed region closes
+    recs = torch.zeros(n_events, rec_len, dtype=torch.float64, device=dev)
     gathered = torch.zeros(n_events, world, rec_len, dtype=torch.float64, device=dev)
     ev_count = [0]
+    pending = []
 
     def step(k):
         eng.tick_prepared(prepared[k % R], tick_fn)
         if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
-            eng.ensemble_partial(rec)
-            slot = gathered[ev_count[0] % n_events]
+            e = ev_count[0] % n_events
+            eng.ensemble_partial(recs[e])
             if distributed:
-                dist.all_gather_into_tensor(slot.view(-1), rec)
+                pending.append(dist.all_gather_into_tensor(gathered[e].view(-1), recs[e],
+                                                           async_op=True))
             else:
-                slot[0].copy_(rec)
+                gathered[e][0].copy_(recs[e])
             ev_count[0] += 1
+
+    def join():
+        while pending:
+            pending.pop().wait()  # the current stream waits for the collective
 
     for k in range(args.warmup):
         step(k)
+    join()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -150,6 +161,7 @@ def main():
     ev0.record(stream)
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
+    join()
     ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
