@@ -59,9 +59,43 @@ struct Wt901Args {
 struct Wt901Parser {
   uint64_t lo, hi;
   uint32_t cnt, flags;
-  __device__ __forceinline__ void byte(uint32_t bv, const Wt901Args &a, uint64_t i) {
+  // CopeWitData on a validated 11-byte window (bytes 0-7 in w0, 8-10 in w1)
+  __device__ __forceinline__ void dispatch(uint64_t w0, uint64_t w1, const Wt901Args &a, uint64_t i) {
     const uint64_t n = a.n;
     int16_t *reg = a.reg;
+    const uint64_t lo = w0, hi = w1;
+    // CopeWitData(type, usData, 4), wit_c_sdk.c:90-130
+    const uint32_t type = (uint32_t)(lo >> 8) & 0xFFu;
+    const uint32_t d[4] = {(uint32_t)(lo >> 16) & 0xFFFFu, (uint32_t)(lo >> 32) & 0xFFFFu,
+                           (uint32_t)(lo >> 48) & 0xFFFFu, (uint32_t)hi & 0xFFFFu};
+    uint32_t reg1 = 0, len1 = 4, reg2 = 0, len2 = 0;
+    bool known = true;
+    switch (type) {
+      case 0x51: reg1 = R_AX; len1 = 3; reg2 = R_TEMP; len2 = 1; break;
+      case 0x53: reg1 = R_ROLL; len1 = 3; reg2 = R_VERSION; len2 = 1; break;
+      case 0x50: reg1 = R_YYMM; break;
+      case 0x52: reg1 = R_GX; len1 = 3; break;
+      case 0x54: reg1 = R_HX; len1 = 3; break;
+      case 0x55: reg1 = R_D0STATUS; break;
+      case 0x56: reg1 = R_PRESSUREL; break;
+      case 0x57: reg1 = R_LONL; break;
+      case 0x58: reg1 = R_GPSHEIGHT; break;
+      case 0x59: reg1 = R_Q0; break;
+      case 0x5A: reg1 = R_SVNUM; break;
+      case 0x5F: reg1 = a.read_reg_index; break;
+      default: known = false; break;
+    }
+    if (known) {
+      for (uint32_t k = 0; k < len1; k++) reg[(reg1 + k) * n + i] = (int16_t)d[k];
+      flags |= flags_of(reg1, len1);
+      if (len2) {
+        reg[reg2 * n + i] = (int16_t)d[3];
+        flags |= flags_of(reg2, 1);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void byte(uint32_t bv, const Wt901Args &a, uint64_t i) {
     const uint64_t byte = bv;
     // s_ucWitDataBuff[s_uiWitDataCnt++] = ucData  (bytes >= cnt are kept zero)
     if (cnt < 8) lo |= byte << (8 * cnt);
@@ -76,35 +110,7 @@ struct Wt901Parser {
       sum += (uint32_t)(hi >> 8) & 0xFFu;
       drop = (sum & 0xFFu) != ((uint32_t)(hi >> 16) & 0xFFu);  // __CaliSum, :150-156
       if (!drop) {
-        // CopeWitData(type, usData, 4), wit_c_sdk.c:90-130
-        const uint32_t type = (uint32_t)(lo >> 8) & 0xFFu;
-        const uint32_t d[4] = {(uint32_t)(lo >> 16) & 0xFFFFu, (uint32_t)(lo >> 32) & 0xFFFFu,
-                               (uint32_t)(lo >> 48) & 0xFFFFu, (uint32_t)hi & 0xFFFFu};
-        uint32_t reg1 = 0, len1 = 4, reg2 = 0, len2 = 0;
-        bool known = true;
-        switch (type) {
-          case 0x51: reg1 = R_AX; len1 = 3; reg2 = R_TEMP; len2 = 1; break;
-          case 0x53: reg1 = R_ROLL; len1 = 3; reg2 = R_VERSION; len2 = 1; break;
-          case 0x50: reg1 = R_YYMM; break;
-          case 0x52: reg1 = R_GX; len1 = 3; break;
-          case 0x54: reg1 = R_HX; len1 = 3; break;
-          case 0x55: reg1 = R_D0STATUS; break;
-          case 0x56: reg1 = R_PRESSUREL; break;
-          case 0x57: reg1 = R_LONL; break;
-          case 0x58: reg1 = R_GPSHEIGHT; break;
-          case 0x59: reg1 = R_Q0; break;
-          case 0x5A: reg1 = R_SVNUM; break;
-          case 0x5F: reg1 = a.read_reg_index; break;
-          default: known = false; break;
-        }
-        if (known) {
-          for (uint32_t k = 0; k < len1; k++) reg[(reg1 + k) * n + i] = (int16_t)d[k];
-          flags |= flags_of(reg1, len1);
-          if (len2) {
-            reg[reg2 * n + i] = (int16_t)d[3];
-            flags |= flags_of(reg2, 1);
-          }
-        }
+        dispatch(lo, hi, a, i);
         cnt = 0;
         lo = 0;
         hi = 0;
@@ -141,6 +147,42 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
 #pragma unroll
     for (int c = 0; c < 4; c++)
       ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
+    // Whole-frame fast path.  With an empty parser window and a poll made of complete frames
+    // (0x55 header and a valid checksum every 11 bytes), the byte-serial parser accepts frame
+    // k at bytes 11k..11k+10 and never resyncs: dispatch the frames directly (static byte
+    // offsets -> register selects).  Anything else takes the byte-serial path from the start.
+    const uint32_t nfr = len / 11;
+    bool fast = ps.cnt == 0 && len == nfr * 11 && len <= 55;
+    uint64_t w0[5], w1[5];
+#pragma unroll
+    for (int f = 0; f < 5; f++) {
+      uint32_t b[11];
+#pragma unroll
+      for (int k = 0; k < 11; k++) {
+        const int o = f * 11 + k;  // compile-time byte offset
+        if (o < 64) {
+          const uint4 c = ch[o / 16];
+          const uint32_t w = (o % 16) / 4 == 0 ? c.x : (o % 16) / 4 == 1 ? c.y : (o % 16) / 4 == 2 ? c.z : c.w;
+          b[k] = (w >> (8 * (o % 4))) & 0xFFu;
+        } else {
+          b[k] = 0;
+        }
+      }
+      uint32_t sum = 0;
+#pragma unroll
+      for (int k = 0; k < 10; k++) sum += b[k];
+      const bool ok = b[0] == 0x55u && (sum & 0xFFu) == b[10];
+      if ((uint32_t)f < nfr) fast = fast && ok;
+      w0[f] = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) w0[f] |= (uint64_t)b[k] << (8 * k);
+      w1[f] = (uint64_t)b[8] | ((uint64_t)b[9] << 8) | ((uint64_t)b[10] << 16);
+    }
+    if (fast) {
+#pragma unroll
+      for (int f = 0; f < 5; f++)
+        if ((uint32_t)f < nfr) ps.dispatch(w0[f], w1[f], a, i);
+    } else {
     // one parser body: the next chunk's bytes are consumed from the bottom of a 128-bit
     // shift register
 #pragma unroll 1
@@ -158,6 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
         cur.z = (cur.z >> 8) | (cur.w << 24);
         cur.w >>= 8;
       }
+    }
     }
   } else {
     for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);

@@ -296,18 +296,28 @@ def test_wt901_ingest_matches_reference_golden(orc, golden_wt901):
                     bits_equal(data[:, i], orcs[i].data, f"data {s[1]} poll {k}")
 
 
-def test_wt901_ingest_random_streams(orc):
-    n, polls, stride = 3000, 6, 96
-    rng = np.random.default_rng(99)
+@pytest.mark.parametrize("stride", [48, 64, 96])
+def test_wt901_ingest_random_streams(orc, stride):
+    """Mixed clean / noisy / damaged / short-frame polls.  Strides 48 and 64 take the
+    vector-row kernel (and its whole-frame fast path for clean polls with an empty window),
+    96 the byte-load kernel."""
+    n, polls = 3000, 6
+    rng = np.random.default_rng(99 + stride)
     orcs = [orc.Wt901(0x51) for _ in range(n)]
     with Engine("kf6", n) as e:
         for k in range(polls):
             buf = np.zeros((n, stride), np.uint8)
             lens = rng.integers(0, stride + 1, n).astype(np.uint32)
             for i in range(n):
-                kind = rng.integers(0, 3)
+                kind = rng.integers(0, 4)
                 if kind == 0:  # clean poll
                     b = b"".join(wt901_frame(t, rng.integers(0, 65536, 4)) for t in (0x51, 0x52, 0x53, 0x59))
+                    b = np.frombuffer(b, np.uint8)
+                elif kind == 3:  # 0-5 whole frames of any type, or a torn tail
+                    ts = rng.choice([0x50, 0x51, 0x52, 0x53, 0x54, 0x59, 0x5A, 0x5F, 0x61], int(rng.integers(0, 6)))
+                    b = b"".join(wt901_frame(int(t), rng.integers(0, 65536, 4)) for t in ts)
+                    if rng.random() < 0.3:
+                        b = b[:int(rng.integers(0, len(b) + 1))]
                     b = np.frombuffer(b, np.uint8)
                 elif kind == 1:  # noisy
                     b = rng.integers(0, 256, int(lens[i]), dtype=np.uint8)
