@@ -598,6 +598,68 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
 static const int k_kf12_h1[8] = {2, 5, 3, 4, 6, 7, 8, 11};
 static const int k_kf12_h2[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
 
+/* R = C C^T (C lower with a positive diagonal) and Cinv = C^-1, both packed lower.  Returns 0
+ * when R is not positive definite.  Operation order is part of the canonical KF12D update:
+ * the library computes the same matrix with the same operations on the host. */
+int orc_kf12d_cinv(const double *r, double *ci) {
+  double c[8][8], v[8][8];
+  memset(c, 0, sizeof(c));
+  memset(v, 0, sizeof(v));
+  for (int j = 0; j < 8; j++) {
+    double s = r[orc_pk(j, j)];
+    for (int k = 0; k < j; k++) s = s - c[j][k] * c[j][k];
+    if (!(s > 0.0) || !isfinite(s)) return 0;
+    c[j][j] = sqrt(s);
+    for (int i = j + 1; i < 8; i++) {
+      double t = r[orc_pk(i, j)];
+      for (int k = 0; k < j; k++) t = t - c[i][k] * c[j][k];
+      c[i][j] = t / c[j][j];
+    }
+  }
+  for (int j = 0; j < 8; j++) {
+    v[j][j] = 1.0 / c[j][j];
+    for (int i = j + 1; i < 8; i++) {
+      double t = 0.0;
+      for (int k = j; k < i; k++) t = t + c[i][k] * v[k][j];
+      v[i][j] = -t / c[i][i];
+    }
+  }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j <= i; j++) ci[orc_pk(i, j)] = v[i][j];
+  return 1;
+}
+
+/* Canonical KF12D update when R is positive definite: the 8 measurements decorrelated by
+ * Cinv (z~ = Cinv z, H~ = Cinv H, unit noise) and applied one scalar at a time (sequential
+ * processing, Bierman 1977).  y holds the innovations of the current state: after each
+ * scalar update the correction is subtracted from it.  blk: R has no base/tip cross terms,
+ * so the tip rows of Cinv start at column 4 (the skipped products are exact zeros). */
+static void orc_kf12d_decor_update(double *xs, double *Ps, double *y, const double *ci, int blk) {
+  for (int a = 0; a < 8; a++) {
+    const int b0 = (blk && a >= 4) ? 4 : 0;
+    const double *c = ci + a * (a + 1) / 2;
+    double hp[12];
+    for (int j = 0; j < 12; j++) {
+      double s = c[b0] * Ps[orc_pk(k_kf12_h1[b0], j)];
+      for (int b = b0 + 1; b <= a; b++) s = fma(c[b], Ps[orc_pk(k_kf12_h1[b], j)], s);
+      hp[j] = s;
+    }
+    double s = c[b0] * hp[k_kf12_h1[b0]];
+    for (int b = b0 + 1; b <= a; b++) s = fma(c[b], hp[k_kf12_h1[b]], s);
+    s = s + 1.0;
+    double nu = c[b0] * y[b0];
+    for (int b = b0 + 1; b <= a; b++) nu = fma(c[b], y[b], nu);
+    const double si = 1.0 / s;
+    const double g = nu * si;
+    for (int j = 0; j < 12; j++) xs[j] = fma(hp[j], g, xs[j]);
+    for (int b = 0; b < 8; b++) y[b] = fma(-hp[k_kf12_h1[b]], g, y[b]);
+    for (int i = 0; i < 12; i++) {
+      const double t = hp[i] * si;
+      for (int j = 0; j <= i; j++) Ps[orc_pk(i, j)] = fma(-t, hp[j], Ps[orc_pk(i, j)]);
+    }
+  }
+}
+
 void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8_t *valid,
                     const orc_kf12d_params *prm, int do_update, int do_predict, int nthreads) {
   double F[ORC_NMAX][ORC_NMAX];
@@ -609,12 +671,16 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
     F[pos[a]][pos[a] + 3] = prm->dt;
     pat[pos[a]][pos[a] + 3] = 1;
   }
-  /* R without base/tip cross terms: the joint update is the base-group update followed by
-   * the tip-group update (innovation taken from the updated state); canonical order then */
+  /* R positive definite: decorrelated scalar-sequential update.  Otherwise (R only positive
+   * semi-definite or indefinite, S still invertible): without base/tip cross terms the joint
+   * update is the base-group update followed by the tip-group update (innovation taken from
+   * the updated state), else the joint 8-measurement update; LDL^T form for both */
   int seq = 1;
   for (int a = 4; a < 8; a++)
     for (int b = 0; b < 4; b++)
       if (prm->r[a * (a + 1) / 2 + b] != 0.0) seq = 0;
+  double ci[36];
+  const int decor = orc_kf12d_cinv(prm->r, ci);
   double r1[10], r2[10];
   for (int a = 0; a < 4; a++)
     for (int b = 0; b <= a; b++) {
@@ -632,7 +698,11 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
     for (int k = 0; k < 78; k++) Ps[k] = P[k * n + i];
     if (do_update && (!valid || valid[i])) {
       double y[8];
-      if (seq) {
+      if (decor) {
+        for (int a = 0; a < 8; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
+        y[0] = orc_wrap_innov_d(y[0]);
+        orc_kf12d_decor_update(xs, Ps, y, ci, seq);
+      } else if (seq) {
         for (int a = 0; a < 4; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
         y[0] = orc_wrap_innov_d(y[0]);
         orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1, k_kf12_h2, y, r1);

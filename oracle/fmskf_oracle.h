@@ -135,6 +135,8 @@ typedef struct {
   double q[78];
   double r[36];
 } orc_kf12d_params;
+/* Cinv of R = C C^T (packed lower); 0 when R is not positive definite */
+int orc_kf12d_cinv(const double *r /*[36]*/, double *ci /*[36]*/);
 /* x [12][n], P [78][n], z [8][n] */
 void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8_t *valid,
                     const orc_kf12d_params *prm, int do_update, int do_predict, int nthreads);

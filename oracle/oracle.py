@@ -154,6 +154,8 @@ def lib():
         L.orc_ekf9_measure.argtypes = [C.c_size_t, _i16p, _f32p]
         L.orc_kf12d_tick.argtypes = [C.c_size_t, _f64p, _f64p, _vp, _vp,
                                      C.POINTER(Kf12dParams), C.c_int, C.c_int, C.c_int]
+        L.orc_kf12d_cinv.restype = C.c_int
+        L.orc_kf12d_cinv.argtypes = [_f64p, _f64p]
         L.orc_ens_record_len.restype = C.c_size_t
         L.orc_ens_record_len.argtypes = [C.c_int]
         L.orc_ens_partial_f32.argtypes = [C.c_size_t, C.c_int, _f32p, C.c_size_t, C.c_size_t, _f64p]
@@ -346,6 +348,13 @@ def kf12d_params(dt, q_packed, r_packed):
     for i, v in enumerate(np.asarray(r_packed, np.float64)):
         p.r[i] = v
     return p
+
+
+def kf12d_cinv(r_packed):
+    """(ok, Cinv packed [36]) of R = C C^T; ok False when R is not positive definite."""
+    ci = np.zeros(36, np.float64)
+    ok = lib().orc_kf12d_cinv(np.ascontiguousarray(r_packed, np.float64), ci)
+    return ok, ci
 
 
 def kf12d_tick(x, P, z, valid, prm, do_update=True, do_predict=True, nthreads=1):

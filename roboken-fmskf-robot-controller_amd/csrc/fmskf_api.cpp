@@ -299,6 +299,7 @@ void convert_params(fmskf_ctx *h) {
   for (int k = 0; k < 36; k++) h->kf12.r[k] = c.r[k];
   for (int a = 0; a < 4; a++)
     for (int b = 0; b <= a; b++) h->kf12.r2[a * (a + 1) / 2 + b] = c.r[(a + 4) * (a + 5) / 2 + (b + 4)];
+  h->kf12.decor = kf12d_cinv(h->kf12.r, h->kf12.cinv) ? 1 : 0;
 }
 
 void do_reset(fmskf_ctx *h) {
@@ -569,6 +570,12 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
       hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
       convert_params(h);
+      {
+        double *coef = h->alloc<double>(36 + 78);
+        hip_check(hipMemcpy(coef, h->kf12.cinv, 36 * sizeof(double), hipMemcpyHostToDevice), "coef upload");
+        hip_check(hipMemcpy(coef + 36, h->kf12.q, 78 * sizeof(double), hipMemcpyHostToDevice), "coef upload");
+        h->kf12.coef = coef;
+      }
       do_reset(h);
       hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
     } catch (...) {

@@ -1,6 +1,7 @@
 // fmskf_internal.hpp -- structures shared by the C-ABI layer (fmskf_api.cpp) and the
 // kernel launchers (kernels_*.hip).  Not part of the public ABI.
 #pragma once
+#include <cmath>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,7 +74,38 @@ struct Kf12dParams {
   double q[78];
   double r[36];   // full packed 8x8 R (joint update)
   double r2[10];  // packed R of the arm-tip group (rows/cols 4..7), used by the sequential path
+  double cinv[36];  // C^-1 of R = C C^T (packed lower), the decorrelated update's coefficients
+  int decor;        // R positive definite: decorrelated scalar-sequential update
+  const double *coef;  // device copy: cinv [36] then q [78] (read by scalar loads at their use)
 };
+// Cinv of R = C C^T, packed lower; false when R is not positive definite.  Same operations,
+// in the same order, as the oracle's orc_kf12d_cinv (the canonical KF12D update uses it).
+inline bool kf12d_cinv(const double *r, double *ci) {
+  auto pk2 = [](int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; };
+  double c[8][8] = {}, v[8][8] = {};
+  for (int j = 0; j < 8; j++) {
+    double s = r[pk2(j, j)];
+    for (int k = 0; k < j; k++) s = s - c[j][k] * c[j][k];
+    if (!(s > 0.0) || !std::isfinite(s)) return false;
+    c[j][j] = std::sqrt(s);
+    for (int i = j + 1; i < 8; i++) {
+      double t = r[pk2(i, j)];
+      for (int k = 0; k < j; k++) t = t - c[i][k] * c[j][k];
+      c[i][j] = t / c[j][j];
+    }
+  }
+  for (int j = 0; j < 8; j++) {
+    v[j][j] = 1.0 / c[j][j];
+    for (int i = j + 1; i < 8; i++) {
+      double t = 0.0;
+      for (int k = j; k < i; k++) t = t + c[i][k] * v[k][j];
+      v[i][j] = -t / c[i][i];
+    }
+  }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j <= i; j++) ci[pk2(i, j)] = v[i][j];
+  return true;
+}
 // true when R has no terms between the base group (0..3) and the tip group (4..7)
 inline bool kf12d_sequential(const double *r36) {
   for (int i = 4; i < 8; i++)

@@ -204,6 +204,145 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
   nan_guard(x, P, a.counters);
 }
 
+// ---------------------------------------------------------------------------
+// KF12D, R positive definite: decorrelated scalar-sequential update (oracle
+// orc_kf12d_decor_update) and the F P F^T + Q predict done per 2x2 (pos, vel) pair block.
+// Only one 12-entry HP row is live at a time (the joint / group LDL^T updates hold 8x12 or
+// 4x12 update matrices), so x, P and the temporaries fit 256 VGPRs: two waves per SIMD to
+// overlap the fp64 arithmetic (~4 cycles per wave64 FMA) with the 1504-byte stream.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ constexpr int kf12_pos(int k) { return k < 3 ? k : k + 3; }
+
+// Cinv and Q are 114 wave-uniform doubles (a device buffer, prm.coef).  Loaded all at once
+// they exceed the scalar register file and spill through v_writelane / v_readlane; a pointer
+// the compiler cannot see through keeps each group's scalar loads at the point of use.
+typedef const __attribute__((address_space(4))) double *kparam_ptr;
+__device__ __forceinline__ kparam_ptr opaque_param(const double *p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (kparam_ptr)v;
+}
+
+template <bool BLK>
+__device__ __forceinline__ void kf12d_decor_update(double (&x)[12], double (&P)[78], double (&y)[8],
+                                                   const double *ci) {
+#pragma unroll
+  for (int a = 0; a < 8; a++) {
+    const int b0 = (BLK && a >= 4) ? 4 : 0;
+    const kparam_ptr c = opaque_param(ci + a * (a + 1) / 2);
+    double hp[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+      double s = c[b0] * P[pk(MdKF12D::h1(b0), j)];
+#pragma unroll
+      for (int b = b0 + 1; b <= a; b++) s = dfma(c[b], P[pk(MdKF12D::h1(b), j)], s);
+      hp[j] = s;
+    }
+    double s = c[b0] * hp[MdKF12D::h1(b0)];
+#pragma unroll
+    for (int b = b0 + 1; b <= a; b++) s = dfma(c[b], hp[MdKF12D::h1(b)], s);
+    s = s + 1.0;
+    double nu = c[b0] * y[b0];
+#pragma unroll
+    for (int b = b0 + 1; b <= a; b++) nu = dfma(c[b], y[b], nu);
+    const double si = 1.0 / s;
+    const double g = nu * si;
+#pragma unroll
+    for (int j = 0; j < 12; j++) x[j] = dfma(hp[j], g, x[j]);
+#pragma unroll
+    for (int b = 0; b < 8; b++) y[b] = dfma(-hp[MdKF12D::h1(b)], g, y[b]);
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const double t = hp[i] * si;
+#pragma unroll
+      for (int j = 0; j <= i; j++) P[pk(i, j)] = dfma(-t, hp[j], P[pk(i, j)]);
+    }
+  }
+}
+
+// P <- F P F^T + Q with F = I + dt (pos <- vel): every 2x2 block {p_k, v_k} x {p_l, v_l} maps
+// from its own four entries (a b / c d): pp = (a + dt c) + dt (b + dt d), vp = c + dt d,
+// pv = b + dt d, vv = d; bit-identical to the generic T = F P, T F^T form (kf_predict_cov)
+__device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, const double *Q) {
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const kparam_ptr q = opaque_param(Q);
+#pragma unroll
+    for (int l = 0; l <= k; l++) {
+      const int pk_ = kf12_pos(k), vk = pk_ + 3, pl = kf12_pos(l), vl = pl + 3;
+      const double a = P[pk(pk_, pl)], b = P[pk(pk_, vl)], c = P[pk(vk, pl)], d = P[pk(vk, vl)];
+      const double t01 = dfma(dt, d, b);
+      P[pk(pk_, pl)] = dfma(dt, t01, dfma(dt, c, a)) + q[pk(pk_, pl)];
+      P[pk(vk, pl)] = dfma(dt, d, c) + q[pk(vk, pl)];
+      if (k != l) P[pk(pk_, vl)] = t01 + q[pk(pk_, vl)];
+      P[pk(vk, vl)] = d + q[pk(vk, vl)];
+    }
+  }
+}
+
+// Planes through buffer descriptors: a 32-bit lane offset per access and no 64-bit address
+// math.  SMALL: the 78 P planes fit one 4 GiB window (pitch < 6.8M), one descriptor per array
+// and a scalar plane offset; otherwise one descriptor per plane (n < 2^29 lanes of 8 bytes).
+template <bool BLK, bool UPD, bool PRED, bool SMALL>
+__global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
+  constexpr int N = 12, NP = 78, M = 8;
+  const uint64_t n = a.n, pp = a.pitch;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double x[N], P[NP];
+  const auto rx = rsrc(a.x, pp * 8 * N), rp = rsrc(a.P, pp * 8 * NP);
+  const uint32_t vo = (uint32_t)i * 8u;
+  uint32_t ps = (uint32_t)pp * 8u;
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, const double *base, int k) -> double {
+    if constexpr (SMALL) {
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, k * ps, 0));
+    } else {  // one descriptor per plane (scalar work only)
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc(base + k * pp, pp * 8),
+                                                                              vo, 0, 0));
+    }
+  };
+  auto st = [&](__amdgpu_buffer_rsrc_t r, double *base, int k, double v) {
+    if constexpr (SMALL) {
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * ps, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), rsrc(base + k * pp, pp * 8),
+                                            vo, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = ld(rx, a.x, k);
+#pragma unroll
+  for (int k = 0; k < NP; k++) P[k] = ld(rp, a.P, k);
+  const double dt = a.prm.dt;
+  for (uint32_t t = 0; t < a.in.n_ticks; t++) {
+    if (UPD) {
+      if (a.in.valid == nullptr || a.in.valid[(uint64_t)t * a.in.stride + i]) {
+        const double *z = a.in.z + (uint64_t)t * a.in.stride * M;
+        double y[M];
+#pragma unroll
+        for (int q = 0; q < M; q++) y[q] = z[q * a.in.stride + i] - x[MdKF12D::h1(q)];
+        y[0] = wrap_innov(y[0]);
+        kf12d_decor_update<BLK>(x, P, y, a.prm.coef);
+      }
+    }
+    if (PRED) {
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const int p = kf12_pos(q);
+        x[p] = dfma(dt, x[p + 3], x[p]);
+      }
+      x[2] = wrap_pi(x[2]);
+      kf12d_predict_cov(P, dt, a.prm.coef + 36);
+    }
+  }
+  asm volatile("" : "+s"(ps));  // the store offsets are recomputed here, not held from the loads
+#pragma unroll
+  for (int k = 0; k < N; k++) st(rx, a.x, k, x[k]);
+#pragma unroll
+  for (int k = 0; k < NP; k++) st(rp, a.P, k, P[k]);
+  nan_guard(x, P, a.counters);
+}
+
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
                 bool pred, hipStream_t st) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
@@ -234,7 +373,19 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
                  hipStream_t st) {
   KfArgs<MdKF12D, Kf12dParams> a{s.n, s.pitch, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
-  if (kf12d_sequential(p.r)) {
+  const bool small = s.pitch * 8 * 78 < 0xFFFFFFFFull;
+  if (p.decor) {
+    const bool blk = kf12d_sequential(p.r);
+#define KF12S(B, S)                                                          \
+  if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, 0, st>>>(a);       \
+  else if (upd) k_kf12s<B, true, false, S><<<g, kBlock, 0, st>>>(a);        \
+  else k_kf12s<B, false, true, S><<<g, kBlock, 0, st>>>(a);
+    if (blk && small) { KF12S(true, true) }
+    else if (blk) { KF12S(true, false) }
+    else if (small) { KF12S(false, true) }
+    else { KF12S(false, false) }
+#undef KF12S
+  } else if (kf12d_sequential(p.r)) {
     if (upd && pred) k_kf12d<true, true, true><<<g, kBlock, 0, st>>>(a);
     else if (upd) k_kf12d<true, true, false><<<g, kBlock, 0, st>>>(a);
     else k_kf12d<true, false, true><<<g, kBlock, 0, st>>>(a);

@@ -37,12 +37,6 @@ struct Kf6In {
   uint32_t valid;
 };
 
-// Buffer descriptor (MI355X SRD, cdna_hip_programming.md T8) from wave-uniform values.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void *>(base), 0, (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes),
-      0x00020000);
-}
 __device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }

@@ -65,6 +65,14 @@ struct MdKF12D_G2 {
   __host__ __device__ static constexpr int h2(int) { return -1; }
 };
 
+// Buffer descriptor (MI355X SRD, cdna_hip_programming.md T8) from wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(base), 0, (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes),
+      0x00020000);
+}
+typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
+
 template <class Md, typename Prm>
 struct KfArgs {
   uint64_t n;

@@ -90,13 +90,49 @@ def test_ekf9_fp32_vs_fp64(orc):
         _check(x[:, i], P[:, i], x64, P64)
 
 
-def test_kf12d_oracle_vs_dense(orc):
-    """fp64 restatement vs dense fp64: only summation order differs -> 1e-10."""
+def _r_with(r, terms):
+    r = r.copy()
+    for (i, j), v in terms.items():
+        r[i * (i + 1) // 2 + j] = v
+    return r
+
+
+def test_kf12d_cinv_matches_numpy(orc):
+    """Cinv of R = C C^T (the decorrelated update's coefficients) and its PD test."""
+    cfg = fmskf.default_config("kf12d", 1)
+    for terms in ({}, {(4, 0): 1e-6, (7, 3): -2e-6, (5, 1): 3e-7}):
+        r = _r_with(np.array(cfg.r[:36]), terms)
+        R = np.zeros((8, 8))
+        for i in range(8):
+            for j in range(i + 1):
+                R[i, j] = R[j, i] = r[i * (i + 1) // 2 + j]
+        ok, ci = orc.kf12d_cinv(r)
+        assert ok
+        ref = np.linalg.inv(np.linalg.cholesky(R))
+        got = np.zeros((8, 8))
+        for i in range(8):
+            for j in range(i + 1):
+                got[i, j] = ci[i * (i + 1) // 2 + j]
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-9)
+        if not terms:  # block-diagonal R: the cross-group block of Cinv is exactly zero
+            assert not got[4:, :4].any()
+    assert not orc.kf12d_cinv(_r_with(np.array(cfg.r[:36]), {(4, 0): 1e-5}))[0]   # indefinite
+    assert not orc.kf12d_cinv(_r_with(np.array(cfg.r[:36]), {(7, 7): 0.0}))[0]    # semidefinite
+
+
+@pytest.mark.parametrize("terms", [{}, {(4, 0): 1e-6, (7, 3): -2e-6, (5, 1): 3e-7},
+                                   {(4, 0): 1e-5, (7, 3): -2e-5}, {(7, 7): 0.0}],
+                         ids=["decorrelated_blockdiag", "decorrelated_cross", "joint_indefinite",
+                              "groups_semidefinite"])
+def test_kf12d_oracle_vs_dense(orc, terms):
+    """fp64 restatement vs dense fp64 (every update path): only the order of operations
+    differs -> 1e-10."""
     T, n = 200, 4
     tr = Trajectory(n, T, seed=13)
     z = tr.kf12d_z()
     cfg = fmskf.default_config("kf12d", n)
     q, r, p0 = np.array(cfg.q[:78]), np.array(cfg.r[:36]), np.array(cfg.p0[:78])
+    r = _r_with(r, terms)
     prm = orc.kf12d_params(1e-3, q, r)
     x = np.zeros((12, n))
     P = np.repeat(p0[:, None], n, 1).copy()

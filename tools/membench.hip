@@ -154,6 +154,53 @@ __global__ __launch_bounds__(256) void k_pattern_chain(float *st, const float *y
   for (int k = 0; k < 27; k++) st[k * pitch + v] = s[k] + t * sink;
 }
 
+// the EKF9 (54 fp32 state planes + a 16-byte raw record) and KF12D (90 fp64 state planes +
+// 8 fp64 measurement planes) access patterns, pitched like the engine's planes
+template <typename T, int NS, int NIN>
+__global__ __launch_bounds__(256) void k_model_pattern(T *st, const T *in, uint64_t n, uint64_t pitch,
+                                                       T sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  T s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = st[k * pitch + v];
+  T m = sink;
+#pragma unroll
+  for (int k = 0; k < NIN; k++) m = m * in[k * n + v];
+#pragma unroll
+  for (int k = 0; k < NS; k++) st[k * pitch + v] = s[k] + m;
+}
+// the same bytes streamed CH planes at a time (few registers, full occupancy)
+template <typename T, int NS, int NIN, int CH>
+__global__ __launch_bounds__(256) void k_model_stream(T *st, const T *in, uint64_t n, uint64_t pitch,
+                                                      T sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  T m = sink;
+#pragma unroll
+  for (int k = 0; k < NIN; k++) m = m * in[k * n + v];
+#pragma unroll 1
+  for (int c = 0; c < NS; c += CH) {
+    T s[CH];
+#pragma unroll
+    for (int k = 0; k < CH; k++) s[k] = st[(c + k) * pitch + v];
+#pragma unroll
+    for (int k = 0; k < CH; k++) st[(c + k) * pitch + v] = s[k] + m;
+  }
+}
+__global__ __launch_bounds__(256) void k_ekf9_pattern(float *st, const uint4 *raw, uint64_t n,
+                                                      uint64_t pitch, float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float s[54];
+#pragma unroll
+  for (int k = 0; k < 54; k++) s[k] = st[k * pitch + v];
+  const uint4 r = raw[v];
+  const float m = sink * (float)(r.x & r.y & r.z & r.w & 1);
+#pragma unroll
+  for (int k = 0; k < 54; k++) st[k * pitch + v] = s[k] + m;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -190,6 +237,42 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3) {  // membench LG 1 models: the EKF9 and KF12D patterns only
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t pitch = ((n + 511) / 512) * 512 + 256;
+    void *sb, *ib;
+    CK(hipMalloc(&sb, 90 * pitch * 8));
+    CK(hipMalloc(&ib, 8 * n * 8));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, 90 * pitch * 2, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, 8 * n * 2, 8);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, double bpi, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)n, name, us, bpi * n / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)((n + 255) / 256);
+    tm("ekf9_pattern_448B", 448, [&] { k_ekf9_pattern<<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
+    tm("kf12d_pattern_1504B", 1504, [&] {
+      k_model_pattern<double, 90, 8><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
+    });
+    tm("kf12d_stream10_1504B", 1504, [&] {
+      k_model_stream<double, 90, 8, 10><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
+    });
+    tm("kf12d_stream30_1504B", 1504, [&] {
+      k_model_stream<double, 90, 8, 30><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
+    });
+    return 0;
+  }
   if (!zeros) {
     k_fill_rand<<<4096, 256>>>((uint32_t *)st, 27 * (n + 4 * pad), 1);
     k_fill_rand<<<4096, 256>>>((uint32_t *)yaw, n, 2);
