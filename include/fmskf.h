@@ -248,6 +248,14 @@ int fmskf_set_target_vel(fmskf_handle h, const float *vel, const float *acl, con
 int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem);
 /* CAN_CTRL::tx_routine: frames [N][8] = the 0x200 payload (big-endian raw currents) */
 int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem);
+/* The firmware ISR in one call (VDT::can_tx_routine_intr, VD_task_main.cpp:366-372): correct,
+ * VEHICLE_CTRL::update (estimator time update, then the control half on the same rpm record),
+ * M_CAN.tx_routine.  Inputs as fmskf_tick (NULL planes = the device-resident ingest state);
+ * frames [N][8] receives the 0x200 payloads (NULL: no frame, the current targets are still
+ * kept).  Model RS runs as ONE kernel (one pass over pose, encoder sums and control state);
+ * the KF models run their tick kernel, then the control step and the frame.  Results are
+ * identical to fmskf_tick + fmskf_control + fmskf_can_tx in sequence. */
+int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem);
 /* readout: vel_tgt [3][N] (get_vehicle_vel_tgt_mmps_latest), curr_raw [N][4]
  * (get_rawCurr_tgt), wheel_tgt / wheel_ctrl [4][N] (FF_PI_D get_target / last output).
  * Any pointer may be NULL. */

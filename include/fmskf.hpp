@@ -72,11 +72,8 @@ class Robots {
   void can_tx_routine(uint8_t *tx_frames = nullptr, uint32_t mem = FMSKF_MEM_HOST) {
     fmskf_tick_inputs in{};
     in.mem = FMSKF_MEM_HOST;
-    check(fmskf_tick(h_, &in), "fmskf_tick");
-    if (tx_frames) {
-      check(fmskf_control(h_, nullptr, FMSKF_MEM_HOST), "fmskf_control");
-      check(fmskf_can_tx(h_, tx_frames, mem), "fmskf_can_tx");
-    }
+    if (tx_frames) check(fmskf_isr_tick(h_, &in, tx_frames, mem), "fmskf_isr_tick");
+    else check(fmskf_tick(h_, &in), "fmskf_tick");
   }
 
  private:

@@ -1191,6 +1191,39 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
   });
 }
 
+int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (frames && mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    const uint64_t n = h->s.n;
+    TickIn t = resolve_inputs(h, in, true, true, 1, n);
+    const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+    const size_t bytes = n * 8;
+    uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)h->out_for(bytes);
+    const CtrlPrm p = make_ctrl_prm(h);
+    h->time_begin();
+    if (h->cfg.model == FMSKF_MODEL_RS) {
+      launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
+    } else {  // estimator tick, then the control step and the frame (three launches)
+      int e = 0;
+      switch (h->cfg.model) {
+        case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream); break;
+        case FMSKF_MODEL_EKF9: e = launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream); break;
+        case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream); break;
+      }
+      launch_check(e, "tick kernel launch");
+      const int16_t *rpm = t.rpm ? t.rpm : h->s.m_rpm;
+      launch_check(launch_ctrl_step(h->ctrl, p, rpm, h->stream), "control launch");
+      if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
+    }
+    h->time_end();
+    if (frames && mem == FMSKF_MEM_HOST) copy_out(h, frames, dst, bytes, mem);
+    if (frames) finish_out(h, mem);
+  });
+}
+
 int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *wheel_tgt,
                    float *wheel_ctrl, uint32_t mem) {
   return guarded([&] {

@@ -171,6 +171,9 @@ int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl,
                            const uint8_t *mask, hipStream_t st);
 int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hipStream_t st);
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st);
+// the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
+int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
+                  const CtrlPrm &p, uint8_t *frames, hipStream_t st);
 int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
                         const float *cam_pitch, const uint32_t *fault, hipStream_t st);
 // readout helpers

@@ -14,6 +14,7 @@
 // FF_PI_D (tests/golden/ctrl_ref.npz).  HBM-bound: ~370 B per robot-tick, no reuse.
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
+#include "lane_rs.hpp"
 
 #pragma clang fp contract(off)
 
@@ -153,107 +154,175 @@ struct Planes {
   }
 };
 
+// One robot's control step, split in its load phase (every load issued up front: vmcnt
+// retires in order) and its compute + store phase, so a fused kernel can issue the loads of
+// several steps before computing any of them.
+template <bool SMALL>
+struct CtrlLane {
+  uint8_t on;
+  Interp ax[3];
+  float pv[4][4];
+
+  __device__ __forceinline__ void load(const CtrlDev &c, uint32_t i) {
+    const Planes<SMALL> AX(c.ax, c.pitch, 3 * kAxF), PD(c.pid, c.pitch, 4 * kPidF);
+    on = c.power[i];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int k = 0; k < kAxF; k++) ax[a].f[k] = AX.ld(a * kAxF + k, i);
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
+  }
+
+  // rw: the four s16_rawSpeedRpm (FL, BL, BR, FR) packed in 8 bytes.  Returns the packed
+  // raw current targets (also stored to c.curr).
+  __device__ __forceinline__ uint2 step(const CtrlDev &c, const CtrlPrm &p, uint32_t i, uint2 rw) {
+    const uint64_t pp = c.pitch;
+    const Planes<SMALL> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
+    float v[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
+    // conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
+    float mt[4];
+    mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+    mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+    mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+    mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+    const int16_t r[4] = {(int16_t)(rw.x & 0xFFFFu), (int16_t)(rw.x >> 16),
+                          (int16_t)(rw.y & 0xFFFFu), (int16_t)(rw.y >> 16)};
+    float po[4][kPidF];
+    int16_t cur[4];
+    if (on) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        // FF_PI_D::update with now_tgt_ = Mvel_tgt * GEAR_RATIO, _nowval = Mvel * GEAR_RATIO
+        const float tgt = mt[w] * 36.0f;
+        const float val = rpm_to_mvel(r[w]) * 36.0f;
+        const float err = tgt - val;
+        const float lx = (val - pv[w][PD_VAL]) * p.freq;
+        const float ly = p.a1 * pv[w][PD_LY] + p.b0 * lx + p.b1 * pv[w][PD_LX];
+        float integ = pv[w][PD_INTEG] + p.i_gain * p.dt * err;
+        integ = (integ >= p.i_limit) ? p.i_limit : ((integ <= -p.i_limit) ? -p.i_limit : integ);
+        float ctrl = p.p_gain * err + integ - p.d_gain * ly;
+        float ff = tgt * p.ff_gain;
+        ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
+        ctrl = ctrl + ff;
+        po[w][PD_VAL] = val;
+        po[w][PD_INTEG] = integ;
+        po[w][PD_LY] = ly;
+        po[w][PD_LX] = lx;
+        po[w][PD_TGT] = tgt;
+        po[w][PD_CTRL] = ctrl;
+        cur[w] = curr_to_raw(ctrl, p.dir[w], p.curr_limit);
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int k = 0; k < kAxF; k++) ax[a].f[k] = 0.0f;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+#pragma unroll
+        for (int k = 0; k < kPidF; k++) po[w][k] = 0.0f;
+        cur[w] = curr_to_raw(0.0f, p.dir[w], p.curr_limit);
+      }
+    }
+    // the interpolator fields update() changes; after a reset (power off) all of them
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      AX.st(a * kAxF + IV_DT, i, ax[a].f[IV_DT]);
+      AX.st(a * kAxF + IV_V, i, ax[a].f[IV_V]);
+      AX.st(a * kAxF + IV_A, i, ax[a].f[IV_A]);
+    }
+    if (!on) {
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int k = 0; k < IV_DT; k++) AX.st(a * kAxF + k, i, 0.0f);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+#pragma unroll
+      for (int k = 0; k < kPidF; k++) PD.st(w * kPidF + k, i, po[w][k]);
+#pragma unroll
+    for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
+    const uint2 cw = make_uint2((uint32_t)(uint16_t)cur[0] | ((uint32_t)(uint16_t)cur[1] << 16),
+                                (uint32_t)(uint16_t)cur[2] | ((uint32_t)(uint16_t)cur[3] << 16));
+    reinterpret_cast<uint2 *>(c.curr)[i] = cw;
+    return cw;
+  }
+};
+
 // The per-tick control step.  rpm [N][4] int16 (MOTOR_IF_M2006::Status.s16_rawSpeedRpm).
 template <bool SMALL>
 __global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, const int16_t *rpm) {
-  const uint64_t n = c.n, pp = c.pitch;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (uint32_t)c.n) return;
+  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[i];
+  CtrlLane<SMALL> L;
+  L.load(c, i);
+  L.step(c, p, i, rw);
+}
+
+// C610 0x200 payload of one robot: bytes (hi, lo) per wheel -> swap the bytes of every 16-bit half
+__device__ __forceinline__ uint2 tx_frame(uint2 c) {
+  auto sw = [](uint32_t v) { return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu); };
+  return make_uint2(sw(c.x), sw(c.y));
+}
+
+// The firmware ISR in one pass (VDT::can_tx_routine_intr, VD_task_main.cpp:366-372), reference
+// semantics: correct (theta <- deg2rad(yaw)), VEHICLE_CTRL::update (velocity, odometry, then the
+// control half on the same rpm record), M_CAN.tx_routine (the 0x200 frame; skipped when frames is
+// NULL).  Every load of both steps is issued before either computes; results are bit-identical
+// to fmskf_tick + fmskf_control + fmskf_can_tx in sequence (the same lane functions).
+struct IsrRsArgs {
+  uint64_t pitch;
+  float *x;
+  int64_t *prev;
+  const float *yaw_deg;
+  const int16_t *rpm;
+  const int64_t *angle_sum;  // [4][N] (plane stride N)
+  const float *sintab;
+  uint8_t *frames;
+};
+template <bool LIBM, bool SMALL>
+__global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p) {
+  const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)n) return;
-  const Planes<SMALL> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
-  // issue every load up front (vmcnt retires in order), then compute
-  const uint8_t on = c.power[i];
-  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[i];
-  Interp ax[3];
+  RsLane s;
+  s.px = a.x[i];
+  s.py = a.x[pp + i];
+  s.th = 0.f;  // overwritten by the correct step
 #pragma unroll
-  for (int a = 0; a < 3; a++)
+  for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
+  const float yaw = a.yaw_deg[i];
+  const uint2 rw = reinterpret_cast<const uint2 *>(a.rpm)[i];
+  int64_t sum[4];
 #pragma unroll
-    for (int k = 0; k < kAxF; k++) ax[a].f[k] = AX.ld(a * kAxF + k, i);
-  float pv[4][4];
+  for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * n + i];
+  CtrlLane<SMALL> L;
+  L.load(c, i);
+  rs_tick1<LIBM, true, true>(s, yaw, rw, sum, a.sintab);
+  const uint2 cw = L.step(c, p, i, rw);
+  a.x[i] = s.px;
+  a.x[pp + i] = s.py;
+  a.x[2 * pp + i] = s.th;
+  a.x[3 * pp + i] = s.vx;
+  a.x[4 * pp + i] = s.vy;
+  a.x[5 * pp + i] = s.vth;
 #pragma unroll
-  for (int w = 0; w < 4; w++)
-#pragma unroll
-    for (int k = 0; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
-
-  float v[3];
-#pragma unroll
-  for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
-  // conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
-  float mt[4];
-  mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-  mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-  mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-  mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-  const int16_t r[4] = {(int16_t)(rw.x & 0xFFFFu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xFFFFu),
-                        (int16_t)(rw.y >> 16)};
-  float po[4][kPidF];
-  int16_t cur[4];
-  if (on) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      // FF_PI_D::update with now_tgt_ = Mvel_tgt * GEAR_RATIO, _nowval = Mvel * GEAR_RATIO
-      const float tgt = mt[w] * 36.0f;
-      const float val = rpm_to_mvel(r[w]) * 36.0f;
-      const float err = tgt - val;
-      const float lx = (val - pv[w][PD_VAL]) * p.freq;
-      const float ly = p.a1 * pv[w][PD_LY] + p.b0 * lx + p.b1 * pv[w][PD_LX];
-      float integ = pv[w][PD_INTEG] + p.i_gain * p.dt * err;
-      integ = (integ >= p.i_limit) ? p.i_limit : ((integ <= -p.i_limit) ? -p.i_limit : integ);
-      float ctrl = p.p_gain * err + integ - p.d_gain * ly;
-      float ff = tgt * p.ff_gain;
-      ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
-      ctrl = ctrl + ff;
-      po[w][PD_VAL] = val;
-      po[w][PD_INTEG] = integ;
-      po[w][PD_LY] = ly;
-      po[w][PD_LX] = lx;
-      po[w][PD_TGT] = tgt;
-      po[w][PD_CTRL] = ctrl;
-      cur[w] = curr_to_raw(ctrl, p.dir[w], p.curr_limit);
-    }
-  } else {
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-      for (int k = 0; k < kAxF; k++) ax[a].f[k] = 0.0f;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-#pragma unroll
-      for (int k = 0; k < kPidF; k++) po[w][k] = 0.0f;
-      cur[w] = curr_to_raw(0.0f, p.dir[w], p.curr_limit);
-    }
-  }
-  // the interpolator fields update() changes; after a reset (power off) all of them
-#pragma unroll
-  for (int a = 0; a < 3; a++) {
-    AX.st(a * kAxF + IV_DT, i, ax[a].f[IV_DT]);
-    AX.st(a * kAxF + IV_V, i, ax[a].f[IV_V]);
-    AX.st(a * kAxF + IV_A, i, ax[a].f[IV_A]);
-  }
-  if (!on) {
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-      for (int k = 0; k < IV_DT; k++) AX.st(a * kAxF + k, i, 0.0f);
-  }
-#pragma unroll
-  for (int w = 0; w < 4; w++)
-#pragma unroll
-    for (int k = 0; k < kPidF; k++) PD.st(w * kPidF + k, i, po[w][k]);
-#pragma unroll
-  for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
-  reinterpret_cast<uint2 *>(c.curr)[i] =
-      make_uint2((uint32_t)(uint16_t)cur[0] | ((uint32_t)(uint16_t)cur[1] << 16),
-                 (uint32_t)(uint16_t)cur[2] | ((uint32_t)(uint16_t)cur[3] << 16));
+  for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+  if (a.frames) reinterpret_cast<uint2 *>(a.frames)[i] = tx_frame(cw);
 }
 
 // CAN_CTRL::tx_routine, VD_can_controller.hpp:43-55: frames [N][8], big-endian raw currents
 __global__ __launch_bounds__(kBlock) void k_can_tx(const int16_t *curr, uint64_t n, uint8_t *frames) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint2 c = reinterpret_cast<const uint2 *>(curr)[i];
-  // bytes (hi, lo) per wheel: swap the bytes of every 16-bit half
-  auto sw = [](uint32_t v) { return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu); };
-  reinterpret_cast<uint2 *>(frames)[i] = make_uint2(sw(c.x), sw(c.y));
+  reinterpret_cast<uint2 *>(frames)[i] = tx_frame(reinterpret_cast<const uint2 *>(curr)[i]);
 }
 
 // VehicleInfo export (RM_task_main.cpp:772-823), 84-byte records (fmskf_vehicle_info).  Each
@@ -320,6 +389,22 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hip
     k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
   else
     k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
+  return (int)hipGetLastError();
+}
+
+int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
+                  const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+  if (c.n == 0) return 0;
+  const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum,
+                    in.sintab, frames};
+  const bool small = c.pitch * 4 * 4 * kPidF < 0xFFFFFFFFull;
+  if (libm) {
+    if (small) k_isr_rs<true, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+    else k_isr_rs<true, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+  } else {
+    if (small) k_isr_rs<false, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+    else k_isr_rs<false, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+  }
   return (int)hipGetLastError();
 }
 

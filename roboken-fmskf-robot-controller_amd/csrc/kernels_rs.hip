@@ -11,6 +11,7 @@
 // sums 32 B, yaw 4 B, rpm 8 B, vel 12 B w  -> 12*2 + 32*2 + 32 + 4 + 8 + 12 = 144 B.
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
+#include "lane_rs.hpp"
 
 #pragma clang fp contract(off)
 
@@ -29,50 +30,39 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  float px = a.x[i], py = a.x[pp + i], th = a.x[2 * pp + i];
-  float vx = 0.f, vy = 0.f, vth = 0.f;
-  int64_t prev[4];
+  RsLane s;
+  s.px = a.x[i];
+  s.py = a.x[pp + i];
+  s.th = a.x[2 * pp + i];
+  s.vx = s.vy = s.vth = 0.f;
   if (PRED) {
 #pragma unroll
-    for (int w = 0; w < 4; w++) prev[w] = a.prev[w * pp + i];
+    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
   }
   const uint64_t st = a.in.stride;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t j = (uint64_t)t * st + i;
-    if (CORR) th = deg2rad(a.in.yaw_deg[j]);
+    const float yaw = CORR ? a.in.yaw_deg[j] : 0.f;
+    uint2 r = make_uint2(0u, 0u);
+    int64_t sum[4] = {0, 0, 0, 0};
     if (PRED) {
-      const uint2 r = reinterpret_cast<const uint2 *>(a.in.rpm)[j];
-      const int16_t r0 = (int16_t)(r.x & 0xFFFFu), r1 = (int16_t)(r.x >> 16);
-      const int16_t r2 = (int16_t)(r.y & 0xFFFFu), r3 = (int16_t)(r.y >> 16);
-      mdir_to_vdir(rpm_to_mvel(r0), rpm_to_mvel(r1), rpm_to_mvel(r2), rpm_to_mvel(r3), vx, vy, vth);
-      float mrad[4];
-      const int64_t *sum = a.in.angle_sum + (uint64_t)t * st * 4;
+      r = reinterpret_cast<const uint2 *>(a.in.rpm)[j];
+      const int64_t *sp = a.in.angle_sum + (uint64_t)t * st * 4;
 #pragma unroll
-      for (int w = 0; w < 4; w++) {
-        const int64_t s = sum[w * st + i];
-        mrad[w] = (float)((double)(s - prev[w]) * (double)K::out_rad_per_raw *
-                          (double)K::gear_ratio_inv);
-        prev[w] = s;
-      }
-      float lx, ly, lth;
-      mdir_to_vdir(mrad[0], mrad[1], mrad[2], mrad[3], lx, ly, lth);
-      const float rr = normalize_rad_0to2pi(th);
-      const float c = cos_p<LIBM>(rr, a.in.sintab);
-      const float s = sin_p<LIBM>(rr, a.in.sintab);
-      px = px + (lx * c - ly * s) * 0.001f;
-      py = py + (lx * s + ly * c) * 0.001f;
+      for (int w = 0; w < 4; w++) sum[w] = sp[w * st + i];
     }
+    rs_tick1<LIBM, CORR, PRED>(s, yaw, r, sum, a.in.sintab);
   }
   if (PRED) {
-    a.x[i] = px;
-    a.x[pp + i] = py;
-    a.x[3 * pp + i] = vx;
-    a.x[4 * pp + i] = vy;
-    a.x[5 * pp + i] = vth;
+    a.x[i] = s.px;
+    a.x[pp + i] = s.py;
+    a.x[3 * pp + i] = s.vx;
+    a.x[4 * pp + i] = s.vy;
+    a.x[5 * pp + i] = s.vth;
 #pragma unroll
-    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = prev[w];
+    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
   }
-  if (CORR) a.x[2 * pp + i] = th;
+  if (CORR) a.x[2 * pp + i] = s.th;
 }
 
 int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool predict,

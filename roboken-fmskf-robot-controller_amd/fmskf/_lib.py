@@ -128,6 +128,7 @@ SIGNATURES = {
     "fmskf_set_target_vel": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
     "fmskf_control": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_can_tx": (C.c_int, [_H, _P, C.c_uint32]),
+    "fmskf_isr_tick": (C.c_int, [_H, _P, _P, C.c_uint32]),
     "fmskf_get_ctrl": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
     "fmskf_export_vehicle_info": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
     "fmskf_eval_trig": (C.c_int, [_H, _P, _P, _P, C.c_uint64, C.c_uint32]),

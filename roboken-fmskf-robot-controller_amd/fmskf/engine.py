@@ -347,6 +347,23 @@ class Engine:
         check(load().fmskf_can_tx(self.h, f.ctypes.data_as(C.c_void_p), MEM_HOST), "can_tx")
         return f
 
+    def isr_tick(self, frames=True, out=None, **kw):
+        """VDT::can_tx_routine_intr in one call (fmskf_isr_tick): correct, update (estimator +
+        control), tx_routine.  Inputs as tick(); returns the [N][8] frames (host numpy, or the
+        device tensor `out`), or None with frames=False."""
+        ti, _keep = self._inputs(kw)
+        if out is not None and _is_torch(out) and out.is_cuda:
+            check(load().fmskf_isr_tick(self.h, C.byref(ti), C.c_void_p(out.data_ptr()), MEM_DEVICE),
+                  "isr_tick")
+            return out
+        if not frames:
+            check(load().fmskf_isr_tick(self.h, C.byref(ti), None, MEM_HOST), "isr_tick")
+            return None
+        f = np.empty((self.n, 8), np.uint8)
+        check(load().fmskf_isr_tick(self.h, C.byref(ti), f.ctypes.data_as(C.c_void_p), MEM_HOST),
+              "isr_tick")
+        return f
+
     def get_ctrl(self):
         vt = np.empty((3, self.n), np.float32)
         cur = np.empty((self.n, 4), np.int16)

@@ -198,3 +198,97 @@ def test_reset_zeroes_control_state():
         assert not g["curr"].any() and not g["vel_tgt"].any() and not g["wheel_ctrl"].any()
         e.control(np.full((n, 4), 50, np.int16))   # power is off after reset
         assert not e.get_ctrl()["curr"].any()
+
+
+@pytest.mark.parametrize("model,n,T", [("rs", 3001, 200), ("rs", 1, 30), ("kf6", 1000, 60)])
+def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
+    """fmskf_isr_tick (the firmware ISR in one call; one fused kernel for RS) leaves the
+    estimator state, the control state and the 0x200 frames bit-identical to fmskf_tick +
+    fmskf_control + fmskf_can_tx, with random power and target events; RS also against the
+    oracle's pose and the oracle's control batch directly."""
+    rng = np.random.default_rng(99 + n)
+    ev = _schedule(rng, n, T)
+    tr = Trajectory(n, T, seed=31)
+    if model == "rs":
+        yaw, sums, rpm = tr.rs_inputs()
+        kw = [dict(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t]) for t in range(T)]
+    else:
+        yaw, gz, rpm = tr.kf6_inputs()
+        kw = [dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t]) for t in range(T)]
+    ref = orc.CtrlBatch(n)
+    pos = np.zeros((3, n), np.float32)
+    vel = np.zeros((3, n), np.float32)
+    prev = np.zeros((4, n), np.int64)
+    with Engine(model, n) as a, Engine(model, n) as b:
+        for t in range(T):
+            for kind, pl in ev.get(t, []):
+                for e in (a, b):
+                    (e.set_target_vel(*pl) if kind == "target" else e.set_power(pl))
+                (ref.set_target_vel(*pl) if kind == "target" else ref.set_power(pl))
+            fa = a.isr_tick(**kw[t]) if t % 7 else a.isr_tick(frames=False, **kw[t])
+            b.tick(**kw[t])
+            b.control(rpm[t])
+            fb = b.can_tx()
+            if t % 7:
+                np.testing.assert_array_equal(fa, fb)
+            ref.step(rpm[t])
+            if model == "rs":
+                orc.rs_tick(pos, vel, prev, yaw[t], np.ascontiguousarray(sums[t]), rpm[t])
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        ga, gb = a.get_ctrl(), b.get_ctrl()
+        if model == "rs":
+            np.testing.assert_array_equal(a.get_prev_sum(), prev)
+    np.testing.assert_array_equal(bits(xa), bits(xb))
+    if Pa is not None:
+        np.testing.assert_array_equal(bits(Pa), bits(Pb))
+    for k in ("vel_tgt", "curr", "wheel_tgt", "wheel_ctrl"):
+        np.testing.assert_array_equal(bits(ga[k]), bits(gb[k]))
+    np.testing.assert_array_equal(ga["curr"], ref.curr())
+    np.testing.assert_array_equal(bits(ga["wheel_ctrl"]), bits(ref.wheel("ctrl")))
+    if model == "rs":
+        np.testing.assert_array_equal(bits(xa[:3]), bits(pos))
+        np.testing.assert_array_equal(bits(xa[3:]), bits(vel))
+
+
+def test_isr_tick_device_resident_and_graph():
+    """The whole firmware pipeline on device-resident state: CAN ingest -> fmskf_isr_tick with
+    NULL planes (IMU yaw page, motor rpm and angle sums) into a device frame buffer, captured
+    as a HIP graph and replayed: identical to direct calls."""
+    import torch
+    n, T = 4099, 12
+    tr = Trajectory(n, T, seed=41)
+    vel = np.zeros((3, n), np.float32)
+    vel[1] = 120.0
+    acl = np.full((3, n), 1000.0, np.float32)
+    jrk = np.full((3, n), 10000.0, np.float32)
+    frames = [tr.can_frames(t) for t in range(T)]
+    dev = [(torch.from_numpy(np.ascontiguousarray(f)).cuda(), torch.from_numpy(np.ascontiguousarray(s)).cuda())
+           for f, s in frames]
+    out_a = torch.zeros((n, 8), dtype=torch.uint8, device="cuda")
+    out_b = torch.zeros((n, 8), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    with Engine("rs", n) as a, Engine("rs", n) as b:
+        for e in (a, b):
+            e.set_stream(st)
+            e.set_power(None)
+            e.set_target_vel(vel, acl, jrk)
+        for t in range(T):
+            a.ingest_can(*dev[t])
+            a.isr_tick(out=out_a)
+            b.ingest_can(*dev[t])
+            b.tick()
+            b.control()
+            b.can_tx(out=out_b)
+            st.synchronize()
+            assert torch.equal(out_a, out_b)
+        # graph replay of the ISR alone on the final motor state, against direct calls
+        a.graph_begin()
+        a.isr_tick(out=out_a)
+        a.graph_end()
+        a.graph_launch(5)
+        for _ in range(5):
+            b.isr_tick(out=out_b)
+        st.synchronize()
+        assert torch.equal(out_a, out_b)
+        np.testing.assert_array_equal(bits(a.get_state()[0]), bits(b.get_state()[0]))

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ticks", type=int, default=300)
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
@@ -60,7 +60,7 @@ def main():
         many = dict(z=z)
     if args.host:
         return bench_host(args, e, n, yaw, gz, rpm)
-    if args.op in ("pipeline", "pipeline_graph"):
+    if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph"):
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
@@ -144,10 +144,13 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
 
     def direct():
+        if args.op.startswith("isr"):  # fmskf_isr_tick: one fused kernel for RS
+            e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+            return
         e.tick(yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
         e.control(dr)
         e.can_tx(fr)
-    if args.op == "pipeline_graph":
+    if args.op.endswith("_graph"):
         e.graph_begin()
         direct()
         e.graph_end()
