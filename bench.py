@@ -5,7 +5,8 @@ A step is one instance-tick (one correct + one predict of one filter); one timed
 iteration ("tick") is one fused fmskf_tick launch over all instances of a GPU.
 Workload (BASELINE.json configs[1] / SURVEY.md 8(d) cfg 2): 2^20 independent
 6-state fp32 KF instances per GPU, inputs (IMU yaw + gyro z + 4 wheel rpm = 16 B
-per instance-tick) pre-generated into an HBM ring of 64 ticks (not timed).  Every
+per instance-tick, one fmskf_kf6_record per robot; --inputs planes feeds the three
+SoA planes instead) pre-generated into an HBM ring of 64 ticks (not timed).  Every
 `--ensemble-every` ticks each rank reduces its ensemble mean/covariance record and,
 for N > 1, all-gathers it over RCCL (the cfg 4 collective).  Weak scaling: per-GPU
 work is fixed as N grows.
@@ -86,6 +87,8 @@ def main():
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused multi-tick figure")
+    ap.add_argument("--inputs", choices=["records", "planes"], default="records",
+                    help="16-byte fmskf_kf6_record per robot (one load per lane) or yaw/gyro/rpm planes")
     args = ap.parse_args()
 
     import numpy as np
@@ -119,7 +122,15 @@ def main():
     eng = fmskf.Engine("kf6", n, device=local, trig=trig)
     eng.set_stream(stream)
     yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 2 ^ (rank << 8), device=dev)
-    prepared = [eng.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
+    planes = [eng.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
+    if args.inputs == "records":
+        krec = fmskf.kf6_records(yaw, gz, rpm)  # [R][N] 16-byte records (same values)
+        prepared = [eng.prepare(kf6_rec=krec[r]) for r in range(R)]
+        many_in = dict(kf6_rec=krec)
+    else:
+        krec = None
+        prepared = planes
+        many_in = dict(yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
     tick_fn = fmskf.load().fmskf_tick
     rec_len = eng.ensemble_record_len()
     rec = torch.empty(rec_len, dtype=torch.float64, device=dev)
@@ -180,10 +191,19 @@ def main():
     ek1.record(stream)
     torch.cuda.synchronize()
     tick_ms = ek0.elapsed_time(ek1)
+    # secondary: the same tick fed the three input planes (when the headline uses records)
+    planes_ms = tick_ms
+    if args.inputs == "records":
+        ek0.record(stream)
+        for k in range(args.steps):
+            eng.tick_prepared(planes[k % R], tick_fn)
+        ek1.record(stream)
+        torch.cuda.synchronize()
+        planes_ms = ek0.elapsed_time(ek1)
     if distributed:
-        t = torch.tensor([elapsed, region_ms, tick_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, region_ms, tick_ms, planes_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, region_ms, tick_ms = (float(v) for v in t.tolist())
+        elapsed, region_ms, tick_ms, planes_ms = (float(v) for v in t.tolist())
     kern_avg_ms = tick_ms / args.steps
 
     total_steps = n * world * args.steps
@@ -227,12 +247,12 @@ def main():
     if not args.no_fused:
         e2 = fmskf.Engine("kf6", n, device=local, trig=trig)
         e2.set_stream(stream)
-        e2.tick_many(R, yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
+        e2.tick_many(R, **many_in)
         torch.cuda.synchronize()
         reps = max(1, args.steps // R)
         ta = time.perf_counter()
         for _ in range(reps):
-            e2.tick_many(R, yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
+            e2.tick_many(R, **many_in)
         torch.cuda.synchronize()
         tb = time.perf_counter()
         fused = {"ticks_per_launch": R, "steps_per_s_per_gpu": n * R * reps / (tb - ta),
@@ -244,7 +264,8 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("n_instances") == n and tj.get("kernel", "").startswith("k_kf6"):
+            if tj.get("n_instances") == n and tj.get("kernel", "").startswith("k_kf6") and \
+                    tj.get("inputs", "planes") == args.inputs:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -263,13 +284,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: WT901 yaw/gyro-z + 4 wheel rpm per robot (fmskf.synth), 64-tick HBM ring",
+        "data": "synthetic: WT901 yaw/gyro-z + 4 wheel rpm per robot (fmskf.synth), 64-tick HBM ring"
+                + (", one 16-byte fmskf_kf6_record per robot-tick" if krec is not None else ", SoA planes"),
         "config": {
             "workload": "cfg2: 2^20 independent 6-state fp32 KF instances per GPU, fused "
                         "correct+predict per tick (fmskf_tick)",
             "instances_per_gpu": n,
             "global_instances": n * world,
             "trig": args.trig,
+            "inputs": args.inputs,
             "ensemble_every": args.ensemble_every,
             "parallelism": f"instance-sharded x{world}" + (", RCCL all-gather of ensemble records"
                                                            if world > 1 else ""),
@@ -283,8 +306,10 @@ def main():
             "traffic": traffic,
             "bytes_per_step": BYTES_PER_STEP["kf6"],
             "kernel_ms": kern_avg_ms,
-            "kernel": "k_kf6t<4, Opt<TABLE512, UPD, PRED, SMALL, !VALID>>",
+            "kernel": "k_kf6t<4, Opt<TABLE512, UPD, PRED, SMALL, !VALID" +
+                      (", REC>>" if krec is not None else ">>"),
             "timed_region_ms_per_step": region_ms / args.steps,
+            "kernel_ms_plane_inputs": planes_ms / args.steps,
         },
         "cpu_baseline": None,
         "fused_replay": fused,

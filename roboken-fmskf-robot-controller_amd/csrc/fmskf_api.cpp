@@ -376,9 +376,13 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
   t.raw = in->raw;
   t.z = in->z;
   t.valid = in->valid;
+  t.rec = (const uint32_t *)in->kf6_rec;
   t.sintab = s.sintab;
   t.stride = stride;
   t.n_ticks = n_ticks;
+  if (t.rec && h->cfg.model != FMSKF_MODEL_KF6) fail(FMSKF_EINVAL, "kf6_rec is a KF6 input");
+  if (t.rec && (t.yaw_deg || t.gyro_z || t.rpm))
+    fail(FMSKF_EINVAL, "kf6_rec replaces yaw_deg / gyro_z_dps / rpm: pass one or the other");
   const uint64_t span = (uint64_t)(n_ticks - 1) * stride + n;  // elements per [N] plane
   Stager sg(h, in->mem);
   sg.add((const void **)&t.yaw_deg, span * 4);
@@ -388,6 +392,7 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
   sg.add((const void **)&t.raw, span * 16);
   sg.add((const void **)&t.z, ((uint64_t)(n_ticks - 1) * stride * 8 + 7 * stride + n) * 8);
   sg.add((const void **)&t.valid, span);
+  sg.add((const void **)&t.rec, span * 16);
   sg.run();
   const bool many = n_ticks > 1 || stride != n;
   auto dev_default = [&](const void *p, const char *name) {
@@ -407,7 +412,7 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
       }
       break;
     case FMSKF_MODEL_KF6:
-      if (need_upd) {
+      if (need_upd && !t.rec) {
         dev_default(t.yaw_deg, "yaw_deg");
         dev_default(t.gyro_z, "gyro_z_dps");
         dev_default(t.rpm, "rpm");
@@ -1170,7 +1175,7 @@ int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem) {
       r = h->s.m_rpm;
     }
     h->time_begin();
-    launch_check(launch_ctrl_step(h->ctrl, make_ctrl_prm(h), (const int16_t *)r, h->stream),
+    launch_check(launch_ctrl_step(h->ctrl, make_ctrl_prm(h), (const int16_t *)r, 1, h->stream),
                  "control launch");
     h->time_end();
   });
@@ -1214,8 +1219,8 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
         case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream); break;
       }
       launch_check(e, "tick kernel launch");
-      const int16_t *rpm = t.rpm ? t.rpm : h->s.m_rpm;
-      launch_check(launch_ctrl_step(h->ctrl, p, rpm, h->stream), "control launch");
+      const int16_t *rpm = t.rec ? (const int16_t *)(t.rec + 2) : t.rpm ? t.rpm : h->s.m_rpm;
+      launch_check(launch_ctrl_step(h->ctrl, p, rpm, t.rec ? 2 : 1, h->stream), "control launch");
       if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
     }
     h->time_end();

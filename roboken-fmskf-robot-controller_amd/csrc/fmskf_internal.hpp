@@ -56,6 +56,7 @@ struct TickIn {
   const int16_t *raw;        // [N][8]
   const double *z;           // [8][N]
   const uint8_t *valid;      // [N] or null
+  const uint32_t *rec;       // KF6 [N] x 16-byte records {yaw, gz, rpm[4]} or null
   const float *sintab;       // 513-entry TABLE512 sine table (device)
   uint64_t stride;
   uint32_t n_ticks;
@@ -169,7 +170,8 @@ int ensemble_nblocks(uint64_t n);
 // vehicle control step, TX frames, VehicleInfo export (kernels_ctrl.hip)
 int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
                            const uint8_t *mask, hipStream_t st);
-int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hipStream_t st);
+int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
+                     hipStream_t st);
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st);
 // the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,

@@ -256,11 +256,14 @@ struct CtrlLane {
 };
 
 // The per-tick control step.  rpm [N][4] int16 (MOTOR_IF_M2006::Status.s16_rawSpeedRpm).
+// rstride: robot i's four rpm at rpm + 4 * rstride * i (1: [N][4] planes; 2: the rpm field of
+// 16-byte fmskf_kf6_record's)
 template <bool SMALL>
-__global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, const int16_t *rpm) {
+__global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, const int16_t *rpm,
+                                                      uint32_t rstride) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)c.n) return;
-  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[i];
+  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[(uint64_t)i * rstride];
   CtrlLane<SMALL> L;
   L.load(c, i);
   L.step(c, p, i, rw);
@@ -383,12 +386,13 @@ int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl,
   return (int)hipGetLastError();
 }
 
-int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, hipStream_t st) {
+int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
+                     hipStream_t st) {
   if (c.n == 0) return 0;
   if (c.pitch * 4 * 4 * kPidF < 0xFFFFFFFFull)
-    k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
+    k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
   else
-    k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm);
+    k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
   return (int)hipGetLastError();
 }
 

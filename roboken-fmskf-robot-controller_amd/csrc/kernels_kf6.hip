@@ -26,9 +26,12 @@
 
 namespace fmskf {
 
-template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_>
+// REC: the inputs come as 16-byte fmskf_kf6_record's (one 16-byte load per lane) instead of
+// the yaw / gyro / rpm planes (three loads): measured 41.6 -> 39.5 us per tick at 2^20
+template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false>
 struct Opt {
-  static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_;
+  static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_,
+                        REC = REC_;
 };
 
 struct Kf6In {
@@ -56,6 +59,18 @@ template <class O>
 __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint64_t t, uint32_t i) {
   const uint64_t tb = t * in.stride;
   Kf6In m;
+  if constexpr (O::REC) {
+    const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc(in.rec + tb * 4, n * 16), i * 16u, 0,
+                                                         FMSKF_IN_CPOL);
+    // bit_cast a prvalue copy: on a vector-element lvalue clang's __builtin_bit_cast reads
+    // element 0 (measured: r[1] came back as r[0])
+    const uint32_t w0 = r[0], w1 = r[1];
+    m.yaw = __builtin_bit_cast(float, w0);
+    m.gz = __builtin_bit_cast(float, w1);
+    m.rpm = make_uint2(r[2], r[3]);
+    m.valid = O::VALID ? (uint32_t)in.valid[tb + i] : 1u;
+    return m;
+  }
   m.yaw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                         rsrc(in.yaw_deg + tb, n * 4), i * 4u, 0, FMSKF_IN_CPOL));
   m.gz = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -295,15 +310,20 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   }
 }
 
+template <bool LIBM, bool UPD, bool PRED, bool REC>
+static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st) {
+  if (small) {
+    if (valid) launch_o<Opt<LIBM, UPD, PRED, true, true, REC>>(a, st);
+    else launch_o<Opt<LIBM, UPD, PRED, true, false, REC>>(a, st);
+  } else {
+    if (valid) launch_o<Opt<LIBM, UPD, PRED, false, true, REC>>(a, st);
+    else launch_o<Opt<LIBM, UPD, PRED, false, false, REC>>(a, st);
+  }
+}
 template <bool LIBM, bool UPD, bool PRED>
 static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st) {
-  if (small) {
-    if (valid) launch_o<Opt<LIBM, UPD, PRED, true, true>>(a, st);
-    else launch_o<Opt<LIBM, UPD, PRED, true, false>>(a, st);
-  } else {
-    if (valid) launch_o<Opt<LIBM, UPD, PRED, false, true>>(a, st);
-    else launch_o<Opt<LIBM, UPD, PRED, false, false>>(a, st);
-  }
+  if (UPD && a.in.rec) launch_lupr<LIBM, UPD, PRED, UPD>(a, small, valid, st);
+  else launch_lupr<LIBM, UPD, PRED, false>(a, small, valid, st);
 }
 
 int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool libm, bool upd,

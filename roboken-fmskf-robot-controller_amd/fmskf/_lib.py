@@ -26,7 +26,7 @@ OK, EINVAL, ENOMEM, EDEVICE, ERCCL, ENOTSUP = range(6)
 MODEL_RS, MODEL_KF6, MODEL_EKF9, MODEL_KF12D = range(4)
 TRIG_TABLE512, TRIG_LIBM = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MODEL_NAMES = {"rs": MODEL_RS, "kf6": MODEL_KF6, "ekf9": MODEL_EKF9, "kf12d": MODEL_KF12D}
 
@@ -64,6 +64,7 @@ class TickInputs(C.Structure):
         ("raw", C.c_void_p),
         ("z", C.c_void_p),
         ("valid", C.c_void_p),
+        ("kf6_rec", C.c_void_p),
     ]
 
 

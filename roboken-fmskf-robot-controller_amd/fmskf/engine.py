@@ -23,14 +23,35 @@ VEHICLE_INFO_DTYPE = np.dtype([("pos_x", "<i4"), ("pos_y", "<i4"), ("pos_theta",
                                ("imu_g", "<f4", 3), ("imu_a", "<f4", 3), ("floor", "u1", 8),
                                ("cam_pitch", "<f4"), ("fault", "<u4")])
 
+# fmskf_kf6_record (include/fmskf.h): one robot's KF6 tick record, 16 bytes
+KF6_RECORD_DTYPE = np.dtype([("yaw_deg", "<f4"), ("gyro_z_dps", "<f4"), ("rpm", "<i2", 4)])
+
 _DTYPES = {
     "yaw_deg": np.float32, "gyro_z_dps": np.float32, "rpm": np.int16, "angle_sum": np.int64,
-    "raw": np.int16, "z": np.float64, "valid": np.uint8,
+    "raw": np.int16, "z": np.float64, "valid": np.uint8, "kf6_rec": np.int32,
 }
 
 
 # elements per instance-tick of each input (fmskf_tick_inputs, include/fmskf.h)
-_PER_TICK = {"yaw_deg": 1, "gyro_z_dps": 1, "rpm": 4, "angle_sum": 4, "raw": 8, "z": 8, "valid": 1}
+_PER_TICK = {"yaw_deg": 1, "gyro_z_dps": 1, "rpm": 4, "angle_sum": 4, "raw": 8, "z": 8, "valid": 1,
+             "kf6_rec": 4}
+
+
+def kf6_records(yaw_deg, gyro_z_dps, rpm):
+    """Pack KF6 inputs ([..., N] yaw and gyro, [..., N, 4] rpm; numpy or torch) into
+    fmskf_kf6_record's: numpy -> [..., N] KF6_RECORD_DTYPE, torch -> [..., N, 4] int32."""
+    if _is_torch(yaw_deg):
+        import torch
+        rec = torch.empty(tuple(yaw_deg.shape) + (4,), dtype=torch.int32, device=yaw_deg.device)
+        rec[..., 0] = yaw_deg.view(torch.int32)
+        rec[..., 1] = gyro_z_dps.view(torch.int32)
+        rec[..., 2:] = rpm.contiguous().view(torch.int32)
+        return rec
+    rec = np.empty(np.shape(yaw_deg), KF6_RECORD_DTYPE)
+    rec["yaw_deg"] = yaw_deg
+    rec["gyro_z_dps"] = gyro_z_dps
+    rec["rpm"] = rpm
+    return rec
 
 
 def _is_torch(a) -> bool:
@@ -174,8 +195,10 @@ class Engine:
         if unknown:
             raise TypeError(f"unknown tick inputs: {sorted(unknown)}")
         stride = self.n if stride is None else stride
-        for name in ("yaw_deg", "gyro_z_dps", "rpm", "angle_sum", "raw", "z", "valid"):
+        for name in ("yaw_deg", "gyro_z_dps", "rpm", "angle_sum", "raw", "z", "valid", "kf6_rec"):
             v = kw.get(name)
+            if name == "kf6_rec" and isinstance(v, np.ndarray) and v.dtype.names:
+                v = np.ascontiguousarray(v).view(np.int32)
             if v is not None:
                 # the C ABI takes bare pointers: check extents here, before the kernel reads
                 need = ((int(n_ticks) - 1) * int(stride) + self.n) * _PER_TICK[name]

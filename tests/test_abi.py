@@ -115,3 +115,24 @@ def test_host_ensemble_combine_matches_oracle(orc):
     np.testing.assert_allclose(cov, c2, rtol=1e-10)
     ref = np.cov(x.astype(np.float64))
     np.testing.assert_allclose(cov[[0, 2, 5, 9, 14, 20]], np.diag(ref), rtol=1e-10)
+
+
+def test_c_struct_layouts_match_python_mirror(tmp_path):
+    """The C compiler's layout of the ABI structs (include/fmskf.h) equals the ctypes / numpy
+    mirrors: fmskf_kf6_record 16 bytes, fmskf_tick_inputs with kf6_rec last."""
+    import subprocess
+    from fmskf import _lib
+    from fmskf.engine import KF6_RECORD_DTYPE
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "fmskf.h"\nint main(void){'
+                   'printf("%zu %zu %zu %zu %zu\\n", sizeof(fmskf_kf6_record), '
+                   'offsetof(fmskf_kf6_record, rpm), sizeof(fmskf_tick_inputs), '
+                   'offsetof(fmskf_tick_inputs, kf6_rec), sizeof(fmskf_vehicle_info)); return 0;}\n')
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    assert got == [16, 8, C.sizeof(_lib.TickInputs), _lib.TickInputs.kf6_rec.offset,
+                   C.sizeof(_lib.VehicleInfo)]
+    assert KF6_RECORD_DTYPE.itemsize == 16 and KF6_RECORD_DTYPE.fields["rpm"][1] == 8

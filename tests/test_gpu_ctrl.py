@@ -200,7 +200,8 @@ def test_reset_zeroes_control_state():
         assert not e.get_ctrl()["curr"].any()
 
 
-@pytest.mark.parametrize("model,n,T", [("rs", 3001, 200), ("rs", 1, 30), ("kf6", 1000, 60)])
+@pytest.mark.parametrize("model,n,T", [("rs", 3001, 200), ("rs", 1, 30), ("kf6", 1000, 60),
+                                       ("kf6rec", 999, 40)])
 def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
     """fmskf_isr_tick (the firmware ISR in one call; one fused kernel for RS) leaves the
     estimator state, the control state and the 0x200 frames bit-identical to fmskf_tick +
@@ -212,9 +213,15 @@ def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
     if model == "rs":
         yaw, sums, rpm = tr.rs_inputs()
         kw = [dict(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t]) for t in range(T)]
-    else:
+    elif model == "kf6":
         yaw, gz, rpm = tr.kf6_inputs()
         kw = [dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t]) for t in range(T)]
+    else:  # KF6 fed 16-byte records: the control step reads the records' rpm field
+        from fmskf import kf6_records
+        yaw, gz, rpm = tr.kf6_inputs()
+        rec = kf6_records(yaw, gz, rpm)
+        kw = [dict(kf6_rec=rec[t]) for t in range(T)]
+        model = "kf6"
     ref = orc.CtrlBatch(n)
     pos = np.zeros((3, n), np.float32)
     vel = np.zeros((3, n), np.float32)
@@ -227,7 +234,7 @@ def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
                 (ref.set_target_vel(*pl) if kind == "target" else ref.set_power(pl))
             fa = a.isr_tick(**kw[t]) if t % 7 else a.isr_tick(frames=False, **kw[t])
             b.tick(**kw[t])
-            b.control(rpm[t])
+            b.control(rpm[t])  # the plane rpm: equal to the records' field
             fb = b.can_tx()
             if t % 7:
                 np.testing.assert_array_equal(fa, fb)

@@ -122,6 +122,49 @@ def test_kf6_split_equals_fused_and_many():
     bits_equal(Pa, Pc, "many P")
 
 
+@pytest.mark.parametrize("n,trig", [(1, TABLE), (3001, TABLE), (777, LIBM)])
+def test_kf6_records_bitexact(orc, n, trig):
+    """fmskf_kf6_record inputs (one 16-byte load per lane) against the oracle, against the
+    plane inputs, with a validity mask; tick_many over [T][N] records; host and device."""
+    import torch
+    T = 30
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 77 + n)
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    assert rec.shape == (T, n) and rec.dtype.itemsize == 16
+    drec = fmskf.kf6_records(*(torch.from_numpy(v).cuda() for v in (yaw, gz, rpm)))
+    assert torch.equal(drec.cpu().view(torch.uint8).reshape(T, n, 16),
+                       torch.from_numpy(rec.view(np.uint8).reshape(T, n, 16)))
+    with Engine("kf6", n, trig=trig) as a, Engine("kf6", n, trig=trig) as b, \
+            Engine("kf6", n, trig=trig) as c, Engine("kf6", n, trig=trig) as d:
+        for t in range(T):
+            a.tick(kf6_rec=rec[t], valid=valid[t])
+            b.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+            d.tick(kf6_rec=drec[t], valid=torch.from_numpy(valid[t]).cuda())
+        c.tick_many(T, kf6_rec=rec, valid=valid)
+        torch.cuda.synchronize()
+        (xa, Pa), (xb, Pb), (xc, Pc), (xd, Pd) = (e.get_state() for e in (a, b, c, d))
+    for x, P, what in ((xb, Pb, "planes"), (xc, Pc, "tick_many"), (xd, Pd, "device")):
+        bits_equal(xa, x, "x vs " + what)
+        bits_equal(Pa, P, "P vs " + what)
+    if trig == TABLE:
+        xo, Po = _kf6_oracle(orc, n, yaw, gz, rpm, valid, orc.TRIG_TABLE512, T)
+        bits_equal(xa, xo, "x vs oracle")
+        bits_equal(Pa, Po, "P vs oracle")
+
+
+def test_kf6_records_rejected_where_ambiguous():
+    n = 64
+    rec = fmskf.kf6_records(np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros((n, 4), np.int16))
+    with Engine("kf6", n) as e:
+        with pytest.raises(fmskf.FmskfError):
+            e.tick(kf6_rec=rec, yaw_deg=np.zeros(n, np.float32))
+        with pytest.raises(ValueError):
+            e.tick(kf6_rec=rec[: n - 1])
+    with Engine("rs", n) as e:
+        with pytest.raises(fmskf.FmskfError):
+            e.tick(kf6_rec=rec)
+
+
 def test_kf6_device_inputs_torch():
     import torch
     n, T = 4099, 5

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--ticks", type=int, default=300)
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
+    ap.add_argument("--packed", action="store_true", help="KF6: fmskf_kf6_record inputs")
+    ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
     ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
@@ -39,7 +41,20 @@ def main():
     st = torch.cuda.current_stream()
     e.set_stream(st)
     yaw, gz, rpm = kf6_ring_torch(n, R, device=dev)
-    if args.model == "kf6":
+    if args.pad:  # input planes at a padded per-tick pitch, each array's base staggered
+        def padded(t, k):
+            T = t.shape[0]
+            w = (n + args.pad) * t[0].numel() // n
+            buf = torch.empty(T * w + k * 4096, dtype=t.dtype, device=dev)
+            v = buf[k * 4096:].view(T, w)[:, : t[0].numel()]
+            v.copy_(t.reshape(T, -1))
+            return v.view(t.shape)
+        yaw, gz, rpm = padded(yaw, 1), padded(gz, 2), padded(rpm, 3)
+    if args.model == "kf6" and args.packed:  # 16-byte fmskf_kf6_record inputs
+        rec = fmskf.kf6_records(yaw, gz, rpm)
+        preps = [e.prepare(kf6_rec=rec[r]) for r in range(R)]
+        many = dict(kf6_rec=rec)
+    elif args.model == "kf6":
         preps = [e.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
         many = dict(yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
     elif args.model == "rs":

@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void k_pat2(float *st, const float *yaw, const
   if constexpr (MODE == 4) {
     const uint32_t i = (uint32_t)vc;
     const auto r = __builtin_amdgcn_raw_buffer_load_b128(mk_rsrc(yaw, n * 16), i * 16u, 0, 2);
-    m = m * __builtin_bit_cast(float, r[0]) * __builtin_bit_cast(float, r[1]) * (float)(r[2] & 1);
+    const uint32_t w0 = r[0], w1 = r[1];  // bit_cast of a vector-element lvalue reads element 0
+    m = m * __builtin_bit_cast(float, w0) * __builtin_bit_cast(float, w1) * (float)(r[2] & 1);
   } else if constexpr (MODE == 1) {
     m = m * yaw[vc] * gz[vc] * (float)(rpm[vc].x & 1);
   } else if constexpr (MODE >= 2) {

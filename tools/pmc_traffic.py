@@ -7,7 +7,7 @@ state planes read + written, yaw/gyro dword planes and the [N][4] int16 rpm plan
 232 B per instance) with no arithmetic.  Its counter readings divided by its known bytes
 give the correction factors, applied to the tick kernel's readings.
 
-  python tools/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json]
+  python tools/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json] [records|planes]
 """
 import csv
 import glob
@@ -29,7 +29,9 @@ def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     out = sys.argv[2] if len(sys.argv) > 2 else None
     n = 1 << 20
-    res = {"n_instances": n, "kernel": "k_kf6 (tick, TABLE512, N=2^20)", "unit": "bytes per launch"}
+    inputs = sys.argv[3] if len(sys.argv) > 3 else "records"
+    res = {"n_instances": n, "kernel": "k_kf6 (tick, TABLE512, N=2^20)", "inputs": inputs,
+           "unit": "bytes per launch"}
     for c, algo in (("FETCH_SIZE", 124 * n), ("WRITE_SIZE", 108 * n)):
         pat = read(os.path.join(root, f"pmc_pat_{c}"), "k_pattern<1>")
         kf = read(os.path.join(root, f"pmc_kf6_{c}"), "k_kf6")

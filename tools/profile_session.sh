@@ -26,7 +26,7 @@ run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof"
   python bench.py --steps 400 --warmup 40 --no-cpu-baseline --no-fused
 for c in FETCH_SIZE WRITE_SIZE; do
   run pmc_kf6_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_kf6_$c" -o run -- \
-    python tools/kbench.py --ticks 30
+    python tools/kbench.py --ticks 30 --packed
   run pmc_pat_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_pat_$c" -o run -- \
     build/membench 20
 done
