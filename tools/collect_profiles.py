@@ -1,0 +1,64 @@
+"""Copy the profiling session's outputs (tools/profile_session.sh, PROF_ALL=1) from gpurun_out/
+into profiles/ under a round prefix:  python tools/collect_profiles.py r1"""
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "gpurun_out")
+P = os.path.join(ROOT, "profiles")
+
+
+def last_json(path):
+    for line in reversed(open(path).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no JSON line in {path}")
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
+    json.dump(last_json(os.path.join(G, "bench.log")), open(os.path.join(P, f"{tag}_bench.json"), "w"), indent=1)
+    json.dump(last_json(os.path.join(G, "prof.log")), open(os.path.join(P, f"{tag}_prof_bench_line.json"), "w"),
+              indent=1)
+    for k in ("kernel_stats", "domain_stats"):
+        shutil.copy(os.path.join(G, "prof", f"run_{k}.csv"), os.path.join(P, f"{tag}_bench_{k}.csv"))
+    with open(os.path.join(G, "prof", "run_kernel_trace.csv")) as fi, \
+            open(os.path.join(P, f"{tag}_bench_kernel_trace_fmskf.csv"), "w", newline="") as fo:
+        r = csv.reader(fi)
+        w = csv.writer(fo)
+        hdr = next(r)
+        w.writerow(hdr)
+        col = hdr.index("Kernel_Name")
+        for row in r:
+            if "fmskf::" in row[col]:
+                w.writerow(row)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for kind in ("kf6", "pat"):
+            src = glob.glob(os.path.join(G, f"pmc_{kind}_{c}", "**", "*counter_collection.csv"), recursive=True)[0]
+            shutil.copy(src, os.path.join(P, f"{tag}_pmc_{'kf6' if kind == 'kf6' else 'pattern'}_{c}.csv"))
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), G,
+                    os.path.join(P, "pmc_traffic.json"), "records"], check=True, stdout=subprocess.DEVNULL)
+    rows = []
+    for d in sorted(glob.glob(os.path.join(G, "prof_*"))):
+        if not os.path.isdir(d):
+            continue
+        f = glob.glob(os.path.join(d, "*kernel_stats.csv"))
+        if not f:
+            continue
+        for r in csv.DictReader(open(f[0])):
+            if "fmskf::" in r["Name"]:
+                rows.append([os.path.basename(d)[5:], r["Name"], r["Calls"], r["AverageNs"], r["MinNs"], r["MaxNs"]])
+    with open(os.path.join(P, f"{tag}_secondary_kernel_stats.csv"), "w", newline="") as fo:
+        w = csv.writer(fo)
+        w.writerow(["workload", "kernel", "calls", "avg_ns", "min_ns", "max_ns"])
+        w.writerows(rows)
+    print(f"profiles/{tag}_* refreshed: {len(rows)} secondary kernel rows")
+
+
+if __name__ == "__main__":
+    main()

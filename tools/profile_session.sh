@@ -34,7 +34,9 @@ echo "=== session done"
 # secondary rows: every tick model and the rows either side of the tick, one rocprofv3 kernel
 # trace each (PROF_ALL=1)
 if [ "${PROF_ALL:-0}" = 1 ]; then
-  for spec in "kf6_2p24:--model kf6 --n 16777216 --ticks 20" "ekf9:--model ekf9 --ticks 100" \
+  for spec in "kf6_2p24:--model kf6 --packed --n 16777216 --ticks 20" "kf6_planes:--model kf6 --ring 64 --ticks 200" \
+              "kf6_2p21:--model kf6 --packed --n 2097152 --ticks 100" "isr_rs:--model rs --op isr --ticks 200" \
+              "ekf9:--model ekf9 --ticks 100" \
               "ekf9_2p22:--model ekf9 --n 4194304 --ticks 30" "kf12d:--model kf12d --ticks 30" \
               "rs:--model rs --ticks 200" "control:--op control --ticks 100" \
               "wt901:--op wt901 --ticks 50" "can:--op can --ticks 100" "ensemble:--op ensemble --ticks 100" \
