@@ -310,7 +310,21 @@ void do_reset(fmskf_ctx *h) {
   hipStream_t st = h->stream;
   const uint64_t pp = s.pitch;
   hip_check(hipMemsetAsync(s.x, 0, (size_t)d.nx * pp * d.elem, st), "reset x");
-  if (d.m > 0) {
+  if (d.m > 0 && s.tile) {  // tiled P: every row filled with its P0 entry in one pass
+    std::vector<uint64_t> bits(np);
+    for (uint32_t k = 0; k < np; k++) {
+      const double v = h->cfg.p0[k];
+      if (d.elem == 4) {
+        const float f = (float)v;
+        uint32_t b;
+        memcpy(&b, &f, 4);
+        bits[k] = b;
+      } else {
+        memcpy(&bits[k], &v, 8);
+      }
+    }
+    launch_check(launch_tiled_fill(s.P, np, n, bits.data(), d.elem, st), "reset P0");
+  } else if (d.m > 0) {
     hip_check(hipMemsetAsync(s.P, 0, (size_t)np * pp * d.elem, st), "reset P");
     for (uint32_t i = 0; i < d.nx; i++) {
       for (uint32_t j = 0; j <= i; j++) {
@@ -544,6 +558,7 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.model = cfg->model;
       const uint32_t np = d.nx * (d.nx + 1) / 2;
       s.pitch = plane_pitch(n);
+      s.tile = FMSKF_TILED && (cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D) ? kTile : 0;
       s.x = h->alloc<char>((size_t)d.nx * s.pitch * d.elem);
       s.P = d.m ? h->alloc<char>((size_t)np * s.pitch * d.elem) : nullptr;
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
@@ -762,10 +777,24 @@ int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem) {
     const uint64_t n = h->s.n;
     const Dims d = h->d;
     const size_t row = (size_t)n * d.elem, pb = (size_t)h->s.pitch * d.elem;
-    copy_planes_out(h, x, h->s.x, row, pb, d.nx, mem);
-    if (p_packed) {
-      if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
-      copy_planes_out(h, p_packed, h->s.P, row, pb, d.nx * (d.nx + 1) / 2, mem);
+    const uint32_t np = d.nx * (d.nx + 1) / 2;
+    if (p_packed && !d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
+    if (h->s.tile) {  // tiled state: gather into dense planes (device), then copy
+      if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+      auto out = [&](void *dst, const void *src, uint32_t rows) {
+        if (!dst) return;
+        void *dense = mem == FMSKF_MEM_DEVICE ? dst : h->out_for(row * rows);
+        launch_check(launch_untile(src, dense, rows, n, d.elem, h->stream), "untile");
+        if (mem == FMSKF_MEM_HOST) {
+          copy_out(h, dst, dense, row * rows, mem);
+          hip_check(hipStreamSynchronize(h->stream), "get_state sync");  // scratch reused next
+        }
+      };
+      out(x, h->s.x, d.nx);
+      if (p_packed) out(p_packed, h->s.P, np);
+    } else {
+      copy_planes_out(h, x, h->s.x, row, pb, d.nx, mem);
+      if (p_packed) copy_planes_out(h, p_packed, h->s.P, row, pb, np, mem);
     }
     finish_out(h, mem);
   });
@@ -779,10 +808,25 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
     const Dims d = h->d;
     if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
     const size_t row = (size_t)n * d.elem, pb = (size_t)h->s.pitch * d.elem;
-    if (x) copy_planes_in(h, h->s.x, x, row, pb, d.nx, mem);
-    if (p_packed) {
-      if (!d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
-      copy_planes_in(h, h->s.P, p_packed, row, pb, d.nx * (d.nx + 1) / 2, mem);
+    const uint32_t np = d.nx * (d.nx + 1) / 2;
+    if (p_packed && !d.m) fail(FMSKF_ENOTSUP, "RS model has no covariance");
+    if (h->s.tile) {  // dense planes (staged to the device when on the host) -> tiled state
+      auto in = [&](void *dst, const void *src, uint32_t rows) {
+        if (!src) return;
+        const void *dense = src;
+        if (mem == FMSKF_MEM_HOST) {
+          void *stg = h->stage_for(row * rows);
+          hip_check(hipMemcpyAsync(stg, src, row * rows, hipMemcpyHostToDevice, h->stream), "stage H2D");
+          dense = stg;
+        }
+        launch_check(launch_tile(dense, dst, rows, n, d.elem, h->stream), "tile");
+        if (mem == FMSKF_MEM_HOST) hip_check(hipStreamSynchronize(h->stream), "set_state sync");
+      };
+      in(h->s.x, x, d.nx);
+      if (p_packed) in(h->s.P, p_packed, np);
+    } else {
+      if (x) copy_planes_in(h, h->s.x, x, row, pb, d.nx, mem);
+      if (p_packed) copy_planes_in(h, h->s.P, p_packed, row, pb, np, mem);
     }
     finish_out(h, mem);
   });

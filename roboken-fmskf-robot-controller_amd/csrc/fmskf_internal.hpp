@@ -17,6 +17,8 @@ struct DevState {
   // large power of two (see plane_pitch): power-of-two plane strides alias in the
   // memory-side cache / channel hash and cost ~20% of bandwidth at N = 2^20 (membench).
   uint64_t pitch = 0;
+  // 0: x / P are planar [rows][pitch]; kTile: tiled [ceil(N/kTile)][rows][kTile] (EKF9, KF12D)
+  uint32_t tile = 0;
   uint32_t model = 0;
   // estimator state: x [nx][pitch], P [np][pitch] (element type float, or double for KF12D);
   // RS: x = (px, py, th, vx, vy, vth) floats
@@ -144,6 +146,21 @@ struct CtrlPrm {
 // 1 KiB (fp32) between planes
 inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; }
 
+// Tiled state layout ("AoSoA"): instance i's row k at ((i / kTile) * rows + k) * kTile + i % kTile.
+// One tile = one 256-thread block, so a block's (and a wave's) rows form one contiguous span
+// and the tile base is wave-uniform.  tools/membench.hip (random data): EKF9's 54 rows at 2^22
+// 374.6 -> 353.6 us, KF12D's 90 fp64 rows 313 -> 295 us at 2^20 and 1203 -> 1165 at 2^22; the
+// 27 KF6 rows gain nothing measurable (36.3 vs 36.0 at 2^20), so KF6 / RS stay planar.  The
+// allocation (rows x plane_pitch) always covers ceil(N / kTile) tiles.
+constexpr uint32_t kTile = kBlock;
+#ifndef FMSKF_TILED
+#define FMSKF_TILED 1
+#endif
+__host__ __device__ inline uint64_t st_at(uint32_t tile, uint64_t pitch, uint32_t rows, uint32_t k,
+                                          uint64_t i) {
+  return tile ? ((i / tile) * rows + k) * tile + i % tile : k * pitch + i;
+}
+
 struct Wt901Cfg {
   uint32_t read_reg_index;
 };
@@ -180,6 +197,14 @@ int launch_vehicle_info(const DevState &s, const float *readout, void *out, cons
                         const float *cam_pitch, const uint32_t *fault, hipStream_t st);
 // readout helpers
 int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st);
+// tiled state arrays (kernels_misc.hip): fill row k with bits[k] (elem 4 or 8 bytes); convert
+// between the tiled array (rows x N) and dense [rows][N] planes
+int launch_tiled_fill(void *base, uint32_t rows, uint64_t n, const uint64_t *bits, uint32_t elem,
+                      hipStream_t st);
+int launch_untile(const void *tiled, void *dense, uint32_t rows, uint64_t n, uint32_t elem,
+                  hipStream_t st);
+int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint32_t elem,
+                hipStream_t st);
 // pose / body velocity readout as float planes: out [6][N] = x, y, th, vx_body_mmps, vy_body_mmps, w
 int launch_readout(const DevState &s, float *out, hipStream_t st);
 

@@ -92,10 +92,19 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
     return a.in.valid == nullptr || a.in.valid[(uint64_t)t * st + ic];
   };
   float x[N], P[NP];
+  const TileRows<float, N> tx(a.x, tile_slot(n));
+  const TileRows<float, NP> tp(a.P, tile_slot(n));
+  if constexpr (FMSKF_TILED) {
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
+    for (int k = 0; k < N; k++) x[k] = tx.ld(k);
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+    for (int k = 0; k < NP; k++) P[k] = tp.ld(k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
+#pragma unroll
+    for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+  }
   uint4 ra = raw_at(0), rb;
   bool ha = have_at(0), hb;
   for (uint32_t t = 0; t < T; t += 2) {
@@ -112,10 +121,17 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
     ekf9_tick1<LIBM, UPD, PRED>(a, rb, hb, stab, x, P);
   }
   if (live) {
+    if constexpr (FMSKF_TILED) {
 #pragma unroll
-    for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+      for (int k = 0; k < N; k++) tx.st(k, x[k]);
 #pragma unroll
-    for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+      for (int k = 0; k < NP; k++) tp.st(k, P[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+#pragma unroll
+      for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+    }
   }
   nan_guard(x, P, a.counters, live);
 }
@@ -133,19 +149,35 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
   WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
+  const TileRows<float, N> tx(a.x, tile_slot(n));
+  const TileRows<float, NP> tp(a.P, tile_slot(n));
+  if constexpr (FMSKF_TILED) {
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
+    for (int k = 0; k < N; k++) x[k] = tx.ld(k);
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+    for (int k = 0; k < NP; k++) P[k] = tp.ld(k);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; k++) x[k] = a.x[k * pp + ic];
+#pragma unroll
+    for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
+  }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
   const uint4 raw = UPD ? reinterpret_cast<const uint4 *>(a.in.raw)[ic] : make_uint4(0, 0, 0, 0);
   tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED>(a, raw, have, stab, x, P);
   if (live) {
+    if constexpr (FMSKF_TILED) {
 #pragma unroll
-    for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+      for (int k = 0; k < N; k++) tx.st(k, x[k]);
 #pragma unroll
-    for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+      for (int k = 0; k < NP; k++) tp.st(k, P[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+#pragma unroll
+      for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+    }
   }
   nan_guard(x, P, a.counters, live);
 }
@@ -159,10 +191,11 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   double x[N], P[NP];
+  const uint32_t tl = FMSKF_TILED ? kTile : 0;
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = a.x[k * pp + i];
+  for (int k = 0; k < N; k++) x[k] = a.x[st_at(tl, pp, N, k, i)];
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + i];
+  for (int k = 0; k < NP; k++) P[k] = a.P[st_at(tl, pp, NP, k, i)];
   const double dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t base = (uint64_t)t * a.in.stride * M;
@@ -198,9 +231,9 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
     }
   }
 #pragma unroll
-  for (int k = 0; k < N; k++) a.x[k * pp + i] = x[k];
+  for (int k = 0; k < N; k++) a.x[st_at(tl, pp, N, k, i)] = x[k];
 #pragma unroll
-  for (int k = 0; k < NP; k++) a.P[k * pp + i] = P[k];
+  for (int k = 0; k < NP; k++) a.P[st_at(tl, pp, NP, k, i)] = P[k];
   nan_guard(x, P, a.counters);
 }
 
@@ -309,10 +342,14 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
                                             vo, 0, 0);
     }
   };
+  // tiled layout (FMSKF_TILED): the block's tile through a scalar descriptor (lanes past N
+  // returned above, so a lane's slot is its thread index)
+  const TileRows<double, N> tx(a.x, threadIdx.x);
+  const TileRows<double, NP> tp(a.P, threadIdx.x);
 #pragma unroll
-  for (int k = 0; k < N; k++) x[k] = ld(rx, a.x, k);
+  for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
 #pragma unroll
-  for (int k = 0; k < NP; k++) P[k] = ld(rp, a.P, k);
+  for (int k = 0; k < NP; k++) P[k] = FMSKF_TILED ? tp.ld(k) : ld(rp, a.P, k);
   const double dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     if (UPD) {
@@ -337,9 +374,15 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   }
   asm volatile("" : "+s"(ps));  // the store offsets are recomputed here, not held from the loads
 #pragma unroll
-  for (int k = 0; k < N; k++) st(rx, a.x, k, x[k]);
+  for (int k = 0; k < N; k++) {
+    if constexpr (FMSKF_TILED) tx.st(k, x[k]);
+    else st(rx, a.x, k, x[k]);
+  }
 #pragma unroll
-  for (int k = 0; k < NP; k++) st(rp, a.P, k, P[k]);
+  for (int k = 0; k < NP; k++) {
+    if constexpr (FMSKF_TILED) tp.st(k, P[k]);
+    else st(rp, a.P, k, P[k]);
+  }
   nan_guard(x, P, a.counters);
 }
 
@@ -373,7 +416,7 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
                  hipStream_t st) {
   KfArgs<MdKF12D, Kf12dParams> a{s.n, s.pitch, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
-  const bool small = s.pitch * 8 * 78 < 0xFFFFFFFFull;
+  const bool small = FMSKF_TILED || s.pitch * 8 * 78 < 0xFFFFFFFFull;  // tiled: any N
   if (p.decor) {
     const bool blk = kf12d_sequential(p.r);
 #define KF12S(B, S)                                                          \

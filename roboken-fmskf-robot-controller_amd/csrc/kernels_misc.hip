@@ -8,6 +8,8 @@
 // all-gather and combine in rank order.  No atomics: bitwise reproducible run to run.
 // (A single-launch "last block folds" variant measured slower: the agent-scope release
 // fence each block needs writes back the XCD's whole L2.)
+#include <type_traits>
+
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
 
@@ -85,7 +87,7 @@ __device__ __forceinline__ void block_sum(const double (&v)[LEN], double (*red)[
 // loop) of its grid-stride instances and writes its record.
 template <int NX, typename T>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
-                                                        uint64_t pp, double *blocks) {
+                                                        uint64_t pp, uint32_t tile, double *blocks) {
   constexpr int LEN = EnsRec<NX>::LEN;
   constexpr int U = 4;
   __shared__ double red[kEnsCh][kBlock];
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
   __shared__ double tot[LEN];
   double sh[NX], v[LEN];
 #pragma unroll
-  for (int k = 0; k < NX; k++) sh[k] = (double)x[k * pp];
+  for (int k = 0; k < NX; k++) sh[k] = (double)x[st_at(tile, pp, NX, k, 0)];
 #pragma unroll
   for (int k = 0; k < LEN; k++) v[k] = 0.0;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
     for (int u = 0; u < U; u++) {
       const uint64_t i = i0 + u * stride;
 #pragma unroll
-      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[k * pp + i] : (T)0;
+      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[st_at(tile, pp, NX, k, i)] : (T)0;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
 // Fold (one block): thread t sums block records t, t + 256, ... in order, then the block sum,
 // then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
 template <int NX, typename T>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp,
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp, uint32_t tile,
                                                      const double *__restrict__ blocks,
                                                      int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, ui
     if (k == 0) {
       r = c;
     } else if (k <= NX) {
-      r = (double)x[(k - 1) * pp] + (c > 0.0 ? tot[k] / c : 0.0);
+      r = (double)x[st_at(tile, pp, NX, k - 1, 0)] + (c > 0.0 ? tot[k] / c : 0.0);
     } else {
       int p = 0, q = k - 1 - NX;
       while (q > p) q -= ++p;
@@ -170,8 +172,8 @@ int ensemble_nblocks(uint64_t n) {
 template <int NX, typename T>
 static void ens_launch(const DevState &s, double *blocks, double *out, hipStream_t st) {
   const int nb = ensemble_nblocks(s.n);
-  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
-  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.pitch, blocks, nb, out);
+  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, s.tile, blocks);
+  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.pitch, s.tile, blocks, nb, out);
 }
 
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
@@ -197,6 +199,58 @@ __global__ __launch_bounds__(kBlock) void k_fill64(uint64_t *p, uint64_t bits, u
   if (i < count) p[i] = bits;
 }
 
+// tiled rows x N arrays (fmskf_internal.hpp st_at): one thread per element of the tiled span
+struct RowBits {
+  uint64_t v[90];
+};
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tiled_fill(T *p, uint32_t rows, uint64_t total, RowBits b) {
+  const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= total) return;
+  const uint32_t k = (uint32_t)((e / kTile) % rows);
+  p[e] = __builtin_bit_cast(T, (typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type)b.v[k]);
+}
+template <typename T, bool TO_DENSE>
+__global__ __launch_bounds__(kBlock) void k_retile(const T *src, T *dst, uint32_t rows, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // instance
+  const uint32_t k = blockIdx.y;                                    // row
+  if (i >= n) return;
+  const uint64_t t = st_at(kTile, 0, rows, k, i), d = (uint64_t)k * n + i;
+  if (TO_DENSE) dst[d] = src[t];
+  else dst[t] = src[d];
+}
+
+int launch_tiled_fill(void *base, uint32_t rows, uint64_t n, const uint64_t *bits, uint32_t elem,
+                      hipStream_t st) {
+  if (n == 0) return 0;
+  if (rows > 90) return (int)hipErrorInvalidValue;
+  RowBits b{};
+  for (uint32_t k = 0; k < rows; k++) b.v[k] = bits[k];
+  const uint64_t total = (n + kTile - 1) / kTile * kTile * rows;
+  const dim3 g((unsigned)((total + kBlock - 1) / kBlock));
+  if (elem == 8) k_tiled_fill<double><<<g, kBlock, 0, st>>>((double *)base, rows, total, b);
+  else k_tiled_fill<float><<<g, kBlock, 0, st>>>((float *)base, rows, total, b);
+  return (int)hipGetLastError();
+}
+
+int launch_untile(const void *tiled, void *dense, uint32_t rows, uint64_t n, uint32_t elem,
+                  hipStream_t st) {
+  if (n == 0 || rows == 0) return 0;
+  const dim3 g((unsigned)((n + kBlock - 1) / kBlock), rows);
+  if (elem == 8) k_retile<double, true><<<g, kBlock, 0, st>>>((const double *)tiled, (double *)dense, rows, n);
+  else k_retile<float, true><<<g, kBlock, 0, st>>>((const float *)tiled, (float *)dense, rows, n);
+  return (int)hipGetLastError();
+}
+
+int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint32_t elem,
+                hipStream_t st) {
+  if (n == 0 || rows == 0) return 0;
+  const dim3 g((unsigned)((n + kBlock - 1) / kBlock), rows);
+  if (elem == 8) k_retile<double, false><<<g, kBlock, 0, st>>>((const double *)dense, (double *)tiled, rows, n);
+  else k_retile<float, false><<<g, kBlock, 0, st>>>((const float *)dense, (float *)tiled, rows, n);
+  return (int)hipGetLastError();
+}
+
 int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st) {
   if (count == 0) return 0;
   const dim3 g((unsigned)((count + kBlock - 1) / kBlock));
@@ -208,13 +262,18 @@ int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st) {
 // get_vehicle_vel_mmps_latest (body frame mm/s, mm/s, rad/s).  The KF6 / KF12D state
 // carries world-frame velocity in m/s: rotate by -theta (libm sin/cos, readout only).
 template <int MODEL>
-__global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, uint64_t pp, float *out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+__global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, uint64_t pitch, uint32_t tile,
+                                                    float *out) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i0 >= n) return;
+  // row k of this instance at [k * pp + i] (planar: pp = pitch, i = i0; tiled: pp = kTile)
+  constexpr uint32_t rows = MODEL == 2 ? 9 : MODEL == 3 ? 12 : 6;
+  const uint64_t i = tile ? st_at(tile, 0, rows, 0, i0) : i0;
+  const uint64_t pp = tile ? tile : pitch;
   if constexpr (MODEL == 0) {  // RS: x = px, py, th, vx, vy, vth (already reference units)
     const float *x = (const float *)xv;
 #pragma unroll
-    for (int k = 0; k < 6; k++) out[k * n + i] = x[k * pp + i];
+    for (int k = 0; k < 6; k++) out[k * n + i0] = x[k * pp + i];
   } else if constexpr (MODEL == 1 || MODEL == 3) {  // KF6 / KF12D base
     double px, py, th, vx, vy, w;
     if constexpr (MODEL == 1) {
@@ -225,30 +284,30 @@ __global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, 
       px = x[i]; py = x[pp + i]; th = x[2 * pp + i]; vx = x[3 * pp + i]; vy = x[4 * pp + i]; w = x[5 * pp + i];
     }
     const double c = cos(th), s = sin(th);
-    out[i] = (float)px;
-    out[n + i] = (float)py;
-    out[2 * n + i] = (float)th;
-    out[3 * n + i] = (float)((vx * c + vy * s) * 1000.0);
-    out[4 * n + i] = (float)((-vx * s + vy * c) * 1000.0);
-    out[5 * n + i] = (float)w;
+    out[i0] = (float)px;
+    out[n + i0] = (float)py;
+    out[2 * n + i0] = (float)th;
+    out[3 * n + i0] = (float)((vx * c + vy * s) * 1000.0);
+    out[4 * n + i0] = (float)((-vx * s + vy * c) * 1000.0);
+    out[5 * n + i0] = (float)w;
   } else {  // EKF9: body-frame velocity already
     const float *x = (const float *)xv;
-    out[i] = x[i];
-    out[n + i] = x[pp + i];
-    out[2 * n + i] = x[2 * pp + i];
-    out[3 * n + i] = x[3 * pp + i] * 1000.0f;
-    out[4 * n + i] = x[4 * pp + i] * 1000.0f;
-    out[5 * n + i] = x[5 * pp + i];
+    out[i0] = x[i];
+    out[n + i0] = x[pp + i];
+    out[2 * n + i0] = x[2 * pp + i];
+    out[3 * n + i0] = x[3 * pp + i] * 1000.0f;
+    out[4 * n + i0] = x[4 * pp + i] * 1000.0f;
+    out[5 * n + i0] = x[5 * pp + i];
   }
 }
 
 int launch_readout(const DevState &s, float *out, hipStream_t st) {
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   switch (s.model) {
-    case 0: k_readout<0><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
-    case 1: k_readout<1><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
-    case 2: k_readout<2><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
-    case 3: k_readout<3><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, out); break;
+    case 0: k_readout<0><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, s.tile, out); break;
+    case 1: k_readout<1><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, s.tile, out); break;
+    case 2: k_readout<2><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, s.tile, out); break;
+    case 3: k_readout<3><<<g, kBlock, 0, st>>>(s.x, s.n, s.pitch, s.tile, out); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

@@ -73,6 +73,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 
+// One tiled state array (ROWS rows, fmskf_internal.hpp st_at) as the calling block sees it:
+// the block's tile base is wave-uniform (a scalar descriptor), rows sit kTile elements apart
+// (a scalar offset per row), the lane offset is t * sizeof(T) with t the lane's slot in the
+// tile (lanes past N pass the last instance's slot).  Any N: the descriptor spans one tile.
+template <typename T, int ROWS>
+struct TileRows {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t vo;
+  __device__ __forceinline__ TileRows(T *base, uint32_t t)
+      : r(rsrc(base + (uint64_t)blockIdx.x * (ROWS * kTile), (uint64_t)ROWS * kTile * sizeof(T))),
+        vo(t * (uint32_t)sizeof(T)) {}
+  __device__ __forceinline__ T ld(int k) const {
+    if constexpr (sizeof(T) == 8)
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, vo, k * kTile * 8, 0));
+    else
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * kTile * 4, 0));
+  }
+  __device__ __forceinline__ void st(int k, T v) const {
+    if constexpr (sizeof(T) == 8)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * kTile * 8, 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * kTile * 4, 0);
+  }
+};
+// the lane's slot in its block's tile; lanes past N take the last instance's slot
+__device__ __forceinline__ uint32_t tile_slot(uint64_t n) {
+  const uint64_t b0 = (uint64_t)blockIdx.x * kTile;
+  return b0 + threadIdx.x < n ? threadIdx.x : (uint32_t)(n - 1 - b0);
+}
+
 template <class Md, typename Prm>
 struct KfArgs {
   uint64_t n;

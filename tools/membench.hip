@@ -201,6 +201,21 @@ __global__ __launch_bounds__(256) void k_ekf9_pattern(float *st, const uint4 *ra
   for (int k = 0; k < 54; k++) st[k * pitch + v] = s[k] + m;
 }
 
+// tiled ("AoSoA") state: [N/T][NS][T] -- a wave's NS rows are one contiguous NS*T*sizeof(T) span
+template <typename TT, int NS, int T>
+__global__ __launch_bounds__(256) void k_model_tiled(TT *st, const uint4 *raw, uint64_t n, TT sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  TT *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
+  TT s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = tile[k * T];
+  const uint4 r = raw[v];
+  const TT m = sink * (TT)(r.x & r.y & r.z & r.w & 1);
+#pragma unroll
+  for (int k = 0; k < NS; k++) tile[k * T] = s[k] + m;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -262,6 +277,10 @@ int main(int argc, char **argv) {
     };
     const unsigned g = (unsigned)((n + 255) / 256);
     tm("ekf9_pattern_448B", 448, [&] { k_ekf9_pattern<<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
+    tm("ekf9_tiled64_448B", 448, [&] { k_model_tiled<float, 54, 64><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("ekf9_tiled256_448B", 448, [&] { k_model_tiled<float, 54, 256><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_tiled256_232B", 232, [&] { k_model_tiled<float, 27, 256><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf12d_tiled64_1504B", 1504, [&] { k_model_tiled<double, 90, 64><<<g, 256>>>((double *)sb, (const uint4 *)ib, n, 0.0); });
     tm("kf12d_pattern_1504B", 1504, [&] {
       k_model_pattern<double, 90, 8><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
     });
