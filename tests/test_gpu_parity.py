@@ -544,3 +544,37 @@ def test_tick_ensemble_fused(orc, model, n):
     # same statistics as the stand-alone partial record of the same state
     mp, cp = fmskf.ensemble_combine(xb.shape[0], rp[None, :])
     np.testing.assert_allclose(mf, mp, rtol=1e-12, atol=1e-12)
+
+
+# ----------------------------------------------------------------------------- state layout
+@pytest.mark.parametrize("model,n", [("kf6", 1000), ("ekf9", 1), ("ekf9", 1000), ("kf12d", 257),
+                                     ("kf12d", 3 * 256), ("rs", 300)])
+def test_state_round_trip_and_reset(model, n):
+    """fmskf_set_state / get_state round-trip the dense planes bit for bit whatever the device
+    layout (tiled for EKF9 / KF12D, planar pitch for KF6 / RS), from host and from device
+    memory, at ragged N; fmskf_reset restores x = 0 and P = P0 in every row."""
+    import torch
+    rng = np.random.default_rng(n)
+    with Engine(model, n) as e:
+        nx, np_ = e.nx, e.np_
+        x = rng.normal(size=(nx, n)).astype(e.dtype)
+        P = rng.normal(size=(np_, n)).astype(e.dtype) if e.m else None
+        e.set_state(x, P)
+        gx, gP = e.get_state()
+        bits_equal(gx, x, "x host")
+        if P is not None:
+            bits_equal(gP, P, "P host")
+        x2 = (x * 2).astype(e.dtype)
+        e.set_state(torch.from_numpy(x2).cuda(), None)
+        torch.cuda.synchronize()
+        bits_equal(e.get_state()[0], x2, "x device")
+        if P is not None:
+            bits_equal(e.get_state()[1], P, "P kept")
+        pose = e.get_pose()
+        bits_equal(pose, x2[:3], "pose readout")
+        e.reset()
+        gx, gP = e.get_state()
+        assert not gx.any()
+        if P is not None:
+            p0 = np.array(fmskf.default_config(model, n).p0[:np_], dtype=e.dtype)
+            bits_equal(gP, np.repeat(p0[:, None], n, 1), "P0")
