@@ -302,6 +302,69 @@ void convert_params(fmskf_ctx *h) {
   h->kf12.decor = kf12d_cinv(h->kf12.r, h->kf12.cinv) ? 1 : 0;
 }
 
+// WT901 / IMU_IF state and M2006 motor state, allocated on first use (an ingest call, a NULL
+// input plane that reads them, a readout of them, or a graph capture) and zero-initialised like
+// the firmware's static objects
+void zero_imu(fmskf_ctx *h) {
+  DevState &s = h->s;
+  const uint64_t n = s.n;
+  hipStream_t st = h->stream;
+  hip_check(hipMemsetAsync(s.imu_reg, 0, 0x90 * n * 2, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_parser, 0, 3 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_cnt, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_flags, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_data, 0, 16 * n * 4, st), "reset imu");
+}
+void zero_motors(fmskf_ctx *h) {
+  DevState &s = h->s;
+  const uint64_t n = s.n;
+  hipStream_t st = h->stream;
+  hip_check(hipMemsetAsync(s.m_micro, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_angle, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * n * 8, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_dlt, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
+}
+void ensure_imu(fmskf_ctx *h) {
+  DevState &s = h->s;
+  if (s.imu_reg) return;
+  if (h->capturing) fail(FMSKF_EINVAL, "IMU state first used inside a graph capture");
+  const uint64_t n = s.n;
+  s.imu_reg = h->alloc<int16_t>(0x90 * n);
+  s.imu_parser = h->alloc<uint32_t>(3 * n);
+  s.imu_cnt = h->alloc<uint8_t>(n);
+  s.imu_flags = h->alloc<uint8_t>(n);
+  s.imu_err = h->alloc<uint8_t>(n);
+  s.imu_qinit = h->alloc<float>(4 * n);
+  s.imu_data = h->alloc<float>(16 * n);
+  zero_imu(h);
+}
+void ensure_motors(fmskf_ctx *h) {
+  DevState &s = h->s;
+  if (s.m_sum) return;
+  if (h->capturing) fail(FMSKF_EINVAL, "motor state first used inside a graph capture");
+  const uint64_t n = s.n;
+  s.m_micro = h->alloc<int16_t>(4 * n);
+  s.m_angle = h->alloc<int16_t>(4 * n);
+  s.m_rpm = h->alloc<int16_t>(4 * n);
+  s.m_curr = h->alloc<int16_t>(4 * n);
+  s.m_head = h->alloc<uint8_t>(4 * n);
+  s.m_sum = h->alloc<int64_t>(4 * n);
+  s.m_dlt = h->alloc<float>(4 * n);
+  s.m_speed = h->alloc<float>(4 * n);
+  s.m_iir_y = h->alloc<float>(4 * n);
+  s.m_iir_x = h->alloc<float>(4 * n);
+  zero_motors(h);
+}
+void ensure_ctrl(fmskf_ctx *h);
+
 void do_reset(fmskf_ctx *h) {
   DevState &s = h->s;
   const uint64_t n = s.n;
@@ -345,23 +408,8 @@ void do_reset(fmskf_ctx *h) {
     }
   }
   if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * pp * 8, st), "reset prev");
-  hip_check(hipMemsetAsync(s.imu_reg, 0, 0x90 * n * 2, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_parser, 0, 3 * n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_cnt, 0, n, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_flags, 0, n, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_data, 0, 16 * n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.m_micro, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_angle, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * n * 8, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_dlt, 0, 4 * n * 4, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
+  if (s.imu_reg) zero_imu(h);
+  if (s.m_sum) zero_motors(h);
   if (h->ctrl_ready) {  // the control objects are static in the firmware too: zero, power off
     const CtrlDev &c = h->ctrl;
     hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, st), "reset ctrl");
@@ -416,11 +464,15 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
     case FMSKF_MODEL_RS:
       if (need_upd) {
         dev_default(t.yaw_deg, "yaw_deg");
-        if (!t.yaw_deg) t.yaw_deg = s.imu_data + 11 * n;  // IMT::get_status_now_yaw
+        if (!t.yaw_deg) {
+          ensure_imu(h);
+          t.yaw_deg = s.imu_data + 11 * n;  // IMT::get_status_now_yaw
+        }
       }
       if (need_pred) {
         dev_default(t.rpm, "rpm");
         dev_default(t.angle_sum, "angle_sum");
+        if (!t.rpm || !t.angle_sum) ensure_motors(h);
         if (!t.rpm) t.rpm = s.m_rpm;
         if (!t.angle_sum) t.angle_sum = s.m_sum;
       }
@@ -430,6 +482,8 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.yaw_deg, "yaw_deg");
         dev_default(t.gyro_z, "gyro_z_dps");
         dev_default(t.rpm, "rpm");
+        if (!t.yaw_deg || !t.gyro_z) ensure_imu(h);
+        if (!t.rpm) ensure_motors(h);
         if (!t.yaw_deg) t.yaw_deg = s.imu_data + 11 * n;
         if (!t.gyro_z) t.gyro_z = s.imu_data + 5 * n;
         if (!t.rpm) t.rpm = s.m_rpm;
@@ -562,23 +616,8 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.x = h->alloc<char>((size_t)d.nx * s.pitch * d.elem);
       s.P = d.m ? h->alloc<char>((size_t)np * s.pitch * d.elem) : nullptr;
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
-      s.imu_reg = h->alloc<int16_t>(0x90 * n);
-      s.imu_parser = h->alloc<uint32_t>(3 * n);
-      s.imu_cnt = h->alloc<uint8_t>(n);
-      s.imu_flags = h->alloc<uint8_t>(n);
-      s.imu_err = h->alloc<uint8_t>(n);
-      s.imu_qinit = h->alloc<float>(4 * n);
-      s.imu_data = h->alloc<float>(16 * n);
-      s.m_micro = h->alloc<int16_t>(4 * n);
-      s.m_angle = h->alloc<int16_t>(4 * n);
-      s.m_rpm = h->alloc<int16_t>(4 * n);
-      s.m_curr = h->alloc<int16_t>(4 * n);
-      s.m_head = h->alloc<uint8_t>(4 * n);
-      s.m_sum = h->alloc<int64_t>(4 * n);
-      s.m_dlt = h->alloc<float>(4 * n);
-      s.m_speed = h->alloc<float>(4 * n);
-      s.m_iir_y = h->alloc<float>(4 * n);
-      s.m_iir_x = h->alloc<float>(4 * n);
+      // the WT901 / motor ingest state (~470 B per robot) is allocated on first use
+      // (ensure_imu / ensure_motors): a handle fed tick inputs by the caller holds only x, P
       s.counters = h->alloc<unsigned long long>(8);
       s.sintab = h->alloc<float>(513);
       h->ens_blocks = h->alloc<double>((size_t)ensemble_nblocks(n) * 91);
@@ -636,6 +675,10 @@ int fmskf_graph_begin(fmskf_handle h) {
     if (h->capturing) fail(FMSKF_EINVAL, "capture already open");
     if (h->timing) fail(FMSKF_EINVAL, "disable per-launch timing before capturing");
     DeviceGuard g(h->cfg.device);
+    // state that is allocated on first use must exist before the capture starts
+    ensure_imu(h);
+    ensure_motors(h);
+    ensure_ctrl(h);
     hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
               "hipStreamBeginCapture");
     h->capturing = true;
@@ -697,6 +740,7 @@ int fmskf_ingest_wt901(fmskf_handle h, const uint8_t *bytes, uint32_t stride, co
       for (uint64_t i = 0; i < n; i++)
         if (len[i] > stride) fail(FMSKF_EINVAL, "len[i] > stride");
     }
+    ensure_imu(h);
     Stager sg(h, mem);
     const void *b = bytes, *l = len;
     sg.add(&b, (size_t)stride * n);
@@ -715,6 +759,7 @@ int fmskf_ingest_can(fmskf_handle h, const uint8_t *frames, const int16_t *stamp
     if (!frames || !stamps) fail(FMSKF_EINVAL, "null frames/stamps");
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
+    ensure_motors(h);
     Stager sg(h, mem);
     const void *f = frames, *s = stamps, *p = present;
     sg.add(&f, n * 32);
@@ -846,6 +891,7 @@ int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem) 
   return guarded([&] {
     check_handle(h);
     DeviceGuard g(h->cfg.device);
+    ensure_imu(h);
     copy_out(h, data, h->s.imu_data, 16 * h->s.n * 4, mem);
     copy_out(h, is_error, h->s.imu_err, h->s.n, mem);
     finish_out(h, mem);
@@ -856,6 +902,7 @@ int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t
   return guarded([&] {
     check_handle(h);
     DeviceGuard g(h->cfg.device);
+    ensure_imu(h);
     copy_out(h, regs, h->s.imu_reg, 0x90 * h->s.n * 2, mem);
     copy_out(h, pending, h->s.imu_cnt, h->s.n, mem);
     finish_out(h, mem);
@@ -868,6 +915,7 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
+    ensure_motors(h);
     copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
@@ -1216,6 +1264,7 @@ int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem) {
       sg.add(&r, h->s.n * 8);
       sg.run();
     } else {
+      ensure_motors(h);
       r = h->s.m_rpm;
     }
     h->time_begin();
@@ -1263,6 +1312,7 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
         case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream); break;
       }
       launch_check(e, "tick kernel launch");
+      if (!t.rec && !t.rpm) ensure_motors(h);
       const int16_t *rpm = t.rec ? (const int16_t *)(t.rec + 2) : t.rpm ? t.rpm : h->s.m_rpm;
       launch_check(launch_ctrl_step(h->ctrl, p, rpm, t.rec ? 2 : 1, h->stream), "control launch");
       if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
@@ -1298,6 +1348,7 @@ int fmskf_export_vehicle_info(fmskf_handle h, fmskf_vehicle_info *out, const uin
     if (!out) fail(FMSKF_EINVAL, "null out");
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
+    ensure_imu(h);
     Stager sg(h, mem);
     const void *f = floor, *c = cam_pitch, *u = fault;
     sg.add(&f, n * 8);

@@ -58,9 +58,16 @@ __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
 template <class O>
 __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint64_t t, uint32_t i) {
   const uint64_t tb = t * in.stride;
+  // Past the SMALL range (N >= ~51M) descriptors start at the block's first instance hb
+  // (wave-uniform: every lane of a block, clamped ones included, lies in [hb, hb + 255]), so the
+  // 32-bit lane offsets stay below 4 KiB for any N up to the 2^30 cap (a lane offset of i * 16
+  // would wrap past 2^28 robots).  SMALL keeps the array-base form: ~0.2 us per 2^20 tick less.
+  const uint32_t hb = O::SMALL ? 0u : __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
+  const uint32_t li = i - hb;
+  const uint64_t base = tb + hb, left = n - hb;
   Kf6In m;
   if constexpr (O::REC) {
-    const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc(in.rec + tb * 4, n * 16), i * 16u, 0,
+    const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc(in.rec + base * 4, left * 16), li * 16u, 0,
                                                          FMSKF_IN_CPOL);
     // bit_cast a prvalue copy: on a vector-element lvalue clang's __builtin_bit_cast reads
     // element 0 (measured: r[1] came back as r[0])
@@ -72,10 +79,10 @@ __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint6
     return m;
   }
   m.yaw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                        rsrc(in.yaw_deg + tb, n * 4), i * 4u, 0, FMSKF_IN_CPOL));
+                                        rsrc(in.yaw_deg + base, left * 4), li * 4u, 0, FMSKF_IN_CPOL));
   m.gz = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                       rsrc(in.gyro_z + tb, n * 4), i * 4u, 0, FMSKF_IN_CPOL));
-  const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + tb * 4, n * 8), i * 8u, 0,
+                                       rsrc(in.gyro_z + base, left * 4), li * 4u, 0, FMSKF_IN_CPOL));
+  const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + base * 4, left * 8), li * 8u, 0,
                                                        FMSKF_IN_CPOL);
   m.rpm = make_uint2(rr[0], rr[1]);
   m.valid = O::VALID ? (uint32_t)in.valid[tb + i] : 1u;

@@ -139,3 +139,37 @@ def test_kf12d_2p18_sampled(orc):
     scale = np.maximum(np.abs(xo).max(axis=1, keepdims=True), 1e-3)
     assert (np.abs(x[:, idx] - xo) / scale).max() <= 1e-12
     assert (np.abs(P[:, idx] - Po) / max(np.abs(Po).max(), 1e-3)).max() <= 1e-12
+
+
+def test_kf6_records_and_planes_past_2p28(orc):
+    """N = 2^28 + 777 KF6 robots (29 GB of state; feasible because the ingest state is only
+    allocated on first use): record and plane inputs are addressed from each block's first
+    robot, so no 32-bit lane offset wraps (robot i's record sits at i * 16 B > 4 GiB here).
+    Both input forms give the same pose bit for bit; a sample matches the oracle."""
+    import torch
+    from fmskf.synth import kf6_ring_torch
+    n, T = (1 << 28) + 777, 2
+    yaw, gz, rpm = kf6_ring_torch(n, T, seed=5, device="cuda")
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    assert rec.numel() * 4 > 0xFFFFFFFF
+    with Engine("kf6", n) as e:
+        for t in range(T):
+            e.tick(kf6_rec=rec[t])
+        pose_rec = e.get_pose()
+        assert e.get_counters()[0] == 0
+        e.reset()
+        del rec
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])
+        pose_pl = e.get_pose()
+    np.testing.assert_array_equal(pose_rec.view(np.uint32), pose_pl.view(np.uint32))
+    idx = _sample(n, seed=3)
+    ys, gs, rs = (a[:, torch.from_numpy(idx).cuda()].cpu().numpy() for a in (yaw, gz, rpm))
+    cfg = fmskf.default_config("kf6", idx.size)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
+    xo = np.zeros((6, idx.size), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], idx.size, 1).copy()
+    for t in range(T):
+        orc.kf6_tick(xo, Po, np.ascontiguousarray(ys[t]), np.ascontiguousarray(gs[t]),
+                     np.ascontiguousarray(rs[t]), None, prm, nthreads=0)
+    np.testing.assert_array_equal(pose_rec[:, idx].view(np.uint32), xo[:3].view(np.uint32))
