@@ -389,7 +389,7 @@ int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl,
 int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
                      hipStream_t st) {
   if (c.n == 0) return 0;
-  if (c.pitch * 4 * 4 * kPidF < 0xFFFFFFFFull)
+  if (c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull)
     k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
   else
     k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
@@ -401,7 +401,7 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
   if (c.n == 0) return 0;
   const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum,
                     in.sintab, frames};
-  const bool small = c.pitch * 4 * 4 * kPidF < 0xFFFFFFFFull;
+  const bool small = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   if (libm) {
     if (small) k_isr_rs<true, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
     else k_isr_rs<true, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);

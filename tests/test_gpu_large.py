@@ -41,10 +41,13 @@ def test_kf6_past_the_buffer_window(orc):
     np.testing.assert_array_equal(P[:, idx].view(np.uint32), Po.view(np.uint32))
 
 
-def test_control_past_the_buffer_window(orc):
+@pytest.mark.parametrize("n", [36_000_000, 46_000_000])
+def test_control_past_the_buffer_window(orc, n):
+    """36M: the 36 interpolator planes (144 B per robot) pass 4 GiB while the 24 FF_PI_D planes
+    do not (the SMALL choice must follow the larger array); 46M: both pass."""
     import torch
-    n, T = 46_000_000, 40         # pitch * 4 B * 24 FF_PI_D planes > 4 GiB
-    assert fmskf_pitch(n) * 4 * 24 > 0xFFFFFFFF
+    T = 40
+    assert fmskf_pitch(n) * 4 * 36 > 0xFFFFFFFF
     g = torch.Generator(device="cuda").manual_seed(4)
     vel = torch.stack([torch.rand(n, generator=g, device="cuda") * 800 - 400,
                        torch.rand(n, generator=g, device="cuda") * 800 - 400,
