@@ -284,6 +284,69 @@ def test_ekf9_bitexact(orc):
     bits_equal(P, Po, "P")
 
 
+@pytest.mark.parametrize("n,T", [(1000, 9), (257, 4)])
+def test_ekf9_many_split_mask_bitexact(orc, n, T):
+    """EKF9 over the tiled state: T ticks in one tick_many launch (the ping-pong loop kernel,
+    odd T exercising its tail), per-tick ticks and correct-then-predict calls, all with a
+    validity mask at ragged N, bit-identical to each other and to the oracle."""
+    tr = Trajectory(n, T, seed=43)
+    raw = tr.ekf9_raw()
+    rng = np.random.default_rng(n)
+    valid = (rng.random((T, n)) > 0.2).astype(np.uint8)
+    cfg = fmskf.default_config("ekf9", n)
+    with Engine("ekf9", n) as a, Engine("ekf9", n) as b, Engine("ekf9", n) as c:
+        a.tick_many(T, raw=raw, valid=valid)
+        for t in range(T):
+            b.tick(raw=raw[t], valid=valid[t])
+            c.correct(raw=raw[t], valid=valid[t])
+            c.predict()
+        (xa, Pa), (xb, Pb), (xc, Pc) = (e.get_state() for e in (a, b, c))
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((9, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    for t in range(T):
+        orc.ekf9_tick(xo, Po, raw[t], valid[t], prm, nthreads=0)
+    for x, P, what in ((xa, Pa, "tick_many"), (xb, Pb, "tick"), (xc, Pc, "split")):
+        bits_equal(x, xo, "x " + what)
+        bits_equal(P, Po, "P " + what)
+
+
+def test_ekf9_libm_within_tolerance(orc):
+    n, T = 600, 30
+    tr = Trajectory(n, T, seed=44)
+    raw = tr.ekf9_raw()
+    cfg = fmskf.default_config("ekf9", n)
+    with Engine("ekf9", n, trig=LIBM) as e:
+        for t in range(T):
+            e.tick(raw=raw[t])
+        x, P = e.get_state()
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_LIBM)
+    xo = np.zeros((9, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    for t in range(T):
+        orc.ekf9_tick(xo, Po, raw[t], None, prm, nthreads=0)
+    # device sinf/cosf vs glibc differ by ulps; the north-star tolerance 1e-5 relative
+    for grp in [(0, 1), (2,), (3, 4), (5, 6), (7, 8)]:
+        rel_close(x[list(grp)], xo[list(grp)], 1e-5, f"x{grp}")
+    rel_close(P, Po, 1e-5, "P")
+
+
+def test_kf12d_many_equals_ticks():
+    """KF12D T ticks in one launch (state held in registers across ticks) == T single ticks,
+    with a validity mask, over the tiled state at ragged N."""
+    n, T = 513, 6
+    tr = Trajectory(n, T, seed=52)
+    z = np.ascontiguousarray(tr.kf12d_z())
+    valid = (np.random.default_rng(5).random((T, n)) > 0.25).astype(np.uint8)
+    with Engine("kf12d", n) as a, Engine("kf12d", n) as b:
+        a.tick_many(T, z=z, valid=valid)
+        for t in range(T):
+            b.tick(z=z[t], valid=valid[t])
+        (xa, Pa), (xb, Pb) = a.get_state(), b.get_state()
+    bits_equal(xa, xb, "x")
+    bits_equal(Pa, Pb, "P")
+
+
 KF12D_R_CASES = {
     # R positive definite -> decorrelated scalar-sequential update (canonical KF12D order)
     "blockdiag_R_decorrelated": {},
