@@ -6,8 +6,10 @@
 // order, and a one-block fold sums the per-block records in block order and converts them
 // to the Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]} that ranks
 // all-gather and combine in rank order.  No atomics: bitwise reproducible run to run.
-// (A single-launch "last block folds" variant measured slower: the agent-scope release
-// fence each block needs writes back the XCD's whole L2.)
+// (Single-launch "last block folds" variants measured slower: with plain stores, the
+// agent-scope release fence each block needs writes back the XCD's whole L2; with
+// write-through (sc1) record stores and sc1 loads in the folding block, 26.4 us against
+// 14.3 at 2^20: the one block's serialised record loads outlast the fold launch.)
 #include <type_traits>
 
 #include "fmskf_device.hpp"
@@ -85,9 +87,12 @@ __device__ __forceinline__ void block_sum(const double (&v)[LEN], double (*red)[
 // Partial: every block accumulates shifted moment sums S1 = sum(x - x0),
 // S2 = sum((x - x0)(x - x0)^T) (x0 = instance 0's state, fp64, no division in the streaming
 // loop) of its grid-stride instances and writes its record.
-template <int NX, typename T>
+// TILED (the EKF9 / KF12D state layout) is a compile-time choice: st_at then divides by the
+// constant kTile (shifts), not by a runtime value (a 64-bit division per load)
+template <int NX, typename T, bool TILED>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
-                                                        uint64_t pp, uint32_t tile, double *blocks) {
+                                                        uint64_t pp, double *blocks) {
+  constexpr uint32_t tile = TILED ? kTile : 0;
   constexpr int LEN = EnsRec<NX>::LEN;
   constexpr int U = 4;
   __shared__ double red[kEnsCh][kBlock];
@@ -172,7 +177,8 @@ int ensemble_nblocks(uint64_t n) {
 template <int NX, typename T>
 static void ens_launch(const DevState &s, double *blocks, double *out, hipStream_t st) {
   const int nb = ensemble_nblocks(s.n);
-  k_ens_partial<NX, T><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, s.tile, blocks);
+  if (s.tile) k_ens_partial<NX, T, true><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
+  else k_ens_partial<NX, T, false><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
   k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.pitch, s.tile, blocks, nb, out);
 }
 
