@@ -187,6 +187,13 @@ int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem);
 int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_t mem);
 /* RS: the int64 s64_rawAngleSumPrev [4][N] (VD_vehicle_controller.hpp:75) */
 int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem);
+/* Checkpoint / resume: every per-robot array of the handle (estimator state,
+ * RS encoder sums, NaN counters, and the IMU / motor ingest and control state when they
+ * exist, with the control parameters) written byte for byte in its device layout, and read
+ * back into a handle of the same model, N and ABI; resuming continues bit-identically.
+ * Synchronous; EINVAL on I/O errors or a checkpoint that does not match the handle. */
+int fmskf_save_state(fmskf_handle h, const char *path);
+int fmskf_load_state(fmskf_handle h, const char *path);
 /* IMU_IF::Data page [16][N] (accel3, gyro3, mag3, angle3, qut4), is_error [N] */
 int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem);
 /* WT901 register file sReg [0x90][N] (int16) and parser bytes pending [N] */

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <string>
@@ -874,6 +875,148 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
       if (p_packed) copy_planes_in(h, h->s.P, p_packed, row, pb, np, mem);
     }
     finish_out(h, mem);
+  });
+}
+
+}  // extern "C"
+
+namespace {
+
+// Checkpoint sections: every per-robot device array of the handle in its device layout (planes
+// at the handle's pitch, tiles), byte for byte.  Groups: 1 estimator (x, P, RS prev sums,
+// counters), 2 IMU ingest, 4 motor ingest, 8 control (state + parameters).
+constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
+struct CkHeader {
+  char magic[8];
+  uint32_t abi, model;
+  uint64_t n, pitch;
+  uint32_t tile, elem, groups, reserved;
+};
+struct CkSection {
+  void *dev;
+  size_t bytes;
+};
+std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
+  DevState &s = h->s;
+  const uint64_t n = s.n, pp = s.pitch;
+  const Dims d = h->d;
+  std::vector<CkSection> v;
+  if (groups & 1) {
+    v.push_back({s.x, (size_t)d.nx * pp * d.elem});
+    if (s.P) v.push_back({s.P, (size_t)d.nx * (d.nx + 1) / 2 * pp * d.elem});
+    if (s.prev_sum) v.push_back({s.prev_sum, (size_t)4 * pp * 8});
+    v.push_back({s.counters, 8 * 8});
+  }
+  if (groups & 2) {
+    v.push_back({s.imu_reg, (size_t)0x90 * n * 2});
+    v.push_back({s.imu_parser, (size_t)3 * n * 4});
+    v.push_back({s.imu_cnt, (size_t)n});
+    v.push_back({s.imu_flags, (size_t)n});
+    v.push_back({s.imu_err, (size_t)n});
+    v.push_back({s.imu_qinit, (size_t)4 * n * 4});
+    v.push_back({s.imu_data, (size_t)16 * n * 4});
+  }
+  if (groups & 4) {
+    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_rpm, (void *)s.m_curr})
+      v.push_back({p, (size_t)4 * n * 2});
+    v.push_back({s.m_head, (size_t)4 * n});
+    v.push_back({s.m_sum, (size_t)4 * n * 8});
+    for (void *p : {(void *)s.m_dlt, (void *)s.m_speed, (void *)s.m_iir_y, (void *)s.m_iir_x})
+      v.push_back({p, (size_t)4 * n * 4});
+  }
+  if (groups & 8) {
+    const CtrlDev &c = h->ctrl;
+    v.push_back({c.ax, (size_t)3 * kAxF * c.pitch * 4});
+    v.push_back({c.pid, (size_t)4 * kPidF * c.pitch * 4});
+    v.push_back({c.vel_tgt, (size_t)3 * c.pitch * 4});
+    v.push_back({c.curr, (size_t)4 * c.n * 2});
+    v.push_back({c.power, (size_t)c.n});
+  }
+  return v;
+}
+
+struct File {
+  FILE *f = nullptr;
+  File(const char *path, const char *mode) : f(fopen(path, mode)) {
+    if (!f) fail(FMSKF_EINVAL, std::string("cannot open ") + path);
+  }
+  ~File() {
+    if (f) fclose(f);
+  }
+  void write(const void *p, size_t b) {
+    if (fwrite(p, 1, b, f) != b) fail(FMSKF_EINVAL, "checkpoint write failed");
+  }
+  void read(void *p, size_t b) {
+    if (fread(p, 1, b, f) != b) fail(FMSKF_EINVAL, "checkpoint truncated");
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int fmskf_save_state(fmskf_handle h, const char *path) {
+  return guarded([&] {
+    check_handle(h);
+    if (!path) fail(FMSKF_EINVAL, "null path");
+    if (h->capturing) fail(FMSKF_EINVAL, "capture open");
+    DeviceGuard g(h->cfg.device);
+    CkHeader hd{};
+    memcpy(hd.magic, kCkMagic, 8);
+    hd.abi = FMSKF_ABI_VERSION;
+    hd.model = h->cfg.model;
+    hd.n = h->s.n;
+    hd.pitch = h->s.pitch;
+    hd.tile = h->s.tile;
+    hd.elem = h->d.elem;
+    hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
+    hip_check(hipStreamSynchronize(h->stream), "save sync");
+    File f(path, "wb");
+    f.write(&hd, sizeof(hd));
+    f.write(&h->cfg, sizeof(h->cfg));
+    if (hd.groups & 8) f.write(&h->cprm, sizeof(h->cprm));
+    std::vector<char> buf;
+    for (const CkSection &c : ck_sections(h, hd.groups)) {
+      const uint64_t b = c.bytes;
+      f.write(&b, 8);
+      buf.resize(c.bytes);
+      hip_check(hipMemcpy(buf.data(), c.dev, c.bytes, hipMemcpyDeviceToHost), "save D2H");
+      f.write(buf.data(), c.bytes);
+    }
+  });
+}
+
+int fmskf_load_state(fmskf_handle h, const char *path) {
+  return guarded([&] {
+    check_handle(h);
+    if (!path) fail(FMSKF_EINVAL, "null path");
+    if (h->capturing) fail(FMSKF_EINVAL, "capture open");
+    DeviceGuard g(h->cfg.device);
+    File f(path, "rb");
+    CkHeader hd{};
+    f.read(&hd, sizeof(hd));
+    if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
+    if (hd.abi != FMSKF_ABI_VERSION || hd.model != h->cfg.model || hd.n != h->s.n ||
+        hd.pitch != h->s.pitch || hd.tile != h->s.tile || hd.elem != h->d.elem || (hd.groups & ~15u))
+      fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, N or layout)");
+    fmskf_config saved;
+    f.read(&saved, sizeof(saved));
+    fmskf_ctrl_params cp{};
+    if (hd.groups & 8) f.read(&cp, sizeof(cp));
+    if (hd.groups & 2) ensure_imu(h);
+    if (hd.groups & 4) ensure_motors(h);
+    if (hd.groups & 8) ensure_ctrl(h);
+    hip_check(hipStreamSynchronize(h->stream), "load sync");
+    std::vector<char> buf;
+    for (const CkSection &c : ck_sections(h, hd.groups)) {
+      uint64_t b = 0;
+      f.read(&b, 8);
+      if (b != c.bytes) fail(FMSKF_EINVAL, "checkpoint section size mismatch");
+      buf.resize(c.bytes);
+      f.read(buf.data(), c.bytes);
+      hip_check(hipMemcpy(c.dev, buf.data(), c.bytes, hipMemcpyHostToDevice), "load H2D");
+    }
+    if (hd.groups & 8) h->cprm = cp;
   });
 }
 

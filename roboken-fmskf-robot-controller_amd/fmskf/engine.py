@@ -255,6 +255,14 @@ class Engine:
         pP = a.ptr(P, self.dtype) if P is not None else None
         check(load().fmskf_set_state(self.h, px, pP, a.mem), "set_state")
 
+    def save_state(self, path):
+        """fmskf_save_state: checkpoint every per-robot array of the handle to `path`"""
+        check(load().fmskf_save_state(self.h, str(path).encode()), "save_state")
+
+    def load_state(self, path):
+        """fmskf_load_state: resume from a checkpoint of a handle of the same model and N"""
+        check(load().fmskf_load_state(self.h, str(path).encode()), "load_state")
+
     def get_pose(self):
         out = np.empty((3, self.n), np.float32)
         p = [out[k].ctypes.data_as(C.c_void_p) for k in range(3)]
