@@ -33,7 +33,7 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   RsLane s;
   s.px = a.x[i];
   s.py = a.x[pp + i];
-  s.th = a.x[2 * pp + i];
+  s.th = CORR ? 0.f : a.x[2 * pp + i];  // correct overwrites theta before any use
   s.vx = s.vy = s.vth = 0.f;
   if (PRED) {
 #pragma unroll
