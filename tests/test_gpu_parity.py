@@ -641,3 +641,46 @@ def test_state_round_trip_and_reset(model, n):
         if P is not None:
             p0 = np.array(fmskf.default_config(model, n).p0[:np_], dtype=e.dtype)
             bits_equal(gP, np.repeat(p0[:, None], n, 1), "P0")
+
+
+def test_tick_many_strided_rings_and_edge_sizes(orc):
+    """tick_many over rings whose per-tick stride exceeds N (records and planes), N = 1 for
+    the tiled models, and an all-zero validity mask (predict only) -- each equal to the same
+    ticks issued one by one."""
+    n, T, pad = 300, 5, 77
+    _, yaw, gz, rpm, valid = _kf6_setup(n, T, 90)
+    st = n + pad
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    ring = np.zeros((T, st), rec.dtype)
+    ring[:, :n] = rec
+    y2, g2, r2 = (np.zeros((T, st) + a.shape[2:], a.dtype) for a in (yaw, gz, rpm))
+    y2[:, :n], g2[:, :n], r2[:, :n] = yaw, gz, rpm
+    v2 = np.zeros((T, st), np.uint8)
+    v2[:, :n] = valid
+    with Engine("kf6", n) as a, Engine("kf6", n) as b, Engine("kf6", n) as c:
+        a.tick_many(T, tick_stride=st, kf6_rec=ring, valid=v2)
+        b.tick_many(T, tick_stride=st, yaw_deg=y2, gyro_z_dps=g2, rpm=r2, valid=v2)
+        for t in range(T):
+            c.tick(kf6_rec=rec[t], valid=valid[t])
+        (xa, Pa), (xb, Pb), (xc, Pc) = (e.get_state() for e in (a, b, c))
+    for x, P, what in ((xa, Pa, "records"), (xb, Pb, "planes")):
+        bits_equal(x, xc, "x " + what)
+        bits_equal(P, Pc, "P " + what)
+    # N = 1, tiled models, tick_many vs ticks; an all-zero mask skips every update
+    tr = Trajectory(1, 4, seed=91)
+    raw = tr.ekf9_raw()
+    z = np.ascontiguousarray(tr.kf12d_z())
+    zero = np.zeros((4, 1), np.uint8)
+    for model, kw_many, kw_t in (("ekf9", dict(raw=raw), lambda t: dict(raw=raw[t])),
+                                 ("kf12d", dict(z=z), lambda t: dict(z=z[t]))):
+        with Engine(model, 1) as a, Engine(model, 1) as b, Engine(model, 1) as c, \
+                Engine(model, 1) as d:
+            a.tick_many(4, **kw_many)
+            c.tick_many(4, valid=zero, **kw_many)
+            for t in range(4):
+                b.tick(**kw_t(t))
+                d.predict()
+            bits_equal(a.get_state()[0], b.get_state()[0], model + " x")
+            bits_equal(a.get_state()[1], b.get_state()[1], model + " P")
+            bits_equal(c.get_state()[0], d.get_state()[0], model + " masked x")
+            bits_equal(c.get_state()[1], d.get_state()[1], model + " masked P")
