@@ -306,8 +306,10 @@ def main():
             "traffic": traffic,
             "bytes_per_step": BYTES_PER_STEP["kf6"],
             "kernel_ms": kern_avg_ms,
-            "kernel": "k_kf6t<4, Opt<TABLE512, UPD, PRED, SMALL, !VALID" +
-                      (", REC>>" if krec is not None else ">>"),
+            # the launcher's choice (kernels_kf6.hip launch_o): 2 robots per lane while the
+            # state and one tick's inputs (124 B per robot) fit the 256 MiB Infinity Cache
+            "kernel": ("k_kf6p<4, 2, " if n * 124 <= (256 << 20) else "k_kf6t<4, ") +
+                      "Opt<TABLE512, UPD, PRED, SMALL, !VALID" + (", REC>>" if krec is not None else ">>"),
             "timed_region_ms_per_step": region_ms / args.steps,
             "kernel_ms_plane_inputs": planes_ms / args.steps,
         },

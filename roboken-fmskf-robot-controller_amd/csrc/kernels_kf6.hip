@@ -234,6 +234,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   nan_guard(x, P, a.counters, live);
 }
 
+// R robots per lane (i, i + G, ..., G = the grid's lane count), the tick inputs of all R
+// loaded up front: robot r's inputs (fresh from HBM) arrive while robots 0..r-1 are loaded,
+// computed and stored; one register set for the state, 1/R of the grid.
+template <int WPE, int R, class O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6p(
+    KfArgs<MdKF6, Kf6Params> a) {
+  const uint64_t n = a.n;
+  const uint32_t nn = (uint32_t)n, last = nn - 1u;
+  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x;
+  float x[6], P[21];
+  __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
+  float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
+  WaveTable<O::LIBM> tv(a.in.sintab);
+  Kf6In m[R];
+  if (O::UPD) {
+#pragma unroll
+    for (int r = 0; r < R; r++) m[r] = kf6_load_in<O>(a.in, n, 0, min(i0 + r * G, last));
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t i = i0 + r * G;
+    const bool live = i < nn;
+    kf6_load_state<O>(a.x, a.P, a.pitch, live ? i : last, x, P);
+    if (r == 0) tv.store(stab);
+    kf6_tick1<O>(m[r], stab, a.prm, x, P);
+    if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+    nan_guard(x, P, a.counters, live);
+  }
+}
+
 // Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no
 // loop-carried copies); while set A is computed and stored, set B's loads are in flight
 // (vmcnt is in-order: B's 30 loads + A's 27 stores stay within the 63-deep counter).
@@ -282,7 +313,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 }
 
 // Variant (FMSKF_KF6_VARIANT, read once) for single-tick launches; default 0:
-//   0: one instance per lane, grid = N/256, straight-line single-tick kernel
+//   0: k_kf6p with 2 robots per lane while 124 B x N fits the Infinity Cache, else 15
+//   15: one instance per lane, grid = N/256, straight-line single-tick kernel (k_kf6t)
+//   12 / 13 / 14: k_kf6p with 2 / 3 / 4 robots per lane
 //   3: the same through the tick-loop kernel (k_kf6, as tick_many uses)
 //   1: double-buffered persistent, 2 blocks/CU   2: same, 3 blocks/CU
 //   4: same at <= 128 VGPRs, 4 blocks/CU          5: same, 8 blocks/CU
@@ -306,7 +339,18 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     const unsigned grid = (unsigned)(g < need ? g : need);
     if (v <= 2) k_kf6db<2, O><<<grid, kBlock, 0, st>>>(a);
     else k_kf6db<4, O><<<grid, kBlock, 0, st>>>(a);
-  } else if (a.in.n_ticks == 1 && v == 0) {
+  } else if (a.in.n_ticks == 1 && v >= 12 && v <= 14) {
+    const int R = v - 10;
+    const unsigned g = (unsigned)((a.n + (uint64_t)R * kBlock - 1) / ((uint64_t)R * kBlock));
+    if (R == 2) k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
+    else if (R == 3) k_kf6p<4, 3, O><<<g, kBlock, 0, st>>>(a);
+    else k_kf6p<4, 4, O><<<g, kBlock, 0, st>>>(a);
+  } else if (a.in.n_ticks == 1 && v == 0 && a.n * 124 <= (256ull << 20)) {
+    // state + one tick's inputs resident in the 256 MiB Infinity Cache: two robots per lane,
+    // both robots' inputs loaded up front, one wave round (2^20: 39.7 -> 37.4-38.1 us,
+    // 2^21: 75.9 -> 71.5; at 2^24, HBM-bound, it is 3% slower than one robot per lane)
+    k_kf6p<4, 2, O><<<(unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock)), kBlock, 0, st>>>(a);
+  } else if (a.in.n_ticks == 1 && (v == 0 || v == 15)) {
     static const unsigned lds = [] {  // occupancy experiment: dynamic LDS per block
       const char *e = getenv("FMSKF_KF6_LDS");
       return e ? (unsigned)atoi(e) : 0u;

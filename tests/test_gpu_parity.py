@@ -684,3 +684,50 @@ def test_tick_many_strided_rings_and_edge_sizes(orc):
             bits_equal(a.get_state()[1], b.get_state()[1], model + " P")
             bits_equal(c.get_state()[0], d.get_state()[0], model + " masked x")
             bits_equal(c.get_state()[1], d.get_state()[1], model + " masked P")
+
+
+_VARIANT_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = sys.argv[1:3]
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+from oracle import oracle as orc
+for n in (1, 777, 5000):
+    T = 6
+    tr = Trajectory(n, T, seed=n)
+    yaw, gz, rpm = tr.kf6_inputs()
+    valid = (np.random.default_rng(n).random((T, n)) > 0.2).astype(np.uint8)
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    with Engine("kf6", n) as e:
+        for t in range(T):
+            e.tick(kf6_rec=rec[t], valid=valid[t]) if t % 2 else e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], valid=valid[t])
+        x, P = e.get_state()
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
+    xo = np.zeros((6, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    for t in range(T):
+        orc.kf6_tick(xo, Po, yaw[t], gz[t], rpm[t], valid[t], prm, nthreads=0)
+    assert np.array_equal(x.view(np.uint32), xo.view(np.uint32)), n
+    assert np.array_equal(P.view(np.uint32), Po.view(np.uint32)), n
+print("variant ok")
+"""
+
+
+@pytest.mark.parametrize("variant", ["15", "14"])
+def test_kf6_single_tick_variants_bitexact(variant):
+    """The other single-tick KF6 kernels (the launcher picks k_kf6p with 2 robots per lane at
+    these sizes): k_kf6t (one robot per lane, the choice past the Infinity Cache) and k_kf6p
+    with 4 robots per lane, forced through FMSKF_KF6_VARIANT in a child process, bit-exact
+    against the oracle with planes, records and a validity mask."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMSKF_KF6_VARIANT=variant)
+    out = subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "variant ok" in out.stdout
