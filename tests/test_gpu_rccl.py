@@ -42,3 +42,33 @@ def test_comm_init_rejects_bad_rank():
     with Engine("kf6", 16) as e:
         with pytest.raises(fmskf.FmskfError):
             e.comm_init(b"\0" * 128, 2, 2)
+
+
+@pytest.mark.parametrize("model", ["kf6", "ekf9", "kf12d"])
+def test_sharded_handles_fold_to_the_whole_fleet(model):
+    """Weak-scaling shards in one process: the fleet split over three handles (one per GPU in
+    a multi-GPU process; here all on device 0), each handle's ensemble record, folded with
+    fmskf_ensemble_combine in shard order, equals the statistics of one handle holding every
+    robot (1e-12 relative) and of numpy on the same states."""
+    import fmskf
+    from fmskf import Engine
+    rng = np.random.default_rng(11)
+    sizes = [1000, 257, 4096]
+    n = sum(sizes)
+    with Engine(model, n) as whole:
+        x = (rng.normal(size=(whole.nx, n)) * 0.5 + 2.0).astype(whole.dtype)
+        whole.set_state(x, None)
+        mw, cw = fmskf.ensemble_combine(whole.nx, whole.ensemble_partial()[None, :])
+    recs, lo = [], 0
+    for sz in sizes:
+        with Engine(model, sz) as e:
+            e.set_state(np.ascontiguousarray(x[:, lo:lo + sz]), None)
+            recs.append(e.ensemble_partial())
+        lo += sz
+    ms, cs = fmskf.ensemble_combine(x.shape[0], np.stack(recs))
+    np.testing.assert_allclose(ms, mw, rtol=1e-12)
+    np.testing.assert_allclose(cs, cw, rtol=1e-10, atol=1e-14)
+    ref = np.cov(x.astype(np.float64))
+    packed = np.array([ref[i, j] for i in range(x.shape[0]) for j in range(i + 1)])
+    np.testing.assert_allclose(cs, packed, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(ms, x.astype(np.float64).mean(axis=1), rtol=1e-12)
