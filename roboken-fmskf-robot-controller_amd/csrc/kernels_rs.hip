@@ -65,10 +65,62 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   if (CORR) a.x[2 * pp + i] = s.th;
 }
 
+// Fused correct + predict, one tick, two robots per lane (i and i + G): the tick inputs of
+// both robots (yaw, rpm, the four encoder sums: 44 B, fresh every tick) are loaded first, so
+// the second robot's arrive while the first one's state is read, stepped and written (the
+// input-latency hiding of the KF6 k_kf6p, kernels_kf6.hip).
+template <bool LIBM>
+__global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
+  const uint64_t n = a.n, pp = a.pitch;
+  const uint64_t G = (uint64_t)gridDim.x * kBlock;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  float yaw[2];
+  uint2 rw[2];
+  int64_t sum[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const uint64_t i = i0 + r * G < n ? i0 + r * G : n - 1;
+    yaw[r] = a.in.yaw_deg[i];
+    rw[r] = reinterpret_cast<const uint2 *>(a.in.rpm)[i];
+#pragma unroll
+    for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * n + i];
+  }
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const uint64_t i = i0 + r * G;
+    if (i >= n) return;
+    RsLane s;
+    s.px = a.x[i];
+    s.py = a.x[pp + i];
+    s.th = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
+    rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], a.in.sintab);
+    a.x[i] = s.px;
+    a.x[pp + i] = s.py;
+    a.x[2 * pp + i] = s.th;
+    a.x[3 * pp + i] = s.vx;
+    a.x[4 * pp + i] = s.vy;
+    a.x[5 * pp + i] = s.vth;
+#pragma unroll
+    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+  }
+}
+
 int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool predict,
               hipStream_t st) {
   RsArgs a{s.n, s.pitch, (float *)s.x, s.prev_sum, in};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
+  static const bool two = [] {  // A/B switch (FMSKF_RS_TWO=0: one robot per lane)
+    const char *e = getenv("FMSKF_RS_TWO");
+    return !e || atoi(e) != 0;
+  }();
+  if (two && correct && predict && in.n_ticks == 1) {
+    const dim3 g2((unsigned)((s.n + 2 * kBlock - 1) / (2 * kBlock)));
+    if (libm) k_rs2<true><<<g2, kBlock, 0, st>>>(a);
+    else k_rs2<false><<<g2, kBlock, 0, st>>>(a);
+    return (int)hipGetLastError();
+  }
   if (libm) {
     if (correct && predict) k_rs<true, true, true><<<g, kBlock, 0, st>>>(a);
     else if (correct) k_rs<true, true, false><<<g, kBlock, 0, st>>>(a);
