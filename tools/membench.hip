@@ -216,6 +216,22 @@ __global__ __launch_bounds__(256) void k_model_tiled(TT *st, const uint4 *raw, u
   for (int k = 0; k < NS; k++) tile[k * T] = s[k] + m;
 }
 
+// the tiled pattern, read from one state buffer and written to another (ping-pong state)
+template <typename TT, int NS, int T>
+__global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, const uint4 *raw, uint64_t n,
+                                                        TT sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  const uint64_t o = (v / T) * ((uint64_t)NS * T) + (v % T);
+  TT s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = src[o + k * T];
+  const uint4 r = raw[v];
+  const TT m = sink * (TT)(r.x & r.y & r.z & r.w & 1);
+#pragma unroll
+  for (int k = 0; k < NS; k++) dst[o + k * T] = s[k] + m;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -280,6 +296,24 @@ int main(int argc, char **argv) {
     tm("ekf9_tiled64_448B", 448, [&] { k_model_tiled<float, 54, 64><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
     tm("ekf9_tiled256_448B", 448, [&] { k_model_tiled<float, 54, 256><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
     tm("kf6_tiled256_232B", 232, [&] { k_model_tiled<float, 27, 256><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    {
+      void *sb2;
+      CK(hipMalloc(&sb2, 90 * pitch * 8));
+      k_fill_rand<<<4096, 256>>>((uint32_t *)sb2, 90 * pitch * 2, 9);
+      CK(hipDeviceSynchronize());
+      int flip = 0;
+      tm("ekf9_tiled256_pingpong_448B", 448, [&] {
+        float *a = (float *)(flip ? sb2 : sb), *b = (float *)(flip ? sb : sb2);
+        flip ^= 1;
+        k_model_tiled_pp<float, 54, 256><<<g, 256>>>(a, b, (const uint4 *)ib, n, 0.f);
+      });
+      tm("kf6_tiled256_pingpong_232B", 232, [&] {
+        float *a = (float *)(flip ? sb2 : sb), *b = (float *)(flip ? sb : sb2);
+        flip ^= 1;
+        k_model_tiled_pp<float, 27, 256><<<g, 256>>>(a, b, (const uint4 *)ib, n, 0.f);
+      });
+      CK(hipFree(sb2));
+    }
     tm("kf12d_tiled64_1504B", 1504, [&] { k_model_tiled<double, 90, 64><<<g, 256>>>((double *)sb, (const uint4 *)ib, n, 0.0); });
     tm("kf12d_pattern_1504B", 1504, [&] {
       k_model_pattern<double, 90, 8><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
