@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused multi-tick figure")
+    ap.add_argument("--gather", choices=["async", "stream"], default="async",
+                    help="N > 1: all-gather on RCCL's stream (async) or in the tick stream")
     ap.add_argument("--inputs", choices=["records", "planes"], default="records",
                     help="16-byte fmskf_kf6_record per robot (one load per lane) or yaw/gyro/rpm planes")
     args = ap.parse_args()
@@ -148,7 +150,9 @@ def main():
         if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
             e = ev_count[0] % n_events
             eng.ensemble_partial(recs[e])
-            if distributed:
+            if distributed and args.gather == "stream":
+                dist.all_gather_into_tensor(gathered[e].view(-1), recs[e])
+            elif distributed:
                 pending.append(dist.all_gather_into_tensor(gathered[e].view(-1), recs[e],
                                                            async_op=True))
             else:
