@@ -191,7 +191,10 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem);
  * RS encoder sums, NaN counters, and the IMU / motor ingest and control state when they
  * exist, with the control parameters) written byte for byte in its device layout, and read
  * back into a handle of the same model, N and ABI; resuming continues bit-identically.
- * Synchronous; EINVAL on I/O errors or a checkpoint that does not match the handle. */
+ * Ingest / control state the checkpoint does not hold is reset to its initial value on load.
+ * The handle's fmskf_config (noise, geometry) is its own: the saved copy is not applied.
+ * Synchronous; EINVAL on I/O errors or a checkpoint that does not match the handle, in which
+ * case load leaves the handle's state untouched (lengths are validated before any copy). */
 int fmskf_save_state(fmskf_handle h, const char *path);
 int fmskf_load_state(fmskf_handle h, const char *path);
 /* IMU_IF::Data page [16][N] (accel3, gyro3, mag3, angle3, qut4), is_error [N] */

@@ -365,6 +365,7 @@ void ensure_motors(fmskf_ctx *h) {
   zero_motors(h);
 }
 void ensure_ctrl(fmskf_ctx *h);
+void zero_ctrl(fmskf_ctx *h);
 
 void do_reset(fmskf_ctx *h) {
   DevState &s = h->s;
@@ -949,6 +950,10 @@ struct File {
   void read(void *p, size_t b) {
     if (fread(p, 1, b, f) != b) fail(FMSKF_EINVAL, "checkpoint truncated");
   }
+  long tell() const { return ftell(f); }
+  void seek(long off, int whence) {
+    if (fseek(f, off, whence) != 0) fail(FMSKF_EINVAL, "checkpoint seek failed");
+  }
 };
 
 }  // namespace
@@ -1006,12 +1011,29 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (hd.groups & 2) ensure_imu(h);
     if (hd.groups & 4) ensure_motors(h);
     if (hd.groups & 8) ensure_ctrl(h);
-    hip_check(hipStreamSynchronize(h->stream), "load sync");
-    std::vector<char> buf;
-    for (const CkSection &c : ck_sections(h, hd.groups)) {
+    // validate every section length and the file's end before touching the handle, so a
+    // truncated or foreign file leaves the state as it was
+    const std::vector<CkSection> secs = ck_sections(h, hd.groups);
+    const long body = f.tell();
+    for (const CkSection &c : secs) {
       uint64_t b = 0;
       f.read(&b, 8);
       if (b != c.bytes) fail(FMSKF_EINVAL, "checkpoint section size mismatch");
+      f.seek((long)c.bytes, SEEK_CUR);
+    }
+    const long end = f.tell();
+    f.seek(0, SEEK_END);
+    if (f.tell() != end) fail(FMSKF_EINVAL, "checkpoint size mismatch (truncated or trailing bytes)");
+    f.seek(body, SEEK_SET);
+    // groups the checkpoint does not hold were never used by the saving handle: reset them here
+    if (!(hd.groups & 2) && h->s.imu_reg) zero_imu(h);
+    if (!(hd.groups & 4) && h->s.m_sum) zero_motors(h);
+    if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
+    hip_check(hipStreamSynchronize(h->stream), "load sync");
+    std::vector<char> buf;
+    for (const CkSection &c : secs) {
+      uint64_t b = 0;
+      f.read(&b, 8);
       buf.resize(c.bytes);
       f.read(buf.data(), c.bytes);
       hip_check(hipMemcpy(c.dev, buf.data(), c.bytes, hipMemcpyHostToDevice), "load H2D");
@@ -1314,6 +1336,16 @@ CtrlPrm make_ctrl_prm(const fmskf_ctx *h) {
   return p;
 }
 
+void zero_ctrl(fmskf_ctx *h) {
+  CtrlDev &c = h->ctrl;
+  hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, h->stream), "ctrl init");
+  ctrl_params_defaults(&h->cprm);
+}
+
 void ensure_ctrl(fmskf_ctx *h) {
   if (h->ctrl_ready) return;
   CtrlDev &c = h->ctrl;
@@ -1324,12 +1356,7 @@ void ensure_ctrl(fmskf_ctx *h) {
   c.vel_tgt = h->alloc<float>((size_t)3 * c.pitch);
   c.curr = h->alloc<int16_t>((size_t)4 * c.n);
   c.power = h->alloc<uint8_t>((size_t)c.n);
-  hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, h->stream), "ctrl init");
-  hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, h->stream), "ctrl init");
-  hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, h->stream), "ctrl init");
-  hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
-  hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, h->stream), "ctrl init");
-  ctrl_params_defaults(&h->cprm);
+  zero_ctrl(h);
   h->ctrl_ready = true;
 }
 

@@ -369,3 +369,28 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
     with Engine(model, n + 1) as d:
         with pytest.raises(fmskf.FmskfError):
             d.load_state(ck)
+    # a truncated file, or one with trailing bytes, is rejected before any copy: the handle
+    # keeps its state
+    blob = ck.read_bytes()
+    with Engine(model, n) as e:
+        e.load_state(ck)
+        before = readout(e)
+        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0")):
+            bad = tmp_path / name
+            bad.write_bytes(data)
+            with pytest.raises(fmskf.FmskfError):
+                e.load_state(bad)
+            after = readout(e)
+            np.testing.assert_array_equal(bits(before["x"]), bits(after["x"]))
+            for k in before["motors"]:
+                np.testing.assert_array_equal(before["motors"][k], after["motors"][k])
+    # state the checkpoint does not hold is reset on load: a handle that has ingested CAN
+    # frames, loaded from a checkpoint saved before any ingest, reads zero motor state
+    fresh = tmp_path / "fresh.ck"
+    with Engine(model, n) as f0:
+        f0.save_state(fresh)
+    with Engine(model, n) as g:
+        step(g, 0)
+        g.load_state(fresh)
+        for k, v in g.get_motors().items():
+            assert not np.any(v), k
