@@ -216,6 +216,29 @@ __global__ __launch_bounds__(256) void k_model_tiled(TT *st, const uint4 *raw, u
   for (int k = 0; k < NS; k++) tile[k * T] = s[k] + m;
 }
 
+// tiled with 4 rows per lane access: [N/T][NS4][T] float4 (row 4q..4q+3 of robot i are one
+// 16-byte word), so one wave instruction covers 1 KB contiguous instead of 256 B
+template <int NS4, int T>
+__global__ __launch_bounds__(256) void k_model_tiled4(float4 *st, const uint4 *raw, uint64_t n, float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float4 *tile = st + (v / T) * ((uint64_t)NS4 * T) + (v % T);
+  float4 s[NS4];
+#pragma unroll
+  for (int k = 0; k < NS4; k++) s[k] = tile[k * T];
+  const uint4 r = raw[v];
+  const float m = sink * (float)(r.x & r.y & r.z & r.w & 1);
+#pragma unroll
+  for (int k = 0; k < NS4; k++) {
+    float4 t = s[k];
+    t.x += m;
+    t.y += m;
+    t.z += m;
+    t.w += m;
+    tile[k * T] = t;
+  }
+}
+
 // the tiled pattern, read from one state buffer and written to another (ping-pong state)
 template <typename TT, int NS, int T>
 __global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, const uint4 *raw, uint64_t n,
@@ -314,6 +337,18 @@ int main(int argc, char **argv) {
       });
       CK(hipFree(sb2));
     }
+    tm("ekf9_tiled4x256_464B_as448", 448, [&] { k_model_tiled4<14, 256><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("ekf9_tiled4x64_464B_as448", 448, [&] { k_model_tiled4<14, 64><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_tiled4x256_240B_as232", 232, [&] { k_model_tiled4<7, 256><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_tiled4x64_240B_as232", 232, [&] { k_model_tiled4<7, 64><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
+    // HBM-scale copy ceilings at the model's byte count (half read, half written)
+    tm("copy_float4_448B", 448, [&] {
+      k_copy4<<<2048, 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n), 224 * n / 16);
+    });
+    tm("copy_float4_448B_fullgrid", 448, [&] {
+      k_copy4<<<(unsigned)(224 * n / 16 / 256), 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n),
+                                                      224 * n / 16);
+    });
     tm("kf12d_tiled64_1504B", 1504, [&] { k_model_tiled<double, 90, 64><<<g, 256>>>((double *)sb, (const uint4 *)ib, n, 0.0); });
     tm("kf12d_pattern_1504B", 1504, [&] {
       k_model_pattern<double, 90, 8><<<g, 256>>>((double *)sb, (const double *)ib, n, pitch, 0.0);
