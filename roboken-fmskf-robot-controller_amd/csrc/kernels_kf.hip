@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
-template <bool LIBM, bool UPD, bool PRED>
+template <bool LIBM, bool UPD, bool PRED, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -149,8 +149,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
   WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
-  const TileRows<float, N> tx(a.x, tile_slot(n));
-  const TileRows<float, NP> tp(a.P, tile_slot(n));
+  const TileRows<float, N, CP> tx(a.x, tile_slot(n));
+  const TileRows<float, NP, CP> tp(a.P, tile_slot(n));
   if constexpr (FMSKF_TILED) {
 #pragma unroll
     for (int k = 0; k < N; k++) x[k] = tx.ld(k);
@@ -316,7 +316,7 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 // Planes through buffer descriptors: a 32-bit lane offset per access and no 64-bit address
 // math.  SMALL: the 78 P planes fit one 4 GiB window (pitch < 6.8M), one descriptor per array
 // and a scalar plane offset; otherwise one descriptor per plane (n < 2^29 lanes of 8 bytes).
-template <bool BLK, bool UPD, bool PRED, bool SMALL>
+template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
   const uint64_t n = a.n, pp = a.pitch;
@@ -344,8 +344,8 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   };
   // tiled layout (FMSKF_TILED): the block's tile through a scalar descriptor (lanes past N
   // returned above, so a lane's slot is its thread index)
-  const TileRows<double, N> tx(a.x, threadIdx.x);
-  const TileRows<double, NP> tp(a.P, threadIdx.x);
+  const TileRows<double, N, CP> tx(a.x, threadIdx.x);
+  const TileRows<double, NP, CP> tp(a.P, threadIdx.x);
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
 #pragma unroll
@@ -390,13 +390,16 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
                 bool pred, hipStream_t st) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
+  const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
   if (in.n_ticks == 1) {
     if (libm) {
-      if (upd && pred) k_ekf9t<true, true, true><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<true, true, true, kStateNT><<<g, kBlock, 0, st>>>(a);
+      else if (upd && pred) k_ekf9t<true, true, true><<<g, kBlock, 0, st>>>(a);
       else if (upd) k_ekf9t<true, true, false><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<true, false, true><<<g, kBlock, 0, st>>>(a);
     } else {
-      if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<false, true, true, kStateNT><<<g, kBlock, 0, st>>>(a);
+      else if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, 0, st>>>(a);
       else if (upd) k_ekf9t<false, true, false><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<false, false, true><<<g, kBlock, 0, st>>>(a);
     }
@@ -417,10 +420,12 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
   KfArgs<MdKF12D, Kf12dParams> a{s.n, s.pitch, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   const bool small = FMSKF_TILED || s.pitch * 8 * 78 < 0xFFFFFFFFull;  // tiled: any N
+  const bool nt = FMSKF_TILED && state_nt(s.n * 90 * 8);
   if (p.decor) {
     const bool blk = kf12d_sequential(p.r);
 #define KF12S(B, S)                                                          \
-  if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, 0, st>>>(a);       \
+  if (upd && pred && nt) k_kf12s<B, true, true, S, kStateNT><<<g, kBlock, 0, st>>>(a); \
+  else if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, 0, st>>>(a); \
   else if (upd) k_kf12s<B, true, false, S><<<g, kBlock, 0, st>>>(a);        \
   else k_kf12s<B, false, true, S><<<g, kBlock, 0, st>>>(a);
     if (blk && small) { KF12S(true, true) }

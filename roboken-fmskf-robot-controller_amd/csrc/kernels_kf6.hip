@@ -28,11 +28,15 @@ namespace fmskf {
 
 // REC: the inputs come as 16-byte fmskf_kf6_record's (one 16-byte load per lane) instead of
 // the yaw / gyro / rpm planes (three loads): measured 41.6 -> 39.5 us per tick at 2^20
-template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false>
+// NT: the state is loaded and stored non-temporal (kf_generic.hpp state_nt)
+template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false, bool NT_ = false>
 struct Opt {
   static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_,
-                        REC = REC_;
+                        REC = REC_, NT = NT_;
+  static constexpr int CP = NT_ ? kStateNT : 0;
 };
+template <class O>
+using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true>;
 
 struct Kf6In {
   float yaw, gz;
@@ -40,12 +44,14 @@ struct Kf6In {
   uint32_t valid;
 };
 
+template <int CP = 0>
 __device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, CP));
 }
+template <int CP = 0>
 __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
                                        float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, CP);
 }
 
 // The per-tick inputs are read exactly once: load them non-temporal (gfx950 `nt`, aux bit 1)
@@ -96,14 +102,14 @@ __device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg,
     const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
     const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = ld_f32(rx, i * 4u, k * ps);
+    for (int k = 0; k < 6; k++) x[k] = ld_f32<O::CP>(rx, i * 4u, k * ps);
 #pragma unroll
-    for (int k = 0; k < 21; k++) P[k] = ld_f32(rp, i * 4u, k * ps);
+    for (int k = 0; k < 21; k++) P[k] = ld_f32<O::CP>(rp, i * 4u, k * ps);
   } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = ld_f32(rsrc(xg + k * pp, pp * 4), i * 4u, 0);
+    for (int k = 0; k < 6; k++) x[k] = ld_f32<O::CP>(rsrc(xg + k * pp, pp * 4), i * 4u, 0);
 #pragma unroll
-    for (int k = 0; k < 21; k++) P[k] = ld_f32(rsrc(Pg + k * pp, pp * 4), i * 4u, 0);
+    for (int k = 0; k < 21; k++) P[k] = ld_f32<O::CP>(rsrc(Pg + k * pp, pp * 4), i * 4u, 0);
   }
 }
 
@@ -114,14 +120,14 @@ __device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t p
     const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
     const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_f32(rx, i * 4u, k * ps, x[k]);
+    for (int k = 0; k < 6; k++) st_f32<O::CP>(rx, i * 4u, k * ps, x[k]);
 #pragma unroll
-    for (int k = 0; k < 21; k++) st_f32(rp, i * 4u, k * ps, P[k]);
+    for (int k = 0; k < 21; k++) st_f32<O::CP>(rp, i * 4u, k * ps, P[k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_f32(rsrc(xg + k * pp, pp * 4), i * 4u, 0, x[k]);
+    for (int k = 0; k < 6; k++) st_f32<O::CP>(rsrc(xg + k * pp, pp * 4), i * 4u, 0, x[k]);
 #pragma unroll
-    for (int k = 0; k < 21; k++) st_f32(rsrc(Pg + k * pp, pp * 4), i * 4u, 0, P[k]);
+    for (int k = 0; k < 21; k++) st_f32<O::CP>(rsrc(Pg + k * pp, pp * 4), i * 4u, 0, P[k]);
   }
 }
 
@@ -355,6 +361,12 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
       const char *e = getenv("FMSKF_KF6_LDS");
       return e ? (unsigned)atoi(e) : 0u;
     }();
+    if constexpr (O::UPD && O::PRED) {
+      if (state_nt(a.n * 108)) {
+        k_kf6t<4, WithNT<O>><<<grid_for(a.n), kBlock, lds, st>>>(a);
+        return;
+      }
+    }
     k_kf6t<4, O><<<grid_for(a.n), kBlock, lds, st>>>(a);
   } else {
     k_kf6<4, O><<<grid_for(a.n), kBlock, 0, st>>>(a);

@@ -731,3 +731,66 @@ def test_kf6_single_tick_variants_bitexact(variant):
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "variant ok" in out.stdout
+
+
+_NT_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = sys.argv[1:3]
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+from oracle import oracle as orc
+for n in (1, 1000):
+    T = 5
+    tr = Trajectory(n, T, seed=60 + n)
+    valid = (np.random.default_rng(n).random((T, n)) > 0.2).astype(np.uint8)
+    raw = tr.ekf9_raw()
+    cfg = fmskf.default_config("ekf9", n)
+    with Engine("ekf9", n) as e:
+        for t in range(T):
+            e.tick(raw=raw[t], valid=valid[t])
+        x, P = e.get_state()
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((9, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    for t in range(T):
+        orc.ekf9_tick(xo, Po, raw[t], valid[t], prm, nthreads=0)
+    assert np.array_equal(x.view(np.uint32), xo.view(np.uint32)), ("ekf9", n)
+    assert np.array_equal(P.view(np.uint32), Po.view(np.uint32)), ("ekf9", n)
+    z = np.ascontiguousarray(tr.kf12d_z())
+    for cross in (False, True):
+        cfg = fmskf.default_config("kf12d", n)
+        r = np.array(cfg.r[:36])
+        if cross:
+            r[4 * 5 // 2 + 0] = 1e-6
+        with Engine("kf12d", n, r=r) as e:
+            for t in range(T):
+                e.tick(z=z[t], valid=valid[t])
+            x, P = e.get_state()
+        prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), r)
+        xo = np.zeros((12, n))
+        Po = np.repeat(np.array(cfg.p0[:78])[:, None], n, 1).copy()
+        for t in range(T):
+            orc.kf12d_tick(xo, Po, np.ascontiguousarray(z[t]), valid[t], prm, nthreads=0)
+        assert np.array_equal(x.view(np.uint64), xo.view(np.uint64)), ("kf12d", n, cross)
+        assert np.array_equal(P.view(np.uint64), Po.view(np.uint64)), ("kf12d", n, cross)
+print("nt ok")
+"""
+
+
+def test_nontemporal_state_kernels_bitexact():
+    """The non-temporal state instantiations (chosen automatically once the state outgrows the
+    Infinity Cache, kf_generic.hpp state_nt) forced on at small N in a child process:
+    EKF9 and KF12D (block-diagonal and correlated R) with a validity mask, and KF6's k_kf6t
+    through the variant script, bit-exact against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMSKF_STATE_NT="1", FMSKF_KF6_VARIANT="15")
+    args = [root, os.path.join(root, "roboken-fmskf-robot-controller_amd")]
+    for script, ok in ((_NT_SCRIPT, "nt ok"), (_VARIANT_SCRIPT, "variant ok")):
+        out = subprocess.run([sys.executable, "-c", script] + args,
+                             capture_output=True, text=True, timeout=240, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert ok in out.stdout
