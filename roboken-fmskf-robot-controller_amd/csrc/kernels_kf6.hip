@@ -348,6 +348,12 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   } else if (a.in.n_ticks == 1 && v >= 12 && v <= 14) {
     const int R = v - 10;
     const unsigned g = (unsigned)((a.n + (uint64_t)R * kBlock - 1) / ((uint64_t)R * kBlock));
+    if constexpr (O::UPD && O::PRED) {
+      if (R == 2 && state_nt(a.n * 108)) {
+        k_kf6p<4, 2, WithNT<O>><<<g, kBlock, 0, st>>>(a);
+        return;
+      }
+    }
     if (R == 2) k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
     else if (R == 3) k_kf6p<4, 3, O><<<g, kBlock, 0, st>>>(a);
     else k_kf6p<4, 4, O><<<g, kBlock, 0, st>>>(a);
@@ -355,7 +361,14 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     // state + one tick's inputs resident in the 256 MiB Infinity Cache: two robots per lane,
     // both robots' inputs loaded up front, one wave round (2^20: 39.7 -> 37.4-38.1 us,
     // 2^21: 75.9 -> 71.5; at 2^24, HBM-bound, it is 3% slower than one robot per lane)
-    k_kf6p<4, 2, O><<<(unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock)), kBlock, 0, st>>>(a);
+    const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
+    if constexpr (O::UPD && O::PRED) {
+      if (state_nt(a.n * 108)) {  // only when forced: this branch's state fits the cache
+        k_kf6p<4, 2, WithNT<O>><<<g, kBlock, 0, st>>>(a);
+        return;
+      }
+    }
+    k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
   } else if (a.in.n_ticks == 1 && (v == 0 || v == 15)) {
     static const unsigned lds = [] {  // occupancy experiment: dynamic LDS per block
       const char *e = getenv("FMSKF_KF6_LDS");

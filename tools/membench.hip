@@ -239,6 +239,38 @@ __global__ __launch_bounds__(256) void k_model_tiled4(float4 *st, const uint4 *r
   }
 }
 
+// HBM-regime probes of the tiled pattern. MODE 0: loads only (one 4-byte store per lane);
+// 1: stores only; 2: non-temporal loads and stores; 3: non-temporal stores only
+template <int NS, int T, int MODE>
+__global__ __launch_bounds__(256) void k_tiled_probe(float *st, const uint4 *raw, uint64_t n, float sink) {
+  extern __shared__ float occ_cap[];  // dynamic LDS only limits the blocks per CU
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
+  const uint4 r = raw[v];
+  const float m = sink * (float)(r.x & r.y & r.z & r.w & 1);
+  if (MODE == 1) {
+#pragma unroll
+    for (int k = 0; k < NS; k++) tile[k * T] = m + (float)k;
+    return;
+  }
+  float s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = MODE == 2 ? __builtin_nontemporal_load(tile + k * T) : tile[k * T];
+  if (MODE == 0) {
+    float acc = m;
+#pragma unroll
+    for (int k = 0; k < NS; k++) acc += s[k];
+    if (acc == 12345.f) occ_cap[threadIdx.x] = acc, tile[0] = occ_cap[threadIdx.x ^ 1];
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    if (MODE >= 2) __builtin_nontemporal_store(s[k] + m, tile + k * T);
+    else tile[k * T] = s[k] + m;
+  }
+}
+
 // the tiled pattern, read from one state buffer and written to another (ping-pong state)
 template <typename TT, int NS, int T>
 __global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, const uint4 *raw, uint64_t n,
@@ -341,6 +373,19 @@ int main(int argc, char **argv) {
     tm("ekf9_tiled4x64_464B_as448", 448, [&] { k_model_tiled4<14, 64><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
     tm("kf6_tiled4x256_240B_as232", 232, [&] { k_model_tiled4<7, 256><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
     tm("kf6_tiled4x64_240B_as232", 232, [&] { k_model_tiled4<7, 64><<<g, 256>>>((float4 *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_t256_loads_only_as232", 232, [&] { k_tiled_probe<27, 256, 0><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_t256_stores_only_as232", 232, [&] { k_tiled_probe<27, 256, 1><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_t256_nt_ldst", 232, [&] { k_tiled_probe<27, 256, 2><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_t256_nt_st", 232, [&] { k_tiled_probe<27, 256, 3><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_t256_plain", 232, [&] { k_tiled_probe<27, 256, 4><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    for (int kb : {16, 32, 48, 80})
+      tm(kb == 16 ? "kf6_t256_lds16K" : kb == 32 ? "kf6_t256_lds32K" : kb == 48 ? "kf6_t256_lds48K" : "kf6_t256_lds80K", 232,
+         [&] { k_tiled_probe<27, 256, 4><<<g, 256, kb * 1024>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("ekf9_t256_nt_st", 448, [&] { k_tiled_probe<54, 256, 3><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("ekf9_t256_nt_ldst", 448, [&] { k_tiled_probe<54, 256, 2><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    for (int kb : {16, 32, 48})
+      tm(kb == 16 ? "ekf9_t256_lds16K" : kb == 32 ? "ekf9_t256_lds32K" : "ekf9_t256_lds48K", 448,
+         [&] { k_tiled_probe<54, 256, 4><<<g, 256, kb * 1024>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
     // HBM-scale copy ceilings at the model's byte count (half read, half written)
     tm("copy_float4_448B", 448, [&] {
       k_copy4<<<2048, 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n), 224 * n / 16);
