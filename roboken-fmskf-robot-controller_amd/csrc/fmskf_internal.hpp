@@ -1,6 +1,7 @@
 // fmskf_internal.hpp -- structures shared by the C-ABI layer (fmskf_api.cpp) and the
 // kernel launchers (kernels_*.hip).  Not part of the public ABI.
 #pragma once
+#include <cstdlib>
 #include <cmath>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -153,6 +154,22 @@ inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; 
 // 27 KF6 rows gain nothing measurable (36.3 vs 36.0 at 2^20), so KF6 / RS stay planar.  The
 // allocation (rows x plane_pitch) always covers ceil(N / kTile) tiles.
 constexpr uint32_t kTile = kBlock;
+
+// Cache policy of the per-tick state stream.  When the state is several times the 256 MiB
+// Infinity Cache, every state byte is read once and written once per tick from HBM; loading
+// and storing it non-temporal (gfx950 `nt`, buffer aux bit 1) measured 15% faster on the
+// tiled pattern at 2^22 EKF9 robots (tools/membench.hip: 352 -> 299 us), while it is slower
+// when the state fits the Infinity Cache.  FMSKF_STATE_NT=0|1 forces it off or on.
+constexpr int kStateNT = 2;
+inline bool state_nt(uint64_t state_bytes) {
+  static const int force = [] {
+    const char *e = getenv("FMSKF_STATE_NT");
+    return e ? atoi(e) : -1;
+  }();
+  if (force >= 0) return force != 0;
+  return state_bytes > (256ull << 20);
+}
+
 #ifndef FMSKF_TILED
 #define FMSKF_TILED 1
 #endif

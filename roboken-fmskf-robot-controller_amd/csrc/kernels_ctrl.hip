@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_set_target(CtrlDev c, const flo
 // Plane access for the control state: SMALL (every array within a 4 GiB buffer window) uses
 // buffer descriptors with a 32-bit lane offset and a scalar per-plane offset; otherwise plain
 // 64-bit global addressing.
-template <bool SMALL>
+template <bool SMALL, int CP = 0>
 struct Planes {
   __amdgpu_buffer_rsrc_t r;
   float *base;
@@ -141,14 +141,14 @@ struct Planes {
   __device__ __forceinline__ float ld(int plane, uint32_t i) const {
     if constexpr (SMALL)
       return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                           r, i * 4u, (uint32_t)(plane * pp * 4), 0));
+                                           r, i * 4u, (uint32_t)(plane * pp * 4), CP));
     else
       return base[plane * pp + i];
   }
   __device__ __forceinline__ void st(int plane, uint32_t i, float v) const {
     if constexpr (SMALL)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u,
-                                            (uint32_t)(plane * pp * 4), 0);
+                                            (uint32_t)(plane * pp * 4), CP);
     else
       base[plane * pp + i] = v;
   }
@@ -157,14 +157,14 @@ struct Planes {
 // One robot's control step, split in its load phase (every load issued up front: vmcnt
 // retires in order) and its compute + store phase, so a fused kernel can issue the loads of
 // several steps before computing any of them.
-template <bool SMALL>
+template <bool SMALL, int CP = 0>
 struct CtrlLane {
   uint8_t on;
   Interp ax[3];
   float pv[4][4];
 
   __device__ __forceinline__ void load(const CtrlDev &c, uint32_t i) {
-    const Planes<SMALL> AX(c.ax, c.pitch, 3 * kAxF), PD(c.pid, c.pitch, 4 * kPidF);
+    const Planes<SMALL, CP> AX(c.ax, c.pitch, 3 * kAxF), PD(c.pid, c.pitch, 4 * kPidF);
     on = c.power[i];
 #pragma unroll
     for (int a = 0; a < 3; a++)
@@ -180,7 +180,7 @@ struct CtrlLane {
   // raw current targets (also stored to c.curr).
   __device__ __forceinline__ uint2 step(const CtrlDev &c, const CtrlPrm &p, uint32_t i, uint2 rw) {
     const uint64_t pp = c.pitch;
-    const Planes<SMALL> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
+    const Planes<SMALL, CP> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
     float v[3];
 #pragma unroll
     for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
@@ -258,13 +258,13 @@ struct CtrlLane {
 // The per-tick control step.  rpm [N][4] int16 (MOTOR_IF_M2006::Status.s16_rawSpeedRpm).
 // rstride: robot i's four rpm at rpm + 4 * rstride * i (1: [N][4] planes; 2: the rpm field of
 // 16-byte fmskf_kf6_record's)
-template <bool SMALL>
+template <bool SMALL, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, const int16_t *rpm,
                                                       uint32_t rstride) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)c.n) return;
   const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[(uint64_t)i * rstride];
-  CtrlLane<SMALL> L;
+  CtrlLane<SMALL, CP> L;
   L.load(c, i);
   L.step(c, p, i, rw);
 }
@@ -290,7 +290,7 @@ struct IsrRsArgs {
   const float *sintab;
   uint8_t *frames;
 };
-template <bool LIBM, bool SMALL>
+template <bool LIBM, bool SMALL, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p) {
   const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   int64_t sum[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * n + i];
-  CtrlLane<SMALL> L;
+  CtrlLane<SMALL, CP> L;
   L.load(c, i);
   rs_tick1<LIBM, true, true>(s, yaw, rw, sum, a.sintab);
   const uint2 cw = L.step(c, p, i, rw);
@@ -378,6 +378,8 @@ __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, const 
 }
 
 static inline dim3 grid1(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+// bytes of the per-robot control state the step streams (interpolators + wheel loops)
+static inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * 4ull * (3 * kAxF + 4 * kPidF); }
 
 int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
                            const uint8_t *mask, hipStream_t st) {
@@ -389,7 +391,9 @@ int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl,
 int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
                      hipStream_t st) {
   if (c.n == 0) return 0;
-  if (c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull)
+  if (c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull && state_nt(ctrl_state_bytes(c)))
+    k_ctrl_step<true, kStateNT><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
+  else if (c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull)
     k_ctrl_step<true><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
   else
     k_ctrl_step<false><<<grid1(c.n), kBlock, 0, st>>>(c, p, rpm, rstride);
@@ -402,7 +406,11 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
   const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum,
                     in.sintab, frames};
   const bool small = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
-  if (libm) {
+  const bool nt = small && state_nt(ctrl_state_bytes(c) + s.n * 56);
+  if (nt) {
+    if (libm) k_isr_rs<true, true, kStateNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+    else k_isr_rs<false, true, kStateNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+  } else if (libm) {
     if (small) k_isr_rs<true, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
     else k_isr_rs<true, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
   } else {

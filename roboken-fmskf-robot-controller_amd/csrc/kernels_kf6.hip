@@ -28,7 +28,7 @@ namespace fmskf {
 
 // REC: the inputs come as 16-byte fmskf_kf6_record's (one 16-byte load per lane) instead of
 // the yaw / gyro / rpm planes (three loads): measured 41.6 -> 39.5 us per tick at 2^20
-// NT: the state is loaded and stored non-temporal (kf_generic.hpp state_nt)
+// NT: the state is loaded and stored non-temporal (fmskf_internal.hpp state_nt)
 template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false, bool NT_ = false>
 struct Opt {
   static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_,

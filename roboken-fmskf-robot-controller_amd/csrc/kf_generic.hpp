@@ -97,21 +97,6 @@ struct TileRows {
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * kTile * 4, CP);
   }
 };
-// Cache policy of the per-tick state stream.  When the state is several times the 256 MiB
-// Infinity Cache, every state byte is read once and written once per tick from HBM; loading
-// and storing it non-temporal (gfx950 `nt`, buffer aux bit 1) measured 15% faster on the
-// tiled pattern at 2^22 EKF9 robots (tools/membench.hip: 352 -> 299 us), while it is slower
-// when the state fits the Infinity Cache.  FMSKF_STATE_NT=0|1 forces it off or on.
-constexpr int kStateNT = 2;
-inline bool state_nt(uint64_t state_bytes) {
-  static const int force = [] {
-    const char *e = getenv("FMSKF_STATE_NT");
-    return e ? atoi(e) : -1;
-  }();
-  if (force >= 0) return force != 0;
-  return state_bytes > (256ull << 20);
-}
-
 // the lane's slot in its block's tile; lanes past N take the last instance's slot
 __device__ __forceinline__ uint32_t tile_slot(uint64_t n) {
   const uint64_t b0 = (uint64_t)blockIdx.x * kTile;

@@ -394,3 +394,33 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
         g.load_state(fresh)
         for k, v in g.get_motors().items():
             assert not np.any(v), k
+
+
+_NT_SCRIPT = r"""
+import sys
+sys.path[:0] = sys.argv[1:4]
+from oracle import oracle as orc
+import test_gpu_ctrl as T
+T.test_isr_tick_equals_tick_control_can_tx(orc, "rs", 3001, 60)
+T.test_isr_tick_equals_tick_control_can_tx(orc, "kf6rec", 999, 30)
+T.test_control_step_bitexact(orc, 3001, 100)
+print("nt ok")
+"""
+
+
+def test_nontemporal_control_and_isr_bitexact():
+    """The non-temporal control-state instantiations of k_ctrl_step and k_isr_rs (chosen
+    automatically once the state outgrows the Infinity Cache, fmskf_internal.hpp state_nt)
+    forced on at small N in a child process: the ISR and control parity tests above, against
+    the three-call sequence and the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMSKF_STATE_NT="1")
+    out = subprocess.run([sys.executable, "-c", _NT_SCRIPT, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd"),
+                          os.path.join(root, "tests")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "nt ok" in out.stdout

@@ -780,7 +780,7 @@ print("nt ok")
 
 def test_nontemporal_state_kernels_bitexact():
     """The non-temporal state instantiations (chosen automatically once the state outgrows the
-    Infinity Cache, kf_generic.hpp state_nt) forced on at small N in a child process:
+    Infinity Cache, fmskf_internal.hpp state_nt) forced on at small N in a child process:
     EKF9 and KF12D (block-diagonal and correlated R) with a validity mask, and KF6's k_kf6t
     through the variant script, bit-exact against the oracle."""
     import os
