@@ -38,7 +38,7 @@ if [ "${PROF_ALL:-0}" = 1 ]; then
               "kf6_2p21:--model kf6 --packed --n 2097152 --ticks 100" "isr_rs:--model rs --op isr --ticks 200" \
               "ekf9:--model ekf9 --ticks 100" \
               "ekf9_2p22:--model ekf9 --n 4194304 --ticks 30" "kf12d:--model kf12d --ticks 30" \
-              "rs:--model rs --ticks 200" "control:--op control --ticks 100" \
+              "rs:--model rs --ticks 200" "control:--op control --ticks 100" "control_2p22:--op control --n 4194304 --ticks 30" \
               "wt901:--op wt901 --ticks 50" "can:--op can --ticks 100" "ensemble:--op ensemble --ticks 100" \
               "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000"; do
     name=${spec%%:*}; args=${spec#*:}
