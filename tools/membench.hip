@@ -271,6 +271,21 @@ __global__ __launch_bounds__(256) void k_tiled_probe(float *st, const uint4 *raw
   }
 }
 
+// the pitched (planar) KF6 pattern with non-temporal state loads and stores and a 16-byte record
+template <int NS>
+__global__ __launch_bounds__(256) void k_pitch_nt(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
+                                                  float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(st + k * pitch + v);
+  const uint4 r = raw[v];
+  const float m = sink * (float)(r.x & r.y & r.z & r.w & 1);
+#pragma unroll
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m, st + k * pitch + v);
+}
+
 // the tiled pattern, read from one state buffer and written to another (ping-pong state)
 template <typename TT, int NS, int T>
 __global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, const uint4 *raw, uint64_t n,
@@ -386,6 +401,8 @@ int main(int argc, char **argv) {
     for (int kb : {16, 32, 48})
       tm(kb == 16 ? "ekf9_t256_lds16K" : kb == 32 ? "ekf9_t256_lds32K" : "ekf9_t256_lds48K", 448,
          [&] { k_tiled_probe<54, 256, 4><<<g, 256, kb * 1024>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    tm("kf6_pitch_nt_232B", 232, [&] { k_pitch_nt<27><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
+    tm("ekf9_pitch_nt_448B", 448, [&] { k_pitch_nt<54><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
     // HBM-scale copy ceilings at the model's byte count (half read, half written)
     tm("copy_float4_448B", 448, [&] {
       k_copy4<<<2048, 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n), 224 * n / 16);
