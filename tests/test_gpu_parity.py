@@ -715,12 +715,13 @@ print("variant ok")
 """
 
 
-@pytest.mark.parametrize("variant", ["15", "14"])
+@pytest.mark.parametrize("variant", ["15", "14", "13", "12", "1", "4"])
 def test_kf6_single_tick_variants_bitexact(variant):
     """The other single-tick KF6 kernels (the launcher picks k_kf6p with 2 robots per lane at
-    these sizes): k_kf6t (one robot per lane, the choice past the Infinity Cache) and k_kf6p
-    with 4 robots per lane, forced through FMSKF_KF6_VARIANT in a child process, bit-exact
-    against the oracle with planes, records and a validity mask."""
+    these sizes): k_kf6t (one robot per lane, the choice past the Infinity Cache), k_kf6p
+    with 2-4 robots per lane and the persistent double-buffered kernel, forced through
+    FMSKF_KF6_VARIANT in a child process, bit-exact against the oracle with planes, records
+    and a validity mask."""
     import os
     import subprocess
     import sys
@@ -794,3 +795,27 @@ def test_nontemporal_state_kernels_bitexact():
                              capture_output=True, text=True, timeout=240, env=env)
         assert out.returncode == 0, out.stderr[-3000:]
         assert ok in out.stdout
+
+
+def test_rs_one_robot_per_lane_bitexact():
+    """FMSKF_RS_TWO=0 (k_rs, one robot per lane, instead of k_rs2) in a child process: the RS
+    tick parity test against the oracle, both trig policies."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys\n"
+        "sys.path[:0] = sys.argv[1:4]\n"
+        "from oracle import oracle as orc\n"
+        "import test_gpu_parity as T\n"
+        "T.test_rs_tick_bitexact(orc, T.TABLE)\n"
+        "T.test_rs_tick_bitexact(orc, T.LIBM)\n"
+        "print('rs ok')\n")
+    env = dict(os.environ, FMSKF_RS_TWO="0")
+    out = subprocess.run([sys.executable, "-c", script, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd"),
+                          os.path.join(root, "tests")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "rs ok" in out.stdout
