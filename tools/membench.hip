@@ -241,24 +241,24 @@ __global__ __launch_bounds__(256) void k_model_tiled4(float4 *st, const uint4 *r
 
 // HBM-regime probes of the tiled pattern. MODE 0: loads only (one 4-byte store per lane);
 // 1: stores only; 2: non-temporal loads and stores; 3: non-temporal stores only
-template <int NS, int T, int MODE>
-__global__ __launch_bounds__(256) void k_tiled_probe(float *st, const uint4 *raw, uint64_t n, float sink) {
-  extern __shared__ float occ_cap[];  // dynamic LDS only limits the blocks per CU
+template <int NS, int T, int MODE, typename TT = float>
+__global__ __launch_bounds__(256) void k_tiled_probe(TT *st, const uint4 *raw, uint64_t n, TT sink) {
+  extern __shared__ double occ_cap[];  // dynamic LDS only limits the blocks per CU
   const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= n) return;
-  float *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
+  TT *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
   const uint4 r = raw[v];
-  const float m = sink * (float)(r.x & r.y & r.z & r.w & 1);
+  const TT m = sink * (TT)(r.x & r.y & r.z & r.w & 1);
   if (MODE == 1) {
 #pragma unroll
-    for (int k = 0; k < NS; k++) tile[k * T] = m + (float)k;
+    for (int k = 0; k < NS; k++) tile[k * T] = m + (TT)k;
     return;
   }
-  float s[NS];
+  TT s[NS];
 #pragma unroll
   for (int k = 0; k < NS; k++) s[k] = MODE == 2 ? __builtin_nontemporal_load(tile + k * T) : tile[k * T];
   if (MODE == 0) {
-    float acc = m;
+    TT acc = m;
 #pragma unroll
     for (int k = 0; k < NS; k++) acc += s[k];
     if (acc == 12345.f) occ_cap[threadIdx.x] = acc, tile[0] = occ_cap[threadIdx.x ^ 1];
@@ -403,6 +403,8 @@ int main(int argc, char **argv) {
          [&] { k_tiled_probe<54, 256, 4><<<g, 256, kb * 1024>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
     tm("kf6_pitch_nt_232B", 232, [&] { k_pitch_nt<27><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
     tm("ekf9_pitch_nt_448B", 448, [&] { k_pitch_nt<54><<<g, 256>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
+    tm("kf12d_t256_1504B", 1504, [&] { k_tiled_probe<90, 256, 4, double><<<g, 256>>>((double *)sb, (const uint4 *)ib, n, 0.0); });
+    tm("kf12d_t256_nt_ldst_1504B", 1504, [&] { k_tiled_probe<90, 256, 2, double><<<g, 256>>>((double *)sb, (const uint4 *)ib, n, 0.0); });
     // HBM-scale copy ceilings at the model's byte count (half read, half written)
     tm("copy_float4_448B", 448, [&] {
       k_copy4<<<2048, 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n), 224 * n / 16);
