@@ -79,10 +79,12 @@ def fmskf_pitch(n):
     return ((n + 511) // 512) * 512 + 256
 
 
-def test_ekf9_2p20_sampled_with_mask(orc):
-    """cfg 3's model at 2^20 robots with a random validity mask: a sample bit for bit."""
+@pytest.mark.parametrize("n", [1 << 20, 1 << 22])
+def test_ekf9_sampled_with_mask(orc, n):
+    """cfg 3's model with a random validity mask: a sample bit for bit. At 2^20 the state fits
+    the Infinity Cache; at 2^22 (cfg 3's size) the tick streams it non-temporal."""
     from fmskf.synth import Trajectory
-    n, T = 1 << 20, 4
+    T = 4
     tr = Trajectory(n, T, seed=12)
     raw = tr.ekf9_raw()
     valid = (np.random.default_rng(5).random((T, n)) > 0.2).astype(np.uint8)
@@ -123,9 +125,11 @@ def test_rs_2p20_sampled(orc):
     np.testing.assert_array_equal(prev[:, idx], pv)
 
 
-def test_kf12d_2p18_sampled(orc):
+@pytest.mark.parametrize("n", [1 << 18, 1 << 20])
+def test_kf12d_sampled(orc, n):
+    """KF12D sampled against the oracle; 2^20 is cfg 5's size (non-temporal state stream)."""
     from fmskf.synth import Trajectory
-    n, T = 1 << 18, 4
+    T = 4
     tr = Trajectory(n, T, seed=14)
     z = tr.kf12d_z()
     with Engine("kf12d", n) as e:
