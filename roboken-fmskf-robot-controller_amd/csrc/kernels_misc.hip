@@ -129,30 +129,35 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
     }
   }
   block_sum<LEN>(v, red, part, tot);
-  for (int k = threadIdx.x; k < LEN; k += kBlock) blocks[(uint64_t)blockIdx.x * LEN + k] = tot[k];
+  // element-major block records ([LEN][gridDim.x]): the fold's loads of one element across
+  // consecutive blocks are then one coalesced access
+  for (int k = threadIdx.x; k < LEN; k += kBlock) blocks[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
 }
 
-// Fold (one block): thread t sums block records t, t + 256, ... in order, then the block sum,
+// Fold (one block): thread t sums block records t, t + 256, ... in order (records stored
+// element-major, [LEN][nblocks]), then the block sum,
 // then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
 template <int NX, typename T>
 __global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp, uint32_t tile,
                                                      const double *__restrict__ blocks,
                                                      int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
+  static_assert(LEN <= kBlock, "one record element per thread in the conversion");
   __shared__ double red[kEnsCh][kBlock];
   __shared__ double part[kEnsCh][kEnsCh];
   __shared__ double tot[LEN];
+  const int t = threadIdx.x;
   double v[LEN];
 #pragma unroll
   for (int k = 0; k < LEN; k++) v[k] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-    const double *rb = blocks + (uint64_t)b * LEN;
 #pragma unroll
-    for (int k = 0; k < LEN; k++) v[k] = v[k] + rb[k];
+    for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)k * nblocks + b];
   }
   block_sum<LEN>(v, red, part, tot);
   const double c = tot[0];
-  for (int k = threadIdx.x; k < LEN; k += kBlock) {
+  if (t < LEN) {
+    const int k = t;
     double r;
     if (k == 0) {
       r = c;
