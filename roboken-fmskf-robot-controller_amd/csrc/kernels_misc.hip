@@ -140,27 +140,68 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
   for (int k = threadIdx.x; k < LEN; k += kBlock) blocks[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
 }
 
-// Fold (one block): thread t sums block records t, t + 256, ... in order (records stored
-// element-major, [LEN][nblocks]), then the block sum,
-// then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
+// Fold (one block): sums the block records (stored element-major, [LEN][nblocks]) in a fixed
+// order, then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
 template <int NX, typename T>
 __global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp, uint32_t tile,
                                                      const double *__restrict__ blocks,
                                                      int nblocks, double *out) {
   constexpr int LEN = EnsRec<NX>::LEN;
   static_assert(LEN <= kBlock, "one record element per thread in the conversion");
-  __shared__ double red[kEnsCh][kBlock];
-  __shared__ double part[kEnsCh][kEnsSeg];
   __shared__ double tot[LEN];
   const int t = threadIdx.x;
-  double v[LEN];
+  // Records of up to 64 elements (KF6 28, EKF9 55): element-parallel, G threads per record
+  // element; thread g of element e sums blocks g, g + G, ... (8 rotating accumulators,
+  // combined in order), then the G partials of an element are summed in order: no LEN-wide
+  // register record, one barrier.  A/B at 2^20 (partial + fold, 512 blocks): KF6 13.8 ->
+  // 12.9 us, EKF9 30.5 -> 29.3.  KF12D's 91 elements would leave 2 threads per element
+  // (256 serial loads each): 38.6 -> 40.6 us, so it keeps the register-record fold.
+  if constexpr (LEN * 4 <= kBlock) {
+    constexpr int G = LEN * 8 <= kBlock ? 8 : 4;
+    constexpr int A = 8;
+    __shared__ double part[LEN][G];
+    {
+      const int e = t / G, g = t % G;
+      if (e < LEN) {
+        const double *row = blocks + (uint64_t)e * nblocks;
+        double a[A];
 #pragma unroll
-  for (int k = 0; k < LEN; k++) v[k] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+        for (int j = 0; j < A; j++) a[j] = 0.0;
+        int b = g;
+        for (; b + (4 * A - 1) * G < nblocks; b += 4 * A * G) {
+          double l[4 * A];
 #pragma unroll
-    for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)k * nblocks + b];
+          for (int j = 0; j < 4 * A; j++) l[j] = row[b + j * G];
+#pragma unroll
+          for (int j = 0; j < 4 * A; j++) a[j % A] = a[j % A] + l[j];
+        }
+        for (int j = 0; b < nblocks; b += G, j++) a[j % A] = a[j % A] + row[b];
+        double s = a[0];
+#pragma unroll
+        for (int j = 1; j < A; j++) s = s + a[j];
+        part[e][g] = s;
+      }
+    }
+    __syncthreads();
+    if (t < LEN) {
+      double s = part[t][0];
+#pragma unroll
+      for (int j = 1; j < G; j++) s = s + part[t][j];
+      tot[t] = s;
+    }
+    __syncthreads();
+  } else {
+    __shared__ double red[kEnsCh][kBlock];
+    __shared__ double part[kEnsCh][kEnsSeg];
+    double v[LEN];
+#pragma unroll
+    for (int k = 0; k < LEN; k++) v[k] = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+      for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)k * nblocks + b];
+    }
+    block_sum<LEN>(v, red, part, tot);
   }
-  block_sum<LEN>(v, red, part, tot);
   const double c = tot[0];
   if (t < LEN) {
     const int k = t;
