@@ -39,9 +39,22 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model() -> str:
+    """The host CPU's model string (/proc/cpuinfo, as lscpu prints it)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(yaw, gz, rpm, sample_s: float):
     """The oracle's C restatement of the same KF6 tick (OpenMP over instances, -O3,
-    contraction off) timed on this host on a bounded sample."""
+    contraction off) timed on this host on a bounded sample: all threads, then one thread on
+    the same instance count (so the two rates are per the same working set)."""
     import numpy as np
     import fmskf
     from oracle import oracle as orc
@@ -51,28 +64,85 @@ def cpu_baseline(yaw, gz, rpm, sample_s: float):
     prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
     threads = orc.max_threads()
     res = {}
-    for label, nt, budget in (("all", threads, sample_s), ("one", 1, max(1.0, sample_s / 4))):
-        nn = n if nt > 1 else max(4096, n // 16)
-        x = np.zeros((6, nn), np.float32)
-        P = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], nn, 1).copy()
-        ys, gs, rs = (np.ascontiguousarray(a[:, :nn]) for a in (yaw, gz, rpm))
+    for label, nt, budget in (("all", threads, sample_s), ("one", 1, max(2.0, sample_s / 3))):
+        x = np.zeros((6, n), np.float32)
+        P = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
         ticks = 0
         t0 = time.perf_counter()
         while True:
             t = ticks % T
-            orc.kf6_tick(x, P, ys[t], gs[t], rs[t], None, prm, nthreads=nt)
+            orc.kf6_tick(x, P, yaw[t], gz[t], rpm[t], None, prm, nthreads=nt)
             ticks += 1
             el = time.perf_counter() - t0
             if el >= budget and ticks >= 3:
                 break
-        res[label] = (nn * ticks / el, nn, ticks, el)
-    v, nn, ticks, el = res["all"]
+        res[label] = (n * ticks / el, ticks, el)
+    v, ticks, el = res["all"]
     return {
         "value": v, "unit": "steps/s", "cores": threads, "kind": "port",
-        "sample": f"{nn} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick, "
-                  f"oracle/fmskf_oracle.c -O3 -ffp-contract=off, OpenMP {threads} threads",
+        "sample": f"{n} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick, "
+                  f"oracle/fmskf_oracle.c -O3 -ffp-contract=off, OpenMP {threads} threads; "
+                  f"1 thread: {n} instances x {res['one'][1]} ticks ({res['one'][2]:.1f} s)",
+        "cpu_model": cpu_model(),
         "value_1core": res["one"][0],
     }
+
+
+def secondary_configs(dev, stream, ticks: int, trig):
+    """BASELINE.json configs[2] (EKF9 2^22), configs[4] (KF12D fp64 2^20) and the cache-busting
+    cfg 2 at 2^24: each model's single-tick kernel, back to back, HIP events
+    on the stream it runs on; one line each with kernel_ms and its HBM roofline."""
+    import torch
+    import fmskf
+    from fmskf.synth import SEED, kf6_ring_torch
+    out = {}
+    specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 448), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504),
+             ("cfg2_kf6_2p24", "kf6", 1 << 24, 232)]
+    R = 4
+    for key, model, n, bps in specs:
+        e = fmskf.Engine(model, n, device=dev.index, trig=trig)
+        e.set_stream(stream)
+        yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 7, device=dev)
+        if model == "kf6":
+            rec = fmskf.kf6_records(yaw, gz, rpm)
+            preps = [e.prepare(kf6_rec=rec[r]) for r in range(R)]
+            keep = (rec,)
+        elif model == "ekf9":
+            raw = torch.cat([torch.round(yaw / 180.0 * 32768).clamp(-32768, 32767).to(torch.int16)[..., None],
+                             torch.round(-gz / 2000.0 * 32768).clamp(-32768, 32767).to(torch.int16)[..., None],
+                             torch.zeros(R, n, 2, dtype=torch.int16, device=dev), rpm], -1).contiguous()
+            preps = [e.prepare(raw=raw[r]) for r in range(R)]
+            keep = (raw,)
+        else:
+            z = torch.zeros(R, 8, n, dtype=torch.float64, device=dev)
+            z[:, 0] = torch.deg2rad(yaw.double())
+            z[:, 1] = -torch.deg2rad(gz.double())
+            z[:, 2] = 0.3
+            z[:, 4] = 0.5
+            preps = [e.prepare(z=z[r]) for r in range(R)]
+            keep = (z,)
+        del yaw, gz, rpm
+        for k in range(3):
+            e.tick_prepared(preps[k % R])
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for k in range(ticks):
+            e.tick_prepared(preps[k % R])
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / ticks
+        cnt = e.get_counters()
+        e.close()
+        del preps, keep
+        torch.cuda.empty_cache()
+        gbps = bps * n / (ms * 1e-3) / 1e9
+        out[key] = {"model": model, "instances": n, "steps_per_s": n / (ms * 1e-3), "kernel_ms": ms,
+                    "ticks": ticks, "nonfinite_instances": int(cnt[0]),
+                    "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                 "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": bps}}
+    return out
 
 
 def main():
@@ -87,8 +157,16 @@ def main():
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused multi-tick figure")
-    ap.add_argument("--gather", choices=["async", "stream"], default="async",
-                    help="N > 1: all-gather on RCCL's stream (async) or in the tick stream")
+    ap.add_argument("--gather", choices=["async", "stream", "native"], default="async",
+                    help="N > 1: torch.distributed all-gather on RCCL's stream (async) or in the tick "
+                         "stream; native: the handle's own communicator (fmskf_comm_init + "
+                         "fmskf_ensemble_stats, the path C callers bind; host-synchronous)")
+    ap.add_argument("--ensemble", choices=["fused", "separate"], default="fused",
+                    help="ensemble ticks: fmskf_tick_ensemble (the tick kernel writes the record) or "
+                         "fmskf_tick + fmskf_ensemble_partial")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the cfg 3 / cfg 5 / 2^24 single-GPU kernel lines")
+    ap.add_argument("--secondary-ticks", type=int, default=20)
     ap.add_argument("--inputs", choices=["records", "planes"], default="records",
                     help="16-byte fmskf_kf6_record per robot (one load per lane) or yaw/gyro/rpm planes")
     args = ap.parse_args()
@@ -136,7 +214,7 @@ def main():
     tick_fn = fmskf.load().fmskf_tick
     rec_len = eng.ensemble_record_len()
     rec = torch.empty(rec_len, dtype=torch.float64, device=dev)
-    n_events = max(1, (args.steps + args.warmup) // max(1, args.ensemble_every) + 1)
+    n_events = max(1, (2 * args.steps + args.warmup) // max(1, args.ensemble_every) + 2)
     # one record and one gather slot per ensemble event: the all-gather runs asynchronously
     # on RCCL's stream (ordered after the record by RCCL's stream dependency) while the next
     # ticks proceed; pending gathers are joined before the timed region closes
@@ -145,11 +223,28 @@ def main():
     ev_count = [0]
     pending = []
 
-    def step(k):
-        eng.tick_prepared(prepared[k % R], tick_fn)
-        if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
-            e = ev_count[0] % n_events
-            eng.ensemble_partial(recs[e])
+    if args.gather == "native":
+        # the handle's own RCCL communicator: rank 0's unique id reaches the others over the
+        # torch.distributed group (or stays local at world 1)
+        uid = [fmskf.comm_unique_id() if rank == 0 else None]
+        if distributed:
+            dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0], rank, world)
+    native_stats = [None]
+
+    def ens_event(k):
+        """one ensemble event after tick k: record (fused into the tick, or a separate pass),
+        then this rank's share of the all-gather"""
+        e = ev_count[0] % n_events
+        if args.gather == "native":
+            eng.tick_prepared(prepared[k % R], tick_fn)
+            native_stats[0] = eng.ensemble_stats()
+        else:
+            if args.ensemble == "fused":
+                eng.tick_ensemble_prepared(prepared[k % R], recs[e])
+            else:
+                eng.tick_prepared(prepared[k % R], tick_fn)
+                eng.ensemble_partial(recs[e])
             if distributed and args.gather == "stream":
                 dist.all_gather_into_tensor(gathered[e].view(-1), recs[e])
             elif distributed:
@@ -157,7 +252,13 @@ def main():
                                                            async_op=True))
             else:
                 gathered[e][0].copy_(recs[e])
-            ev_count[0] += 1
+        ev_count[0] += 1
+
+    def step(k):
+        if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
+            ens_event(k)
+        else:
+            eng.tick_prepared(prepared[k % R], tick_fn)
 
     def join():
         while pending:
@@ -165,23 +266,34 @@ def main():
 
     for k in range(args.warmup):
         step(k)
+    # every path the timed region runs has run once before it (kernels load lazily on their
+    # first launch: ~2 ms for the ensemble kernels, measured inside the timed region in round 1)
+    if args.ensemble_every > 0 and (args.warmup < args.ensemble_every or args.warmup == 0):
+        ens_event(args.warmup)
     join()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    # HIP events on the stream the kernels run on, around exactly the K timed ticks
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # exactly the K timed ticks, wall clock between the two synchronisations (no event
+    # record inside: its host call would delay the first launch)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
     join()
-    ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    # the same K-step sequence once more between HIP events on the tick stream: the GPU-side
+    # duration of the timed region's work (diagnostic; `value` is the wall clock above)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for k in range(args.warmup + args.steps, args.warmup + 2 * args.steps):
+        step(k)
+    join()
+    ev1.record(stream)
+    torch.cuda.synchronize()
     region_ms = ev0.elapsed_time(ev1)
 
     # the tick kernel's own average launch duration (the roofline's denominator): K more
@@ -223,8 +335,15 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for k in range(k1_steps):
-            eng.tick_prepared(prepared[k % R], tick_fn)
-            eng.ensemble_partial(rec)
+            if args.gather == "native":
+                eng.tick_prepared(prepared[k % R], tick_fn)
+                eng.ensemble_stats()
+                continue
+            if args.ensemble == "fused":
+                eng.tick_ensemble_prepared(prepared[k % R], rec)
+            else:
+                eng.tick_prepared(prepared[k % R], tick_fn)
+                eng.ensemble_partial(rec)
             if distributed:
                 dist.all_gather_into_tensor(gathered[0].view(-1), rec)
         torch.cuda.synchronize()
@@ -240,7 +359,10 @@ def main():
     # ensemble sanity (outside the timed region): fold the last gathered records in rank order
     last = gathered[(ev_count[0] - 1) % n_events].cpu().numpy() if ev_count[0] else None
     ens = None
-    if last is not None:
+    if args.gather == "native" and native_stats[0] is not None:
+        mean, cov = native_stats[0]
+        ens = {"count": float(n * world), "mean_theta": float(mean[2]), "var_vx": float(cov[9])}
+    elif last is not None:
         mean, cov = fmskf.ensemble_combine(6, last)
         ens = {"count": float(last[:, 0].sum()), "mean_theta": float(mean[2]),
                "var_vx": float(cov[9])}
@@ -292,12 +414,15 @@ def main():
                 + (", one 16-byte fmskf_kf6_record per robot-tick" if krec is not None else ", SoA planes"),
         "config": {
             "workload": "cfg2: 2^20 independent 6-state fp32 KF instances per GPU, fused "
-                        "correct+predict per tick (fmskf_tick)",
+                        "correct+predict per tick (fmskf_tick; every ensemble_every-th tick "
+                        "fmskf_tick_ensemble, which also writes the ensemble record)",
             "instances_per_gpu": n,
             "global_instances": n * world,
             "trig": args.trig,
             "inputs": args.inputs,
             "ensemble_every": args.ensemble_every,
+            "ensemble": args.ensemble,
+            "gather": args.gather if world > 1 else None,
             "parallelism": f"instance-sharded x{world}" + (", RCCL all-gather of ensemble records"
                                                            if world > 1 else ""),
         },
@@ -323,12 +448,18 @@ def main():
         "ensemble": ens,
         "nonfinite_instances": int(counters[0]),
     }
+    eng.close()
+    del prepared, planes, krec, many_in
+    if not args.no_secondary and world == 1:  # single-GPU configs: one line at N=1
+        torch.cuda.empty_cache()
+        out["secondary"] = secondary_configs(dev, stream, args.secondary_ticks, trig)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         y = yaw[:8, : 1 << 18].cpu().numpy()
         g = gz[:8, : 1 << 18].cpu().numpy()
         r = rpm[:8, : 1 << 18].cpu().numpy()
-        out["cpu_baseline"] = cpu_baseline(y, g, r, args.cpu_sample_s)
-    eng.close()
+        cb = cpu_baseline(y, g, r, args.cpu_sample_s)
+        cb["gpu_over_cpu"] = value / cb["value"]  # the driver-timed value, not the kernel time
+        out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:

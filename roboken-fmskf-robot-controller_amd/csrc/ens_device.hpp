@@ -1,0 +1,131 @@
+// ens_device.hpp -- device side of the ensemble statistics record: per-lane
+// shifted moment sums and their fixed-order block reduction, shared by the stand-alone
+// partial kernel (kernels_misc.hip) and the tick kernels that emit the record of the state
+// they just wrote (kernels_kf6.hip, fmskf_tick_ensemble).
+//
+// Record of a set of robots (fp64): {count, S1[n] = sum(x - s), S2 packed = sum((x-s)(x-s)^T)}
+// with s the handle's shift vector (robot 0's state when the handle's first record was asked
+// for, refreshed by reset / set_state / load_state).  No division in the streaming part.
+//
+// Block reduction without an LDS transpose (the round-1 design pushed every lane's 28-91
+// doubles through LDS: 57 KB per KF6 block).  A wave of 64 lanes reduces its LEN4 = 4Q values
+// by recursive halving: v_permlane32_swap pairs value j with value j + 2Q so the lower half
+// of the wave sums one and the upper half the other (one swap per dword, no selects), then
+// v_permlane16_swap does the same across 16-lane rows, leaving Q values per row; four DPP
+// butterfly steps reduce each row.  Row r's lanes then hold elements [rQ, rQ + Q).  LDS holds
+// only 4 waves x LEN4 doubles.  Every element goes through the same addition tree (fp add is
+// commutative, the pairings are lane-position based), so a value reduced at any position of
+// the record gets bitwise the same sum: the parallel fold relies on that.
+#pragma once
+#include "fmskf_internal.hpp"
+
+namespace fmskf {
+
+template <int NX>
+struct EnsRec {
+  static constexpr int NP = NX * (NX + 1) / 2;
+  static constexpr int LEN = 1 + NX + NP;
+  static constexpr int LEN4 = (LEN + 3) & ~3;
+  static constexpr int Q = LEN4 / 4;
+};
+
+__device__ __forceinline__ uint2 dsplit(double v) { return __builtin_bit_cast(uint2, v); }
+__device__ __forceinline__ double djoin(uint32_t lo, uint32_t hi) {
+  return __builtin_bit_cast(double, make_uint2(lo, hi));
+}
+
+// lanes 0-31: a(lane) + a(lane + 32); lanes 32-63: b(lane - 32) + b(lane)
+__device__ __forceinline__ double halve32(double a, double b) {
+  const uint2 ua = dsplit(a), ub = dsplit(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap(ua.x, ub.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(ua.y, ub.y, false, false);
+  return djoin(lo[0], hi[0]) + djoin(lo[1], hi[1]);
+}
+// within each 32-lane half: rows 0 / 2 sum a over rows (0,1) / (2,3), rows 1 / 3 sum b
+__device__ __forceinline__ double halve16(double a, double b) {
+  const uint2 ua = dsplit(a), ub = dsplit(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+  return djoin(lo[0], hi[0]) + djoin(lo[1], hi[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_sum(double v) {
+  const uint2 u = dsplit(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)u.x, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)u.y, CTRL, 0xF, 0xF, true);
+  return v + djoin(lo, hi);
+}
+// 16-lane row sum, every lane of the row ends with it: xor 1, xor 2 (quad_perm), then
+// lane i with 7 - i (row_half_mirror) and with 15 - i (row_mirror)
+__device__ __forceinline__ double row_sum(double v) {
+  v = dpp_sum<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_sum<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_sum<0x141>(v);  // row_half_mirror
+  v = dpp_sum<0x140>(v);  // row_mirror
+  return v;
+}
+
+// Sum v[LEN4] over the block's 256 lanes; thread t < LEN4 gets element t (returned), the
+// other threads get 0.  `red` is LDS of 4 * LEN4 doubles.  Ends with the block's threads
+// synchronised (the caller may reuse nothing of `red` without another barrier).
+template <int LEN4>
+__device__ __forceinline__ double block_reduce(double (&v)[LEN4], double *red) {
+  constexpr int Q = LEN4 / 4;
+  double w[2 * Q];
+#pragma unroll
+  for (int j = 0; j < 2 * Q; j++) w[j] = halve32(v[j], v[j + 2 * Q]);
+  double u[Q];
+#pragma unroll
+  for (int j = 0; j < Q; j++) u[j] = row_sum(halve16(w[j], w[j + Q]));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((lane & 15) == 0) {
+    const int r = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < Q; j++) red[wave * LEN4 + r * Q + j] = u[j];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  double s = 0.0;
+  if (t < LEN4) {
+    s = red[t];
+#pragma unroll
+    for (int wv = 1; wv < kBlock / 64; wv++) s = s + red[wv * LEN4 + t];
+  }
+  return s;
+}
+
+// Accumulate one robot's shifted moments into v (v[0] count, v[1..NX] S1, then S2 packed).
+template <int NX, typename T, int LEN4>
+__device__ __forceinline__ void ens_add(double (&v)[LEN4], const T (&x)[NX], const double (&sh)[NX]) {
+  double d[NX];
+#pragma unroll
+  for (int k = 0; k < NX; k++) {
+    d[k] = (double)x[k] - sh[k];
+    v[1 + k] = v[1 + k] + d[k];
+  }
+#pragma unroll
+  for (int p = 0; p < NX; p++)
+#pragma unroll
+    for (int q = 0; q <= p; q++) {
+      double &a = v[1 + NX + p * (p + 1) / 2 + q];
+      a = __builtin_fma(d[p], d[q], a);
+    }
+  v[0] = v[0] + 1.0;
+}
+
+template <int NX>
+__device__ __forceinline__ void ens_load_shift(const double *shift, double (&sh)[NX]) {
+#pragma unroll
+  for (int k = 0; k < NX; k++) sh[k] = shift[k];
+}
+
+// Block record (element-major [LEN][nblocks], so the fold reads one element coalesced)
+template <int NX>
+__device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], double *blocks) {
+  __shared__ double red[4 * EnsRec<NX>::LEN4];
+  const double s = block_reduce<EnsRec<NX>::LEN4>(v, red);
+  if (threadIdx.x < EnsRec<NX>::LEN)
+    blocks[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+}
+
+}  // namespace fmskf

@@ -92,9 +92,13 @@ struct fmskf_ctx {
   // staging for host-resident inputs
   void *stage = nullptr;
   size_t stage_bytes = 0;
-  // ensemble scratch
+  // ensemble scratch: block records [LEN][blocks], the record, the shift vector (robot 0's
+  // state when the first record after create / reset / set_state / load_state was asked for)
   double *ens_blocks = nullptr;
   double *ens_out = nullptr;
+  double *ens_shift = nullptr;
+  bool ens_shift_ok = false;
+  size_t ens_gather_cap = 0;
   // readout scratch [6][N] float
   float *readout = nullptr;
   // output scratch for host-destined results of the control / export entry points
@@ -152,6 +156,17 @@ struct fmskf_ctx {
     if (e != hipSuccess) fail(FMSKF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     allocs.push_back(p);
     return (T *)p;
+  }
+  // free one allocation made by alloc() (after the stream has drained)
+  void release(void *p) {
+    if (!p) return;
+    for (size_t i = 0; i < allocs.size(); i++)
+      if (allocs[i] == p) {
+        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        (void)hipFree(p);
+        allocs.erase(allocs.begin() + (long)i);
+        return;
+      }
   }
   void *stage_for(size_t bytes) {
     if (bytes > stage_bytes) {
@@ -333,6 +348,15 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
 }
+// the ensemble shift vector: robot 0's state, taken once per create / reset / set_state /
+// load_state, so successive records of one state are bitwise identical
+void ensure_shift(fmskf_ctx *h) {
+  if (h->ens_shift_ok) return;
+  launch_check(launch_ens_shift(h->s, (int)h->d.nx, h->d.elem == 8, h->ens_shift, h->stream),
+               "ensemble shift launch");
+  h->ens_shift_ok = true;
+}
+
 void ensure_imu(fmskf_ctx *h) {
   DevState &s = h->s;
   if (s.imu_reg) return;
@@ -421,6 +445,7 @@ void do_reset(fmskf_ctx *h) {
     hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, st), "reset ctrl");
   }
   hip_check(hipMemsetAsync(s.counters, 0, 8 * 8, st), "reset counters");
+  h->ens_shift_ok = false;
 }
 
 // Resolve the tick inputs of a call (NULL -> device-resident ingest state), stage host
@@ -622,8 +647,15 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       // (ensure_imu / ensure_motors): a handle fed tick inputs by the caller holds only x, P
       s.counters = h->alloc<unsigned long long>(8);
       s.sintab = h->alloc<float>(513);
-      h->ens_blocks = h->alloc<double>((size_t)ensemble_nblocks(n) * 91);
-      h->ens_out = h->alloc<double>(91);
+      {
+        // the fused KF6 tick + record (fmskf_tick_ensemble) writes one record per tick block
+        const size_t len = 1 + d.nx + np;
+        size_t nb = (size_t)ensemble_nblocks(n);
+        if (cfg->model == FMSKF_MODEL_KF6) nb = std::max(nb, (size_t)((n + kBlock - 1) / kBlock));
+        h->ens_blocks = h->alloc<double>(nb * len);
+        h->ens_out = h->alloc<double>(91);
+        h->ens_shift = h->alloc<double>(12);
+      }
       h->readout = h->alloc<float>(6 * n);
       float tab[513];
       for (int i = 0; i <= 512; i++) tab[i] = (float)sin(2.0 * 3.14159265358979323846 * (double)i / 512.0);
@@ -875,6 +907,7 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
       if (x) copy_planes_in(h, h->s.x, x, row, pb, d.nx, mem);
       if (p_packed) copy_planes_in(h, h->s.P, p_packed, row, pb, np, mem);
     }
+    if (x) h->ens_shift_ok = false;
     finish_out(h, mem);
   });
 }
@@ -1004,6 +1037,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (hd.abi != FMSKF_ABI_VERSION || hd.model != h->cfg.model || hd.n != h->s.n ||
         hd.pitch != h->s.pitch || hd.tile != h->s.tile || hd.elem != h->d.elem || (hd.groups & ~15u))
       fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, N or layout)");
+    if (!(hd.groups & 1u)) fail(FMSKF_EINVAL, "checkpoint holds no estimator state");
     fmskf_config saved;
     f.read(&saved, sizeof(saved));
     fmskf_ctrl_params cp{};
@@ -1025,20 +1059,23 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     f.seek(0, SEEK_END);
     if (f.tell() != end) fail(FMSKF_EINVAL, "checkpoint size mismatch (truncated or trailing bytes)");
     f.seek(body, SEEK_SET);
+    // read every section into host memory first: a read failure leaves the handle untouched
+    std::vector<std::vector<char>> bufs(secs.size());
+    for (size_t k = 0; k < secs.size(); k++) {
+      uint64_t b = 0;
+      f.read(&b, 8);
+      bufs[k].resize(secs[k].bytes);
+      f.read(bufs[k].data(), secs[k].bytes);
+    }
     // groups the checkpoint does not hold were never used by the saving handle: reset them here
     if (!(hd.groups & 2) && h->s.imu_reg) zero_imu(h);
     if (!(hd.groups & 4) && h->s.m_sum) zero_motors(h);
     if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
     hip_check(hipStreamSynchronize(h->stream), "load sync");
-    std::vector<char> buf;
-    for (const CkSection &c : secs) {
-      uint64_t b = 0;
-      f.read(&b, 8);
-      buf.resize(c.bytes);
-      f.read(buf.data(), c.bytes);
-      hip_check(hipMemcpy(c.dev, buf.data(), c.bytes, hipMemcpyHostToDevice), "load H2D");
-    }
+    for (size_t k = 0; k < secs.size(); k++)
+      hip_check(hipMemcpy(secs[k].dev, bufs[k].data(), secs[k].bytes, hipMemcpyHostToDevice), "load H2D");
     if (hd.groups & 8) h->cprm = cp;
+    h->ens_shift_ok = false;
   });
 }
 
@@ -1119,7 +1156,9 @@ int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem) {
     const uint32_t nx = h->d.nx;
     const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
     double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
-    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, dst, h->stream),
+    ensure_shift(h);
+    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, h->ens_shift, dst,
+                                 h->stream),
                  "ensemble launch");
     if (mem == FMSKF_MEM_HOST) {
       copy_out(h, out, h->ens_out, len * 8, mem);
@@ -1139,9 +1178,26 @@ int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out
     const uint32_t nx = h->d.nx;
     const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
     double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
-    run_tick(h, in, true, true, 1, h->s.n);
-    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, dst, h->stream),
-                 "ensemble launch");
+    ensure_shift(h);
+    if (h->cfg.model == FMSKF_MODEL_KF6) {
+      // one kernel: the tick writes each block's record of the state it just stored (no
+      // second pass over x), then the fold
+      TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
+      t.ens_blocks = h->ens_blocks;
+      t.ens_shift = h->ens_shift;
+      int nb = 0;
+      h->time_begin();
+      launch_check(launch_kf6(h->s, t, h->kf6, h->cfg.trig == FMSKF_TRIG_LIBM, true, true, h->stream, &nb),
+                   "tick kernel launch");
+      h->time_end();
+      launch_check(launch_ens_fold((int)nx, h->ens_blocks, nb, h->ens_shift, dst, h->stream),
+                   "ensemble fold launch");
+    } else {
+      run_tick(h, in, true, true, 1, h->s.n);
+      launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, h->ens_shift, dst,
+                                   h->stream),
+                   "ensemble launch");
+    }
     if (mem == FMSKF_MEM_HOST) {
       copy_out(h, out, h->ens_out, len * 8, mem);
       finish_out(h, mem);
@@ -1259,12 +1315,22 @@ int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int r
     const RcclApi &a = need_rccl();
     DeviceGuard g(h->cfg.device);
     h->destroy_comm();
+    h->rank = 0;
+    h->world = 1;
+    // the gather buffer is reused while the new world fits it (re-initialising does not leak)
+    if ((size_t)world > h->ens_gather_cap) {
+      double *buf = h->alloc<double>((size_t)world * 91);
+      h->release(h->ens_gather);
+      h->ens_gather = buf;
+      h->ens_gather_cap = (size_t)world;
+    }
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
-    nccl_check(a.comm_init_rank(&h->comm, world, u, rank), "ncclCommInitRank");
+    ncclComm_t c = nullptr;
+    nccl_check(a.comm_init_rank(&c, world, u, rank), "ncclCommInitRank");
+    h->comm = c;
     h->rank = rank;
     h->world = world;
-    h->ens_gather = h->alloc<double>((size_t)world * 91);
   });
 }
 
@@ -1273,7 +1339,9 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed) {
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
-    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, h->ens_out, h->stream),
+    ensure_shift(h);
+    launch_check(launch_ensemble(h->s, (int)nx, h->d.elem == 8, h->ens_blocks, h->ens_shift, h->ens_out,
+                                 h->stream),
                  "ensemble launch");
     const double *src = h->ens_out;
     int ranks = 1;

@@ -63,6 +63,10 @@ struct TickIn {
   const float *sintab;       // 513-entry TABLE512 sine table (device)
   uint64_t stride;
   uint32_t n_ticks;
+  // fmskf_tick_ensemble: the tick kernel also writes its blocks' ensemble records of the
+  // post-tick state ([LEN][grid], ens_device.hpp) against the shift vector; null otherwise
+  double *ens_blocks;
+  const double *ens_shift;
 };
 
 template <typename T, int NP, int MP>
@@ -185,8 +189,9 @@ struct Wt901Cfg {
 // launchers (return hipError_t as int)
 int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool predict,
               hipStream_t st);
+// in.ens_blocks set (upd and pred only): *ens_nb receives the grid, i.e. the record count
 int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool libm, bool upd,
-               bool pred, hipStream_t st);
+               bool pred, hipStream_t st, int *ens_nb = nullptr);
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
                 bool pred, hipStream_t st);
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,
@@ -197,9 +202,14 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
                const uint8_t *present, const int8_t dir[4], hipStream_t st);
 int launch_trig(const float *x, float *sv, float *cv, uint64_t n, bool libm, const float *tab,
                 hipStream_t st);
-// ensemble: per-block partial records, then a single-block fold in block order
-int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
+// ensemble (kernels_misc.hip): per-block partial records of x, then the fold (one block per
+// record element); launch_ens_fold folds records a tick kernel wrote (nb = its grid);
+// launch_ens_shift sets the shift vector to robot 0's state
+int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
+                    double *out, hipStream_t st);
+int launch_ens_fold(int nx, const double *blocks, int nb, const double *shift, double *out,
                     hipStream_t st);
+int launch_ens_shift(const DevState &s, int nx, bool f64, double *shift, hipStream_t st);
 int ensemble_nblocks(uint64_t n);
 // vehicle control step, TX frames, VehicleInfo export (kernels_ctrl.hip)
 int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,

@@ -20,6 +20,7 @@
 //  * tick_many loads the inputs of tick t+1 before computing tick t; the double-buffered
 //    persistent variant loads the next instance's state + inputs before computing the
 //    current one (two register sets, loop unrolled by two: no loop-carried copies).
+#include "ens_device.hpp"
 #include "kf_generic.hpp"
 
 #pragma clang fp contract(off)
@@ -29,14 +30,32 @@ namespace fmskf {
 // REC: the inputs come as 16-byte fmskf_kf6_record's (one 16-byte load per lane) instead of
 // the yaw / gyro / rpm planes (three loads): measured 41.6 -> 39.5 us per tick at 2^20
 // NT: the state is loaded and stored non-temporal (fmskf_internal.hpp state_nt)
-template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false, bool NT_ = false>
+// ENS: the tick also writes its block's ensemble record of the post-tick state
+// (fmskf_tick_ensemble; ens_device.hpp), so the record costs no second pass over x
+template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false, bool NT_ = false,
+          bool ENS_ = false>
 struct Opt {
   static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_,
-                        REC = REC_, NT = NT_;
+                        REC = REC_, NT = NT_, ENS = ENS_;
   static constexpr int CP = NT_ ? kStateNT : 0;
 };
 template <class O>
-using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true>;
+using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true, O::ENS>;
+template <class O>
+using WithEns = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, true>;
+
+// the record of the robots this lane ticked (live ones only), reduced over the block
+template <int R>
+__device__ __forceinline__ void kf6_ens(const TickIn &in, const float (&xs)[R][6], const bool (&live)[R]) {
+  double sh[6], v[EnsRec<6>::LEN4];
+  ens_load_shift<6>(in.ens_shift, sh);
+#pragma unroll
+  for (int k = 0; k < EnsRec<6>::LEN4; k++) v[k] = 0.0;
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (live[r]) ens_add<6>(v, xs[r], sh);
+  ens_block_write<6>(v, in.ens_blocks);
+}
 
 struct Kf6In {
   float yaw, gz;
@@ -238,6 +257,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   kf6_tick1<O>(m, stab, a.prm, x, P);
   if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
   nan_guard(x, P, a.counters, live);
+  if constexpr (O::ENS) {
+    float xs[1][6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) xs[0][k] = x[k];
+    const bool lv[1] = {live};
+    kf6_ens<1>(a.in, xs, lv);
+  }
 }
 
 // R robots per lane (i, i + G, ..., G = the grid's lane count), the tick inputs of all R
@@ -255,6 +281,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
   WaveTable<O::LIBM> tv(a.in.sintab);
   Kf6In m[R];
+  float xs[O::ENS ? R : 1][6];
+  bool lv[R];
   if (O::UPD) {
 #pragma unroll
     for (int r = 0; r < R; r++) m[r] = kf6_load_in<O>(a.in, n, 0, min(i0 + r * G, last));
@@ -268,7 +296,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     kf6_tick1<O>(m[r], stab, a.prm, x, P);
     if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
     nan_guard(x, P, a.counters, live);
+    if constexpr (O::ENS) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) xs[r][k] = x[k];
+    }
+    lv[r] = live;
   }
+  if constexpr (O::ENS) kf6_ens<R>(a.in, xs, lv);
 }
 
 // Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no
@@ -386,35 +420,67 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   }
 }
 
+// fused tick + ensemble record (fmskf_tick_ensemble): the kernel launch_o picks by default,
+// with the record epilogue; returns the grid (= the number of block records)
+template <class O>
+static int launch_ens_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
+  using E = WithEns<O>;
+  if (a.n * 124 <= (256ull << 20)) {
+    const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
+    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g, kBlock, 0, st>>>(a);
+    else k_kf6p<4, 2, E><<<g, kBlock, 0, st>>>(a);
+    return (int)g;
+  }
+  const dim3 g = grid_for(a.n);
+  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g, kBlock, 0, st>>>(a);
+  else k_kf6t<4, E><<<g, kBlock, 0, st>>>(a);
+  return (int)g.x;
+}
+
+template <class O>
+static void launch_sel(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st, int *ens_nb) {
+  if constexpr (O::UPD && O::PRED) {
+    if (ens_nb) {
+      *ens_nb = launch_ens_o<O>(a, st);
+      return;
+    }
+  }
+  launch_o<O>(a, st);
+}
+
 template <bool LIBM, bool UPD, bool PRED, bool REC>
-static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st) {
+static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,
+                        int *nb) {
   if (small) {
-    if (valid) launch_o<Opt<LIBM, UPD, PRED, true, true, REC>>(a, st);
-    else launch_o<Opt<LIBM, UPD, PRED, true, false, REC>>(a, st);
+    if (valid) launch_sel<Opt<LIBM, UPD, PRED, true, true, REC>>(a, st, nb);
+    else launch_sel<Opt<LIBM, UPD, PRED, true, false, REC>>(a, st, nb);
   } else {
-    if (valid) launch_o<Opt<LIBM, UPD, PRED, false, true, REC>>(a, st);
-    else launch_o<Opt<LIBM, UPD, PRED, false, false, REC>>(a, st);
+    if (valid) launch_sel<Opt<LIBM, UPD, PRED, false, true, REC>>(a, st, nb);
+    else launch_sel<Opt<LIBM, UPD, PRED, false, false, REC>>(a, st, nb);
   }
 }
 template <bool LIBM, bool UPD, bool PRED>
-static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st) {
-  if (UPD && a.in.rec) launch_lupr<LIBM, UPD, PRED, UPD>(a, small, valid, st);
-  else launch_lupr<LIBM, UPD, PRED, false>(a, small, valid, st);
+static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,
+                       int *nb) {
+  if (UPD && a.in.rec) launch_lupr<LIBM, UPD, PRED, UPD>(a, small, valid, st, nb);
+  else launch_lupr<LIBM, UPD, PRED, false>(a, small, valid, st, nb);
 }
 
 int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool libm, bool upd,
-               bool pred, hipStream_t st) {
+               bool pred, hipStream_t st, int *ens_nb) {
   KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const bool small = s.pitch * 84 < 0xFFFFFFFFull;
   const bool valid = upd && in.valid != nullptr;
+  int *nb = in.ens_blocks && upd && pred && in.n_ticks == 1 ? ens_nb : nullptr;
+  if (in.ens_blocks && !nb) return (int)hipErrorInvalidValue;
   if (libm) {
-    if (upd && pred) launch_lup<true, true, true>(a, small, valid, st);
-    else if (upd) launch_lup<true, true, false>(a, small, valid, st);
-    else launch_lup<true, false, true>(a, small, false, st);
+    if (upd && pred) launch_lup<true, true, true>(a, small, valid, st, nb);
+    else if (upd) launch_lup<true, true, false>(a, small, valid, st, nullptr);
+    else launch_lup<true, false, true>(a, small, false, st, nullptr);
   } else {
-    if (upd && pred) launch_lup<false, true, true>(a, small, valid, st);
-    else if (upd) launch_lup<false, true, false>(a, small, valid, st);
-    else launch_lup<false, false, true>(a, small, false, st);
+    if (upd && pred) launch_lup<false, true, true>(a, small, valid, st, nb);
+    else if (upd) launch_lup<false, true, false>(a, small, valid, st, nullptr);
+    else launch_lup<false, false, true>(a, small, false, st, nullptr);
   }
   return (int)hipGetLastError();
 }

@@ -2,18 +2,18 @@
 //
 // Ensemble: mean and covariance of the state x across all instances of a rank, in fp64.
 // Each thread accumulates shifted moment sums of its grid-stride instances (no division in
-// the streaming loop), each block sums its threads through an LDS transpose in a fixed
-// order, and a one-block fold sums the per-block records in block order and converts them
-// to the Chan/Golub/LeVeque record {count, mean[n], M2 packed[n(n+1)/2]} that ranks
-// all-gather and combine in rank order.  No atomics: bitwise reproducible run to run.
-// (Single-launch "last block folds" variants measured slower: with plain stores, the
-// agent-scope release fence each block needs writes back the XCD's whole L2; with
-// write-through (sc1) record stores and sc1 loads in the folding block, 26.4 us against
-// 14.3 at 2^20: the one block's serialised record loads outlast the fold launch.)
+// the streaming loop), each block reduces its lanes with cross-lane swaps and DPP
+// (ens_device.hpp), and a fold of one block per record element sums the block records in a
+// fixed order and converts them to the Chan/Golub/LeVeque record {count, mean[n],
+// M2 packed[n(n+1)/2]} that ranks all-gather and combine in rank order.  No atomics:
+// bitwise reproducible run to run.  (Round 1 measured single-launch "last block folds"
+// variants slower: the agent-scope release fence each block needs writes back the XCD's
+// whole L2.)
 #include <type_traits>
 
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
+#include "ens_device.hpp"
 
 #pragma clang fp contract(off)
 
@@ -38,221 +38,148 @@ int launch_trig(const float *x, float *sv, float *cv, uint64_t n, bool libm, con
 }
 
 // ---------------------------------------------------------------------------
-// ensemble
+// ensemble (ens_device.hpp: record layout, lane accumulation, block reduction)
 // ---------------------------------------------------------------------------
+// robots per thread per pass (loads of all of them issued before any accumulation) and the
+// block cap: 2^20 KF6 robots -> 1024 blocks of 4 robots per lane, one pass
 template <int NX>
-struct EnsRec {
-  static constexpr int NP = NX * (NX + 1) / 2;
-  static constexpr int LEN = 1 + NX + NP;
-};
-
-constexpr int kEnsPerThread = 8;  // instances per thread at full grid (n = 2^20: 512 blocks)
-#ifndef FMSKF_ENS_CH
-#define FMSKF_ENS_CH 32
-#endif
-constexpr int kEnsCh = FMSKF_ENS_CH;   // record elements reduced per LDS pass
-constexpr int kEnsSeg = kBlock / kEnsCh;  // threads (column segments) per element
-#ifndef FMSKF_ENS_PAD
-#define FMSKF_ENS_PAD 8
-#endif
-// LDS transpose row pitch (doubles).  The segment reads red[e][j*kEnsSeg+seg] put 4 rows e in
-// one 32-lane ds_read_b64 group; unpadded rows (2 KiB) land them on the same banks (4-way),
-// 8 doubles of padding shift each row by 16 banks (conflict-free).  A/B at 2^20, record
-// partial + fold: KF6 12.78 -> 12.58 us, EKF9 29.29 -> 29.18, KF12D 38.37 -> 38.04.
-constexpr int kEnsRow = kBlock + FMSKF_ENS_PAD;
-
-// Sum v[LEN] over the 256 threads of the block into tot[LEN] (LDS, visible to all threads
-// after return).  Transpose through LDS in chunks of kEnsCh elements: thread t writes column
-// t; then kEnsSeg threads per element sum kEnsCh columns each (column j*kEnsSeg+seg, j
-// ascending), then one thread per element sums the kEnsSeg segment partials in order.
-// Chunks of 32 (64 KiB of LDS) against 16: EKF9 record 35.8 -> 30.4 us at 2^20, KF12D
-// 39.4 -> 38.5, KF6 13.9 -> 13.7 (fewer passes and barriers).  Fixed order -> deterministic;
-// no cross-lane shuffles (the LDS bandwidth of a shuffle butterfly is ~6x this).
-template <int LEN>
-__device__ __forceinline__ void block_sum(const double (&v)[LEN], double (*red)[kEnsRow],
-                                          double (*part)[kEnsSeg], double *tot) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int c = 0; c < LEN; c += kEnsCh) {
-#pragma unroll
-    for (int e = 0; e < kEnsCh; e++)
-      if (c + e < LEN) red[e][t] = v[c + e];
-    __syncthreads();
-    {
-      const int e = t / kEnsSeg, seg = t % kEnsSeg;
-      if (c + e < LEN) {
-        double s = red[e][seg];
-#pragma unroll
-        for (int j = 1; j < kEnsCh; j++) s = s + red[e][j * kEnsSeg + seg];
-        part[e][seg] = s;
-      }
-    }
-    __syncthreads();
-    if (t < kEnsCh && c + t < LEN) {
-      double s = part[t][0];
-#pragma unroll
-      for (int j = 1; j < kEnsSeg; j++) s = s + part[t][j];
-      tot[c + t] = s;
-    }
-    __syncthreads();
-  }
-}
-
-// Partial: every block accumulates shifted moment sums S1 = sum(x - x0),
-// S2 = sum((x - x0)(x - x0)^T) (x0 = instance 0's state, fp64, no division in the streaming
-// loop) of its grid-stride instances and writes its record.
-// TILED (the EKF9 / KF12D state layout) is a compile-time choice: st_at then divides by the
-// constant kTile (shifts), not by a runtime value (a 64-bit division per load)
-template <int NX, typename T, bool TILED>
-__global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
-                                                        uint64_t pp, double *blocks) {
-  constexpr uint32_t tile = TILED ? kTile : 0;
-  constexpr int LEN = EnsRec<NX>::LEN;
-  constexpr int U = 4;
-  __shared__ double red[kEnsCh][kEnsRow];
-  __shared__ double part[kEnsCh][kEnsSeg];
-  __shared__ double tot[LEN];
-  double sh[NX], v[LEN];
-#pragma unroll
-  for (int k = 0; k < NX; k++) sh[k] = (double)x[st_at(tile, pp, NX, k, 0)];
-#pragma unroll
-  for (int k = 0; k < LEN; k++) v[k] = 0.0;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += U * stride) {
-    T xv[U][NX];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t i = i0 + u * stride;
-#pragma unroll
-      for (int k = 0; k < NX; k++) xv[u][k] = i < n ? x[st_at(tile, pp, NX, k, i)] : (T)0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (i0 + u * stride >= n) break;
-      double d[NX];
-#pragma unroll
-      for (int k = 0; k < NX; k++) {
-        d[k] = (double)xv[u][k] - sh[k];
-        v[1 + k] = v[1 + k] + d[k];
-      }
-#pragma unroll
-      for (int p = 0; p < NX; p++)
-#pragma unroll
-        for (int q = 0; q <= p; q++) v[1 + NX + p * (p + 1) / 2 + q] += d[p] * d[q];
-      v[0] = v[0] + 1.0;
-    }
-  }
-  block_sum<LEN>(v, red, part, tot);
-  // element-major block records ([LEN][gridDim.x]): the fold's loads of one element across
-  // consecutive blocks are then one coalesced access
-  for (int k = threadIdx.x; k < LEN; k += kBlock) blocks[(uint64_t)k * gridDim.x + blockIdx.x] = tot[k];
-}
-
-// Fold (one block): sums the block records (stored element-major, [LEN][nblocks]) in a fixed
-// order, then the conversion to {count, mean = x0 + S1/c, M2 = S2 - S1 S1^T / c}.
-template <int NX, typename T>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const T *__restrict__ x, uint64_t pp, uint32_t tile,
-                                                     const double *__restrict__ blocks,
-                                                     int nblocks, double *out) {
-  constexpr int LEN = EnsRec<NX>::LEN;
-  static_assert(LEN <= kBlock, "one record element per thread in the conversion");
-  __shared__ double tot[LEN];
-  const int t = threadIdx.x;
-  // Records of up to 64 elements (KF6 28, EKF9 55): element-parallel, G threads per record
-  // element; thread g of element e sums blocks g, g + G, ... (8 rotating accumulators,
-  // combined in order), then the G partials of an element are summed in order: no LEN-wide
-  // register record, one barrier.  A/B at 2^20 (partial + fold, 512 blocks): KF6 13.8 ->
-  // 12.9 us, EKF9 30.5 -> 29.3.  KF12D's 91 elements would leave 2 threads per element
-  // (256 serial loads each): 38.6 -> 40.6 us, so it keeps the register-record fold.
-  if constexpr (LEN * 4 <= kBlock) {
-    constexpr int G = LEN * 8 <= kBlock ? 8 : 4;
-    constexpr int A = 8;
-    __shared__ double part[LEN][G];
-    {
-      const int e = t / G, g = t % G;
-      if (e < LEN) {
-        const double *row = blocks + (uint64_t)e * nblocks;
-        double a[A];
-#pragma unroll
-        for (int j = 0; j < A; j++) a[j] = 0.0;
-        int b = g;
-        for (; b + (4 * A - 1) * G < nblocks; b += 4 * A * G) {
-          double l[4 * A];
-#pragma unroll
-          for (int j = 0; j < 4 * A; j++) l[j] = row[b + j * G];
-#pragma unroll
-          for (int j = 0; j < 4 * A; j++) a[j % A] = a[j % A] + l[j];
-        }
-        for (int j = 0; b < nblocks; b += G, j++) a[j % A] = a[j % A] + row[b];
-        double s = a[0];
-#pragma unroll
-        for (int j = 1; j < A; j++) s = s + a[j];
-        part[e][g] = s;
-      }
-    }
-    __syncthreads();
-    if (t < LEN) {
-      double s = part[t][0];
-#pragma unroll
-      for (int j = 1; j < G; j++) s = s + part[t][j];
-      tot[t] = s;
-    }
-    __syncthreads();
-  } else {
-    __shared__ double red[kEnsCh][kEnsRow];
-    __shared__ double part[kEnsCh][kEnsSeg];
-    double v[LEN];
-#pragma unroll
-    for (int k = 0; k < LEN; k++) v[k] = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-#pragma unroll
-      for (int k = 0; k < LEN; k++) v[k] = v[k] + blocks[(uint64_t)k * nblocks + b];
-    }
-    block_sum<LEN>(v, red, part, tot);
-  }
-  const double c = tot[0];
-  if (t < LEN) {
-    const int k = t;
-    double r;
-    if (k == 0) {
-      r = c;
-    } else if (k <= NX) {
-      r = (double)x[st_at(tile, pp, NX, k - 1, 0)] + (c > 0.0 ? tot[k] / c : 0.0);
-    } else {
-      int p = 0, q = k - 1 - NX;
-      while (q > p) q -= ++p;
-      r = c > 0.0 ? tot[k] - tot[1 + p] * tot[1 + q] / c : 0.0;
-    }
-    out[k] = r;
-  }
-}
+constexpr int ens_r() { return NX >= 12 ? 2 : 4; }
+constexpr int kEnsMaxBlocks = 2048;
 
 int ensemble_nblocks(uint64_t n) {
-  uint64_t b = (n + (uint64_t)kBlock * kEnsPerThread - 1) / ((uint64_t)kBlock * kEnsPerThread);
-  if (b > 1024) b = 1024;
+  const uint64_t per = (uint64_t)kBlock * 4;
+  uint64_t b = (n + per - 1) / per;
+  if (b > (uint64_t)kEnsMaxBlocks) b = kEnsMaxBlocks;
   if (b < 1) b = 1;
   return (int)b;
 }
 
-template <int NX, typename T>
-static void ens_launch(const DevState &s, double *blocks, double *out, hipStream_t st) {
-  const int nb = ensemble_nblocks(s.n);
-  if (s.tile) k_ens_partial<NX, T, true><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
-  else k_ens_partial<NX, T, false><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, blocks);
-  k_ens_fold<NX, T><<<1, kBlock, 0, st>>>((const T *)s.x, s.pitch, s.tile, blocks, nb, out);
+// Partial: every block accumulates the shifted moment sums of its grid-stride robots and
+// writes its block record.  TILED (the EKF9 / KF12D state layout) is a compile-time choice:
+// st_at then divides by the constant kTile (shifts), not by a runtime value.
+template <int NX, typename T, bool TILED>
+__global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
+                                                        uint64_t pp, const double *__restrict__ shift,
+                                                        double *blocks) {
+  constexpr uint32_t tile = TILED ? kTile : 0;
+  constexpr int LEN4 = EnsRec<NX>::LEN4;
+  constexpr int R = ens_r<NX>();
+  double sh[NX], v[LEN4];
+  ens_load_shift<NX>(shift, sh);
+#pragma unroll
+  for (int k = 0; k < LEN4; k++) v[k] = 0.0;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += R * stride) {
+    T xv[R][NX];
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+      const uint64_t i = i0 + u * stride, ic = i < n ? i : n - 1;
+#pragma unroll
+      for (int k = 0; k < NX; k++) xv[u][k] = x[st_at(tile, pp, NX, k, ic)];
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++)
+      if (i0 + u * stride < n) ens_add<NX>(v, xv[u], sh);
+  }
+  ens_block_write<NX>(v, blocks);
 }
 
-int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, double *out,
-                    hipStream_t st) {
-  if (nx == 6 && !f64) {
-    ens_launch<6, float>(s, blocks, out, st);
-  } else if (nx == 9 && !f64) {
-    ens_launch<9, float>(s, blocks, out, st);
-  } else if (nx == 12 && f64) {
-    ens_launch<12, double>(s, blocks, out, st);
-  } else {
-    return (int)hipErrorInvalidValue;
+// Fold: one block per record element k.  Block k sums, over the nb block records in a fixed
+// order (thread t: blocks t, t + 256, ... ascending; then block_reduce), the count row, the
+// two S1 rows its element needs and its own row, then converts: count; mean = s + S1 / c;
+// M2 = S2 - S1 S1^T / c.  A row summed by several blocks gets bitwise the same total in each
+// (same per-thread order, same reduction tree), so the record is consistent.  LEN blocks in
+// parallel, each one load round trip at 2^20: the round-1 one-block fold was 4.2-10 us.
+template <int NX>
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const double *__restrict__ blocks, int nb,
+                                                     const double *__restrict__ shift, double *out) {
+  const int k = blockIdx.x;
+  int ra = k, rb = k;
+  if (k > NX) {
+    int p = 0, q = k - 1 - NX;
+    while (q > p) q -= ++p;
+    ra = 1 + p;
+    rb = 1 + q;
   }
+  const double *r0 = blocks, *r1 = blocks + (uint64_t)ra * nb, *r2 = blocks + (uint64_t)rb * nb,
+               *r3 = blocks + (uint64_t)k * nb;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  constexpr int U = 8;
+  int b = threadIdx.x;
+  for (; b + (U - 1) * kBlock < nb; b += U * kBlock) {
+    double l[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      l[u][0] = r0[b + u * kBlock];
+      l[u][1] = r1[b + u * kBlock];
+      l[u][2] = r2[b + u * kBlock];
+      l[u][3] = r3[b + u * kBlock];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[j] = v[j] + l[u][j];
+  }
+  for (; b < nb; b += kBlock) {
+    v[0] = v[0] + r0[b];
+    v[1] = v[1] + r1[b];
+    v[2] = v[2] + r2[b];
+    v[3] = v[3] + r3[b];
+  }
+  __shared__ double red[16];
+  __shared__ double tot[4];
+  const double s = block_reduce<4>(v, red);
+  if (threadIdx.x < 4) tot[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double c = tot[0];
+    double r;
+    if (k == 0) r = c;
+    else if (k <= NX) r = shift[k - 1] + (c > 0.0 ? tot[3] / c : 0.0);
+    else r = c > 0.0 ? tot[3] - tot[1] * tot[2] / c : 0.0;
+    out[k] = r;
+  }
+}
+
+// the shift vector: robot 0's state
+template <int NX, typename T>
+__global__ void k_ens_shift(const T *x, uint64_t pp, uint32_t tile, double *shift) {
+  const int k = threadIdx.x;
+  if (k < NX) shift[k] = (double)x[st_at(tile, pp, NX, k, 0)];
+}
+
+template <int NX, typename T>
+static void ens_launch(const DevState &s, double *blocks, const double *shift, double *out,
+                       hipStream_t st) {
+  const int nb = ensemble_nblocks(s.n);
+  if (s.tile) k_ens_partial<NX, T, true><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
+  else k_ens_partial<NX, T, false><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
+  k_ens_fold<NX><<<EnsRec<NX>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+}
+
+int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
+                    double *out, hipStream_t st) {
+  if (nx == 6 && !f64) ens_launch<6, float>(s, blocks, shift, out, st);
+  else if (nx == 9 && !f64) ens_launch<9, float>(s, blocks, shift, out, st);
+  else if (nx == 12 && f64) ens_launch<12, double>(s, blocks, shift, out, st);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+int launch_ens_fold(int nx, const double *blocks, int nb, const double *shift, double *out,
+                    hipStream_t st) {
+  if (nx == 6) k_ens_fold<6><<<EnsRec<6>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+  else if (nx == 9) k_ens_fold<9><<<EnsRec<9>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+  else if (nx == 12) k_ens_fold<12><<<EnsRec<12>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+int launch_ens_shift(const DevState &s, int nx, bool f64, double *shift, hipStream_t st) {
+  if (nx == 6 && !f64) k_ens_shift<6, float><<<1, 64, 0, st>>>((const float *)s.x, s.pitch, s.tile, shift);
+  else if (nx == 9 && !f64) k_ens_shift<9, float><<<1, 64, 0, st>>>((const float *)s.x, s.pitch, s.tile, shift);
+  else if (nx == 12 && f64) k_ens_shift<12, double><<<1, 64, 0, st>>>((const double *)s.x, s.pitch, s.tile, shift);
+  else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -526,7 +526,10 @@ def test_full_pipeline_rs_device_resident(orc):
 
 
 # ----------------------------------------------------------------------------- ensemble
-@pytest.mark.parametrize("model,n", [("kf6", 100003), ("ekf9", 5000), ("kf12d", 3000)])
+# 2^20 (KF6 / EKF9: one pass of 4 robots per lane over 1024 blocks) and 3 * 2^20 + 5 (past the
+# 2048-block cap: grid-stride passes, a ragged last pass)
+@pytest.mark.parametrize("model,n", [("kf6", 100003), ("ekf9", 5000), ("kf12d", 3000), ("kf6", 1 << 20),
+                                     ("ekf9", 1 << 20), ("kf6", 3 * (1 << 20) + 5), ("kf12d", 300001)])
 def test_ensemble_partial(orc, model, n):
     rng = np.random.default_rng(5)
     with Engine(model, n) as e:
@@ -572,7 +575,11 @@ def test_bad_inputs_rejected():
 
 
 # ----------------------------------------------------------------------------- fused ensemble
-@pytest.mark.parametrize("model,n", [("kf6", 100003), ("kf6", 1), ("kf6", 70000), ("ekf9", 3000)])
+# KF6 at 2^20 runs the two-robots-per-lane tick (k_kf6p) with the record epilogue; at
+# 3 * 2^20 + 5 the state outgrows the Infinity Cache and the one-robot-per-lane tick (k_kf6t)
+# carries it, 6145 block records
+@pytest.mark.parametrize("model,n", [("kf6", 100003), ("kf6", 1), ("kf6", 70000), ("ekf9", 3000),
+                                     ("kf6", 1 << 20), ("kf6", 3 * (1 << 20) + 5)])
 def test_tick_ensemble_fused(orc, model, n):
     """fmskf_tick_ensemble = fmskf_tick + the record of the post-tick state: state bit-exact
     vs a plain tick, record vs the oracle's two-pass moments of that state, and bitwise
