@@ -167,6 +167,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the cfg 3 / cfg 5 / 2^24 single-GPU kernel lines")
     ap.add_argument("--secondary-ticks", type=int, default=20)
+    ap.add_argument("--check-ensemble", action="store_true",
+                    help="after the timed region: the gathered record vs each rank's stand-alone "
+                         "record of the same state (reported as ensemble_check)")
     ap.add_argument("--inputs", choices=["records", "planes"], default="records",
                     help="16-byte fmskf_kf6_record per robot (one load per lane) or yaw/gyro/rpm planes")
     args = ap.parse_args()
@@ -214,7 +217,7 @@ def main():
     tick_fn = fmskf.load().fmskf_tick
     rec_len = eng.ensemble_record_len()
     rec = torch.empty(rec_len, dtype=torch.float64, device=dev)
-    n_events = max(1, (2 * args.steps + args.warmup) // max(1, args.ensemble_every) + 2)
+    n_events = max(1, (2 * args.steps + args.warmup) // max(1, args.ensemble_every) + 3)
     # one record and one gather slot per ensemble event: the all-gather runs asynchronously
     # on RCCL's stream (ordered after the record by RCCL's stream dependency) while the next
     # ticks proceed; pending gathers are joined before the timed region closes
@@ -368,6 +371,32 @@ def main():
                "var_vx": float(cov[9])}
     counters = eng.get_counters()
 
+    # --check-ensemble: one more ensemble event through the measured path (fused record or
+    # separate partial, then the gather), against each rank's stand-alone record of the same
+    # state folded the same way: max relative difference of mean and covariance
+    ens_check = None
+    if args.check_ensemble and args.ensemble_every > 0:
+        k = args.warmup + 2 * args.steps
+        e = ev_count[0] % n_events
+        ens_event(k)
+        join()
+        torch.cuda.synchronize()
+        own = torch.from_numpy(eng.ensemble_partial()).to(dev)
+        allown = torch.zeros(world, rec_len, dtype=torch.float64, device=dev)
+        if distributed:
+            dist.all_gather_into_tensor(allown.view(-1), own)
+        else:
+            allown[0].copy_(own)
+        mr, cr = fmskf.ensemble_combine(6, allown.cpu().numpy())
+        if args.gather == "native":
+            mg, cg = native_stats[0]
+        else:
+            mg, cg = fmskf.ensemble_combine(6, gathered[e].cpu().numpy())
+        import numpy as np
+        rel = lambda a, b: float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)))  # noqa: E731
+        ens_check = {"mean_max_rel": rel(mg, mr), "cov_max_rel": rel(cg, cr),
+                     "count": float(allown[:, 0].sum().item())}
+
     # secondary figure: the same ring replayed by one fused multi-tick launch per ring pass
     fused = None
     if not args.no_fused:
@@ -448,6 +477,8 @@ def main():
         "ensemble": ens,
         "nonfinite_instances": int(counters[0]),
     }
+    if ens_check is not None:
+        out["ensemble_check"] = ens_check
     eng.close()
     del prepared, planes, krec, many_in
     if not args.no_secondary and world == 1:  # single-GPU configs: one line at N=1

@@ -1,0 +1,86 @@
+"""Config 4 (BASELINE.json configs[3]: 2^24 KF6 robots over 8 GPUs, ensemble mean / covariance
+all-gathered over RCCL) on the one-GPU test box.
+
+* the per-GPU shard (2^21 robots, 16-byte tick records) ticked and recorded by the fused
+  tick + ensemble kernel, sampled bit-exact against the oracle, the record against the oracle's
+  two-pass moments of the same state;
+* bench.py's distributed code path under torch.distributed.run at world size 1, for each
+  gather mode (torch all-gather on RCCL's stream, in the tick stream, and the handle-owned
+  communicator fmskf_comm_init / fmskf_ensemble_stats that C callers bind): the gathered
+  record must fold to the statistics of the rank's stand-alone record.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_cfg4_shard_2p21_records_and_record(orc):
+    import torch
+    n, T = 1 << 21, 4
+    tr = Trajectory(n, T, seed=404)
+    yaw, gz, rpm = tr.kf6_inputs()
+    dy, dg, dr = (torch.from_numpy(a).cuda() for a in (yaw, gz, rpm))
+    recs = fmskf.kf6_records(dy, dg, dr)
+    with Engine("kf6", n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        for t in range(T - 1):
+            e.tick(kf6_rec=recs[t])
+        rec = e.tick_ensemble(kf6_rec=recs[T - 1])
+        x, P = e.get_state()
+        assert e.get_counters()[0] == 0
+    idx = np.sort(np.random.default_rng(4).choice(n, 2048, replace=False))
+    cfg = fmskf.default_config("kf6", idx.size)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
+    xo = np.zeros((6, idx.size), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], idx.size, 1).copy()
+    for t in range(T):
+        orc.kf6_tick(xo, Po, np.ascontiguousarray(yaw[t, idx]), np.ascontiguousarray(gz[t, idx]),
+                     np.ascontiguousarray(rpm[t, idx]), None, prm)
+    assert np.array_equal(x[:, idx].view(np.uint32), xo.view(np.uint32))
+    assert np.array_equal(P[:, idx].view(np.uint32), Po.view(np.uint32))
+    assert rec[0] == n
+    mo, co = orc.ens_finalize(6, orc.ens_partial(x))
+    mf, cf = fmskf.ensemble_combine(6, rec[None, :])
+    np.testing.assert_allclose(mf, mo, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(cf, co, rtol=1e-9, atol=1e-15)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("gather", ["async", "stream", "native"])
+@pytest.mark.parametrize("ensemble", ["fused", "separate"])
+def test_bench_distributed_path_world1(gather, ensemble):
+    if gather == "native" and ensemble == "separate":
+        pytest.skip("the native path records with fmskf_ensemble_stats itself")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+           "--steps", "40", "--warmup", "5", "--ensemble-every", "8", "--no-cpu-baseline", "--no-fused",
+           "--no-secondary", "--gather", gather, "--ensemble", ensemble, "--check-ensemble"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 1
+    chk = out["ensemble_check"]
+    assert chk["count"] == 1 << 20
+    assert chk["mean_max_rel"] < 1e-12, chk
+    assert chk["cov_max_rel"] < 1e-9, chk
+    assert out["nonfinite_instances"] == 0
+    assert out["value"] > 1e9
