@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
-template <bool LIBM, bool UPD, bool PRED, int CP = 0>
+template <bool LIBM, bool UPD, bool PRED, int CP = 0, bool PRIO = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -148,6 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
+  if (PRIO) __builtin_amdgcn_s_setprio(3);
   WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
   const TileRows<float, N, CP> tx(a.x, tile_slot(n));
   const TileRows<float, NP, CP> tp(a.P, tile_slot(n));
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
   const uint4 raw = UPD ? reinterpret_cast<const uint4 *>(a.in.raw)[ic] : make_uint4(0, 0, 0, 0);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED>(a, raw, have, stab, x, P);
   if (live) {
@@ -180,6 +182,65 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
     }
   }
   nan_guard(x, P, a.counters, live);
+}
+
+// Two robots per lane (tiles b and b + gridDim.x of the tiled state): robot B's 54 state
+// loads and its raw record are issued before robot A's update, so they stream in while A
+// computes (FMSKF_EKF9_VARIANT experiments; see launch_ekf9).  PRIO: the waves issue their
+// loads at raised priority (s_setprio 3) and compute at the base priority.
+template <bool LIBM, int CP, bool PRIO>
+__global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
+  constexpr int N = 9, NP = 45;
+  __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
+  float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
+  const uint64_t n = a.n;
+  const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
+  const uint32_t ta = blockIdx.x, tb0 = blockIdx.x + gridDim.x;
+  const bool has_b = tb0 < ntiles;  // block-uniform
+  const uint32_t tb = has_b ? tb0 : ta;
+  const uint32_t t = threadIdx.x;
+  auto slot = [&](uint32_t tile) -> uint32_t {
+    const uint64_t b0 = (uint64_t)tile * kTile;
+    return b0 + t < n ? t : (uint32_t)(n - 1 - b0);
+  };
+  const uint64_t ia = (uint64_t)ta * kTile + t, ib = (uint64_t)tb * kTile + t;
+  const bool live_a = ia < n, live_b = has_b && ib < n;
+  const uint64_t iac = live_a ? ia : n - 1, ibc = ib < n ? ib : n - 1;
+  if (PRIO) __builtin_amdgcn_s_setprio(3);
+  WaveTable<LIBM> tv(a.in.sintab);
+  const TileRows<float, N, CP> txa(a.x, ta, slot(ta), 0), txb(a.x, tb, slot(tb), 0);
+  const TileRows<float, NP, CP> tpa(a.P, ta, slot(ta), 0), tpb(a.P, tb, slot(tb), 0);
+  float xa[N], Pa[NP], xb[N], Pb[NP];
+#pragma unroll
+  for (int k = 0; k < N; k++) xa[k] = txa.ld(k);
+#pragma unroll
+  for (int k = 0; k < NP; k++) Pa[k] = tpa.ld(k);
+  const uint4 ra = reinterpret_cast<const uint4 *>(a.in.raw)[iac];
+  const uint4 rb = reinterpret_cast<const uint4 *>(a.in.raw)[ibc];
+  const bool ha = a.in.valid == nullptr || a.in.valid[iac];
+  const bool hb = a.in.valid == nullptr || a.in.valid[ibc];
+#pragma unroll
+  for (int k = 0; k < N; k++) xb[k] = txb.ld(k);
+#pragma unroll
+  for (int k = 0; k < NP; k++) Pb[k] = tpb.ld(k);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
+  tv.store(stab);
+  ekf9_tick1<LIBM, true, true>(a, ra, ha, stab, xa, Pa);
+  if (live_a) {
+#pragma unroll
+    for (int k = 0; k < N; k++) txa.st(k, xa[k]);
+#pragma unroll
+    for (int k = 0; k < NP; k++) tpa.st(k, Pa[k]);
+  }
+  nan_guard(xa, Pa, a.counters, live_a);
+  ekf9_tick1<LIBM, true, true>(a, rb, hb, stab, xb, Pb);
+  if (live_b) {
+#pragma unroll
+    for (int k = 0; k < N; k++) txb.st(k, xb[k]);
+#pragma unroll
+    for (int k = 0; k < NP; k++) tpb.st(k, Pb[k]);
+  }
+  nan_guard(xb, Pb, a.counters, live_b);
 }
 
 // SEQ: R has no base/tip cross terms -> group-sequential update (base group, then tip group
@@ -316,7 +377,7 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 // Planes through buffer descriptors: a 32-bit lane offset per access and no 64-bit address
 // math.  SMALL: the 78 P planes fit one 4 GiB window (pitch < 6.8M), one descriptor per array
 // and a scalar plane offset; otherwise one descriptor per plane (n < 2^29 lanes of 8 bytes).
-template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0>
+template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool PRIO = false>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
   const uint64_t n = a.n, pp = a.pitch;
@@ -346,10 +407,12 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   // returned above, so a lane's slot is its thread index)
   const TileRows<double, N, CP> tx(a.x, threadIdx.x);
   const TileRows<double, NP, CP> tp(a.P, threadIdx.x);
+  if (PRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = FMSKF_TILED ? tp.ld(k) : ld(rp, a.P, k);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
   const double dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     if (UPD) {
@@ -391,6 +454,31 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
+  // Single-tick kernel choice (FMSKF_EKF9_VARIANT, read once, forces one): 0 (default) two
+  // robots per lane (k_ekf9p) while the 216-byte state fits the 256 MiB Infinity Cache, else
+  // one per lane (k_ekf9t); 1 k_ekf9t with a raised-priority load phase; 2 k_ekf9p; 3 k_ekf9p
+  // with the raised-priority load phase; 4 k_ekf9t.  Measured (kbench, one box, two passes):
+  // 2^20: k_ekf9t 74.8-74.9 us, 1: 71.2-71.3, 2: 71.2-71.9, 3: 73.7-73.9;
+  // 2^22 (HBM): k_ekf9t 336-338, 1: 342, 2: 339, 3: 342-343.
+  static const int var = [] {
+    const char *e = getenv("FMSKF_EKF9_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  const int v = var == 0 ? (s.n * 216 <= (256ull << 20) ? 2 : 4) : var;
+  if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v >= 1 && v <= 3) {
+    if (var == 1) {
+      if (nt) k_ekf9t<false, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<false, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+    } else {
+      const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
+      const dim3 g2((ntiles + 1) / 2);
+      if (var == 2 && nt) k_ekf9p<false, kStateNT, false><<<g2, kBlock, 0, st>>>(a);
+      else if (var == 2) k_ekf9p<false, 0, false><<<g2, kBlock, 0, st>>>(a);
+      else if (nt) k_ekf9p<false, kStateNT, true><<<g2, kBlock, 0, st>>>(a);
+      else k_ekf9p<false, 0, true><<<g2, kBlock, 0, st>>>(a);
+    }
+    return (int)hipGetLastError();
+  }
   if (in.n_ticks == 1) {
     if (libm) {
       if (upd && pred && nt) k_ekf9t<true, true, true, kStateNT><<<g, kBlock, 0, st>>>(a);
@@ -423,6 +511,17 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
   const bool nt = FMSKF_TILED && state_nt(s.n * 90 * 8);
   if (p.decor) {
     const bool blk = kf12d_sequential(p.r);
+    static const int var = [] {  // FMSKF_KF12D_VARIANT=1: raised-priority load phase
+      const char *e = getenv("FMSKF_KF12D_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+    if (var == 1 && FMSKF_TILED && upd && pred && in.n_ticks == 1) {
+      if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+      else if (blk) k_kf12s<true, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+      else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+      else k_kf12s<false, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+      return (int)hipGetLastError();
+    }
 #define KF12S(B, S)                                                          \
   if (upd && pred && nt) k_kf12s<B, true, true, S, kStateNT><<<g, kBlock, 0, st>>>(a); \
   else if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, 0, st>>>(a); \

@@ -84,6 +84,10 @@ struct TileRows {
   __device__ __forceinline__ TileRows(T *base, uint32_t t)
       : r(rsrc(base + (uint64_t)blockIdx.x * (ROWS * kTile), (uint64_t)ROWS * kTile * sizeof(T))),
         vo(t * (uint32_t)sizeof(T)) {}
+  // tile `tile` (wave-uniform) instead of the block's own
+  __device__ __forceinline__ TileRows(T *base, uint32_t tile, uint32_t t, int)
+      : r(rsrc(base + (uint64_t)tile * (ROWS * kTile), (uint64_t)ROWS * kTile * sizeof(T))),
+        vo(t * (uint32_t)sizeof(T)) {}
   __device__ __forceinline__ T ld(int k) const {
     if constexpr (sizeof(T) == 8)
       return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, vo, k * kTile * 8, CP));

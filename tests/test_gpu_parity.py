@@ -748,7 +748,7 @@ import fmskf
 from fmskf import Engine
 from fmskf.synth import Trajectory
 from oracle import oracle as orc
-for n in (1, 1000):
+for n in (1, 700, 1000):
     T = 5
     tr = Trajectory(n, T, seed=60 + n)
     valid = (np.random.default_rng(n).random((T, n)) > 0.2).astype(np.uint8)
@@ -802,6 +802,25 @@ def test_nontemporal_state_kernels_bitexact():
                              capture_output=True, text=True, timeout=240, env=env)
         assert out.returncode == 0, out.stderr[-3000:]
         assert ok in out.stdout
+
+
+@pytest.mark.parametrize("ekf9,kf12d", [("1", "1"), ("3", "0"), ("4", "0"), ("2", "0")])
+def test_ekf9_kf12d_kernel_variants_bitexact(ekf9, kf12d):
+    """Every EKF9 single-tick kernel (FMSKF_EKF9_VARIANT: 1 raised-priority load phase, 2 two
+    robots per lane -- the default while the state fits the Infinity Cache --, 3 both, 4 one
+    robot per lane) and the raised-priority KF12D kernel, forced in a child process, with a
+    validity mask at N = 1, 700 (an odd tile count: the last two-robot block has no second
+    tile) and 1000, bit-exact against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMSKF_EKF9_VARIANT=ekf9, FMSKF_KF12D_VARIANT=kf12d)
+    out = subprocess.run([sys.executable, "-c", _NT_SCRIPT, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "nt ok" in out.stdout
 
 
 def test_rs_one_robot_per_lane_bitexact():
