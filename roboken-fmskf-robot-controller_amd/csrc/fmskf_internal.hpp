@@ -174,6 +174,18 @@ inline bool state_nt(uint64_t state_bytes) {
   return state_bytes > (256ull << 20);
 }
 
+// Occupancy cap for the kernels that stream their state from HBM: dynamic LDS per block limits
+// the resident blocks per CU (160 KiB / bytes), so fewer tile / plane streams compete for the
+// HBM channels.  The environment variable (read once per call site) overrides the byte count.
+#define FMSKF_LDS_CAP(NAME, HBM, DFLT)                              \
+  ([&]() -> unsigned {                                              \
+    static const int v_ = [] {                                      \
+      const char *e_ = getenv(NAME);                                \
+      return e_ ? atoi(e_) : -1;                                    \
+    }();                                                            \
+    return v_ >= 0 ? (unsigned)v_ : ((HBM) ? (unsigned)(DFLT) : 0u); \
+  }())
+
 #ifndef FMSKF_TILED
 #define FMSKF_TILED 1
 #endif

@@ -35,6 +35,21 @@ __device__ __forceinline__ void ekf9_innov(const uint4 w, const float (&x)[9], f
   y[5] = z5 - x[4];
 }
 
+// one robot's 16-byte raw record of a single tick, read once; NT: non-temporal (gfx950 `nt`).
+// Measured (kbench, one box, two passes): 2^20 (two robots per lane) 74.1-74.2 -> 73.0-73.4 us
+// with nt; 2^22 (one per lane, HBM) 334.6-335.6 plain vs 337.5-338.3 nt: k_ekf9p uses nt,
+// k_ekf9t plain loads
+template <bool NT>
+__device__ __forceinline__ uint4 ekf9_raw_at(const int16_t *raw, uint64_t i) {
+  if constexpr (NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(raw) + i);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+    return reinterpret_cast<const uint4 *>(raw)[i];
+  }
+}
+
 // one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
 template <bool LIBM, bool UPD, bool PRED>
 __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, const uint4 raw,
@@ -164,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
     for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
   }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
-  const uint4 raw = UPD ? reinterpret_cast<const uint4 *>(a.in.raw)[ic] : make_uint4(0, 0, 0, 0);
+  const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
   if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED>(a, raw, have, stab, x, P);
@@ -215,8 +230,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   for (int k = 0; k < N; k++) xa[k] = txa.ld(k);
 #pragma unroll
   for (int k = 0; k < NP; k++) Pa[k] = tpa.ld(k);
-  const uint4 ra = reinterpret_cast<const uint4 *>(a.in.raw)[iac];
-  const uint4 rb = reinterpret_cast<const uint4 *>(a.in.raw)[ibc];
+  const uint4 ra = ekf9_raw_at<true>(a.in.raw, iac);
+  const uint4 rb = ekf9_raw_at<true>(a.in.raw, ibc);
   const bool ha = a.in.valid == nullptr || a.in.valid[iac];
   const bool hb = a.in.valid == nullptr || a.in.valid[ibc];
 #pragma unroll
@@ -466,16 +481,18 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
   }();
   const int v = var == 0 ? (s.n * 216 <= (256ull << 20) ? 2 : 4) : var;
   if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v >= 1 && v <= 3) {
-    if (var == 1) {
+    if (v == 1) {
       if (nt) k_ekf9t<false, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<false, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
     } else {
       const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
       const dim3 g2((ntiles + 1) / 2);
-      if (var == 2 && nt) k_ekf9p<false, kStateNT, false><<<g2, kBlock, 0, st>>>(a);
-      else if (var == 2) k_ekf9p<false, 0, false><<<g2, kBlock, 0, st>>>(a);
-      else if (nt) k_ekf9p<false, kStateNT, true><<<g2, kBlock, 0, st>>>(a);
-      else k_ekf9p<false, 0, true><<<g2, kBlock, 0, st>>>(a);
+      // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
+      const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
+      if (v == 2 && nt) k_ekf9p<false, kStateNT, false><<<g2, kBlock, lds, st>>>(a);
+      else if (v == 2) k_ekf9p<false, 0, false><<<g2, kBlock, lds, st>>>(a);
+      else if (nt) k_ekf9p<false, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
+      else k_ekf9p<false, 0, true><<<g2, kBlock, lds, st>>>(a);
     }
     return (int)hipGetLastError();
   }
@@ -486,8 +503,14 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
       else if (upd) k_ekf9t<true, true, false><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<true, false, true><<<g, kBlock, 0, st>>>(a);
     } else {
-      if (upd && pred && nt) k_ekf9t<false, true, true, kStateNT><<<g, kBlock, 0, st>>>(a);
-      else if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, 0, st>>>(a);
+      // Past the Infinity Cache (non-temporal state) the occupancy is capped at 2 blocks per CU
+      // with 64 KiB of dynamic LDS: fewer concurrent tile streams per HBM channel.  2^22:
+      // 334.3-338.7 us uncapped, 332 at 32 KiB, 329.7-331.0 at 48 KiB, 326.8-330.9 at 64 KiB,
+      // 382-383 at 80 KiB (kbench, two boxes, two passes each); the same-bytes tiled pattern
+      // (membench) 299 us.  FMSKF_EKF9_LDS overrides the byte count.
+      const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
+      if (upd && pred && nt) k_ekf9t<false, true, true, kStateNT><<<g, kBlock, lds, st>>>(a);
+      else if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, lds, st>>>(a);
       else if (upd) k_ekf9t<false, true, false><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<false, false, true><<<g, kBlock, 0, st>>>(a);
     }
@@ -522,9 +545,10 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
       else k_kf12s<false, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
       return (int)hipGetLastError();
     }
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF12D_LDS", nt, 0u);
 #define KF12S(B, S)                                                          \
-  if (upd && pred && nt) k_kf12s<B, true, true, S, kStateNT><<<g, kBlock, 0, st>>>(a); \
-  else if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, 0, st>>>(a); \
+  if (upd && pred && nt) k_kf12s<B, true, true, S, kStateNT><<<g, kBlock, lds, st>>>(a); \
+  else if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, lds, st>>>(a); \
   else if (upd) k_kf12s<B, true, false, S><<<g, kBlock, 0, st>>>(a);        \
   else k_kf12s<B, false, true, S><<<g, kBlock, 0, st>>>(a);
     if (blk && small) { KF12S(true, true) }

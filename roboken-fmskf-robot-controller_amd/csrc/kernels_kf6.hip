@@ -396,18 +396,21 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     // both robots' inputs loaded up front, one wave round (2^20: 39.7 -> 37.4-38.1 us,
     // 2^21: 75.9 -> 71.5; at 2^24, HBM-bound, it is 3% slower than one robot per lane)
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
+    // 32 KiB of dynamic LDS: at most 5 blocks per CU.  kbench, records, two passes: 2^20
+    // 38.2-38.5 -> 37.2-37.3 us (24 KiB 37.6-37.7, 40 KiB 37.4-37.5); 2^21 71.6-71.8 -> 70.5-70.9
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
     if constexpr (O::UPD && O::PRED) {
       if (state_nt(a.n * 108)) {  // only when forced: this branch's state fits the cache
-        k_kf6p<4, 2, WithNT<O>><<<g, kBlock, 0, st>>>(a);
+        k_kf6p<4, 2, WithNT<O>><<<g, kBlock, lds, st>>>(a);
         return;
       }
     }
-    k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
+    k_kf6p<4, 2, O><<<g, kBlock, lds, st>>>(a);
   } else if (a.in.n_ticks == 1 && (v == 0 || v == 15)) {
-    static const unsigned lds = [] {  // occupancy experiment: dynamic LDS per block
-      const char *e = getenv("FMSKF_KF6_LDS");
-      return e ? (unsigned)atoi(e) : 0u;
-    }();
+    // past the Infinity Cache: at most 3 blocks per CU (48 KiB of dynamic LDS).  2^24, records,
+    // kbench, one box, two passes: 691-704 us uncapped, 671-684 at 32 KiB, 627-641 at 48 KiB,
+    // 626-639 at 64 KiB, 809-826 at 80 KiB (two blocks of 4 waves per CU are too few)
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6_LDS", state_nt(a.n * 108), 48u * 1024u);
     if constexpr (O::UPD && O::PRED) {
       if (state_nt(a.n * 108)) {
         k_kf6t<4, WithNT<O>><<<grid_for(a.n), kBlock, lds, st>>>(a);
@@ -427,13 +430,15 @@ static int launch_ens_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   using E = WithEns<O>;
   if (a.n * 124 <= (256ull << 20)) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
-    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g, kBlock, 0, st>>>(a);
-    else k_kf6p<4, 2, E><<<g, kBlock, 0, st>>>(a);
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
+    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g, kBlock, lds, st>>>(a);
+    else k_kf6p<4, 2, E><<<g, kBlock, lds, st>>>(a);
     return (int)g;
   }
   const dim3 g = grid_for(a.n);
-  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g, kBlock, 0, st>>>(a);
-  else k_kf6t<4, E><<<g, kBlock, 0, st>>>(a);
+  const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6_LDS", state_nt(a.n * 108), 48u * 1024u);
+  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g, kBlock, lds, st>>>(a);
+  else k_kf6t<4, E><<<g, kBlock, lds, st>>>(a);
   return (int)g.x;
 }
 

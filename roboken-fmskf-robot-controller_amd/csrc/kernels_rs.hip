@@ -117,8 +117,11 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
   }();
   if (two && correct && predict && in.n_ticks == 1) {
     const dim3 g2((unsigned)((s.n + 2 * kBlock - 1) / (2 * kBlock)));
-    if (libm) k_rs2<true><<<g2, kBlock, 0, st>>>(a);
-    else k_rs2<false><<<g2, kBlock, 0, st>>>(a);
+    // past the Infinity Cache: 2 blocks per CU (64 KiB of dynamic LDS).  2^24, kbench, two
+    // passes: 436.7-448.2 us uncapped, 429-430 at 48 KiB, 418.5-424.5 at 64 KiB
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_RS_LDS", state_nt(s.n * 124), 64u * 1024u);
+    if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
+    else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
     return (int)hipGetLastError();
   }
   if (libm) {
