@@ -167,6 +167,11 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the cfg 3 / cfg 5 / 2^24 single-GPU kernel lines")
     ap.add_argument("--secondary-ticks", type=int, default=20)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend (gloo: test rehearsal of the N > 1 path, the "
+                         "records staged through host memory)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsing N > 1 on a one-GPU box; not a scaling run)")
     ap.add_argument("--check-ensemble", action="store_true",
                     help="after the timed region: the gathered record vs each rank's stand-alone "
                          "record of the same state (reported as ensemble_check)")
@@ -186,17 +191,40 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # a torch.distributed.run launch (RANK set) always builds the RCCL group, also at N=1,
     # so the collective path is the one measured whenever the launcher is used
     distributed = world > 1 or "RANK" in os.environ
+    gloo = args.backend == "gloo"
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if distributed:
-            dist.barrier(device_ids=[local])
+            if gloo:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
+
+    def all_gather(out, inp, async_op=False):
+        """all-gather of device tensors (gloo: staged through host memory, synchronous)"""
+        if not gloo:
+            return dist.all_gather_into_tensor(out, inp, async_op=async_op)
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
+        return None
+
+    def max_over_ranks(vals):
+        t = torch.tensor(vals, dtype=torch.float64, device="cpu" if gloo else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.tolist()]
 
     n = args.n_per_gpu
     R = args.ring
@@ -248,11 +276,10 @@ def main():
             else:
                 eng.tick_prepared(prepared[k % R], tick_fn)
                 eng.ensemble_partial(recs[e])
-            if distributed and args.gather == "stream":
-                dist.all_gather_into_tensor(gathered[e].view(-1), recs[e])
+            if distributed and (args.gather == "stream" or gloo):
+                all_gather(gathered[e].view(-1), recs[e])
             elif distributed:
-                pending.append(dist.all_gather_into_tensor(gathered[e].view(-1), recs[e],
-                                                           async_op=True))
+                pending.append(all_gather(gathered[e].view(-1), recs[e], async_op=True))
             else:
                 gathered[e][0].copy_(recs[e])
         ev_count[0] += 1
@@ -320,9 +347,7 @@ def main():
         torch.cuda.synchronize()
         planes_ms = ek0.elapsed_time(ek1)
     if distributed:
-        t = torch.tensor([elapsed, region_ms, tick_ms, planes_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, region_ms, tick_ms, planes_ms = (float(v) for v in t.tolist())
+        elapsed, region_ms, tick_ms, planes_ms = max_over_ranks([elapsed, region_ms, tick_ms, planes_ms])
     kern_avg_ms = tick_ms / args.steps
 
     total_steps = n * world * args.steps
@@ -348,14 +373,12 @@ def main():
                 eng.tick_prepared(prepared[k % R], tick_fn)
                 eng.ensemble_partial(rec)
             if distributed:
-                dist.all_gather_into_tensor(gathered[0].view(-1), rec)
+                all_gather(gathered[0].view(-1), rec)
         torch.cuda.synchronize()
         tb = time.perf_counter()
         k1_el = tb - ta
         if distributed:
-            t = torch.tensor([k1_el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            k1_el = float(t.item())
+            k1_el = max_over_ranks([k1_el])[0]
         k1 = {"steps_per_s": n * world * k1_steps / k1_el, "ms_per_step": k1_el * 1e3 / k1_steps,
               "ticks": k1_steps}
 
@@ -384,7 +407,7 @@ def main():
         own = torch.from_numpy(eng.ensemble_partial()).to(dev)
         allown = torch.zeros(world, rec_len, dtype=torch.float64, device=dev)
         if distributed:
-            dist.all_gather_into_tensor(allown.view(-1), own)
+            all_gather(allown.view(-1), own)
         else:
             allown[0].copy_(own)
         mr, cr = fmskf.ensemble_combine(6, allown.cpu().numpy())
@@ -452,8 +475,9 @@ def main():
             "ensemble_every": args.ensemble_every,
             "ensemble": args.ensemble,
             "gather": args.gather if world > 1 else None,
-            "parallelism": f"instance-sharded x{world}" + (", RCCL all-gather of ensemble records"
-                                                           if world > 1 else ""),
+            "parallelism": f"instance-sharded x{world}" + (
+                (", RCCL all-gather of ensemble records" if not gloo else ", gloo all-gather of ensemble records")
+                if world > 1 else "") + (" (rehearsal: every rank on cuda:0)" if args.same_device else ""),
         },
         "roofline": {
             "bound": "hbm",

@@ -84,3 +84,28 @@ def test_bench_distributed_path_world1(gather, ensemble):
     assert chk["cov_max_rel"] < 1e-9, chk
     assert out["nonfinite_instances"] == 0
     assert out["value"] > 1e9
+
+
+def test_bench_world2_rehearsal_same_gpu():
+    """bench.py's N > 1 code path with two ranks (torch.distributed.run, gloo, both ranks on the
+    one GPU of the test box; RCCL refuses two ranks on one device): per-rank shards with their
+    own seeds, fused records all-gathered every 8 ticks, max-over-ranks timing, the whole-job
+    count, and every rank's gathered records folding to the statistics of the stand-alone
+    records."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    n = 1 << 18
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "32", "--warmup", "4", "--ensemble-every", "8", "--n-per-gpu", str(n),
+           "--no-cpu-baseline", "--no-fused", "--no-secondary", "--backend", "gloo", "--same-device",
+           "--check-ensemble"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["global_instances"] == 2 * n
+    chk = out["ensemble_check"]
+    assert chk["count"] == 2 * n
+    assert chk["mean_max_rel"] < 1e-12, chk
+    assert chk["cov_max_rel"] < 1e-9, chk
+    assert out["ensemble"]["count"] == 2 * n
+    assert out["nonfinite_instances"] == 0
