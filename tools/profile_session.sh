@@ -21,9 +21,10 @@ run() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!!! stopping"; exit $rc; fi
 }
 [ -x build/membench ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench
-run bench 600 python bench.py
+run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
+# the driver's command under the kernel trace (its secondary cfg 3 / 5 / 2^24 lines included)
 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python bench.py --steps 400 --warmup 40 --no-cpu-baseline --no-fused
+  python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 for c in FETCH_SIZE WRITE_SIZE; do
   run pmc_kf6_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_kf6_$c" -o run -- \
     python tools/kbench.py --ticks 30 --packed
@@ -40,6 +41,8 @@ if [ "${PROF_ALL:-0}" = 1 ]; then
               "ekf9_2p22:--model ekf9 --n 4194304 --ticks 30" "kf12d:--model kf12d --ticks 30" \
               "rs:--model rs --ticks 200" "control:--op control --ticks 100" "control_2p22:--op control --n 4194304 --ticks 30" \
               "wt901:--op wt901 --ticks 50" "can:--op can --ticks 100" "ensemble:--op ensemble --ticks 100" \
+              "ens_ekf9:--op ensemble --model ekf9 --ticks 100" "ens_kf12d:--op ensemble --model kf12d --ticks 50" \
+              "ens_ekf9_2p22:--op ensemble --model ekf9 --n 4194304 --ticks 50" "rs_2p24:--model rs --n 16777216 --ticks 20" \
               "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000"; do
     name=${spec%%:*}; args=${spec#*:}
     run prof_$name 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
