@@ -65,10 +65,10 @@ __device__ __forceinline__ double row_sum(double v) {
   return v;
 }
 
-// Sum v[LEN4] over the block's 256 lanes; thread t < LEN4 gets element t (returned), the
-// other threads get 0.  `red` is LDS of 4 * LEN4 doubles.  Ends with the block's threads
-// synchronised (the caller may reuse nothing of `red` without another barrier).
-template <int LEN4>
+// Sum v[LEN4] over the block's NT lanes; thread t < LEN4 gets element t (returned), the
+// other threads get 0.  `red` is LDS of NT / 64 * LEN4 doubles.  Ends with the block's
+// threads synchronised (the caller may reuse nothing of `red` without another barrier).
+template <int LEN4, int NT = kBlock>
 __device__ __forceinline__ double block_reduce(double (&v)[LEN4], double *red) {
   constexpr int Q = LEN4 / 4;
   double w[2 * Q];
@@ -89,7 +89,7 @@ __device__ __forceinline__ double block_reduce(double (&v)[LEN4], double *red) {
   if (t < LEN4) {
     s = red[t];
 #pragma unroll
-    for (int wv = 1; wv < kBlock / 64; wv++) s = s + red[wv * LEN4 + t];
+    for (int wv = 1; wv < NT / 64; wv++) s = s + red[wv * LEN4 + t];
   }
   return s;
 }

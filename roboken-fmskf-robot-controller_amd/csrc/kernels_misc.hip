@@ -90,9 +90,9 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
 // M2 = S2 - S1 S1^T / c.  A row summed by several blocks gets bitwise the same total in each
 // (same per-thread order, same reduction tree), so the record is consistent.  LEN blocks in
 // parallel, each one load round trip at 2^20: the round-1 one-block fold was 4.2-10 us.
-template <int NX>
-__global__ __launch_bounds__(kBlock) void k_ens_fold(const double *__restrict__ blocks, int nb,
-                                                     const double *__restrict__ shift, double *out) {
+template <int NX, int FT>
+__global__ __launch_bounds__(FT) void k_ens_fold(const double *__restrict__ blocks, int nb,
+                                                 const double *__restrict__ shift, double *out) {
   const int k = blockIdx.x;
   int ra = k, rb = k;
   if (k > NX) {
@@ -106,29 +106,29 @@ __global__ __launch_bounds__(kBlock) void k_ens_fold(const double *__restrict__ 
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   constexpr int U = 8;
   int b = threadIdx.x;
-  for (; b + (U - 1) * kBlock < nb; b += U * kBlock) {
+  for (; b + (U - 1) * FT < nb; b += U * FT) {
     double l[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      l[u][0] = r0[b + u * kBlock];
-      l[u][1] = r1[b + u * kBlock];
-      l[u][2] = r2[b + u * kBlock];
-      l[u][3] = r3[b + u * kBlock];
+      l[u][0] = r0[b + u * FT];
+      l[u][1] = r1[b + u * FT];
+      l[u][2] = r2[b + u * FT];
+      l[u][3] = r3[b + u * FT];
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < 4; j++) v[j] = v[j] + l[u][j];
   }
-  for (; b < nb; b += kBlock) {
+  for (; b < nb; b += FT) {
     v[0] = v[0] + r0[b];
     v[1] = v[1] + r1[b];
     v[2] = v[2] + r2[b];
     v[3] = v[3] + r3[b];
   }
-  __shared__ double red[16];
+  __shared__ double red[FT / 64 * 4];
   __shared__ double tot[4];
-  const double s = block_reduce<4>(v, red);
+  const double s = block_reduce<4, FT>(v, red);
   if (threadIdx.x < 4) tot[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -139,6 +139,26 @@ __global__ __launch_bounds__(kBlock) void k_ens_fold(const double *__restrict__ 
     else r = c > 0.0 ? tot[3] - tot[1] * tot[2] / c : 0.0;
     out[k] = r;
   }
+}
+
+// fold block size (FMSKF_ENS_FOLD_THREADS 256 | 512 | 1024; default 1024: 2 record loads per
+// row per thread at 2^20).  KF6 record at 2^20 (partial + fold, back to back): 8.9 us with 256,
+// 8.4 / 11.5 with 512, 8.3 with 1024; EKF9 13.8-15.5 / 13.3-13.4 / 13.2-13.9; a record every
+// tick in the bench: 2.46-2.48e10 steps/s with either (kbench, bench, two passes)
+static int fold_threads() {
+  static const int t = [] {
+    const char *e = getenv("FMSKF_ENS_FOLD_THREADS");
+    const int v = e ? atoi(e) : 1024;
+    return v == 256 || v == 512 ? v : 1024;
+  }();
+  return t;
+}
+template <int NX>
+static void fold_launch(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
+  const int ft = fold_threads();
+  if (ft == 1024) k_ens_fold<NX, 1024><<<EnsRec<NX>::LEN, 1024, 0, st>>>(blocks, nb, shift, out);
+  else if (ft == 512) k_ens_fold<NX, 512><<<EnsRec<NX>::LEN, 512, 0, st>>>(blocks, nb, shift, out);
+  else k_ens_fold<NX, 256><<<EnsRec<NX>::LEN, 256, 0, st>>>(blocks, nb, shift, out);
 }
 
 // the shift vector: robot 0's state
@@ -154,7 +174,7 @@ static void ens_launch(const DevState &s, double *blocks, const double *shift, d
   const int nb = ensemble_nblocks(s.n);
   if (s.tile) k_ens_partial<NX, T, true><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
   else k_ens_partial<NX, T, false><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
-  k_ens_fold<NX><<<EnsRec<NX>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+  fold_launch<NX>(blocks, nb, shift, out, st);
 }
 
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
@@ -168,9 +188,9 @@ int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const d
 
 int launch_ens_fold(int nx, const double *blocks, int nb, const double *shift, double *out,
                     hipStream_t st) {
-  if (nx == 6) k_ens_fold<6><<<EnsRec<6>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
-  else if (nx == 9) k_ens_fold<9><<<EnsRec<9>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
-  else if (nx == 12) k_ens_fold<12><<<EnsRec<12>::LEN, kBlock, 0, st>>>(blocks, nb, shift, out);
+  if (nx == 6) fold_launch<6>(blocks, nb, shift, out, st);
+  else if (nx == 9) fold_launch<9>(blocks, nb, shift, out, st);
+  else if (nx == 12) fold_launch<12>(blocks, nb, shift, out, st);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
