@@ -271,17 +271,18 @@ def main():
             eng.tick_prepared(prepared[k % R], tick_fn)
             native_stats[0] = eng.ensemble_stats()
         else:
+            # without a process group the "gather" is the identity: the record is written in
+            # place into its gather slot
+            dst = recs[e] if distributed else gathered[e][0]
             if args.ensemble == "fused":
-                eng.tick_ensemble_prepared(prepared[k % R], recs[e])
+                eng.tick_ensemble_prepared(prepared[k % R], dst)
             else:
                 eng.tick_prepared(prepared[k % R], tick_fn)
-                eng.ensemble_partial(recs[e])
+                eng.ensemble_partial(dst)
             if distributed and (args.gather == "stream" or gloo):
                 all_gather(gathered[e].view(-1), recs[e])
             elif distributed:
                 pending.append(all_gather(gathered[e].view(-1), recs[e], async_op=True))
-            else:
-                gathered[e][0].copy_(recs[e])
         ev_count[0] += 1
 
     def step(k):

@@ -823,6 +823,33 @@ def test_ekf9_kf12d_kernel_variants_bitexact(ekf9, kf12d):
     assert "nt ok" in out.stdout
 
 
+@pytest.mark.parametrize("threads", ["256", "512"])
+def test_ensemble_fold_block_sizes(threads):
+    """The fold's other block sizes (FMSKF_ENS_FOLD_THREADS; the default is 1024) in a child
+    process: the stand-alone and fused record tests against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys\n"
+        "sys.path[:0] = sys.argv[1:4]\n"
+        "from oracle import oracle as orc\n"
+        "import test_gpu_parity as T\n"
+        "for m, n in (('kf6', 100003), ('ekf9', 5000), ('kf12d', 3000), ('kf6', 1 << 20)):\n"
+        "    T.test_ensemble_partial(orc, m, n)\n"
+        "for m, n in (('kf6', 70000), ('kf6', 1 << 20)):\n"
+        "    T.test_tick_ensemble_fused(orc, m, n)\n"
+        "print('fold ok')\n")
+    env = dict(os.environ, FMSKF_ENS_FOLD_THREADS=threads)
+    out = subprocess.run([sys.executable, "-c", script, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd"),
+                          os.path.join(root, "tests")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "fold ok" in out.stdout
+
+
 def test_rs_one_robot_per_lane_bitexact():
     """FMSKF_RS_TWO=0 (k_rs, one robot per lane, instead of k_rs2) in a child process: the RS
     tick parity test against the oracle, both trig policies."""
