@@ -616,6 +616,43 @@ def test_tick_ensemble_fused(orc, model, n):
     np.testing.assert_allclose(mf, mp, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("n,trig,masked,records", [(70000, LIBM, False, False), (70000, TABLE, True, False),
+                                                   (3001, TABLE, True, True), (3 * (1 << 20) + 5, TABLE, True, True)])
+def test_tick_ensemble_fused_libm_and_mask(orc, n, trig, masked, records):
+    """The fused KF6 tick + record under the LIBM sin/cos policy, with a validity mask, with
+    16-byte tick records, and past the Infinity Cache (k_kf6t): the state bit-exact against a
+    plain tick of the same inputs, the record against the oracle's moments of that state."""
+    import torch
+    T = 3
+    tr = Trajectory(n, T, seed=91)
+    yaw, gz, rpm = tr.kf6_inputs()
+    valid = (np.random.default_rng(n).random((T, n)) > 0.3).astype(np.uint8) if masked else None
+    if records:
+        recs = fmskf.kf6_records(*(torch.from_numpy(a).cuda() for a in (yaw, gz, rpm)))
+        kw = lambda t: dict(kf6_rec=recs[t], **({"valid": torch.from_numpy(valid[t]).cuda()}  # noqa: E731
+                                                if masked else {}))
+    else:
+        kw = lambda t: dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t],  # noqa: E731
+                            **({"valid": valid[t]} if masked else {}))
+    with Engine("kf6", n, trig=trig) as a, Engine("kf6", n, trig=trig) as b:
+        for e in (a, b):
+            e.set_stream(torch.cuda.current_stream())
+        for t in range(T - 1):
+            a.tick(**kw(t))
+            b.tick(**kw(t))
+        a.tick(**kw(T - 1))
+        rb = b.tick_ensemble(**kw(T - 1))
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+    bits_equal(xa, xb, "x")
+    bits_equal(Pa, Pb, "P")
+    assert rb[0] == n
+    mo, co = orc.ens_finalize(6, orc.ens_partial(xb))
+    mf, cf = fmskf.ensemble_combine(6, rb[None, :])
+    np.testing.assert_allclose(mf, mo, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(cf, co, rtol=1e-9, atol=1e-15)
+
+
 # ----------------------------------------------------------------------------- state layout
 @pytest.mark.parametrize("model,n", [("kf6", 1000), ("ekf9", 1), ("ekf9", 1000), ("kf12d", 257),
                                      ("kf12d", 3 * 256), ("rs", 300)])
