@@ -65,9 +65,18 @@ __device__ __forceinline__ double row_sum(double v) {
   return v;
 }
 
+// Block barrier ordering LDS only: __syncthreads() is also a workgroup fence for global
+// memory, i.e. an s_waitcnt vmcnt(0) that would hold a tick kernel's record epilogue until
+// every state store the block issued has drained.  This waits on lgkmcnt only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Sum v[LEN4] over the block's NT lanes; thread t < LEN4 gets element t (returned), the
 // other threads get 0.  `red` is LDS of NT / 64 * LEN4 doubles.  Ends with the block's
-// threads synchronised (the caller may reuse nothing of `red` without another barrier).
+// threads synchronised on LDS (the caller may reuse nothing of `red` without another barrier).
 template <int LEN4, int NT = kBlock>
 __device__ __forceinline__ double block_reduce(double (&v)[LEN4], double *red) {
   constexpr int Q = LEN4 / 4;
@@ -83,7 +92,7 @@ __device__ __forceinline__ double block_reduce(double (&v)[LEN4], double *red) {
 #pragma unroll
     for (int j = 0; j < Q; j++) red[wave * LEN4 + r * Q + j] = u[j];
   }
-  __syncthreads();
+  lds_barrier();
   const int t = threadIdx.x;
   double s = 0.0;
   if (t < LEN4) {
@@ -126,6 +135,20 @@ __device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], d
   const double s = block_reduce<EnsRec<NX>::LEN4>(v, red);
   if (threadIdx.x < EnsRec<NX>::LEN)
     blocks[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+}
+
+// The tick kernels' record epilogue (fmskf_tick_ensemble): the R robots this lane ticked
+// (live ones only), reduced over the block into its record of the post-tick state
+template <int NX, int R, typename T>
+__device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][NX], const bool (&live)[R]) {
+  double sh[NX], v[EnsRec<NX>::LEN4];
+  ens_load_shift<NX>(in.ens_shift, sh);
+#pragma unroll
+  for (int k = 0; k < EnsRec<NX>::LEN4; k++) v[k] = 0.0;
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (live[r]) ens_add<NX>(v, xs[r], sh);
+  ens_block_write<NX>(v, in.ens_blocks);
 }
 
 }  // namespace fmskf

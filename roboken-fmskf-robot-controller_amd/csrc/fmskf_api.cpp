@@ -651,7 +651,8 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
         // the fused KF6 tick + record (fmskf_tick_ensemble) writes one record per tick block
         const size_t len = 1 + d.nx + np;
         size_t nb = (size_t)ensemble_nblocks(n);
-        if (cfg->model == FMSKF_MODEL_KF6) nb = std::max(nb, (size_t)((n + kBlock - 1) / kBlock));
+        if (cfg->model == FMSKF_MODEL_KF6 || cfg->model == FMSKF_MODEL_EKF9)
+          nb = std::max(nb, (size_t)((n + kBlock - 1) / kBlock));
         h->ens_blocks = h->alloc<double>(nb * len);
         h->ens_out = h->alloc<double>(91);
         h->ens_shift = h->alloc<double>(12);
@@ -1179,16 +1180,19 @@ int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out
     const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
     double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
     ensure_shift(h);
-    if (h->cfg.model == FMSKF_MODEL_KF6) {
+    if (h->cfg.model == FMSKF_MODEL_KF6 || (h->cfg.model == FMSKF_MODEL_EKF9 && h->s.tile)) {
       // one kernel: the tick writes each block's record of the state it just stored (no
       // second pass over x), then the fold
       TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
       t.ens_blocks = h->ens_blocks;
       t.ens_shift = h->ens_shift;
       int nb = 0;
+      const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
       h->time_begin();
-      launch_check(launch_kf6(h->s, t, h->kf6, h->cfg.trig == FMSKF_TRIG_LIBM, true, true, h->stream, &nb),
-                   "tick kernel launch");
+      if (h->cfg.model == FMSKF_MODEL_KF6)
+        launch_check(launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream, &nb), "tick kernel launch");
+      else
+        launch_check(launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream, &nb), "tick kernel launch");
       h->time_end();
       launch_check(launch_ens_fold((int)nx, h->ens_blocks, nb, h->ens_shift, dst, h->stream),
                    "ensemble fold launch");

@@ -7,6 +7,7 @@
 // F / H / Q / R are shared: H and the sparsity of F are compile-time model traits
 // (kf_generic.hpp), Q / R / dt ride in the kernarg segment (scalar loads, SGPRs).
 // The 6-state headline kernel lives in kernels_kf6.hip.
+#include "ens_device.hpp"
 #include "kf_generic.hpp"
 
 #pragma clang fp contract(off)
@@ -153,7 +154,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
-template <bool LIBM, bool UPD, bool PRED, int CP = 0, bool PRIO = false>
+// ENS: the record epilogue of fmskf_tick_ensemble (ens_device.hpp)
+template <bool LIBM, bool UPD, bool PRED, int CP = 0, bool PRIO = false, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -197,13 +199,20 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
     }
   }
   nan_guard(x, P, a.counters, live);
+  if constexpr (ENS) {
+    float xs[1][N];
+#pragma unroll
+    for (int k = 0; k < N; k++) xs[0][k] = x[k];
+    const bool lv[1] = {live};
+    ens_epilogue<9, 1>(a.in, xs, lv);
+  }
 }
 
 // Two robots per lane (tiles b and b + gridDim.x of the tiled state): robot B's 54 state
 // loads and its raw record are issued before robot A's update, so they stream in while A
 // computes (FMSKF_EKF9_VARIANT experiments; see launch_ekf9).  PRIO: the waves issue their
 // loads at raised priority (s_setprio 3) and compute at the base priority.
-template <bool LIBM, int CP, bool PRIO>
+template <bool LIBM, int CP, bool PRIO, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -248,6 +257,11 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
     for (int k = 0; k < NP; k++) tpa.st(k, Pa[k]);
   }
   nan_guard(xa, Pa, a.counters, live_a);
+  float xs[ENS ? 2 : 1][N];
+  if constexpr (ENS) {
+#pragma unroll
+    for (int k = 0; k < N; k++) xs[0][k] = xa[k];
+  }
   ekf9_tick1<LIBM, true, true>(a, rb, hb, stab, xb, Pb);
   if (live_b) {
 #pragma unroll
@@ -256,6 +270,12 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
     for (int k = 0; k < NP; k++) tpb.st(k, Pb[k]);
   }
   nan_guard(xb, Pb, a.counters, live_b);
+  if constexpr (ENS) {
+#pragma unroll
+    for (int k = 0; k < N; k++) xs[1][k] = xb[k];
+    const bool lv[2] = {live_a, live_b};
+    ens_epilogue<9, 2>(a.in, xs, lv);
+  }
 }
 
 // SEQ: R has no base/tip cross terms -> group-sequential update (base group, then tip group
@@ -464,11 +484,35 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   nan_guard(x, P, a.counters);
 }
 
+// fused tick + record (fmskf_tick_ensemble): the default single-tick kernel with the record
+// epilogue; returns the grid (= the number of block records)
+template <bool LIBM>
+static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, bool nt, hipStream_t st) {
+  if (!LIBM && s.n * 216 <= (256ull << 20)) {
+    const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
+    const dim3 g2((ntiles + 1) / 2);
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
+    if (nt) k_ekf9p<false, kStateNT, false, true><<<g2, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, 0, false, true><<<g2, kBlock, lds, st>>>(a);
+    return (int)g2.x;
+  }
+  const dim3 g = grid_for(s.n);
+  const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
+  if (nt) k_ekf9t<LIBM, true, true, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
+  else k_ekf9t<LIBM, true, true, 0, false, true><<<g, kBlock, lds, st>>>(a);
+  return (int)g.x;
+}
+
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
-                bool pred, hipStream_t st) {
+                bool pred, hipStream_t st, int *ens_nb) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
+  if (in.ens_blocks) {
+    if (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1) return (int)hipErrorInvalidValue;
+    *ens_nb = libm ? launch_ekf9_ens<true>(a, s, nt, st) : launch_ekf9_ens<false>(a, s, nt, st);
+    return (int)hipGetLastError();
+  }
   // Single-tick kernel choice (FMSKF_EKF9_VARIANT, read once, forces one): 0 (default) two
   // robots per lane (k_ekf9p) while the 216-byte state fits the 256 MiB Infinity Cache, else
   // one per lane (k_ekf9t); 1 k_ekf9t with a raised-priority load phase; 2 k_ekf9p; 3 k_ekf9p

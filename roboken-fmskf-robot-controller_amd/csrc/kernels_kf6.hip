@@ -44,19 +44,6 @@ using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true, O
 template <class O>
 using WithEns = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, true>;
 
-// the record of the robots this lane ticked (live ones only), reduced over the block
-template <int R>
-__device__ __forceinline__ void kf6_ens(const TickIn &in, const float (&xs)[R][6], const bool (&live)[R]) {
-  double sh[6], v[EnsRec<6>::LEN4];
-  ens_load_shift<6>(in.ens_shift, sh);
-#pragma unroll
-  for (int k = 0; k < EnsRec<6>::LEN4; k++) v[k] = 0.0;
-#pragma unroll
-  for (int r = 0; r < R; r++)
-    if (live[r]) ens_add<6>(v, xs[r], sh);
-  ens_block_write<6>(v, in.ens_blocks);
-}
-
 struct Kf6In {
   float yaw, gz;
   uint2 rpm;
@@ -262,7 +249,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 #pragma unroll
     for (int k = 0; k < 6; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    kf6_ens<1>(a.in, xs, lv);
+    ens_epilogue<6, 1>(a.in, xs, lv);
   }
 }
 
@@ -302,7 +289,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     }
     lv[r] = live;
   }
-  if constexpr (O::ENS) kf6_ens<R>(a.in, xs, lv);
+  if constexpr (O::ENS) ens_epilogue<6, R>(a.in, xs, lv);
 }
 
 // Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no

@@ -579,7 +579,8 @@ def test_bad_inputs_rejected():
 # 3 * 2^20 + 5 the state outgrows the Infinity Cache and the one-robot-per-lane tick (k_kf6t)
 # carries it, 6145 block records
 @pytest.mark.parametrize("model,n", [("kf6", 100003), ("kf6", 1), ("kf6", 70000), ("ekf9", 3000),
-                                     ("kf6", 1 << 20), ("kf6", 3 * (1 << 20) + 5)])
+                                     ("kf6", 1 << 20), ("kf6", 3 * (1 << 20) + 5), ("ekf9", 1),
+                                     ("ekf9", 700), ("ekf9", 1 << 20), ("ekf9", 1300001)])
 def test_tick_ensemble_fused(orc, model, n):
     """fmskf_tick_ensemble = fmskf_tick + the record of the post-tick state: state bit-exact
     vs a plain tick, record vs the oracle's two-pass moments of that state, and bitwise
@@ -651,6 +652,34 @@ def test_tick_ensemble_fused_libm_and_mask(orc, n, trig, masked, records):
     mf, cf = fmskf.ensemble_combine(6, rb[None, :])
     np.testing.assert_allclose(mf, mo, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(cf, co, rtol=1e-9, atol=1e-15)
+
+
+@pytest.mark.parametrize("n", [5000, 1300001])
+def test_tick_ensemble_fused_ekf9_libm_mask(orc, n):
+    """EKF9 fused tick + record with the LIBM policy (the one-robot-per-lane kernel) and with a
+    validity mask under TABLE512 (two robots per lane below the Infinity Cache size, one per
+    lane past it): state bit-exact against plain ticks, the record against the oracle."""
+    T = 3
+    tr = Trajectory(n, T, seed=92)
+    raw = tr.ekf9_raw()
+    valid = (np.random.default_rng(n).random((T, n)) > 0.3).astype(np.uint8)
+    for trig, masked in ((LIBM, False), (TABLE, True)):
+        kw = lambda t: dict(raw=raw[t], **({"valid": valid[t]} if masked else {}))  # noqa: E731
+        with Engine("ekf9", n, trig=trig) as a, Engine("ekf9", n, trig=trig) as b:
+            for t in range(T - 1):
+                a.tick(**kw(t))
+                b.tick(**kw(t))
+            a.tick(**kw(T - 1))
+            rb = b.tick_ensemble(**kw(T - 1))
+            xa, Pa = a.get_state()
+            xb, Pb = b.get_state()
+        bits_equal(xa, xb, "x")
+        bits_equal(Pa, Pb, "P")
+        assert rb[0] == n
+        mo, co = orc.ens_finalize(9, orc.ens_partial(xb))
+        mf, cf = fmskf.ensemble_combine(9, rb[None, :])
+        np.testing.assert_allclose(mf, mo, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(cf, co, rtol=1e-9, atol=1e-15)
 
 
 # ----------------------------------------------------------------------------- state layout

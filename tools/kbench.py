@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
     ap.add_argument("--packed", action="store_true", help="KF6: fmskf_kf6_record inputs")
     ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
@@ -79,11 +79,24 @@ def main():
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
-    tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op == "ensemble" else args.op))
+    tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op in ("ensemble", "tick_ensemble") else args.op))
     for k in range(20):
         e.tick_prepared(preps[k % R], tick)
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if args.op == "tick_ensemble":  # fmskf_tick_ensemble: the tick with its record (+ fold)
+        rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
+        e.tick_ensemble_prepared(preps[0], rec)
+        torch.cuda.synchronize()
+        ev0.record(st)
+        for k in range(args.ticks):
+            e.tick_ensemble_prepared(preps[k % R], rec)
+        ev1.record(st)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / args.ticks
+        print(json.dumps({"model": args.model, "n": n, "op": "tick_ensemble", "ms_per_tick": ms,
+                          "steps_per_s": n / (ms * 1e-3)}), flush=True)
+        return
     if args.op == "ensemble":  # the ensemble record reduction alone (partial + fold)
         rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
         e.ensemble_partial(rec)
