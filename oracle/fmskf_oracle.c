@@ -541,6 +541,7 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
   pat[2][5] = 1;
   pat[3][7] = 1;
   pat[4][8] = 1;
+  const int rdiag = orc_r_diagonal_f32(6, prm->r);
   orc_init_tab();
 #ifdef _OPENMP
   if (nthreads <= 0) nthreads = omp_get_max_threads();
@@ -560,7 +561,9 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
       y[3] = z[3] - xs[8];
       y[4] = z[4] - xs[3];
       y[5] = z[5] - xs[4];
-      orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
+      /* canonical order: sequential scalar updates for a diagonal R, else the joint LDL^T */
+      if (rdiag) orc_kf_update_seq_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
+      else orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
     }
     if (do_predict) {
       float dt = prm->dt;

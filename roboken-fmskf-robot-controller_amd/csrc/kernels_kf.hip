@@ -52,7 +52,8 @@ __device__ __forceinline__ uint4 ekf9_raw_at(const int16_t *raw, uint64_t i) {
 }
 
 // one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
-template <bool LIBM, bool UPD, bool PRED>
+// SEQ: R is diagonal -> the sequential scalar update (kf_update_seq), else the joint LDL^T one
+template <bool LIBM, bool UPD, bool PRED, bool SEQ>
 __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, const uint4 raw,
                                            bool have, const float *stab, float (&x)[9],
                                            float (&P)[45]) {
@@ -60,7 +61,8 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
   if (UPD && have) {
     float y[6];
     ekf9_innov(raw, x, y);
-    kf_update<MdEKF9>(x, P, y, a.prm.r);
+    if constexpr (SEQ) kf_update_seq<MdEKF9>(x, P, y, a.prm.r);
+    else kf_update<MdEKF9>(x, P, y, a.prm.r);
   }
   if (PRED) {
     // f(x): mecanum body velocity rotated into the world frame (the reference's
@@ -87,7 +89,7 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
 
 // tick_many: T ticks per launch, state in VGPRs; the next tick's raw record (16 B) and validity
 // byte are loaded while the current tick computes (ping-pong registers, loop unrolled by two)
-template <bool LIBM, bool UPD, bool PRED>
+template <bool LIBM, bool UPD, bool PRED, bool SEQ>
 __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float stab[LIBM ? 1 : 513];
@@ -128,13 +130,13 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
       rb = raw_at(t + 1);
       hb = have_at(t + 1);
     }
-    ekf9_tick1<LIBM, UPD, PRED>(a, ra, ha, stab, x, P);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, ra, ha, stab, x, P);
     if (t + 1 >= T) break;
     if (t + 2 < T) {
       ra = raw_at(t + 2);
       ha = have_at(t + 2);
     }
-    ekf9_tick1<LIBM, UPD, PRED>(a, rb, hb, stab, x, P);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, rb, hb, stab, x, P);
   }
   if (live) {
     if constexpr (FMSKF_TILED) {
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
 // ENS: the record epilogue of fmskf_tick_ensemble (ens_device.hpp)
-template <bool LIBM, bool UPD, bool PRED, int CP = 0, bool PRIO = false, bool ENS = false>
+template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool PRIO = false, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
   if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
-  ekf9_tick1<LIBM, UPD, PRED>(a, raw, have, stab, x, P);
+  ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P);
   if (live) {
     if constexpr (FMSKF_TILED) {
 #pragma unroll
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 // loads and its raw record are issued before robot A's update, so they stream in while A
 // computes (FMSKF_EKF9_VARIANT experiments; see launch_ekf9).  PRIO: the waves issue their
 // loads at raised priority (s_setprio 3) and compute at the base priority.
-template <bool LIBM, int CP, bool PRIO, bool ENS = false>
+template <bool LIBM, bool SEQ, int CP, bool PRIO, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   for (int k = 0; k < NP; k++) Pb[k] = tpb.ld(k);
   if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
-  ekf9_tick1<LIBM, true, true>(a, ra, ha, stab, xa, Pa);
+  ekf9_tick1<LIBM, true, true, SEQ>(a, ra, ha, stab, xa, Pa);
   if (live_a) {
 #pragma unroll
     for (int k = 0; k < N; k++) txa.st(k, xa[k]);
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = xa[k];
   }
-  ekf9_tick1<LIBM, true, true>(a, rb, hb, stab, xb, Pb);
+  ekf9_tick1<LIBM, true, true, SEQ>(a, rb, hb, stab, xb, Pb);
   if (live_b) {
 #pragma unroll
     for (int k = 0; k < N; k++) txb.st(k, xb[k]);
@@ -486,31 +488,29 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 
 // fused tick + record (fmskf_tick_ensemble): the default single-tick kernel with the record
 // epilogue; returns the grid (= the number of block records)
-template <bool LIBM>
+template <bool LIBM, bool SEQ>
 static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, bool nt, hipStream_t st) {
   if (!LIBM && s.n * 216 <= (256ull << 20)) {
     const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
     const dim3 g2((ntiles + 1) / 2);
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) k_ekf9p<false, kStateNT, false, true><<<g2, kBlock, lds, st>>>(a);
-    else k_ekf9p<false, 0, false, true><<<g2, kBlock, lds, st>>>(a);
+    if (nt) k_ekf9p<false, SEQ, kStateNT, false, true><<<g2, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, SEQ, 0, false, true><<<g2, kBlock, lds, st>>>(a);
     return (int)g2.x;
   }
   const dim3 g = grid_for(s.n);
   const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
-  if (nt) k_ekf9t<LIBM, true, true, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
-  else k_ekf9t<LIBM, true, true, 0, false, true><<<g, kBlock, lds, st>>>(a);
+  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
+  else k_ekf9t<LIBM, true, true, SEQ, 0, false, true><<<g, kBlock, lds, st>>>(a);
   return (int)g.x;
 }
 
-int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
-                bool pred, hipStream_t st, int *ens_nb) {
-  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
+template <bool SEQ>
+static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, const TickIn &in, bool libm,
+                         bool upd, bool pred, bool nt, hipStream_t st, int *ens_nb) {
   const dim3 g = grid_for(s.n);
-  const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
   if (in.ens_blocks) {
-    if (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1) return (int)hipErrorInvalidValue;
-    *ens_nb = libm ? launch_ekf9_ens<true>(a, s, nt, st) : launch_ekf9_ens<false>(a, s, nt, st);
+    *ens_nb = libm ? launch_ekf9_ens<true, SEQ>(a, s, nt, st) : launch_ekf9_ens<false, SEQ>(a, s, nt, st);
     return (int)hipGetLastError();
   }
   // Single-tick kernel choice (FMSKF_EKF9_VARIANT, read once, forces one): 0 (default) two
@@ -526,26 +526,27 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
   const int v = var == 0 ? (s.n * 216 <= (256ull << 20) ? 2 : 4) : var;
   if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v >= 1 && v <= 3) {
     if (v == 1) {
-      if (nt) k_ekf9t<false, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<false, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+      if (nt) k_ekf9t<false, true, true, SEQ, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<false, true, true, SEQ, 0, true><<<g, kBlock, 0, st>>>(a);
     } else {
       const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
       const dim3 g2((ntiles + 1) / 2);
       // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-      if (v == 2 && nt) k_ekf9p<false, kStateNT, false><<<g2, kBlock, lds, st>>>(a);
-      else if (v == 2) k_ekf9p<false, 0, false><<<g2, kBlock, lds, st>>>(a);
-      else if (nt) k_ekf9p<false, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
-      else k_ekf9p<false, 0, true><<<g2, kBlock, lds, st>>>(a);
+      if (v == 2 && nt) k_ekf9p<false, SEQ, kStateNT, false><<<g2, kBlock, lds, st>>>(a);
+      else if (v == 2) k_ekf9p<false, SEQ, 0, false><<<g2, kBlock, lds, st>>>(a);
+      else if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
+      else k_ekf9p<false, SEQ, 0, true><<<g2, kBlock, lds, st>>>(a);
     }
     return (int)hipGetLastError();
   }
+  // predict-only launches run no update: one (SEQ = false) instantiation serves both
   if (in.n_ticks == 1) {
     if (libm) {
-      if (upd && pred && nt) k_ekf9t<true, true, true, kStateNT><<<g, kBlock, 0, st>>>(a);
-      else if (upd && pred) k_ekf9t<true, true, true><<<g, kBlock, 0, st>>>(a);
-      else if (upd) k_ekf9t<true, true, false><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<true, false, true><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<true, true, true, SEQ, kStateNT><<<g, kBlock, 0, st>>>(a);
+      else if (upd && pred) k_ekf9t<true, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
+      else if (upd) k_ekf9t<true, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<true, false, true, false><<<g, kBlock, 0, st>>>(a);
     } else {
       // Past the Infinity Cache (non-temporal state) the occupancy is capped at 2 blocks per CU
       // with 64 KiB of dynamic LDS: fewer concurrent tile streams per HBM channel.  2^22:
@@ -553,21 +554,33 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
       // 382-383 at 80 KiB (kbench, two boxes, two passes each); the same-bytes tiled pattern
       // (membench) 299 us.  FMSKF_EKF9_LDS overrides the byte count.
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
-      if (upd && pred && nt) k_ekf9t<false, true, true, kStateNT><<<g, kBlock, lds, st>>>(a);
-      else if (upd && pred) k_ekf9t<false, true, true><<<g, kBlock, lds, st>>>(a);
-      else if (upd) k_ekf9t<false, true, false><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<false, false, true><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<false, true, true, SEQ, kStateNT><<<g, kBlock, lds, st>>>(a);
+      else if (upd && pred) k_ekf9t<false, true, true, SEQ><<<g, kBlock, lds, st>>>(a);
+      else if (upd) k_ekf9t<false, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<false, false, true, false><<<g, kBlock, 0, st>>>(a);
     }
   } else if (libm) {
-    if (upd && pred) k_ekf9<true, true, true><<<g, kBlock, 0, st>>>(a);
-    else if (upd) k_ekf9<true, true, false><<<g, kBlock, 0, st>>>(a);
-    else k_ekf9<true, false, true><<<g, kBlock, 0, st>>>(a);
+    if (upd && pred) k_ekf9<true, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_ekf9<true, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
+    else k_ekf9<true, false, true, false><<<g, kBlock, 0, st>>>(a);
   } else {
-    if (upd && pred) k_ekf9<false, true, true><<<g, kBlock, 0, st>>>(a);
-    else if (upd) k_ekf9<false, true, false><<<g, kBlock, 0, st>>>(a);
-    else k_ekf9<false, false, true><<<g, kBlock, 0, st>>>(a);
+    if (upd && pred) k_ekf9<false, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_ekf9<false, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
+    else k_ekf9<false, false, true, false><<<g, kBlock, 0, st>>>(a);
   }
   return (int)hipGetLastError();
+}
+
+int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
+                bool pred, hipStream_t st, int *ens_nb) {
+  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
+  const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
+  if (in.ens_blocks && (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1))
+    return (int)hipErrorInvalidValue;
+  // canonical update order (oracle orc_ekf9_tick): sequential scalar updates when R is
+  // diagonal, the joint LDL^T update otherwise
+  if (ekf9_r_diagonal(p.r)) return launch_ekf9_s<true>(a, s, in, libm, upd, pred, nt, st, ens_nb);
+  return launch_ekf9_s<false>(a, s, in, libm, upd, pred, nt, st, ens_nb);
 }
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,

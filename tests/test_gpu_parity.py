@@ -266,26 +266,46 @@ def test_rs_many_and_split():
 
 
 # ----------------------------------------------------------------------------- EKF9 / KF12D
-def test_ekf9_bitexact(orc):
+# EKF9 R cases: the default (diagonal: the sequential scalar update), and correlated wheel
+# velocities and accelerations (the joint LDL^T update)
+EKF9_R_CASES = {"diagonal": {}, "correlated": {(5, 4): 1e-4, (3, 2): 0.05, (1, 0): 1e-5}}
+
+
+def _ekf9_r(cfg, terms):
+    r = np.array(cfg.r[:21])
+    for (i, j), v in terms.items():
+        r[i * (i + 1) // 2 + j] = v
+    return r
+
+
+@pytest.mark.parametrize("case", list(EKF9_R_CASES))
+def test_ekf9_bitexact(orc, case):
     n, T = 1500, 30
     tr = Trajectory(n, T, seed=41)
     raw = tr.ekf9_raw()
     cfg = fmskf.default_config("ekf9", n)
-    with Engine("ekf9", n, trig=TABLE) as e:
+    r = _ekf9_r(cfg, EKF9_R_CASES[case])
+    with Engine("ekf9", n, trig=TABLE, r=r) as e:
         for t in range(T):
             e.tick(raw=raw[t])
         x, P = e.get_state()
-    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+        rec = e.tick_ensemble(raw=raw[0])  # the fused record kernel takes the same update path
+        x2, P2 = e.get_state()
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), r, orc.TRIG_TABLE512)
     xo = np.zeros((9, n), np.float32)
     Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
     for t in range(T):
         orc.ekf9_tick(xo, Po, raw[t], None, prm, nthreads=0)
     bits_equal(x, xo, "x")
     bits_equal(P, Po, "P")
+    orc.ekf9_tick(xo, Po, raw[0], None, prm, nthreads=0)
+    bits_equal(x2, xo, "x (tick_ensemble)")
+    bits_equal(P2, Po, "P (tick_ensemble)")
+    assert rec[0] == n
 
 
-@pytest.mark.parametrize("n,T", [(1000, 9), (257, 4)])
-def test_ekf9_many_split_mask_bitexact(orc, n, T):
+@pytest.mark.parametrize("n,T,case", [(1000, 9, "diagonal"), (257, 4, "diagonal"), (1000, 5, "correlated")])
+def test_ekf9_many_split_mask_bitexact(orc, n, T, case):
     """EKF9 over the tiled state: T ticks in one tick_many launch (the ping-pong loop kernel,
     odd T exercising its tail), per-tick ticks and correct-then-predict calls, all with a
     validity mask at ragged N, bit-identical to each other and to the oracle."""
@@ -294,14 +314,15 @@ def test_ekf9_many_split_mask_bitexact(orc, n, T):
     rng = np.random.default_rng(n)
     valid = (rng.random((T, n)) > 0.2).astype(np.uint8)
     cfg = fmskf.default_config("ekf9", n)
-    with Engine("ekf9", n) as a, Engine("ekf9", n) as b, Engine("ekf9", n) as c:
+    r = _ekf9_r(cfg, EKF9_R_CASES[case])
+    with Engine("ekf9", n, r=r) as a, Engine("ekf9", n, r=r) as b, Engine("ekf9", n, r=r) as c:
         a.tick_many(T, raw=raw, valid=valid)
         for t in range(T):
             b.tick(raw=raw[t], valid=valid[t])
             c.correct(raw=raw[t], valid=valid[t])
             c.predict()
         (xa, Pa), (xb, Pb), (xc, Pc) = (e.get_state() for e in (a, b, c))
-    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), r, orc.TRIG_TABLE512)
     xo = np.zeros((9, n), np.float32)
     Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
     for t in range(T):

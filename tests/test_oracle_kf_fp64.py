@@ -67,13 +67,15 @@ def test_kf6_fp32_vs_fp64(orc, trig):
         _check(x[:, i], P[:, i], x64, P64)
 
 
-def test_ekf9_fp32_vs_fp64(orc):
+# diagonal R: the canonical EKF9 update is the sequential scalar one; correlated: the joint LDL^T
+@pytest.mark.parametrize("terms", [{}, {(5, 4): 1e-4, (3, 2): 0.05, (1, 0): 1e-5}])
+def test_ekf9_fp32_vs_fp64(orc, terms):
     T, n = 300, 6
     tr = Trajectory(n, T, seed=12)
     raw = tr.ekf9_raw()
     cfg = fmskf.default_config("ekf9", n)
     q = np.array(cfg.q[:45], np.float32)
-    r = np.array(cfg.r[:21], np.float32)
+    r = _r_with(np.array(cfg.r[:21]), terms).astype(np.float32)
     p0 = np.array(cfg.p0[:45], np.float32)
     prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
     x = np.zeros((9, n), np.float32)

@@ -275,6 +275,8 @@ __global__ __launch_bounds__(256) void k_tiled_probe(TT *st, const uint4 *raw, u
 template <int NS>
 __global__ __launch_bounds__(256) void k_pitch_nt(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
                                                   float sink) {
+  extern __shared__ double occ_cap[];  // dynamic LDS only limits the blocks per CU
+  (void)occ_cap;
   const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= n) return;
   float s[NS];
@@ -338,6 +340,54 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'c') {
+    // membench LG 1 caps: the HBM-regime patterns (non-temporal state) under the occupancy cap
+    // (dynamic LDS per block -> blocks per CU), tiled against planar; LG sizes the EKF9 case,
+    // KF12D runs at LG - 2 and KF6 at LG + 2 (the configs' ratios: 2^22 / 2^20 / 2^24)
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t nk = n >> 2, n6 = n << 2;
+    const uint64_t pitch = ((n + 511) / 512) * 512 + 256, pitch6 = ((n6 + 511) / 512) * 512 + 256;
+    uint64_t words = 54 * pitch > 27 * pitch6 ? 54 * pitch : 27 * pitch6;
+    if (words < 112 * n) words = 112 * n;  // the copy reads 224 n bytes and writes the next 224 n
+    if (words < 45 * n) words = 45 * n;    // KF12D tiles: 90 doubles x n / 4
+    void *sb, *ib;
+    CK(hipMalloc(&sb, words * 4));
+    CK(hipMalloc(&ib, n6 * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, words, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, n6 * 4, 8);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, int kb, uint64_t nn, double bpi, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"lds_KiB\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)nn, name, kb, us, bpi * nn / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)((n + 255) / 256), gk = (unsigned)((nk + 255) / 256),
+                   g6 = (unsigned)((n6 + 255) / 256);
+    for (int kb : {0, 32, 48, 64, 80}) {
+      const size_t L = (size_t)kb * 1024;
+      tm("ekf9_t256_nt", kb, n, 448, [&] { k_tiled_probe<54, 256, 2><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_pitch_nt", kb, n, 448, [&] { k_pitch_nt<54><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, pitch, 0.f); });
+      tm("kf12d_t256_nt", kb, nk, 1504, [&] {
+        k_tiled_probe<90, 256, 2, double><<<gk, 256, L>>>((double *)sb, (const uint4 *)ib, nk, 0.0);
+      });
+      tm("kf6_pitch_nt", kb, n6, 232, [&] { k_pitch_nt<27><<<g6, 256, L>>>((float *)sb, (const uint4 *)ib, n6, pitch6, 0.f); });
+      tm("kf6_t256_nt", kb, n6, 232, [&] { k_tiled_probe<27, 256, 2><<<g6, 256, L>>>((float *)sb, (const uint4 *)ib, n6, 0.f); });
+    }
+    tm("copy_float4_448B_fullgrid", 0, n, 448, [&] {
+      k_copy4<<<(unsigned)(224 * n / 16 / 256), 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n),
+                                                      224 * n / 16);
+    });
+    return 0;
+  }
   if (argc > 3) {  // membench LG 1 models: the EKF9 and KF12D patterns only
     hipEvent_t f0, f1;
     CK(hipEventCreate(&f0));
