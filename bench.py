@@ -142,7 +142,54 @@ def secondary_configs(dev, stream, ticks: int, trig):
                     "ticks": ticks, "nonfinite_instances": int(cnt[0]),
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                  "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": bps}}
+    out["cfg4_shard_kf6_2p21"] = cfg4_shard(dev, stream, max(ticks, 32), trig)
     return out
+
+
+def cfg4_shard(dev, stream, ticks: int, trig):
+    """BASELINE.json configs[3] on one GPU: its 2^21-robot per-GPU shard of the 16M fleet, the
+    tick alone, with the fused ensemble record (+ fold) every 16th tick and every tick (K = 16
+    and K = 1, SURVEY.md 8(d) cfg 4); HIP events on the tick stream, no collective (that is the
+    N > 1 bench run's)."""
+    import torch
+    import fmskf
+    from fmskf.synth import SEED, kf6_ring_torch
+    n, R = 1 << 21, 8
+    e = fmskf.Engine("kf6", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 4, device=dev)
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    del yaw, gz, rpm
+    preps = [e.prepare(kf6_rec=rec[r]) for r in range(R)]
+    out_rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
+
+    def run(every):
+        for k in range(ticks):
+            if every and (k + 1) % every == 0:
+                e.tick_ensemble_prepared(preps[k % R], out_rec)
+            else:
+                e.tick_prepared(preps[k % R])
+
+    res = {"instances": n, "ticks": ticks}
+    for label, every in (("tick_only", 0), ("ensemble_every_16", 16), ("ensemble_every_1", 1)):
+        run(every)  # warm-up: every kernel of this sequence loaded
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        run(every)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / ticks
+        res[label] = {"ms_per_step": ms, "steps_per_s": n / (ms * 1e-3)}
+    gbps = 232 * n / (res["tick_only"]["ms_per_step"] * 1e-3) / 1e9
+    res["roofline"] = {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                       "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": 232}
+    res["ensemble_count"] = float(out_rec[0].item())
+    e.close()
+    del preps, rec
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():

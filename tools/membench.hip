@@ -271,6 +271,34 @@ __global__ __launch_bounds__(256) void k_tiled_probe(TT *st, const uint4 *raw, u
   }
 }
 
+// the non-temporal tiled pattern with FMAS fp32 FMAs (8 independent chains over every loaded
+// row) between the loads and the stores: the tick kernels' compute phase without their math
+template <int NS, int FMAS>
+__global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw, uint64_t n, float sink) {
+  extern __shared__ double occ_cap[];
+  (void)occ_cap;
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  float *tile = st + (v / 256) * ((uint64_t)NS * 256) + (v % 256);
+  const uint4 r = raw[v];
+  float s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * 256);
+  const float a = __builtin_bit_cast(float, r.x | 0x3F800000u) * sink;
+  float c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = s[j];
+#pragma unroll
+  for (int it = 0; it < FMAS / 8; it++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = __builtin_fmaf(c[j], a, s[(it * 8 + j) % NS]);
+  float m = c[0];
+#pragma unroll
+  for (int j = 1; j < 8; j++) m += c[j];
+#pragma unroll
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
+}
+
 // the pitched (planar) KF6 pattern with non-temporal state loads and stores and a 16-byte record
 template <int NS>
 __global__ __launch_bounds__(256) void k_pitch_nt(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
@@ -386,6 +414,19 @@ int main(int argc, char **argv) {
       k_copy4<<<(unsigned)(224 * n / 16 / 256), 256>>>((const float4 *)sb, (float4 *)((char *)sb + 224 * n),
                                                       224 * n / 16);
     });
+    // compute between the loads and the stores (EKF9 tick: ~860 VALU per robot), at the
+    // EKF9 kernel's occupancy cap (64 KiB: 2 blocks per CU) and uncapped
+    for (int kb : {0, 64, 48, 64}) {
+      const size_t L = (size_t)kb * 1024;
+      tm("ekf9_t256_nt_fma0", kb, n, 448, [&] { k_tiled_delay<54, 0><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma1024", kb, n, 448, [&] { k_tiled_delay<54, 1024><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma1536", kb, n, 448, [&] { k_tiled_delay<54, 1536><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma2048", kb, n, 448, [&] { k_tiled_delay<54, 2048><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma256", kb, n, 448, [&] { k_tiled_delay<54, 256><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma512", kb, n, 448, [&] { k_tiled_delay<54, 512><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+      tm("ekf9_t256_nt_fma1280", kb, n, 448, [&] { k_tiled_delay<54, 1280><<<g, 256, L>>>((float *)sb, (const uint4 *)ib, n, 0.f); });
+    }
     return 0;
   }
   if (argc > 3) {  // membench LG 1 models: the EKF9 and KF12D patterns only
