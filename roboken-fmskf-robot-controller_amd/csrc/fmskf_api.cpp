@@ -651,7 +651,7 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
         // the fused KF6 tick + record (fmskf_tick_ensemble) writes one record per tick block
         const size_t len = 1 + d.nx + np;
         size_t nb = (size_t)ensemble_nblocks(n);
-        if (cfg->model == FMSKF_MODEL_KF6 || cfg->model == FMSKF_MODEL_EKF9)
+        if (cfg->model == FMSKF_MODEL_KF6 || cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D)
           nb = std::max(nb, (size_t)((n + kBlock - 1) / kBlock));
         h->ens_blocks = h->alloc<double>(nb * len);
         h->ens_out = h->alloc<double>(91);
@@ -1180,7 +1180,8 @@ int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out
     const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
     double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
     ensure_shift(h);
-    if (h->cfg.model == FMSKF_MODEL_KF6 || (h->cfg.model == FMSKF_MODEL_EKF9 && h->s.tile)) {
+    if (h->cfg.model == FMSKF_MODEL_KF6 || (h->cfg.model == FMSKF_MODEL_EKF9 && h->s.tile) ||
+        (h->cfg.model == FMSKF_MODEL_KF12D && h->s.tile && h->kf12.decor)) {
       // one kernel: the tick writes each block's record of the state it just stored (no
       // second pass over x), then the fold
       TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
@@ -1191,8 +1192,10 @@ int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out
       h->time_begin();
       if (h->cfg.model == FMSKF_MODEL_KF6)
         launch_check(launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream, &nb), "tick kernel launch");
-      else
+      else if (h->cfg.model == FMSKF_MODEL_EKF9)
         launch_check(launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream, &nb), "tick kernel launch");
+      else
+        launch_check(launch_kf12d(h->s, t, h->kf12, true, true, h->stream, &nb), "tick kernel launch");
       h->time_end();
       launch_check(launch_ens_fold((int)nx, h->ens_blocks, nb, h->ens_shift, dst, h->stream),
                    "ensemble fold launch");

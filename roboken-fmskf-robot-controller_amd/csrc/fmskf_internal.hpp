@@ -223,7 +223,7 @@ int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool lib
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
                 bool pred, hipStream_t st, int *ens_nb = nullptr);
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,
-                 hipStream_t st);
+                 hipStream_t st, int *ens_nb = nullptr);
 int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
                  int latch_qinit, uint32_t read_reg_index, hipStream_t st);
 int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,

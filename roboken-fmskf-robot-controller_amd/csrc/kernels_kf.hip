@@ -414,12 +414,16 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 // Planes through buffer descriptors: a 32-bit lane offset per access and no 64-bit address
 // math.  SMALL: the 78 P planes fit one 4 GiB window (pitch < 6.8M), one descriptor per array
 // and a scalar plane offset; otherwise one descriptor per plane (n < 2^29 lanes of 8 bytes).
-template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool PRIO = false>
+// ENS: the record epilogue of fmskf_tick_ensemble; every lane then stays to the block
+// reduction (lanes past N tick instance N-1, a clamped index, and store nothing)
+template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool PRIO = false, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
   const uint64_t n = a.n, pp = a.pitch;
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i0 < n;
+  if (!ENS && !live) return;
+  const uint64_t i = live ? i0 : n - 1;
   double x[N], P[NP];
   const auto rx = rsrc(a.x, pp * 8 * N), rp = rsrc(a.P, pp * 8 * NP);
   const uint32_t vo = (uint32_t)i * 8u;
@@ -440,10 +444,11 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
                                             vo, 0, 0);
     }
   };
-  // tiled layout (FMSKF_TILED): the block's tile through a scalar descriptor (lanes past N
-  // returned above, so a lane's slot is its thread index)
-  const TileRows<double, N, CP> tx(a.x, threadIdx.x);
-  const TileRows<double, NP, CP> tp(a.P, threadIdx.x);
+  // tiled layout (FMSKF_TILED): the block's tile through a scalar descriptor (without ENS
+  // lanes past N returned above, so a lane's slot is its thread index)
+  const uint32_t slot = ENS ? tile_slot(n) : threadIdx.x;
+  const TileRows<double, N, CP> tx(a.x, slot);
+  const TileRows<double, NP, CP> tp(a.P, slot);
   if (PRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
@@ -473,17 +478,26 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
     }
   }
   asm volatile("" : "+s"(ps));  // the store offsets are recomputed here, not held from the loads
+  if (live) {
 #pragma unroll
-  for (int k = 0; k < N; k++) {
-    if constexpr (FMSKF_TILED) tx.st(k, x[k]);
-    else st(rx, a.x, k, x[k]);
-  }
+    for (int k = 0; k < N; k++) {
+      if constexpr (FMSKF_TILED) tx.st(k, x[k]);
+      else st(rx, a.x, k, x[k]);
+    }
 #pragma unroll
-  for (int k = 0; k < NP; k++) {
-    if constexpr (FMSKF_TILED) tp.st(k, P[k]);
-    else st(rp, a.P, k, P[k]);
+    for (int k = 0; k < NP; k++) {
+      if constexpr (FMSKF_TILED) tp.st(k, P[k]);
+      else st(rp, a.P, k, P[k]);
+    }
   }
-  nan_guard(x, P, a.counters);
+  nan_guard(x, P, a.counters, live);
+  if constexpr (ENS) {
+    double xs[1][N];
+#pragma unroll
+    for (int k = 0; k < N; k++) xs[0][k] = x[k];
+    const bool lv[1] = {live};
+    ens_epilogue<12, 1>(a.in, xs, lv);
+  }
 }
 
 // fused tick + record (fmskf_tick_ensemble): the default single-tick kernel with the record
@@ -584,11 +598,23 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
 }
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,
-                 hipStream_t st) {
+                 hipStream_t st, int *ens_nb) {
   KfArgs<MdKF12D, Kf12dParams> a{s.n, s.pitch, (double *)s.x, (double *)s.P, in, s.counters, p};
   const dim3 g = grid_for(s.n);
   const bool small = FMSKF_TILED || s.pitch * 8 * 78 < 0xFFFFFFFFull;  // tiled: any N
   const bool nt = FMSKF_TILED && state_nt(s.n * 90 * 8);
+  if (in.ens_blocks) {
+    // fused tick + record (fmskf_tick_ensemble): the default kernel (decorrelated update,
+    // tiled state) with the record epilogue; one record per tick block
+    if (!FMSKF_TILED || !p.decor || !ens_nb || !upd || !pred || in.n_ticks != 1) return (int)hipErrorInvalidValue;
+    const bool blk = kf12d_sequential(p.r);
+    if (blk && nt) k_kf12s<true, true, true, true, kStateNT, false, true><<<g, kBlock, 0, st>>>(a);
+    else if (blk) k_kf12s<true, true, true, true, 0, false, true><<<g, kBlock, 0, st>>>(a);
+    else if (nt) k_kf12s<false, true, true, true, kStateNT, false, true><<<g, kBlock, 0, st>>>(a);
+    else k_kf12s<false, true, true, true, 0, false, true><<<g, kBlock, 0, st>>>(a);
+    *ens_nb = (int)g.x;
+    return (int)hipGetLastError();
+  }
   if (p.decor) {
     const bool blk = kf12d_sequential(p.r);
     static const int var = [] {  // FMSKF_KF12D_VARIANT=1: raised-priority load phase

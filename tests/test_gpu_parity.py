@@ -601,7 +601,8 @@ def test_bad_inputs_rejected():
 # carries it, 6145 block records
 @pytest.mark.parametrize("model,n", [("kf6", 100003), ("kf6", 1), ("kf6", 70000), ("ekf9", 3000),
                                      ("kf6", 1 << 20), ("kf6", 3 * (1 << 20) + 5), ("ekf9", 1),
-                                     ("ekf9", 700), ("ekf9", 1 << 20), ("ekf9", 1300001)])
+                                     ("ekf9", 700), ("ekf9", 1 << 20), ("ekf9", 1300001),
+                                     ("kf12d", 1), ("kf12d", 3001), ("kf12d", 1 << 20), ("kf12d", 300001)])
 def test_tick_ensemble_fused(orc, model, n):
     """fmskf_tick_ensemble = fmskf_tick + the record of the post-tick state: state bit-exact
     vs a plain tick, record vs the oracle's two-pass moments of that state, and bitwise
@@ -611,9 +612,13 @@ def test_tick_ensemble_fused(orc, model, n):
     if model == "kf6":
         yaw, gz, rpm = tr.kf6_inputs()
         kw = lambda t: dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])  # noqa: E731
-    else:
+    elif model == "ekf9":
         raw = tr.ekf9_raw()
         kw = lambda t: dict(raw=raw[t])  # noqa: E731
+    else:  # KF12D: the decorrelated fp64 tick with the record epilogue (past the Infinity
+        # Cache at 2^20: the non-temporal instantiation)
+        z = np.ascontiguousarray(tr.kf12d_z())
+        kw = lambda t: dict(z=np.ascontiguousarray(z[t]))  # noqa: E731
     with Engine(model, n) as a, Engine(model, n) as b, Engine(model, n) as c:
         for t in range(T - 1):
             for e in (a, b, c):
