@@ -216,9 +216,10 @@ int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
 int fmskf_ensemble_record_len(fmskf_handle h, uint32_t *len);
 int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
 /* fmskf_tick, then this rank's record of the post-tick state (as fmskf_ensemble_partial) in
- * one call.  KF6: one tick kernel that also reduces the state it stores, from registers, to
- * per-block records (cross-lane swaps + DPP, no second pass over x), then the fold; the other
- * models tick, then run the stand-alone record.  Records of one state are bitwise identical
+ * one call.  KF6, EKF9 and KF12D (tiled state, positive-definite R): one tick kernel that also
+ * reduces the state it stores, from registers, to per-block records (cross-lane swaps + DPP,
+ * no second pass over x), then the fold; the RS model and the KF12D fallback updates tick,
+ * then run the stand-alone record.  Records of one state are bitwise identical
  * whichever call produced them only up to fp64 rounding (same shift, different summation
  * order); each call is bitwise reproducible. */
 int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out, uint32_t mem);
