@@ -174,6 +174,7 @@ struct fmskf_ctx {
         hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
         hip_check(hipFree(stage), "hipFree");
         stage = nullptr;
+        stage_bytes = 0;  // a failed hipMalloc below must not leave a stale capacity
       }
       hipError_t e = hipMalloc(&stage, bytes);
       if (e != hipSuccess) fail(FMSKF_ENOMEM, "staging hipMalloc failed");
@@ -188,6 +189,7 @@ struct fmskf_ctx {
         hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
         hip_check(hipFree(oscratch), "hipFree");
         oscratch = nullptr;
+        oscratch_bytes = 0;
       }
       hipError_t e = hipMalloc(&oscratch, bytes);
       if (e != hipSuccess) fail(FMSKF_ENOMEM, "output scratch hipMalloc failed");
