@@ -181,6 +181,19 @@ constexpr uint32_t kTile = kBlock;
 // tiled pattern at 2^22 EKF9 robots (tools/membench.hip: 352 -> 299 us), while it is slower
 // when the state fits the Infinity Cache.  FMSKF_STATE_NT=0|1 forces it off or on.
 constexpr int kStateNT = 2;
+// Cache policy of the state STORES.  Every state line is written once per tick and not read
+// again in the launch, so a store need not keep it in the XCD's L2: `sc1` (buffer aux bit 4)
+// writes it to the memory side and drops it from L2 (MI355X_MICROARCH.md, store flavours).
+// While the state lives in the Infinity Cache that measured 4% faster on the KF6 pattern at
+// 2^20 (tools/membench.hip pol: 39.25 -> 37.6 us); past it the stores follow the loads (nt).
+#ifndef FMSKF_ST_CACHED
+#define FMSKF_ST_CACHED 16
+#endif
+#ifndef FMSKF_ST_STREAM
+#define FMSKF_ST_STREAM 2
+#endif
+// the store policy that goes with a load policy CP (0: cache-resident state, kStateNT: streamed)
+constexpr int st_pol(int cp) { return cp == kStateNT ? FMSKF_ST_STREAM : FMSKF_ST_CACHED; }
 inline bool state_nt(uint64_t state_bytes) {
   static const int force = [] {
     const char *e = getenv("FMSKF_STATE_NT");

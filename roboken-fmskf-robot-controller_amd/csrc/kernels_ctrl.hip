@@ -148,7 +148,7 @@ struct Planes {
   __device__ __forceinline__ void st(int plane, uint32_t i, float v) const {
     if constexpr (SMALL)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u,
-                                            (uint32_t)(plane * pp * 4), CP);
+                                            (uint32_t)(plane * pp * 4), st_pol(CP));
     else
       base[plane * pp + i] = v;
   }

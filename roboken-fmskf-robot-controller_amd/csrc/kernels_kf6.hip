@@ -126,14 +126,14 @@ __device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t p
     const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
     const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_f32<O::CP>(rx, i * 4u, k * ps, x[k]);
+    for (int k = 0; k < 6; k++) st_f32<st_pol(O::CP)>(rx, i * 4u, k * ps, x[k]);
 #pragma unroll
-    for (int k = 0; k < 21; k++) st_f32<O::CP>(rp, i * 4u, k * ps, P[k]);
+    for (int k = 0; k < 21; k++) st_f32<st_pol(O::CP)>(rp, i * 4u, k * ps, P[k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_f32<O::CP>(rsrc(xg + k * pp, pp * 4), i * 4u, 0, x[k]);
+    for (int k = 0; k < 6; k++) st_f32<st_pol(O::CP)>(rsrc(xg + k * pp, pp * 4), i * 4u, 0, x[k]);
 #pragma unroll
-    for (int k = 0; k < 21; k++) st_f32<O::CP>(rsrc(Pg + k * pp, pp * 4), i * 4u, 0, P[k]);
+    for (int k = 0; k < 21; k++) st_f32<st_pol(O::CP)>(rsrc(Pg + k * pp, pp * 4), i * 4u, 0, P[k]);
   }
 }
 

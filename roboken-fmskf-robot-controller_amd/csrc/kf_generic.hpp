@@ -96,9 +96,9 @@ struct TileRows {
   }
   __device__ __forceinline__ void st(int k, T v) const {
     if constexpr (sizeof(T) == 8)
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * kTile * 8, CP);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * kTile * 8, st_pol(CP));
     else
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * kTile * 4, CP);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * kTile * 4, st_pol(CP));
   }
 };
 // the lane's slot in its block's tile; lanes past N take the last instance's slot

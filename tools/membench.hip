@@ -299,6 +299,29 @@ __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw
   for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
 }
 
+// the pitched KF6 pattern (27 state planes + a 16-byte record) through buffer descriptors with
+// explicit cache-policy bits on the state loads (LAUX) and stores (SAUX): gfx950 sc0 = 1,
+// nt = 2, sc1 = 16
+template <int LAUX, int SAUX>
+__global__ __launch_bounds__(256) void k_pitch_pol(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
+                                                   float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(st, 0, (int)(uint32_t)(pitch * 27 * 4), 0x00020000);
+  const uint32_t vo = (uint32_t)v * 4u, ps = (uint32_t)pitch * 4u;
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++)
+    s[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * ps, LAUX));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(raw) + v);
+  const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const float m = sink * (float)(q0 & q1 & q2 & q3 & 1);
+#pragma unroll
+  for (int k = 0; k < 27; k++)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * ps, SAUX);
+}
+
 // the pitched (planar) KF6 pattern with non-temporal state loads and stores and a 16-byte record
 template <int NS>
 __global__ __launch_bounds__(256) void k_pitch_nt(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
@@ -368,6 +391,51 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'p') {
+    // membench LG 1 pol: the KF6 pattern (pitched planes, a 64-tick ring of 16-byte records)
+    // under each load / store cache policy, at LG (2^20: the state resident in the Infinity Cache)
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t pitch = ((n + 511) / 512) * 512 + 256;
+    float *sb;
+    uint4 *ib;
+    const int ring = 64;
+    CK(hipMalloc(&sb, 27 * pitch * 4));
+    CK(hipMalloc(&ib, (size_t)ring * n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, 27 * pitch, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)ring * n * 4, 8);
+    CK(hipDeviceSynchronize());
+    const unsigned g = (unsigned)((n + 255) / 256);
+    int tick = 0;
+    auto tm = [&](const char *name, auto launch) {
+      for (int w = 0; w < 5; w++) launch(ib + (size_t)(tick++ % ring) * n);
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 100; it++) launch(ib + (size_t)(tick++ % ring) * n);
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 100;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n", (unsigned long long)n, name, us,
+             232.0 * n / (us * 1e-6) / 1e9);
+    };
+#define POL(L, S, NAME) tm(NAME, [&](const uint4 *in) { k_pitch_pol<L, S><<<g, 256>>>(sb, in, n, pitch, 0.f); })
+    for (int rep = 0; rep < 2; rep++) {
+      POL(0, 0, "ld_plain_st_plain");
+      POL(0, 2, "ld_plain_st_nt");
+      POL(0, 16, "ld_plain_st_sc1");
+      POL(0, 17, "ld_plain_st_sc0sc1");
+      POL(0, 1, "ld_plain_st_sc0");
+      POL(16, 0, "ld_sc1_st_plain");
+      POL(1, 0, "ld_sc0_st_plain");
+      POL(2, 0, "ld_nt_st_plain");
+      POL(16, 16, "ld_sc1_st_sc1");
+      POL(2, 2, "ld_nt_st_nt");
+    }
+#undef POL
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'c') {
     // membench LG 1 caps: the HBM-regime patterns (non-temporal state) under the occupancy cap
     // (dynamic LDS per block -> blocks per CU), tiled against planar; LG sizes the EKF9 case,
