@@ -150,7 +150,8 @@ def cfg4_shard(dev, stream, ticks: int, trig):
     """BASELINE.json configs[3] on one GPU: its 2^21-robot per-GPU shard of the 16M fleet, the
     tick alone, with the fused ensemble record (+ fold) every 16th tick and every tick (K = 16
     and K = 1, SURVEY.md 8(d) cfg 4); HIP events on the tick stream, no collective (that is the
-    N > 1 bench run's)."""
+    N > 1 bench run's).  Fed the SoA input planes: the record-fed kernel instantiation stays the
+    headline's alone, so a rocprofv3 --stats summary of the bench keeps its 2^20 average."""
     import torch
     import fmskf
     from fmskf.synth import SEED, kf6_ring_torch
@@ -158,9 +159,7 @@ def cfg4_shard(dev, stream, ticks: int, trig):
     e = fmskf.Engine("kf6", n, device=dev.index, trig=trig)
     e.set_stream(stream)
     yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 4, device=dev)
-    rec = fmskf.kf6_records(yaw, gz, rpm)
-    del yaw, gz, rpm
-    preps = [e.prepare(kf6_rec=rec[r]) for r in range(R)]
+    preps = [e.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
     out_rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
 
     def run(every):
@@ -170,7 +169,7 @@ def cfg4_shard(dev, stream, ticks: int, trig):
             else:
                 e.tick_prepared(preps[k % R])
 
-    res = {"instances": n, "ticks": ticks}
+    res = {"instances": n, "ticks": ticks, "inputs": "planes"}
     for label, every in (("tick_only", 0), ("ensemble_every_16", 16), ("ensemble_every_1", 1)):
         run(every)  # warm-up: every kernel of this sequence loaded
         torch.cuda.synchronize()
@@ -187,7 +186,7 @@ def cfg4_shard(dev, stream, ticks: int, trig):
                        "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": 232}
     res["ensemble_count"] = float(out_rec[0].item())
     e.close()
-    del preps, rec
+    del preps, yaw, gz, rpm
     torch.cuda.empty_cache()
     return res
 

@@ -43,7 +43,10 @@ if [ "${PROF_ALL:-0}" = 1 ]; then
               "wt901:--op wt901 --ticks 50" "can:--op can --ticks 100" "ensemble:--op ensemble --ticks 100" \
               "ens_ekf9:--op ensemble --model ekf9 --ticks 100" "ens_kf12d:--op ensemble --model kf12d --ticks 50" \
               "ens_ekf9_2p22:--op ensemble --model ekf9 --n 4194304 --ticks 50" "rs_2p24:--model rs --n 16777216 --ticks 20" \
-              "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000"; do
+              "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000" \
+              "tick_ens_kf6:--model kf6 --packed --op tick_ensemble --ticks 100" \
+              "tick_ens_ekf9:--model ekf9 --op tick_ensemble --ticks 100" \
+              "tick_ens_kf12d:--model kf12d --op tick_ensemble --ticks 30"; do
     name=${spec%%:*}; args=${spec#*:}
     run prof_$name 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
       python tools/kbench.py $args
