@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
 // M2 = S2 - S1 S1^T / c.  A row summed by several blocks gets bitwise the same total in each
 // (same per-thread order, same reduction tree), so the record is consistent.  LEN blocks in
 // parallel, each one load round trip at 2^20: the round-1 one-block fold was 4.2-10 us.
-template <int NX, int FT>
+template <int NX, int FT, int U>
 __global__ __launch_bounds__(FT) void k_ens_fold(const double *__restrict__ blocks, int nb,
                                                  const double *__restrict__ shift, double *out) {
   const int k = blockIdx.x;
@@ -104,27 +104,26 @@ __global__ __launch_bounds__(FT) void k_ens_fold(const double *__restrict__ bloc
   const double *r0 = blocks, *r1 = blocks + (uint64_t)ra * nb, *r2 = blocks + (uint64_t)rb * nb,
                *r3 = blocks + (uint64_t)k * nb;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
-  constexpr int U = 8;
-  int b = threadIdx.x;
-  for (; b + (U - 1) * FT < nb; b += U * FT) {
+  // U strides per row in flight per pass (the launcher sizes U to the record count, so one
+  // pass usually covers it), the ragged last pass predicated: one load round trip per pass;
+  // thread t adds blocks t, t + FT, ... in ascending order either way
+  for (int b = threadIdx.x; b < nb; b += U * FT) {
     double l[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      l[u][0] = r0[b + u * FT];
-      l[u][1] = r1[b + u * FT];
-      l[u][2] = r2[b + u * FT];
-      l[u][3] = r3[b + u * FT];
+      const bool in = b + u * FT < nb;
+      const int bi = in ? b + u * FT : b;
+      l[u][0] = r0[bi];
+      l[u][1] = r1[bi];
+      l[u][2] = r2[bi];
+      l[u][3] = r3[bi];
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
+      if (b + u * FT < nb) {
 #pragma unroll
-      for (int j = 0; j < 4; j++) v[j] = v[j] + l[u][j];
-  }
-  for (; b < nb; b += FT) {
-    v[0] = v[0] + r0[b];
-    v[1] = v[1] + r1[b];
-    v[2] = v[2] + r2[b];
-    v[3] = v[3] + r3[b];
+        for (int j = 0; j < 4; j++) v[j] = v[j] + l[u][j];
+      }
   }
   __shared__ double red[FT / 64 * 4];
   __shared__ double tot[4];
@@ -153,12 +152,21 @@ static int fold_threads() {
   }();
   return t;
 }
+template <int NX, int FT>
+static void fold_launch_ft(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
+  const int per = (nb + FT - 1) / FT;  // record loads per row per thread
+  const dim3 g(EnsRec<NX>::LEN);
+  if (per <= 1) k_ens_fold<NX, FT, 1><<<g, FT, 0, st>>>(blocks, nb, shift, out);
+  else if (per <= 2) k_ens_fold<NX, FT, 2><<<g, FT, 0, st>>>(blocks, nb, shift, out);
+  else if (per <= 4) k_ens_fold<NX, FT, 4><<<g, FT, 0, st>>>(blocks, nb, shift, out);
+  else k_ens_fold<NX, FT, 8><<<g, FT, 0, st>>>(blocks, nb, shift, out);
+}
 template <int NX>
 static void fold_launch(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
   const int ft = fold_threads();
-  if (ft == 1024) k_ens_fold<NX, 1024><<<EnsRec<NX>::LEN, 1024, 0, st>>>(blocks, nb, shift, out);
-  else if (ft == 512) k_ens_fold<NX, 512><<<EnsRec<NX>::LEN, 512, 0, st>>>(blocks, nb, shift, out);
-  else k_ens_fold<NX, 256><<<EnsRec<NX>::LEN, 256, 0, st>>>(blocks, nb, shift, out);
+  if (ft == 1024) fold_launch_ft<NX, 1024>(blocks, nb, shift, out, st);
+  else if (ft == 512) fold_launch_ft<NX, 512>(blocks, nb, shift, out, st);
+  else fold_launch_ft<NX, 256>(blocks, nb, shift, out, st);
 }
 
 // the shift vector: robot 0's state
