@@ -96,6 +96,16 @@ def secondary_configs(dev, stream, ticks: int, trig):
     import fmskf
     from fmskf.synth import SEED, kf6_ring_torch
     out = {}
+    # HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE, calibrated on same-width
+    # patterns (tools/pmc_traffic.py secondary; profiles/pmc_traffic_secondary.json)
+    sec_traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_secondary.json")
+    if os.path.exists(tpath):
+        try:
+            sec_traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
+                           if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
+        except Exception:
+            sec_traffic = {}
     specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 448), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504),
              ("cfg2_kf6_2p24", "kf6", 1 << 24, 232)]
     R = 4
@@ -141,7 +151,8 @@ def secondary_configs(dev, stream, ticks: int, trig):
         out[key] = {"model": model, "instances": n, "steps_per_s": n / (ms * 1e-3), "kernel_ms": ms,
                     "ticks": ticks, "nonfinite_instances": int(cnt[0]),
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                 "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": bps}}
+                                 "frac": gbps / HBM_PEAK_GBPS, "traffic": sec_traffic.get(key),
+                                 "bytes_per_step": bps}}
     out["cfg4_shard_kf6_2p21"] = cfg4_shard(dev, stream, max(ticks, 32), trig)
     return out
 

@@ -8,6 +8,7 @@ state planes read + written, yaw/gyro dword planes and the [N][4] int16 rpm plan
 give the correction factors, applied to the tick kernel's readings.
 
   python tools/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json] [records|planes]
+  python tools/pmc_traffic.py secondary gpurun_out [profiles/pmc_traffic_secondary.json]
 """
 import csv
 import glob
@@ -25,7 +26,59 @@ def read(dirname, kernel_substr):
     return vals
 
 
+# HBM-regime lines of the bench (secondary): the tick kernel and, for calibration, the
+# tools/membench.hip `caps` pattern with the same access widths and cache policy (non-temporal
+# state rows of 4 or 8 bytes per lane, a 16-byte record), at the same N.  Per config:
+# (bench key, kernel substring, pattern substring, pattern N, pattern read / write bytes per
+# robot, algorithmic read / write bytes per robot of the tick, N)
+SECONDARY = [
+    ("cfg3_ekf9_2p22", "k_ekf9t", "k_tiled_probe<54, 256, 2, float>", 1 << 22, 232, 216, 232, 216, 1 << 22),
+    ("cfg5_kf12d_2p20", "k_kf12s", "k_tiled_probe<90, 256, 2, double>", 1 << 20, 736, 720, 784, 720, 1 << 20),
+    ("cfg2_kf6_2p24", "k_kf6t", "k_pitch_nt<27>", 1 << 24, 124, 108, 124, 108, 1 << 24),
+]
+
+
+def read_grid(dirname, kernel_substr, grid):
+    vals = []
+    for f in glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel_substr in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def secondary(root, out):
+    """profiles/pmc_traffic_secondary.json: calibrated HBM bytes per launch of the cfg 3 / cfg 5 /
+    2^24 tick kernels (gpurun_out/pmc_sec_{kernel,pattern}_{FETCH,WRITE}_SIZE)."""
+    res = {"unit": "bytes per launch", "calibration": "tools/membench.hip caps patterns, same widths, same N"}
+    for key, ksub, psub, pn, prd, pwr, ard, awr, n in SECONDARY:
+        ent = {"n_instances": n, "kernel": ksub, "pattern": psub}
+        for c, pbytes, abytes in (("FETCH_SIZE", prd * pn, ard * n), ("WRITE_SIZE", pwr * pn, awr * n)):
+            pat = read_grid(os.path.join(root, f"pmc_sec_pattern_{c}"), psub, pn)
+            kf = read(os.path.join(root, f"pmc_sec_{key}_{c}"), ksub)
+            if not pat or not kf:
+                print(f"missing data for {key} {c}: pattern {len(pat)} kernel {len(kf)}")
+                return 1
+            pv = sorted(pat)[len(pat) // 2] * 1024.0
+            kv = sorted(kf)[len(kf) // 2] * 1024.0
+            factor = pbytes / pv
+            ent[c] = {"raw_kernel_bytes": kv, "raw_pattern_bytes": pv, "pattern_algorithmic_bytes": pbytes,
+                      "calibration_factor": factor, "kernel_bytes_calibrated": kv * factor}
+        ent["hbm_bytes_per_launch"] = ent["FETCH_SIZE"]["kernel_bytes_calibrated"] + \
+            ent["WRITE_SIZE"]["kernel_bytes_calibrated"]
+        ent["algorithmic_bytes_per_launch"] = (ard + awr) * n
+        ent["traffic_over_algorithmic"] = ent["hbm_bytes_per_launch"] / ent["algorithmic_bytes_per_launch"]
+        res[key] = ent
+    print(json.dumps(res, indent=1))
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+    return 0
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "secondary":
+        return secondary(sys.argv[2] if len(sys.argv) > 2 else "gpurun_out",
+                         sys.argv[3] if len(sys.argv) > 3 else None)
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     out = sys.argv[2] if len(sys.argv) > 2 else None
     n = 1 << 20

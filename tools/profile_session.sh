@@ -31,6 +31,20 @@ for c in FETCH_SIZE WRITE_SIZE; do
   run pmc_pat_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_pat_$c" -o run -- \
     build/membench 20
 done
+# the HBM-regime secondary lines (cfg 3, cfg 5, KF6 at 2^24): tick kernels and their
+# same-width calibration patterns, one counter per pass (PMC_SEC=1)
+if [ "${PMC_SEC:-0}" = 1 ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    run pmc_sec_pattern_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_sec_pattern_$c" -o run -- \
+      build/membench 22 1 caps
+    run pmc_sec_cfg3_ekf9_2p22_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_sec_cfg3_ekf9_2p22_$c" -o run -- \
+      python tools/kbench.py --model ekf9 --n 4194304 --ticks 8
+    run pmc_sec_cfg5_kf12d_2p20_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_sec_cfg5_kf12d_2p20_$c" -o run -- \
+      python tools/kbench.py --model kf12d --ticks 8
+    run pmc_sec_cfg2_kf6_2p24_$c 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_sec_cfg2_kf6_2p24_$c" -o run -- \
+      python tools/kbench.py --model kf6 --packed --n 16777216 --ticks 6
+  done
+fi
 echo "=== session done"
 # secondary rows: every tick model and the rows either side of the tick, one rocprofv3 kernel
 # trace each (PROF_ALL=1)
