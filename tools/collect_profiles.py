@@ -43,6 +43,21 @@ def main():
             shutil.copy(src, os.path.join(P, f"{tag}_pmc_{'kf6' if kind == 'kf6' else 'pattern'}_{c}.csv"))
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), G,
                     os.path.join(P, "pmc_traffic.json"), "records"], check=True, stdout=subprocess.DEVNULL)
+    # HBM-regime bench lines (profile_session.sh PMC_SEC=1): calibrated traffic + the counter rows
+    if glob.glob(os.path.join(G, "pmc_sec_*")):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "secondary", G,
+                        os.path.join(P, "pmc_traffic_secondary.json")], check=True, stdout=subprocess.DEVNULL)
+        for d in sorted(glob.glob(os.path.join(G, "pmc_sec_*"))):
+            f = os.path.join(d, "run_counter_collection.csv")
+            if not os.path.isdir(d) or not os.path.exists(f):
+                continue
+            rows_in = list(csv.reader(open(f)))
+            col = rows_in[0].index("Kernel_Name")
+            keep = [r for r in rows_in[1:] if any(k in r[col] for k in ("fmskf::", "k_tiled_probe", "k_pitch_nt"))]
+            with open(os.path.join(P, f"{tag}_{os.path.basename(d)}.csv"), "w", newline="") as fo:
+                w = csv.writer(fo)
+                w.writerow(rows_in[0])
+                w.writerows(keep)
     rows = []
     for d in sorted(glob.glob(os.path.join(G, "prof_*"))):
         if not os.path.isdir(d):
