@@ -299,6 +299,58 @@ __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw
   for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
 }
 
+// the same non-temporal tiled pattern with its compute phase, persistent: block b walks tiles
+// b, b + G, ... with two register sets, the next tile's loads issued before the current tile's
+// compute and stores (software pipelining across tiles; a wave's memory phases overlap its
+// own compute)
+template <int NS, int FMAS>
+__device__ __forceinline__ void tile_ld(const float *st, uint64_t t, float (&s)[NS], uint4 &r,
+                                        const uint4 *raw) {
+  const float *tile = st + t * ((uint64_t)NS * 256) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * 256);
+  r = raw[t * 256 + threadIdx.x];
+}
+template <int NS, int FMAS>
+__device__ __forceinline__ void tile_cs(float *st, uint64_t t, const float (&s)[NS], uint4 r, float sink) {
+  const float a = __builtin_bit_cast(float, r.x | 0x3F800000u) * sink;
+  float c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = s[j];
+#pragma unroll
+  for (int it = 0; it < FMAS / 8; it++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = __builtin_fmaf(c[j], a, s[(it * 8 + j) % NS]);
+  float m = c[0];
+#pragma unroll
+  for (int j = 1; j < 8; j++) m += c[j];
+  float *tile = st + t * ((uint64_t)NS * 256) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
+}
+template <int NS, int FMAS, bool PIPE>
+__global__ __launch_bounds__(256) void k_tiled_persist(float *st, const uint4 *raw, uint64_t n, float sink) {
+  const uint64_t ntiles = n / 256, G = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  float sa[NS], sb[NS];
+  uint4 ra, rb;
+  tile_ld<NS, FMAS>(st, t, sa, ra, raw);
+  for (;;) {
+    const uint64_t tb = t + G;
+    if (PIPE && tb < ntiles) tile_ld<NS, FMAS>(st, tb, sb, rb, raw);
+    tile_cs<NS, FMAS>(st, t, sa, ra, sink);
+    if (tb >= ntiles) break;
+    if (!PIPE) tile_ld<NS, FMAS>(st, tb, sb, rb, raw);
+    const uint64_t ta = tb + G;
+    if (PIPE && ta < ntiles) tile_ld<NS, FMAS>(st, ta, sa, ra, raw);
+    tile_cs<NS, FMAS>(st, tb, sb, rb, sink);
+    if (ta >= ntiles) break;
+    if (!PIPE) tile_ld<NS, FMAS>(st, ta, sa, ra, raw);
+    t = ta;
+  }
+}
+
 // the pitched KF6 pattern (27 state planes + a 16-byte record) through buffer descriptors with
 // explicit cache-policy bits on the state loads (LAUX) and stores (SAUX): gfx950 sc0 = 1,
 // nt = 2, sc1 = 16
@@ -391,6 +443,47 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'x') {
+    // membench LG 1 x: the EKF9-shaped tiled pattern (54 non-temporal rows, a compute phase of
+    // 864 FMAs) one tile per block against persistent blocks that pipeline tiles (PIPE) or not
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    float *sb;
+    uint4 *ib;
+    CK(hipMalloc(&sb, (size_t)54 * n * 4));
+    CK(hipMalloc(&ib, (size_t)n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)54 * n, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)n * 4, 8);
+    CK(hipDeviceSynchronize());
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    auto tm = [&](const char *name, int par, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"param\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)n, name, par, us, 448.0 * n / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)(n / 256);
+    for (int rep = 0; rep < 2; rep++) {
+      for (int kb : {0, 64})
+        tm("delay864_one_tile_per_block", kb, [&] {
+          k_tiled_delay<54, 864><<<g, 256, (size_t)kb * 1024>>>(sb, ib, n, 0.f);
+        });
+      for (int bpc : {1, 2, 3, 4}) {
+        const unsigned gp = (unsigned)(cus * bpc) < g ? (unsigned)(cus * bpc) : g;
+        tm("persist_pipe_blocks_per_cu", bpc, [&] { k_tiled_persist<54, 864, true><<<gp, 256>>>(sb, ib, n, 0.f); });
+        tm("persist_nopipe_blocks_per_cu", bpc, [&] { k_tiled_persist<54, 864, false><<<gp, 256>>>(sb, ib, n, 0.f); });
+      }
+    }
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'p') {
     // membench LG 1 pol: the KF6 pattern (pitched planes, a 64-tick ring of 16-byte records)
     // under each load / store cache policy, at LG (2^20: the state resident in the Infinity Cache)
