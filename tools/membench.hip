@@ -273,6 +273,32 @@ __global__ __launch_bounds__(256) void k_tiled_probe(TT *st, const uint4 *raw, u
 
 // the non-temporal tiled pattern with FMAS fp32 FMAs (8 independent chains over every loaded
 // row) between the loads and the stores: the tick kernels' compute phase without their math
+// the KF12D shape: NS non-temporal fp64 rows per robot, FMAS fp64 FMAs (8 chains) between
+// the loads and the stores, VG extra live doubles to hold the kernel's occupancy (2 waves/SIMD)
+template <int NS, int FMAS>
+__global__ __launch_bounds__(256) void k_tiled_delay64(double *st, const uint4 *raw, uint64_t n, double sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  double *tile = st + (v / 256) * ((uint64_t)NS * 256) + (v % 256);
+  const uint4 r = raw[v];
+  double s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * 256);
+  const double a = (double)(r.x & 0xFF) * sink + 1.0;
+  double c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = s[j];
+#pragma unroll
+  for (int it = 0; it < FMAS / 8; it++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = __builtin_fma(c[j], a, s[(it * 8 + j) % NS]);
+  double m = c[0];
+#pragma unroll
+  for (int j = 1; j < 8; j++) m += c[j];
+#pragma unroll
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
+}
+
 template <int NS, int FMAS>
 __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw, uint64_t n, float sink) {
   extern __shared__ double occ_cap[];
@@ -443,6 +469,44 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'd') {
+    // membench LG 1 d: the KF12D-shaped pattern (90 fp64 rows, non-temporal) with fp64 compute
+    // phases of increasing length, at 2 blocks per CU (the kernel's 2 waves per SIMD) and uncapped
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    double *sb;
+    uint4 *ib;
+    CK(hipMalloc(&sb, (size_t)90 * n * 8));
+    CK(hipMalloc(&ib, (size_t)n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)180 * n, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)n * 4, 8);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, int par, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"lds_KiB\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)n, name, par, us, 1504.0 * n / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)(n / 256);
+    for (int rep = 0; rep < 2; rep++)
+      for (int kb : {64, 0}) {
+        const size_t L = (size_t)kb * 1024;
+        tm("kf12d_nt_fma0", kb, [&] { k_tiled_delay64<90, 0><<<g, 256, L>>>(sb, ib, n, 0.0); });
+        tm("kf12d_nt_fma512", kb, [&] { k_tiled_delay64<90, 512><<<g, 256, L>>>(sb, ib, n, 0.0); });
+        tm("kf12d_nt_fma1024", kb, [&] { k_tiled_delay64<90, 1024><<<g, 256, L>>>(sb, ib, n, 0.0); });
+        tm("kf12d_nt_fma1280", kb, [&] { k_tiled_delay64<90, 1280><<<g, 256, L>>>(sb, ib, n, 0.0); });
+        tm("kf12d_nt_fma1536", kb, [&] { k_tiled_delay64<90, 1536><<<g, 256, L>>>(sb, ib, n, 0.0); });
+        tm("kf12d_nt_fma2048", kb, [&] { k_tiled_delay64<90, 2048><<<g, 256, L>>>(sb, ib, n, 0.0); });
+      }
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'x') {
     // membench LG 1 x: the EKF9-shaped tiled pattern (54 non-temporal rows, a compute phase of
     // 864 FMAs) one tile per block against persistent blocks that pipeline tiles (PIPE) or not
