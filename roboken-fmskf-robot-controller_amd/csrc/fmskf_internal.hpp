@@ -123,15 +123,8 @@ inline bool kf12d_sequential(const double *r36) {
 }
 
 // true when the EKF9 R (packed 6x6, as the kernels receive it) has no off-diagonal terms:
-// the canonical EKF9 update is then the sequential scalar one (oracle orc_ekf9_tick).
-// FMSKF_EKF9_SEQ=0 forces the joint update (timing A/B only: the result then leaves the
-// oracle's canonical order in the last bits).
+// the canonical EKF9 update is then the sequential scalar one (oracle orc_ekf9_tick)
 inline bool ekf9_r_diagonal(const float *r21) {
-  static const int force = [] {
-    const char *e = getenv("FMSKF_EKF9_SEQ");
-    return e ? atoi(e) : -1;
-  }();
-  if (force == 0) return false;
   for (int i = 1; i < 6; i++)
     for (int j = 0; j < i; j++)
       if (r21[i * (i + 1) / 2 + j] != 0.0f) return false;
