@@ -12,99 +12,14 @@
 // expression keeps the reference's operation order (library built with -ffp-contract=off), so
 // results are bit-identical to oracle/fmskf_oracle.c, itself pinned to the reference's own
 // FF_PI_D (tests/golden/ctrl_ref.npz).  HBM-bound: ~370 B per robot-tick, no reuse.
-#include "fmskf_device.hpp"
-#include "fmskf_internal.hpp"
+#include "ctrl_lane.hpp"
+#include "kf6_lane.hpp"
 #include "lane_rs.hpp"
 
 #pragma clang fp contract(off)
 
 namespace fmskf {
 
-namespace {
-
-enum { IV_TGT, IV_AMAX, IV_JP, IV_JM, IV_DT1, IV_DT2, IV_DT3, IV_VINI, IV_AINI, IV_DT, IV_V, IV_A };
-enum { PD_VAL, PD_INTEG, PD_LY, PD_LX, PD_TGT, PD_CTRL };
-
-struct Interp {
-  float f[kAxF];
-};
-
-// VelInterpConstJerk::set_target_params, util_vel_interp.hpp:55-104 (one active page:
-// the reference rewrites every field of the inactive page, then flips)
-__device__ __forceinline__ void interp_set(Interp &s, float v_t, float a_m, float jrk) {
-  float *f = s.f;
-  f[IV_TGT] = v_t;
-  f[IV_AMAX] = a_m;
-  f[IV_VINI] = f[IV_V];
-  f[IV_AINI] = f[IV_A];
-  if ((f[IV_TGT] - f[IV_VINI]) < 0) f[IV_AMAX] = -a_m;
-  f[IV_JM] = (f[IV_AMAX] >= 0) ? -jrk : jrk;
-  const float jm_inv = 1.0f / f[IV_JM];
-  f[IV_JP] = (f[IV_AMAX] - f[IV_AINI] >= 0) ? jrk : -jrk;
-  const float jp_inv = 1.0f / f[IV_JP];
-  f[IV_DT1] = (f[IV_AMAX] - f[IV_AINI]) * jp_inv;
-  f[IV_DT3] = f[IV_AMAX] * (-jm_inv);
-  f[IV_DT2] = 1.0f / f[IV_AMAX] *
-              (f[IV_TGT] - f[IV_VINI] - f[IV_AINI] * f[IV_DT1] * 0.5f -
-               f[IV_AMAX] * (f[IV_DT1] + f[IV_DT3]) * 0.5f);
-  if (f[IV_DT2] < 0.0f) {
-    const float sq_in = (f[IV_AINI] * jp_inv) * (f[IV_AINI] * jp_inv) * 0.5f +
-                        (f[IV_TGT] - f[IV_VINI]) * jp_inv;
-    const float sq = sq_in >= 0.0f ? __builtin_sqrtf(sq_in) : 0.0f;  // arm_sqrt_f32
-    f[IV_DT1] = sq - f[IV_AINI] * jp_inv;
-    f[IV_AMAX] = f[IV_AINI] + f[IV_JP] * f[IV_DT1];
-    f[IV_DT2] = 0.0f;
-    f[IV_DT3] = f[IV_AMAX] * (-jm_inv);
-  }
-  f[IV_DT1] = (f[IV_DT1] < 0.0f) ? 0.0f : f[IV_DT1];
-  f[IV_DT3] = (f[IV_DT3] < 0.0f) ? 0.0f : f[IV_DT3];
-  f[IV_DT] = 0.0f;
-}
-
-// VelInterpConstJerk::update, util_vel_interp.hpp:106-133
-__device__ __forceinline__ float interp_update(Interp &s, float ts) {
-  float *f = s.f;
-  if (f[IV_DT] <= f[IV_DT1] + ts) {
-    f[IV_A] = f[IV_AINI] + f[IV_JP] * f[IV_DT];
-    f[IV_V] = f[IV_VINI] + (f[IV_AINI] + f[IV_A]) * f[IV_DT] * 0.5f;
-    f[IV_DT] = f[IV_DT] + ts;
-  } else if (f[IV_DT] <= f[IV_DT1] + f[IV_DT2] + ts) {
-    f[IV_A] = f[IV_AMAX];
-    f[IV_V] = f[IV_V] + f[IV_A] * ts;
-    f[IV_DT] = f[IV_DT] + ts;
-  } else if (f[IV_DT] <= f[IV_DT1] + f[IV_DT2] + f[IV_DT3] + ts) {
-    f[IV_A] = f[IV_AMAX] + f[IV_JM] * (f[IV_DT] - f[IV_DT1] - f[IV_DT2]);
-    f[IV_V] = f[IV_V] + f[IV_A] * ts;
-    f[IV_DT] = f[IV_DT] + ts;
-  } else {
-    f[IV_A] = 0.0f;
-    f[IV_V] = f[IV_TGT];
-  }
-  return f[IV_V];
-}
-
-// ARM VCVT.S32.F32: truncate, saturate, NaN -> 0
-__device__ __forceinline__ int32_t f2i32_arm(float f) {
-  if (f != f) return 0;
-  if (f >= 2147483648.0f) return 2147483647;
-  if (f <= -2147483648.0f) return (int32_t)0x80000000u;
-  return (int32_t)f;
-}
-
-// set_CurrA_tgt -> set_rawCurr_tgt -> sat_curr (VD_motor_if_m2006.hpp:36-37,59-60)
-__device__ __forceinline__ int16_t curr_to_raw(float amp, int dir, int lim) {
-  const int16_t raw = (int16_t)(uint16_t)(uint32_t)f2i32_arm(amp * 1000.0f);
-  const int16_t t = (int16_t)(uint16_t)(uint32_t)((int)raw * dir);
-  return (t > lim) ? (int16_t)lim : ((t < -lim) ? (int16_t)-lim : t);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void *>(base), 0, (int)(uint32_t)(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes),
-      0x00020000);
-}
-
-}  // namespace
 
 // set_target_vel: VEHICLE_CTRL::set_target_vel (VD_vehicle_controller.cpp:100-104) per robot
 // with mask[i] != 0 (or all); vel/acl/jrk [3][N] (x mm/s, y mm/s, th rad/s)
@@ -127,134 +42,6 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_set_target(CtrlDev c, const flo
   }
 }
 
-// Plane access for the control state: SMALL (every array within a 4 GiB buffer window) uses
-// buffer descriptors with a 32-bit lane offset and a scalar per-plane offset; otherwise plain
-// 64-bit global addressing.
-template <bool SMALL, int CP = 0>
-struct Planes {
-  __amdgpu_buffer_rsrc_t r;
-  float *base;
-  uint64_t pp;
-  __device__ __forceinline__ Planes(float *b, uint64_t pitch, int nplanes) : base(b), pp(pitch) {
-    if constexpr (SMALL) r = rsrc(b, pitch * 4 * nplanes);
-  }
-  __device__ __forceinline__ float ld(int plane, uint32_t i) const {
-    if constexpr (SMALL)
-      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                           r, i * 4u, (uint32_t)(plane * pp * 4), CP));
-    else
-      return base[plane * pp + i];
-  }
-  __device__ __forceinline__ void st(int plane, uint32_t i, float v) const {
-    if constexpr (SMALL)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u,
-                                            (uint32_t)(plane * pp * 4), st_pol(CP));
-    else
-      base[plane * pp + i] = v;
-  }
-};
-
-// One robot's control step, split in its load phase (every load issued up front: vmcnt
-// retires in order) and its compute + store phase, so a fused kernel can issue the loads of
-// several steps before computing any of them.
-template <bool SMALL, int CP = 0>
-struct CtrlLane {
-  uint8_t on;
-  Interp ax[3];
-  float pv[4][4];
-
-  __device__ __forceinline__ void load(const CtrlDev &c, uint32_t i) {
-    const Planes<SMALL, CP> AX(c.ax, c.pitch, 3 * kAxF), PD(c.pid, c.pitch, 4 * kPidF);
-    on = c.power[i];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-      for (int k = 0; k < kAxF; k++) ax[a].f[k] = AX.ld(a * kAxF + k, i);
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-#pragma unroll
-      for (int k = 0; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
-  }
-
-  // rw: the four s16_rawSpeedRpm (FL, BL, BR, FR) packed in 8 bytes.  Returns the packed
-  // raw current targets (also stored to c.curr).
-  __device__ __forceinline__ uint2 step(const CtrlDev &c, const CtrlPrm &p, uint32_t i, uint2 rw) {
-    const uint64_t pp = c.pitch;
-    const Planes<SMALL, CP> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
-    float v[3];
-#pragma unroll
-    for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
-    // conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
-    float mt[4];
-    mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    const int16_t r[4] = {(int16_t)(rw.x & 0xFFFFu), (int16_t)(rw.x >> 16),
-                          (int16_t)(rw.y & 0xFFFFu), (int16_t)(rw.y >> 16)};
-    float po[4][kPidF];
-    int16_t cur[4];
-    if (on) {
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-        // FF_PI_D::update with now_tgt_ = Mvel_tgt * GEAR_RATIO, _nowval = Mvel * GEAR_RATIO
-        const float tgt = mt[w] * 36.0f;
-        const float val = rpm_to_mvel(r[w]) * 36.0f;
-        const float err = tgt - val;
-        const float lx = (val - pv[w][PD_VAL]) * p.freq;
-        const float ly = p.a1 * pv[w][PD_LY] + p.b0 * lx + p.b1 * pv[w][PD_LX];
-        float integ = pv[w][PD_INTEG] + p.i_gain * p.dt * err;
-        integ = (integ >= p.i_limit) ? p.i_limit : ((integ <= -p.i_limit) ? -p.i_limit : integ);
-        float ctrl = p.p_gain * err + integ - p.d_gain * ly;
-        float ff = tgt * p.ff_gain;
-        ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
-        ctrl = ctrl + ff;
-        po[w][PD_VAL] = val;
-        po[w][PD_INTEG] = integ;
-        po[w][PD_LY] = ly;
-        po[w][PD_LX] = lx;
-        po[w][PD_TGT] = tgt;
-        po[w][PD_CTRL] = ctrl;
-        cur[w] = curr_to_raw(ctrl, p.dir[w], p.curr_limit);
-      }
-    } else {
-#pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int k = 0; k < kAxF; k++) ax[a].f[k] = 0.0f;
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-#pragma unroll
-        for (int k = 0; k < kPidF; k++) po[w][k] = 0.0f;
-        cur[w] = curr_to_raw(0.0f, p.dir[w], p.curr_limit);
-      }
-    }
-    // the interpolator fields update() changes; after a reset (power off) all of them
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      AX.st(a * kAxF + IV_DT, i, ax[a].f[IV_DT]);
-      AX.st(a * kAxF + IV_V, i, ax[a].f[IV_V]);
-      AX.st(a * kAxF + IV_A, i, ax[a].f[IV_A]);
-    }
-    if (!on) {
-#pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int k = 0; k < IV_DT; k++) AX.st(a * kAxF + k, i, 0.0f);
-    }
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-#pragma unroll
-      for (int k = 0; k < kPidF; k++) PD.st(w * kPidF + k, i, po[w][k]);
-#pragma unroll
-    for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
-    const uint2 cw = make_uint2((uint32_t)(uint16_t)cur[0] | ((uint32_t)(uint16_t)cur[1] << 16),
-                                (uint32_t)(uint16_t)cur[2] | ((uint32_t)(uint16_t)cur[3] << 16));
-    reinterpret_cast<uint2 *>(c.curr)[i] = cw;
-    return cw;
-  }
-};
-
 // The per-tick control step.  rpm [N][4] int16 (MOTOR_IF_M2006::Status.s16_rawSpeedRpm).
 // rstride: robot i's four rpm at rpm + 4 * rstride * i (1: [N][4] planes; 2: the rpm field of
 // 16-byte fmskf_kf6_record's)
@@ -267,12 +54,6 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, cons
   CtrlLane<SMALL, CP> L;
   L.load(c, i);
   L.step(c, p, i, rw);
-}
-
-// C610 0x200 payload of one robot: bytes (hi, lo) per wheel -> swap the bytes of every 16-bit half
-__device__ __forceinline__ uint2 tx_frame(uint2 c) {
-  auto sw = [](uint32_t v) { return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu); };
-  return make_uint2(sw(c.x), sw(c.y));
 }
 
 // The firmware ISR in one pass (VDT::can_tx_routine_intr, VD_task_main.cpp:366-372), reference
