@@ -1536,6 +1536,15 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
   });
 }
 
+// FMSKF_ISR_FUSED=0: the KF6 ISR as three kernels (A/B, and the tests' cross-check)
+static bool isr_kf6_fused() {
+  static const bool v = [] {
+    const char *e = getenv("FMSKF_ISR_FUSED");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem) {
   return guarded([&] {
     check_handle(h);
@@ -1549,9 +1558,15 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
     uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)h->out_for(bytes);
     const CtrlPrm p = make_ctrl_prm(h);
     h->time_begin();
+    int fused = (int)hipErrorNotSupported;
+    if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused()) {
+      if (!t.rec && !t.rpm) ensure_motors(h);
+      fused = launch_isr_kf6(h->s, t, h->kf6, libm, h->ctrl, p, dst, h->stream);
+      if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
+    }
     if (h->cfg.model == FMSKF_MODEL_RS) {
       launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
-    } else {  // estimator tick, then the control step and the frame (three launches)
+    } else if (fused == (int)hipErrorNotSupported) {  // estimator tick, then the control step and the frame (three launches)
       int e = 0;
       switch (h->cfg.model) {
         case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream); break;

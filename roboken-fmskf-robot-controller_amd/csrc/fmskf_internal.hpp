@@ -251,6 +251,10 @@ int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl,
 int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
                      hipStream_t st);
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st);
+// the firmware ISR for the 6-state KF in one kernel (tick + control step + TX frame);
+// hipErrorNotSupported where the three-kernel path applies instead (streamed state, huge N)
+int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                   const CtrlPrm &p, uint8_t *frames, hipStream_t st);
 // the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
                   const CtrlPrm &p, uint8_t *frames, hipStream_t st);

@@ -102,6 +102,38 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   if (a.frames) reinterpret_cast<uint2 *>(a.frames)[i] = tx_frame(cw);
 }
 
+// The firmware ISR in one pass for the 6-state KF: the KF6 tick (correct with the IMU yaw /
+// gyro / wheel velocity, predict), then the control half of VEHICLE_CTRL::update on the same
+// rpm, then the 0x200 frame (NULL frames: none).  Lane functions shared with k_kf6t /
+// k_ctrl_step / k_can_tx (kf6_lane.hpp, ctrl_lane.hpp): bit-identical to fmskf_tick +
+// fmskf_control + fmskf_can_tx in sequence.  One robot per lane, the clamped-index form of
+// k_kf6t (lanes past N load instance N-1 and store nothing); every load of both steps is
+// issued before either computes.  CPC: the control planes' cache policy.
+template <class O, int CPC>
+__global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, CtrlDev c, CtrlPrm p,
+                                                   uint8_t *frames) {
+  const uint64_t n = a.n;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = i < (uint32_t)n;
+  const uint32_t ic = live ? i : (uint32_t)n - 1u;
+  float x[6], P[21];
+  __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
+  float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
+  WaveTable<O::LIBM> tv(a.in.sintab);
+  kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
+  const Kf6In m = kf6_load_in<O>(a.in, n, 0, ic);
+  CtrlLane<true, CPC> L;
+  L.load(c, ic);
+  tv.store(stab);
+  kf6_tick1<O>(m, stab, a.prm, x, P);
+  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  nan_guard(x, P, a.counters, live);
+  if (live) {
+    const uint2 cw = L.step(c, p, i, m.rpm);
+    if (frames) reinterpret_cast<uint2 *>(frames)[i] = tx_frame(cw);
+  }
+}
+
 // CAN_CTRL::tx_routine, VD_can_controller.hpp:43-55: frames [N][8], big-endian raw currents
 __global__ __launch_bounds__(kBlock) void k_can_tx(const int16_t *curr, uint64_t n, uint8_t *frames) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -202,6 +234,43 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
     else k_isr_rs<false, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
   }
   return (int)hipGetLastError();
+}
+
+// The fused KF6 ISR where it applies: one tick of the default single-tick form (state in one
+// 4 GiB window, cached, not the two-robot cache-resident kernel's layout question: one robot
+// per lane), the control planes in one window.  Returns hipErrorNotSupported otherwise (the
+// caller then runs the three kernels).  Past the Infinity Cache (KF6 state + control state
+// > 256 MiB) the control planes are non-temporal, as in k_isr_rs.
+template <bool LIBM, bool VALID, bool REC>
+static int isr_kf6_v(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
+                     bool nt, hipStream_t st) {
+  using O = Opt<LIBM, true, true, true, VALID, REC>;
+  if (nt) {
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
+    k_isr_kf6<O, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames);
+  } else {
+    k_isr_kf6<O, 0><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames);
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                   const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+  if (c.n == 0) return 0;
+  const bool small_state = s.pitch * 84 < 0xFFFFFFFFull;
+  const bool small_ctrl = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
+  // the tick kernel alone streams its state non-temporal past the cache: keep that regime on
+  // the three-kernel path (its own occupancy caps)
+  if (!small_state || !small_ctrl || state_nt(s.n * 108)) return (int)hipErrorNotSupported;
+  const KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, kp};
+  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * 108);
+  const bool valid = in.valid != nullptr, rec = in.rec != nullptr;
+  if (libm) {
+    if (valid) return rec ? isr_kf6_v<true, true, true>(a, c, p, frames, nt, st) : isr_kf6_v<true, true, false>(a, c, p, frames, nt, st);
+    return rec ? isr_kf6_v<true, false, true>(a, c, p, frames, nt, st) : isr_kf6_v<true, false, false>(a, c, p, frames, nt, st);
+  }
+  if (valid) return rec ? isr_kf6_v<false, true, true>(a, c, p, frames, nt, st) : isr_kf6_v<false, true, false>(a, c, p, frames, nt, st);
+  return rec ? isr_kf6_v<false, false, true>(a, c, p, frames, nt, st) : isr_kf6_v<false, false, false>(a, c, p, frames, nt, st);
 }
 
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {

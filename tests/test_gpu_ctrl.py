@@ -5,6 +5,7 @@ Bar: bit-exact (float results compared as bit patterns, integers exactly)."""
 import numpy as np
 import pytest
 
+import fmskf
 from fmskf import Engine
 from fmskf.synth import Trajectory
 
@@ -200,33 +201,41 @@ def test_reset_zeroes_control_state():
         assert not e.get_ctrl()["curr"].any()
 
 
+# KF6: one fused kernel (k_isr_kf6) for planes / records, TABLE512 / LIBM, with or without a
+# validity mask; at 2^20 + 17 the KF6 + control state outgrows the Infinity Cache and the
+# fused kernel's control planes go non-temporal
 @pytest.mark.parametrize("model,n,T", [("rs", 3001, 200), ("rs", 1, 30), ("kf6", 1000, 60),
-                                       ("kf6rec", 999, 40)])
+                                       ("kf6rec", 999, 40), ("kf6libm", 777, 30), ("kf6mask", 1001, 30),
+                                       ("kf6recmask", 1, 20), ("kf6rec", (1 << 20) + 17, 4)])
 def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
-    """fmskf_isr_tick (the firmware ISR in one call; one fused kernel for RS) leaves the
-    estimator state, the control state and the 0x200 frames bit-identical to fmskf_tick +
+    """fmskf_isr_tick (the firmware ISR in one call; one fused kernel for RS and KF6) leaves
+    the estimator state, the control state and the 0x200 frames bit-identical to fmskf_tick +
     fmskf_control + fmskf_can_tx, with random power and target events; RS also against the
-    oracle's pose and the oracle's control batch directly."""
+    oracle's pose, and both against the oracle's control batch directly."""
     rng = np.random.default_rng(99 + n)
     ev = _schedule(rng, n, T)
     tr = Trajectory(n, T, seed=31)
+    trig = fmskf.TRIG_LIBM if model.endswith("libm") else fmskf.TRIG_TABLE512
+    valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if model.endswith("mask") else None
+    vk = (lambda t: {}) if valid is None else (lambda t: dict(valid=valid[t]))  # noqa: E731
     if model == "rs":
         yaw, sums, rpm = tr.rs_inputs()
         kw = [dict(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t]) for t in range(T)]
-    elif model == "kf6":
+    elif not model.startswith("kf6rec"):
         yaw, gz, rpm = tr.kf6_inputs()
-        kw = [dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t]) for t in range(T)]
+        kw = [dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t], **vk(t)) for t in range(T)]
+        model = "kf6"
     else:  # KF6 fed 16-byte records: the control step reads the records' rpm field
         from fmskf import kf6_records
         yaw, gz, rpm = tr.kf6_inputs()
         rec = kf6_records(yaw, gz, rpm)
-        kw = [dict(kf6_rec=rec[t]) for t in range(T)]
+        kw = [dict(kf6_rec=rec[t], **vk(t)) for t in range(T)]
         model = "kf6"
     ref = orc.CtrlBatch(n)
     pos = np.zeros((3, n), np.float32)
     vel = np.zeros((3, n), np.float32)
     prev = np.zeros((4, n), np.int64)
-    with Engine(model, n) as a, Engine(model, n) as b:
+    with Engine(model, n, trig=trig) as a, Engine(model, n, trig=trig) as b:
         for t in range(T):
             for kind, pl in ev.get(t, []):
                 for e in (a, b):
