@@ -60,7 +60,9 @@ if [ "${PROF_ALL:-0}" = 1 ]; then
               "pipeline_graph_4096:--op pipeline_graph --n 4096 --ticks 1000" \
               "tick_ens_kf6:--model kf6 --packed --op tick_ensemble --ticks 100" \
               "tick_ens_ekf9:--model ekf9 --op tick_ensemble --ticks 100" \
-              "tick_ens_kf12d:--model kf12d --op tick_ensemble --ticks 30"; do
+              "tick_ens_kf12d:--model kf12d --op tick_ensemble --ticks 30" \
+              "isr_kf6:--model kf6 --packed --op isr --ticks 200" \
+              "isr_kf6_4096:--model kf6 --packed --op isr --n 4096 --ticks 1000"; do
     name=${spec%%:*}; args=${spec#*:}
     run prof_$name 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
       python tools/kbench.py $args
