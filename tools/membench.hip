@@ -589,6 +589,9 @@ int main(int argc, char **argv) {
       POL(2, 0, "ld_nt_st_plain");
       POL(16, 16, "ld_sc1_st_sc1");
       POL(2, 2, "ld_nt_st_nt");
+      POL(2, 16, "ld_nt_st_sc1");
+      POL(17, 16, "ld_sc0sc1_st_sc1");
+      POL(1, 16, "ld_sc0_st_sc1");
     }
 #undef POL
     return 0;
