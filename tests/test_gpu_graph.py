@@ -54,6 +54,52 @@ def test_graph_replay_matches_direct_calls():
         assert torch.equal(fa, fb)
 
 
+@pytest.mark.parametrize("n", [4099, 65536])
+def test_graph_isr_tick_kf6_fused(n):
+    """KF6 fmskf_isr_tick (the fused one-kernel ISR, k_isr_kf6) captured with device input
+    planes and a device frame buffer: each replay equals a direct isr_tick and the three-call
+    tick + control + can_tx sequence, state and frames bit for bit."""
+    import torch
+    T = 16
+    tr = Trajectory(n, T, seed=73)
+    yaw, gz, rpm = tr.kf6_inputs()
+    st = torch.cuda.Stream()
+    vel = np.zeros((3, n), np.float32)
+    vel[2] = 0.8
+    acl = np.full((3, n), 1000.0, np.float32)
+    jrk = np.full((3, n), 10000.0, np.float32)
+    with torch.cuda.stream(st), Engine("kf6", n) as a, Engine("kf6", n) as b, Engine("kf6", n) as c:
+        for e in (a, b, c):
+            e.set_stream(st)
+            e.set_power(None)
+            e.set_target_vel(vel, acl, jrk)
+        dy = torch.empty(n, dtype=torch.float32, device="cuda")
+        dg = torch.empty(n, dtype=torch.float32, device="cuda")
+        dr = torch.empty((n, 4), dtype=torch.int16, device="cuda")
+        fa, fb, fc = (torch.empty((n, 8), dtype=torch.uint8, device="cuda") for _ in range(3))
+        b.graph_begin()
+        b.isr_tick(out=fb, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+        b.graph_end()
+        for t in range(T):
+            dy.copy_(torch.from_numpy(yaw[t]))
+            dg.copy_(torch.from_numpy(gz[t]))
+            dr.copy_(torch.from_numpy(rpm[t]))
+            a.tick(yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+            a.control(dr)
+            a.can_tx(fa)
+            b.graph_launch(1)
+            c.isr_tick(out=fc, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+            st.synchronize()
+            assert torch.equal(fa, fb), f"tick {t}: graph frames"
+            assert torch.equal(fa, fc), f"tick {t}: direct isr frames"
+        xa, Pa = a.get_state()
+        for e in (b, c):
+            x, P = e.get_state()
+            np.testing.assert_array_equal(xa.view(np.uint32), x.view(np.uint32))
+            np.testing.assert_array_equal(Pa.view(np.uint32), P.view(np.uint32))
+            np.testing.assert_array_equal(a.get_ctrl()["curr"], e.get_ctrl()["curr"])
+
+
 def test_graph_errors():
     with Engine("kf6", 64) as e:
         with pytest.raises(fmskf.FmskfError):
