@@ -325,6 +325,37 @@ __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw
   for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
 }
 
+// the same pattern out of place: the tile is read from src and written to dst (a ping-pong
+// state pair), fp32 (EKF9 shape) or fp64 (KF12D shape)
+template <int NS, int FMAS, class T>
+__global__ __launch_bounds__(256) void k_tiled_oop(const T *src, T *dst, const uint4 *raw, uint64_t n, T sink) {
+  extern __shared__ double occ_cap[];
+  (void)occ_cap;
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  const uint64_t off = (v / 256) * ((uint64_t)NS * 256) + (v % 256);
+  const uint4 r = raw[v];
+  T s[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(src + off + k * 256);
+  const T a = (T)(r.x & 0xFF) * sink + (T)1;
+  T c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = s[j];
+#pragma unroll
+  for (int it = 0; it < FMAS / 8; it++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if constexpr (sizeof(T) == 4) c[j] = __builtin_fmaf(c[j], a, s[(it * 8 + j) % NS]);
+      else c[j] = __builtin_fma(c[j], a, s[(it * 8 + j) % NS]);
+    }
+  T m = c[0];
+#pragma unroll
+  for (int j = 1; j < 8; j++) m += c[j];
+#pragma unroll
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, dst + off + k * 256);
+}
+
 // the same non-temporal tiled pattern with its compute phase, persistent: block b walks tiles
 // b, b + G, ... with two register sets, the next tile's loads issued before the current tile's
 // compute and stores (software pipelining across tiles; a wave's memory phases overlap its
@@ -504,6 +535,57 @@ int main(int argc, char **argv) {
         tm("kf12d_nt_fma1280", kb, [&] { k_tiled_delay64<90, 1280><<<g, 256, L>>>(sb, ib, n, 0.0); });
         tm("kf12d_nt_fma1536", kb, [&] { k_tiled_delay64<90, 1536><<<g, 256, L>>>(sb, ib, n, 0.0); });
         tm("kf12d_nt_fma2048", kb, [&] { k_tiled_delay64<90, 2048><<<g, 256, L>>>(sb, ib, n, 0.0); });
+      }
+    return 0;
+  }
+  if (argc > 3 && argv[3][0] == 'o') {
+    // membench LG 1 oop: in-place read-modify-write of the tiled state against a ping-pong pair
+    // (read one buffer, write the other, swap per launch); EKF9 shape at LG, KF12D at LG - 2
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t nk = n >> 2;
+    float *sa, *sb;
+    uint4 *ib;
+    CK(hipMalloc(&sa, (size_t)54 * n * 4));
+    CK(hipMalloc(&sb, (size_t)54 * n * 4));
+    CK(hipMalloc(&ib, (size_t)n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sa, (uint64_t)54 * n, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)54 * n, 9);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)n * 4, 8);
+    CK(hipDeviceSynchronize());
+    int flip = 0;
+    auto tm = [&](const char *name, int kb, uint64_t nn, double bpi, auto launch) {
+      for (int w = 0; w < 4; w++) launch(flip++ & 1);
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch(flip++ & 1);
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"lds_KiB\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)nn, name, kb, us, bpi * nn / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)(n / 256), gk = (unsigned)(nk / 256);
+    double *da = (double *)sa, *db = (double *)sb;  // 90 doubles x n/4 fit 54 floats x n
+    for (int rep = 0; rep < 2; rep++)
+      for (int kb : {0, 64}) {
+        const size_t L = (size_t)kb * 1024;
+        tm("ekf9_inplace_fma0", kb, n, 448, [&](int) { k_tiled_oop<54, 0, float><<<g, 256, L>>>(sa, sa, ib, n, 0.f); });
+        tm("ekf9_pingpong_fma0", kb, n, 448, [&](int f) {
+          k_tiled_oop<54, 0, float><<<g, 256, L>>>(f ? sb : sa, f ? sa : sb, ib, n, 0.f);
+        });
+        tm("ekf9_inplace_fma864", kb, n, 448, [&](int) { k_tiled_oop<54, 864, float><<<g, 256, L>>>(sa, sa, ib, n, 0.f); });
+        tm("ekf9_pingpong_fma864", kb, n, 448, [&](int f) {
+          k_tiled_oop<54, 864, float><<<g, 256, L>>>(f ? sb : sa, f ? sa : sb, ib, n, 0.f);
+        });
+        tm("kf12d_inplace_fma1280", kb, nk, 1504, [&](int) {
+          k_tiled_oop<90, 1280, double><<<gk, 256, L>>>(da, da, ib, nk, 0.0);
+        });
+        tm("kf12d_pingpong_fma1280", kb, nk, 1504, [&](int f) {
+          k_tiled_oop<90, 1280, double><<<gk, 256, L>>>(f ? db : da, f ? da : db, ib, nk, 0.0);
+        });
       }
     return 0;
   }
