@@ -22,6 +22,8 @@ def last_json(path):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
+    if not tag.isidentifier():  # a round prefix such as r2, never an option
+        raise SystemExit(__doc__)
     json.dump(last_json(os.path.join(G, "bench.log")), open(os.path.join(P, f"{tag}_bench.json"), "w"), indent=1)
     json.dump(last_json(os.path.join(G, "prof.log")), open(os.path.join(P, f"{tag}_prof_bench_line.json"), "w"),
               indent=1)
