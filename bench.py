@@ -208,6 +208,9 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--n-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--n-total", type=int, default=0,
+                    help="strong scaling: this many robots over all ranks (contiguous shards, the "
+                         "remainder on the first ranks) instead of --n-per-gpu per rank")
     ap.add_argument("--ring", type=int, default=64)
     ap.add_argument("--ensemble-every", type=int, default=16)
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
@@ -283,7 +286,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return [float(v) for v in t.tolist()]
 
-    n = args.n_per_gpu
+    if args.n_total > 0:  # SURVEY 8(d) cfg 4 strong scaling: the same 2^24 total at every N
+        base, rem = divmod(args.n_total, world)
+        n = base + (1 if rank < rem else 0)
+        n_global = args.n_total
+    else:
+        n = args.n_per_gpu
+        n_global = n * world
     R = args.ring
     stream = torch.cuda.current_stream()
     trig = fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512
@@ -408,7 +417,7 @@ def main():
         elapsed, region_ms, tick_ms, planes_ms = max_over_ranks([elapsed, region_ms, tick_ms, planes_ms])
     kern_avg_ms = tick_ms / args.steps
 
-    total_steps = n * world * args.steps
+    total_steps = n_global * args.steps
     value = total_steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
@@ -437,7 +446,7 @@ def main():
         k1_el = tb - ta
         if distributed:
             k1_el = max_over_ranks([k1_el])[0]
-        k1 = {"steps_per_s": n * world * k1_steps / k1_el, "ms_per_step": k1_el * 1e3 / k1_steps,
+        k1 = {"steps_per_s": n_global * k1_steps / k1_el, "ms_per_step": k1_el * 1e3 / k1_steps,
               "ticks": k1_steps}
 
     # ensemble sanity (outside the timed region): fold the last gathered records in rank order
@@ -445,7 +454,7 @@ def main():
     ens = None
     if args.gather == "native" and native_stats[0] is not None:
         mean, cov = native_stats[0]
-        ens = {"count": float(n * world), "mean_theta": float(mean[2]), "var_vx": float(cov[9])}
+        ens = {"count": float(n_global), "mean_theta": float(mean[2]), "var_vx": float(cov[9])}
     elif last is not None:
         mean, cov = fmskf.ensemble_combine(6, last)
         ens = {"count": float(last[:, 0].sum()), "mean_theta": float(mean[2]),
@@ -517,17 +526,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.n_total > 0 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: WT901 yaw/gyro-z + 4 wheel rpm per robot (fmskf.synth), 64-tick HBM ring"
                 + (", one 16-byte fmskf_kf6_record per robot-tick" if krec is not None else ", SoA planes"),
         "config": {
-            "workload": "cfg2: 2^20 independent 6-state fp32 KF instances per GPU, fused "
-                        "correct+predict per tick (fmskf_tick; every ensemble_every-th tick "
+            "workload": ("cfg2: 2^20 independent 6-state fp32 KF instances per GPU" if args.n_total <= 0 else
+                         f"cfg4 strong scaling: {n_global} independent 6-state fp32 KF instances over "
+                         f"{world} GPU(s)") +
+                        ", fused correct+predict per tick (fmskf_tick; every ensemble_every-th tick "
                         "fmskf_tick_ensemble, which also writes the ensemble record)",
             "instances_per_gpu": n,
-            "global_instances": n * world,
+            "global_instances": n_global,
             "trig": args.trig,
             "inputs": args.inputs,
             "ensemble_every": args.ensemble_every,

@@ -86,26 +86,30 @@ def test_bench_distributed_path_world1(gather, ensemble):
     assert out["value"] > 1e9
 
 
-def test_bench_world2_rehearsal_same_gpu():
+@pytest.mark.parametrize("strong", [False, True])
+def test_bench_world2_rehearsal_same_gpu(strong):
     """bench.py's N > 1 code path with two ranks (torch.distributed.run, gloo, both ranks on the
     one GPU of the test box; RCCL refuses two ranks on one device): per-rank shards with their
     own seeds, fused records all-gathered every 8 ticks, max-over-ranks timing, the whole-job
     count, and every rank's gathered records folding to the statistics of the stand-alone
-    records."""
+    records.  strong: cfg 4's strong-scaling form (--n-total, an odd total split unevenly)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     n = 1 << 18
+    total = 2 * n + 3 if strong else 2 * n
+    size = ["--n-total", str(total)] if strong else ["--n-per-gpu", str(n)]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "32", "--warmup", "4", "--ensemble-every", "8", "--n-per-gpu", str(n),
+           "--steps", "32", "--warmup", "4", "--ensemble-every", "8", *size,
            "--no-cpu-baseline", "--no-fused", "--no-secondary", "--backend", "gloo", "--same-device",
            "--check-ensemble"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert out["n_gpus"] == 2 and out["config"]["global_instances"] == 2 * n
+    assert out["n_gpus"] == 2 and out["config"]["global_instances"] == total
+    assert out["scaling"] == ("strong" if strong else "weak")
     chk = out["ensemble_check"]
-    assert chk["count"] == 2 * n
+    assert chk["count"] == total
     assert chk["mean_max_rel"] < 1e-12, chk
     assert chk["cov_max_rel"] < 1e-9, chk
-    assert out["ensemble"]["count"] == 2 * n
+    assert out["ensemble"]["count"] == total
     assert out["nonfinite_instances"] == 0
