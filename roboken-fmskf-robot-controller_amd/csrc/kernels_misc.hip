@@ -40,14 +40,30 @@ int launch_trig(const float *x, float *sv, float *cv, uint64_t n, bool libm, con
 // ---------------------------------------------------------------------------
 // ensemble (ens_device.hpp: record layout, lane accumulation, block reduction)
 // ---------------------------------------------------------------------------
-// robots per thread per pass (loads of all of them issued before any accumulation) and the
-// block cap: 2^20 KF6 robots -> 1024 blocks of 4 robots per lane, one pass
+// robots per thread per pass (loads of all of them issued before any accumulation; at most 2
+// for the fp64 12-state x) and the block cap: 2^20 KF6 robots -> 1024 blocks of 4 robots per
+// lane, one pass
 template <int NX>
-constexpr int ens_r() { return NX >= 12 ? 2 : 4; }
+constexpr int ens_r() { return NX >= 12 ? 2 : 8; }
 constexpr int kEnsMaxBlocks = 2048;
 
+// robots per lane of the stand-alone partial: sizes the partial's grid, hence the block-record
+// count the fold reads.  FMSKF_ENS_R 2 | 4 | 8 forces it; by default 8 while n <= 2^21 (a
+// small grid: half the block records for the fold), else 4.  Measured (rocprof, one box):
+// KF6 2^20 partial + fold 6.35 + 4.42 us with 4 -> 5.86 + 2.77 with 8; EKF9 2^20 10.66 + 4.30
+// -> 9.71 + 4.47; at 2^22 8 is neutral (KF6 18.9 / 18.7) or slower (EKF9 27.6 -> 31.0)
+static int ens_rpl(uint64_t n) {
+  static const int forced = [] {
+    const char *e = getenv("FMSKF_ENS_R");
+    const int v = e ? atoi(e) : 0;
+    return v == 2 || v == 4 || v == 8 ? v : 0;
+  }();
+  if (forced) return forced;
+  return n <= (2ull << 20) ? 8 : 4;
+}
+
 int ensemble_nblocks(uint64_t n) {
-  const uint64_t per = (uint64_t)kBlock * 4;
+  const uint64_t per = (uint64_t)kBlock * ens_rpl(n);
   uint64_t b = (n + per - 1) / per;
   if (b > (uint64_t)kEnsMaxBlocks) b = kEnsMaxBlocks;
   if (b < 1) b = 1;
@@ -57,13 +73,12 @@ int ensemble_nblocks(uint64_t n) {
 // Partial: every block accumulates the shifted moment sums of its grid-stride robots and
 // writes its block record.  TILED (the EKF9 / KF12D state layout) is a compile-time choice:
 // st_at then divides by the constant kTile (shifts), not by a runtime value.
-template <int NX, typename T, bool TILED>
+template <int NX, typename T, bool TILED, int R>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
                                                         uint64_t pp, const double *__restrict__ shift,
                                                         double *blocks) {
   constexpr uint32_t tile = TILED ? kTile : 0;
   constexpr int LEN4 = EnsRec<NX>::LEN4;
-  constexpr int R = ens_r<NX>();
   double sh[NX], v[LEN4];
   ens_load_shift<NX>(shift, sh);
 #pragma unroll
@@ -180,8 +195,25 @@ template <int NX, typename T>
 static void ens_launch(const DevState &s, double *blocks, const double *shift, double *out,
                        hipStream_t st) {
   const int nb = ensemble_nblocks(s.n);
-  if (s.tile) k_ens_partial<NX, T, true><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
-  else k_ens_partial<NX, T, false><<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
+  const int r = ens_r<NX>() < ens_rpl(s.n) ? ens_r<NX>() : ens_rpl(s.n);
+  auto go = [&](auto tiled, auto rr) {
+    k_ens_partial<NX, T, decltype(tiled)::value, decltype(rr)::value>
+        <<<nb, kBlock, 0, st>>>((const T *)s.x, s.n, s.pitch, shift, blocks);
+  };
+  using TT = std::true_type;
+  using TF = std::false_type;
+  using R2 = std::integral_constant<int, 2>;
+  using R4 = std::integral_constant<int, 4>;
+  using R8 = std::integral_constant<int, 8>;
+  if (s.tile) {
+    if (r == 2) go(TT{}, R2{});
+    else if (r == 8) go(TT{}, R8{});
+    else go(TT{}, R4{});
+  } else {
+    if (r == 2) go(TF{}, R2{});
+    else if (r == 8) go(TF{}, R8{});
+    else go(TF{}, R4{});
+  }
   fold_launch<NX>(blocks, nb, shift, out, st);
 }
 
