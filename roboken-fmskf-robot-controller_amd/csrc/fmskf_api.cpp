@@ -92,6 +92,15 @@ struct fmskf_ctx {
   // staging for host-resident inputs
   void *stage = nullptr;
   size_t stage_bytes = 0;
+  // pinned host slots for small host-resident inputs and outputs: the planes of one call are
+  // packed into a slot by the CPU and cross PCIe as one DMA (instead of one pageable copy per
+  // plane); two input slots, each reused only after its event (the DMA that read it) completed
+  static constexpr size_t kPinned = (size_t)1 << 20;
+  void *pin_in[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  bool pin_open[2] = {false, false};
+  int pin_slot = 0;
+  void *pin_out = nullptr;
   // ensemble scratch: block records [LEN][blocks], the record, the shift vector (robot 0's
   // state when the first record after create / reset / set_state / load_state was asked for)
   double *ens_blocks = nullptr;
@@ -182,6 +191,35 @@ struct fmskf_ctx {
     }
     return stage;
   }
+  // the next pinned input slot.  The slot the previous staging call used gets its event now,
+  // behind everything that call queued (its DMA, or the kernels that read the slot in place);
+  // a slot is rewritten only once the event recorded after its last use has completed
+  char *pinned_in() {
+    const int prev = pin_slot ^ 1, slot = pin_slot;
+    if (pin_open[prev]) {
+      hip_check(hipEventRecord(pin_ev[prev], stream), "hipEventRecord");
+      pin_open[prev] = false;
+    }
+    pin_slot ^= 1;
+    if (!pin_in[slot]) {
+      hip_check(hipHostMalloc(&pin_in[slot], kPinned, hipHostMallocDefault), "hipHostMalloc");
+      hip_check(hipEventCreateWithFlags(&pin_ev[slot], hipEventDisableTiming), "hipEventCreate");
+    } else {
+      hip_check(hipEventSynchronize(pin_ev[slot]), "hipEventSynchronize");
+    }
+    pin_open[slot] = true;
+    return (char *)pin_in[slot];
+  }
+  char *pinned_out() {
+    if (!pin_out) hip_check(hipHostMalloc(&pin_out, kPinned, hipHostMallocDefault), "hipHostMalloc");
+    return (char *)pin_out;
+  }
+  // the device's address of a pinned host slot (kernels read / write it over PCIe)
+  static void *dev_ptr(void *host) {
+    void *d = nullptr;
+    hip_check(hipHostGetDevicePointer(&d, host, 0), "hipHostGetDevicePointer");
+    return d;
+  }
   void destroy_comm();
   void *out_for(size_t bytes) {
     if (bytes > oscratch_bytes) {
@@ -203,6 +241,11 @@ struct fmskf_ctx {
     for (void *p : allocs) (void)hipFree(p);
     if (stage) (void)hipFree(stage);
     if (oscratch) (void)hipFree(oscratch);
+    for (int k = 0; k < 2; k++) {
+      if (pin_in[k]) (void)hipHostFree(pin_in[k]);
+      if (pin_ev[k]) (void)hipEventDestroy(pin_ev[k]);
+    }
+    if (pin_out) (void)hipHostFree(pin_out);
     destroy_comm();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -216,6 +259,19 @@ namespace {
 
 void check_handle(fmskf_handle h) {
   if (!h) fail(FMSKF_EINVAL, "null handle");
+}
+
+// Small host-resident inputs / outputs (<= 1 MiB per call): FMSKF_PINNED_STAGE=0 copies every
+// host plane as its own pageable hipMemcpyAsync; 1 packs them into a pinned slot and moves it
+// with one DMA; 2 (zero-copy) lets the kernels read the packed inputs from, and write their
+// host-destined result into, the pinned slots over PCIe, with no DMA at all
+int pinned_stage() {
+  static const int v = [] {
+    const char *e = getenv("FMSKF_PINNED_STAGE");
+    const int m = e ? atoi(e) : 2;
+    return m >= 0 && m <= 2 ? m : 2;
+  }();
+  return v;
 }
 
 // Host->device staging of a set of planes; returns device pointers.
@@ -233,8 +289,21 @@ struct Stager {
     if (!host || items.empty()) return;
     size_t total = 0;
     for (auto &it : items) total += (it.second + 255) & ~size_t(255);
-    char *base = (char *)h->stage_for(total);
     size_t off = 0;
+    const int mode = pinned_stage();
+    if (total <= fmskf_ctx::kPinned && !h->capturing && mode) {  // pack into a pinned slot
+      char *pin = h->pinned_in();
+      char *base = mode == 2 ? (char *)fmskf_ctx::dev_ptr(pin) : (char *)h->stage_for(total);
+      for (auto &it : items) {
+        memcpy(pin + off, *it.first, it.second);
+        *it.first = base + off;
+        off += (it.second + 255) & ~size_t(255);
+      }
+      if (mode == 1)
+        hip_check(hipMemcpyAsync(base, pin, total, hipMemcpyHostToDevice, h->stream), "stage H2D");
+      return;
+    }
+    char *base = (char *)h->stage_for(total);
     for (auto &it : items) {
       hip_check(hipMemcpyAsync(base + off, *it.first, it.second, hipMemcpyHostToDevice, h->stream),
                 "stage H2D");
@@ -573,6 +642,32 @@ void copy_planes_in(fmskf_ctx *h, void *dst, const void *src, size_t row, size_t
 void finish_out(fmskf_ctx *h, uint32_t mem) {
   if (mem == FMSKF_MEM_HOST) hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
 }
+// where a kernel writes a result of `bytes` bound for the caller's host memory: the pinned
+// output slot itself under zero-copy staging, else device scratch
+void *host_result(fmskf_ctx *h, size_t bytes) {
+  if (bytes <= fmskf_ctx::kPinned && !h->capturing && pinned_stage() == 2)
+    return fmskf_ctx::dev_ptr(h->pinned_out());
+  return h->out_for(bytes);
+}
+// one device buffer to the caller's host (or device) buffer, complete on return: a small host
+// result goes through the pinned slot (written there by the kernel under zero-copy staging, or
+// one DMA), then a CPU copy
+void copy_out_sync(fmskf_ctx *h, void *dst, const void *src, size_t bytes, uint32_t mem) {
+  if (mem == FMSKF_MEM_HOST && h->pin_out && src == fmskf_ctx::dev_ptr(h->pin_out)) {
+    hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    memcpy(dst, h->pin_out, bytes);
+    return;
+  }
+  if (mem == FMSKF_MEM_HOST && bytes <= fmskf_ctx::kPinned && !h->capturing && pinned_stage()) {
+    char *pin = h->pinned_out();
+    hip_check(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    memcpy(dst, pin, bytes);
+    return;
+  }
+  if (mem == FMSKF_MEM_HOST) copy_out(h, dst, src, bytes, mem);
+  finish_out(h, mem);
+}
 
 }  // namespace
 
@@ -701,6 +796,10 @@ int fmskf_reset(fmskf_handle h) {
 int fmskf_set_stream(fmskf_handle h, void *stream) {
   return guarded([&] {
     check_handle(h);
+    // work queued on the old stream (staging buffers, pinned slots) completes before the new
+    // stream can reuse what it reads
+    if (h->stream != (hipStream_t)stream && !h->capturing)
+      hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
     h->stream = (hipStream_t)stream;
   });
 }
@@ -1529,10 +1628,9 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
     DeviceGuard g(h->cfg.device);
     ensure_ctrl(h);
     const size_t bytes = h->s.n * 8;
-    uint8_t *dst = mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)h->out_for(bytes);
+    uint8_t *dst = mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)host_result(h, bytes);
     launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
-    if (mem == FMSKF_MEM_HOST) copy_out(h, frames, dst, bytes, mem);
-    finish_out(h, mem);
+    copy_out_sync(h, frames, dst, bytes, mem);
   });
 }
 
@@ -1555,7 +1653,7 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
     TickIn t = resolve_inputs(h, in, true, true, 1, n);
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     const size_t bytes = n * 8;
-    uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)h->out_for(bytes);
+    uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)host_result(h, bytes);
     const CtrlPrm p = make_ctrl_prm(h);
     h->time_begin();
     int fused = (int)hipErrorNotSupported;
@@ -1580,8 +1678,7 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
       if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
     }
     h->time_end();
-    if (frames && mem == FMSKF_MEM_HOST) copy_out(h, frames, dst, bytes, mem);
-    if (frames) finish_out(h, mem);
+    if (frames) copy_out_sync(h, frames, dst, bytes, mem);
   });
 }
 
@@ -1619,12 +1716,11 @@ int fmskf_export_vehicle_info(fmskf_handle h, fmskf_vehicle_info *out, const uin
     sg.run();
     launch_check(launch_readout(h->s, h->readout, h->stream), "readout");
     const size_t bytes = n * sizeof(fmskf_vehicle_info);
-    void *dst = mem == FMSKF_MEM_DEVICE ? (void *)out : h->out_for(bytes);
+    void *dst = mem == FMSKF_MEM_DEVICE ? (void *)out : host_result(h, bytes);
     launch_check(launch_vehicle_info(h->s, h->readout, dst, (const uint8_t *)f, (const float *)c,
                                      (const uint32_t *)u, h->stream),
                  "vehicle_info launch");
-    if (mem == FMSKF_MEM_HOST) copy_out(h, out, dst, bytes, mem);
-    finish_out(h, mem);
+    copy_out_sync(h, out, dst, bytes, mem);
   });
 }
 

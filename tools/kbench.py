@@ -138,21 +138,31 @@ def main():
 
 
 def bench_host(args, e, n, yaw, gz, rpm):
-    """PCIe-inclusive rate: every tick's 16 B/robot of inputs start in host memory."""
+    """PCIe-inclusive rate: every tick's 16 B/robot of inputs start in host memory (--op isr:
+    the fused ISR, its 0x200 frames returned to host memory every tick)."""
+    import numpy as np
     import torch
     R = yaw.shape[0]
     pin = args.host == "pinned"
     hy, hg, hr = (t.cpu().pin_memory() if pin else t.cpu() for t in (yaw, gz, rpm))
     hy, hg, hr = (t.numpy() for t in (hy, hg, hr))
+    if args.op == "isr":  # the host-fed firmware ISR: inputs from host, 0x200 frames back to host
+        e.set_power(None)
+        vel = np.zeros((3, n), np.float32)
+        vel[0] = 150.0
+        e.set_target_vel(vel, np.full((3, n), 1000.0, np.float32), np.full((3, n), 10000.0, np.float32))
+        step = lambda k: e.isr_tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])  # noqa: E731
+    else:
+        step = lambda k: e.tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])  # noqa: E731
     for k in range(5):
-        e.tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])
+        step(k)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.ticks):
-        e.tick(yaw_deg=hy[k % R], gyro_z_dps=hg[k % R], rpm=hr[k % R])
+        step(k)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.ticks
-    print(json.dumps({"model": args.model, "n": n, "op": "tick", "host_inputs": args.host,
+    print(json.dumps({"model": args.model, "n": n, "op": args.op, "host_inputs": args.host,
                       "ms_per_tick": dt * 1e3, "steps_per_s": n / dt,
                       "pcie_GBps": 16 * n / dt / 1e9}), flush=True)
 
