@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
+    ap.add_argument("--valid", action="store_true", help="a validity mask per tick (9 in 10 robots valid)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -73,6 +74,12 @@ def main():
         z[:, 1] = -torch.deg2rad(gz.double())
         preps = [e.prepare(z=z[r]) for r in range(R)]
         many = dict(z=z)
+    if args.valid:  # every tick's prepared inputs carry a [N] u8 validity mask
+        vm = (torch.rand(R, n, device=dev) < 0.9).to(torch.uint8)
+        kws = [dict(kf6_rec=rec[r]) if args.model == "kf6" and args.packed else
+               dict(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) if args.model == "kf6" else
+               dict(raw=raw[r]) if args.model == "ekf9" else dict(z=z[r]) for r in range(R)]
+        preps = [e.prepare(valid=vm[r], **kws[r]) for r in range(R)]
     if args.host:
         return bench_host(args, e, n, yaw, gz, rpm)
     if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph"):
@@ -131,6 +138,7 @@ def main():
     x, P = e.get_state()
     ok = bool(np.isfinite(x).all() and (P is None or np.isfinite(P).all()))
     print(json.dumps({"model": args.model, "n": n, "variant": os.environ.get("FMSKF_KF6_VARIANT", "0"),
+                      "valid_mask": args.valid,
                       "op": args.op, "trig": args.trig, "many": args.many, "ms_per_tick": ms_tick,
                       "steps_per_s": n / (ms_tick * 1e-3),
                       "algo_GBps": BYTES[args.model] * n / (ms_tick * 1e-3) / 1e9, "finite": ok}),
