@@ -7,7 +7,8 @@
 //           updateData (:91-129).  Integer parts bit exact; the parser window (never
 //           more than 11 bytes in NORMAL mode) is held in two 64-bit registers and
 //           shifted, so no per-lane dynamic indexing (no scratch).
-//  k_can:   one wheel per lane (4 lanes per robot).  MOTOR_IF_M2006::rx_callback
+//  k_can4 / k_can: one robot per lane (every wheel present), or one wheel per lane (a
+//           `present` mask).  MOTOR_IF_M2006::rx_callback
 //           (VD_motor_if_m2006.cpp:32-72): big-endian decode, reversed motors, 13-bit
 //           angle unwrap into the int64 sum, and the speed path with Cortex-M7 integer
 //           semantics (wrapping MUL, SDIV x/0 = 0) and its IIR1 low-pass.
@@ -293,26 +294,27 @@ __device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
   return a / b;
 }
 
-__global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
-  const uint64_t n = a.n;
-  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // (instance, wheel)
-  if (g >= 4 * n) return;
-  const uint64_t i = g >> 2;
-  const int w = (int)(g & 3);
-  if (a.present && !((a.present[i] >> w) & 1)) return;
-  const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
-  const uint32_t b0 = f.x & 0xFF, b1 = (f.x >> 8) & 0xFF, b2 = (f.x >> 16) & 0xFF, b3 = f.x >> 24;
-  const uint32_t b4 = f.y & 0xFF, b5 = (f.y >> 8) & 0xFF;
-  const int16_t micro = a.stamps[g];
-  const int dir = a.dir[w];
-  const int16_t old_micro = a.micro[g], old_angle = a.angle[g];
-  uint32_t head = a.head[g] + 1u;
-  if (head >= 3u) head = 0;
-
+// one wheel's rx_callback on its 8-byte frame and microsecond stamp (VD_motor_if_m2006.cpp:
+// 32-72): the decoded fields, the ring-buffer head, the IIR1 speed state and the int64 sum
+struct CanWheel {
+  int16_t angle, rpm, curr;
+  uint32_t head;
+  float iir_y, iir_x, dlt;
+  int64_t sum;
+};
+__device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t micro, int dir,
+                                              int16_t old_micro, int16_t old_angle, uint32_t old_head,
+                                              float py, float pxv, int64_t sum) {
+  const uint32_t b0 = fx & 0xFF, b1 = (fx >> 8) & 0xFF, b2 = (fx >> 16) & 0xFF, b3 = fx >> 24;
+  const uint32_t b4 = fy & 0xFF, b5 = (fy >> 8) & 0xFF;
+  CanWheel o;
+  o.head = old_head + 1u;
+  if (o.head >= 3u) o.head = 0;
   const int16_t new_angle =
       dir == 1 ? s16_of(b0, b1) : (int16_t)(K::raw_per_rot - s16_of(b0, b1));
-  const int16_t new_rpm = (int16_t)(s16_of(b2, b3) * dir);
-  const int16_t new_curr = (int16_t)(s16_of(b4, b5) * dir);
+  o.angle = new_angle;
+  o.rpm = (int16_t)(s16_of(b2, b3) * dir);
+  o.curr = (int16_t)(s16_of(b4, b5) * dir);
 
   int32_t raw_ang_dlt = new_angle - old_angle;
   int32_t usec_dlt = micro - old_micro;
@@ -322,21 +324,101 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
   else if (usec_dlt < -0x7FFF) usec_dlt = usec_dlt + 0x7FFF;
   const int32_t num = mul_wrap(mul_wrap(raw_ang_dlt, 2), 3141593);
   const float x = (float)sdiv_arm(num, usec_dlt) / (float)K::raw_per_rot;
-  const uint64_t pw = (uint64_t)w * n + i;
-  const float py = a.iir_y[pw], pxv = a.iir_x[pw];
-  const float y = 0.8f * py + 0.1f * x + 0.1f * pxv;  // UTIL::IIR1::update, util_iir.hpp:39-45
-  a.iir_y[pw] = y;
-  a.iir_x[pw] = x;
-  a.speed[pw] = y;
-  a.dlt[pw] = (float)(new_angle - old_angle) * K::out_rad_per_raw * K::gear_ratio_inv;
+  o.iir_y = 0.8f * py + 0.1f * x + 0.1f * pxv;  // UTIL::IIR1::update, util_iir.hpp:39-45
+  o.iir_x = x;
+  o.dlt = (float)(new_angle - old_angle) * K::out_rad_per_raw * K::gear_ratio_inv;
   int16_t d = (int16_t)(new_angle - old_angle);
   d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
-  a.sum[pw] = a.sum[pw] + d;
-  a.micro[g] = micro;
-  a.angle[g] = new_angle;
-  a.rpm[g] = new_rpm;
-  a.curr[g] = new_curr;
-  a.head[g] = (uint8_t)head;
+  o.sum = sum + d;
+  return o;
+}
+
+// one wheel per lane: any `present` mask (absent wheels keep their state)
+__global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
+  const uint64_t n = a.n;
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // (instance, wheel)
+  if (g >= 4 * n) return;
+  const uint64_t i = g >> 2;
+  const int w = (int)(g & 3);
+  if (a.present && !((a.present[i] >> w) & 1)) return;
+  const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
+  const uint64_t pw = (uint64_t)w * n + i;
+  const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g], a.head[g],
+                               a.iir_y[pw], a.iir_x[pw], a.sum[pw]);
+  a.iir_y[pw] = o.iir_y;
+  a.iir_x[pw] = o.iir_x;
+  a.speed[pw] = o.iir_y;
+  a.dlt[pw] = o.dlt;
+  a.sum[pw] = o.sum;
+  a.micro[g] = a.stamps[g];
+  a.angle[g] = o.angle;
+  a.rpm[g] = o.rpm;
+  a.curr[g] = o.curr;
+  a.head[g] = (uint8_t)o.head;
+}
+
+// one robot per lane, every wheel present (no mask): the robot's 32 frame bytes, its four
+// stamps and its [N][4] int16 / u8 state in single 16-, 8- and 4-byte accesses, and each
+// [4][N] plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines)
+template <bool NT, class T>
+__device__ __forceinline__ T can_ld(const T *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, class T>
+__device__ __forceinline__ void can_st(T *p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+// NT: the motor state streams from HBM (past the Infinity Cache): non-temporal state accesses
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
+  extern __shared__ double occ_cap[];
+  (void)occ_cap;
+  const uint64_t n = a.n;
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4 f01 = reinterpret_cast<const uint4 *>(a.frames)[2 * i];
+  const uint4 f23 = reinterpret_cast<const uint4 *>(a.frames)[2 * i + 1];
+  const uint2 st = reinterpret_cast<const uint2 *>(a.stamps)[i];
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 omv = can_ld<NT>(reinterpret_cast<const u32x2 *>(a.micro) + i);
+  const u32x2 oav = can_ld<NT>(reinterpret_cast<const u32x2 *>(a.angle) + i);
+  const uint2 om = make_uint2(omv[0], omv[1]), oa = make_uint2(oav[0], oav[1]);
+  const uint32_t oh = can_ld<NT>(reinterpret_cast<const uint32_t *>(a.head) + i);
+  float py[4], px[4];
+  int64_t sm[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    py[w] = can_ld<NT>(a.iir_y + (uint64_t)w * n + i);
+    px[w] = can_ld<NT>(a.iir_x + (uint64_t)w * n + i);
+    sm[w] = can_ld<NT>(a.sum + (uint64_t)w * n + i);
+  }
+  const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
+  const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
+  uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0}, nh = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int sh = 16 * (w & 1);
+    const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
+                                 (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
+                                 (oh >> (8 * w)) & 0xFF, py[w], px[w], sm[w]);
+    const uint64_t pw = (uint64_t)w * n + i;
+    can_st<NT>(a.iir_y + pw, o.iir_y);
+    can_st<NT>(a.iir_x + pw, o.iir_x);
+    can_st<NT>(a.speed + pw, o.iir_y);
+    can_st<NT>(a.dlt + pw, o.dlt);
+    can_st<NT>(a.sum + pw, o.sum);
+    na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
+    nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
+    nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
+    nh |= o.head << (8 * w);
+  }
+  can_st<NT>(reinterpret_cast<u32x2 *>(a.micro) + i, u32x2{st.x, st.y});
+  can_st<NT>(reinterpret_cast<u32x2 *>(a.angle) + i, u32x2{na[0], na[1]});
+  can_st<NT>(reinterpret_cast<u32x2 *>(a.rpm) + i, u32x2{nr[0], nr[1]});
+  can_st<NT>(reinterpret_cast<u32x2 *>(a.curr) + i, u32x2{nc[0], nc[1]});
+  can_st<NT>(reinterpret_cast<uint32_t *>(a.head) + i, nh);
 }
 
 int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
@@ -357,8 +439,27 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.speed = s.m_speed;
   a.iir_y = s.m_iir_y;
   a.iir_x = s.m_iir_x;
-  const dim3 g((unsigned)((4 * s.n + kBlock - 1) / kBlock));
-  k_can<<<g, kBlock, 0, st>>>(a);
+  // every wheel present and the caller's frames / stamps aligned for the wide loads: one robot
+  // per lane (FMSKF_CAN_WHEEL=1 keeps the wheel-per-lane kernel, for A/B)
+  static const bool wheel = [] {
+    const char *e = getenv("FMSKF_CAN_WHEEL");
+    return e && atoi(e) != 0;
+  }();
+  if (!present && !wheel && ((uintptr_t)frames & 15) == 0 && ((uintptr_t)stamps & 7) == 0) {
+    const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
+    // 132 B of motor state per robot.  Non-temporal with 2 blocks per CU once it is well past
+    // the Infinity Cache; measured (kbench, two passes): 2^22 plain 191.6-192.8 us, nt
+    // 183.9-187.2, nt + 64 KiB cap 176.7-179.8; at 2^21 (277 MB) plain 83.3-85.1, nt 87.5-87.9
+    if (state_nt(s.n * 66)) {
+      const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
+      k_can4<true><<<g, kBlock, lds, st>>>(a);
+    } else {
+      k_can4<false><<<g, kBlock, 0, st>>>(a);
+    }
+  } else {
+    const dim3 g((unsigned)((4 * s.n + kBlock - 1) / kBlock));
+    k_can<<<g, kBlock, 0, st>>>(a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -413,12 +413,15 @@ import test_gpu_ctrl as T
 T.test_isr_tick_equals_tick_control_can_tx(orc, "rs", 3001, 60)
 T.test_isr_tick_equals_tick_control_can_tx(orc, "kf6rec", 999, 30)
 T.test_control_step_bitexact(orc, 3001, 100)
+import test_gpu_parity as P
+P.test_can_ingest_bitexact(orc, False, 777)
 print("nt ok")
 """
 
 
 def test_nontemporal_control_and_isr_bitexact():
-    """The non-temporal control-state instantiations of k_ctrl_step and k_isr_rs (chosen
+    """The non-temporal control-state instantiations of k_ctrl_step and k_isr_rs, and the
+    non-temporal motor-state CAN ingest k_can4<true> (chosen
     automatically once the state outgrows the Infinity Cache, fmskf_internal.hpp state_nt)
     forced on at small N in a child process: the ISR and control parity tests above, against
     the three-call sequence and the oracle."""

@@ -483,8 +483,9 @@ def test_wt901_ingest_random_streams(orc, stride):
 
 
 # ----------------------------------------------------------------------------- CAN ingest
-def test_can_ingest_bitexact(orc):
-    n, T = 1001, 25
+@pytest.mark.parametrize("masked", [True, False])  # wheel per lane (k_can) / robot per lane (k_can4)
+def test_can_ingest_bitexact(orc, masked, n=1001):
+    T = 25
     rng = np.random.default_rng(7)
     dirs = [1, 1, -1, -1]
     motors = [[orc.M2006(d) for d in dirs] for _ in range(n)]
@@ -495,8 +496,8 @@ def test_can_ingest_bitexact(orc):
             frames[rng.random((n, 4)) < 0.05, 0] |= 0x80  # some out-of-range / negative
             stamps = rng.integers(0, 0x8000, (n, 4)).astype(np.int16)
             stamps[rng.random((n, 4)) < 0.05] = 1234  # equal stamps -> usec_dlt == 0
-            present = rng.integers(0, 16, n).astype(np.uint8)
-            e.ingest_can(frames, stamps, present)
+            present = rng.integers(0, 16, n).astype(np.uint8) if masked else np.full(n, 15, np.uint8)
+            e.ingest_can(frames, stamps, present if masked else None)
             for i in range(n):
                 for w in range(4):
                     if (present[i] >> w) & 1:

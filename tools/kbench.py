@@ -259,7 +259,9 @@ def bench_io(args, e, n, R, dev, rpm, st):
         stp = [torch.from_numpy((np.arange(4)[None, :] * 250 + k * 1000 + np.zeros((n, 1))).astype(np.int16)).to(dev)
                for k in range(4)]
         run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
-        bpr = 4 * (8 + 2)
+        # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), head 1, IIR y / x (4 + 4) and
+        # the int64 sum read and written; speed, dlt (4 + 4), rpm, curr (2 + 2) written
+        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 4 + 4 + 2 + 2)
     for k in range(10):
         run(k)
     torch.cuda.synchronize()
