@@ -11,6 +11,7 @@
 // sums 32 B, yaw 4 B, rpm 8 B, vel 12 B w  -> 12*2 + 32*2 + 32 + 4 + 8 + 12 = 144 B.
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
+#include "kf_generic.hpp"
 #include "lane_rs.hpp"
 
 #pragma clang fp contract(off)
@@ -69,11 +70,19 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 // both robots (yaw, rpm, the four encoder sums: 44 B, fresh every tick) are loaded first, so
 // the second robot's arrive while the first one's state is read, stepped and written (the
 // input-latency hiding of the KF6 k_kf6p, kernels_kf6.hip).
-template <bool LIBM>
+// LTAB (TABLE512): the sine table as a wave-private LDS copy (its loads issued first, as in
+// the KF kernels) instead of gathers from the global table after the state arrives
+template <bool LIBM, bool LTAB = true>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
+  extern __shared__ double occ_cap[];
+  (void)occ_cap;
+  constexpr bool WT = !LIBM && LTAB;
+  __shared__ float wtab[WT ? kBlock / 64 : 1][WT ? kWaveTab : 1];
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t G = (uint64_t)gridDim.x * kBlock;
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  WaveTable<!WT> tv(a.in.sintab);
+  const float *tab = WT ? wtab[threadIdx.x >> 6] : a.in.sintab;
   float yaw[2];
   uint2 rw[2];
   int64_t sum[2][4];
@@ -85,6 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
 #pragma unroll
     for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * n + i];
   }
+  tv.store(wtab[WT ? threadIdx.x >> 6 : 0]);
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const uint64_t i = i0 + r * G;
@@ -95,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     s.th = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
-    rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], a.in.sintab);
+    rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], tab);
     a.x[i] = s.px;
     a.x[pp + i] = s.py;
     a.x[2 * pp + i] = s.th;
@@ -120,7 +130,12 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
     // past the Infinity Cache: 2 blocks per CU (64 KiB of dynamic LDS).  2^24, kbench, two
     // passes: 436.7-448.2 us uncapped, 429-430 at 48 KiB, 418.5-424.5 at 64 KiB
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_RS_LDS", state_nt(s.n * 124), 64u * 1024u);
+    static const bool gtab = [] {  // A/B switch (FMSKF_RS_GTAB=1: the global sine table)
+      const char *e = getenv("FMSKF_RS_GTAB");
+      return e && atoi(e) != 0;
+    }();
     if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
+    else if (gtab) k_rs2<false, false><<<g2, kBlock, lds, st>>>(a);
     else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
     return (int)hipGetLastError();
   }
