@@ -431,6 +431,43 @@ __global__ __launch_bounds__(256) void k_pitch_pol(float *st, const uint4 *raw, 
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * ps, SAUX);
 }
 
+// L2 pinning across launches: blocks b with b / 8 < pinb (the first pinb blocks of each XCD,
+// with blocks dealt round-robin to the 8 XCDs) load / store their state with policies PL / PS,
+// the others with SL / SS: can a state subset written back with plain stores stay in its
+// XCD's L2 for the next launch while the rest streams past it (nt = evict first)?
+template <int PL, int PS, int SL, int SS>
+__global__ __launch_bounds__(256) void k_pitch_pin(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
+                                                   float sink, uint32_t pinb) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(st, 0, (int)(uint32_t)(pitch * 27 * 4), 0x00020000);
+  const uint32_t vo = (uint32_t)v * 4u, ps = (uint32_t)pitch * 4u;
+  const bool pin = (blockIdx.x >> 3) < pinb;
+  float s[27];
+  if (pin) {
+#pragma unroll
+    for (int k = 0; k < 27; k++)
+      s[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * ps, PL));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 27; k++)
+      s[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * ps, SL));
+  }
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(raw) + v);
+  const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const float m = sink * (float)(q0 & q1 & q2 & q3 & 1);
+  if (pin) {
+#pragma unroll
+    for (int k = 0; k < 27; k++)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * ps, PS);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 27; k++)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * ps, SS);
+  }
+}
+
 // the pitched (planar) KF6 pattern with non-temporal state loads and stores and a 16-byte record
 template <int NS>
 __global__ __launch_bounds__(256) void k_pitch_nt(float *st, const uint4 *raw, uint64_t n, uint64_t pitch,
@@ -659,6 +696,19 @@ int main(int argc, char **argv) {
       printf("{\"n\": %llu, \"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n", (unsigned long long)n, name, us,
              232.0 * n / (us * 1e-6) / 1e9);
     };
+    if (argv[3][1] == 'i') {  // membench LG 1 pin: the L2-pinning sweep
+      for (int rep = 0; rep < 2; rep++)
+        for (unsigned pb : {0u, 32u, 64u, 96u, 128u}) {
+          char nm[96];
+          snprintf(nm, sizeof nm, "pin%u_plain_plain__stream_plain_sc1", pb);
+          tm(nm, [&](const uint4 *in) { k_pitch_pin<0, 0, 0, 16><<<g, 256>>>(sb, in, n, pitch, 0.f, pb); });
+          snprintf(nm, sizeof nm, "pin%u_plain_plain__stream_nt_sc1", pb);
+          tm(nm, [&](const uint4 *in) { k_pitch_pin<0, 0, 2, 16><<<g, 256>>>(sb, in, n, pitch, 0.f, pb); });
+          snprintf(nm, sizeof nm, "pin%u_plain_plain__stream_nt_nt", pb);
+          tm(nm, [&](const uint4 *in) { k_pitch_pin<0, 0, 2, 2><<<g, 256>>>(sb, in, n, pitch, 0.f, pb); });
+        }
+      return 0;
+    }
 #define POL(L, S, NAME) tm(NAME, [&](const uint4 *in) { k_pitch_pol<L, S><<<g, 256>>>(sb, in, n, pitch, 0.f); })
     for (int rep = 0; rep < 2; rep++) {
       POL(0, 0, "ld_plain_st_plain");
