@@ -735,8 +735,10 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.n = n;
       s.model = cfg->model;
       const uint32_t np = d.nx * (d.nx + 1) / 2;
-      s.pitch = plane_pitch(n);
-      s.tile = FMSKF_TILED && (cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D) ? kTile : 0;
+      s.tile = FMSKF_TILED && (cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D)
+                   ? tile_w_elem(d.elem) : 0;
+      // a tiled array's rows x pitch elements cover ceil(N / tile) whole tiles
+      s.pitch = s.tile ? std::max(plane_pitch(n), (n + s.tile - 1) / s.tile * s.tile) : plane_pitch(n);
       s.x = h->alloc<char>((size_t)d.nx * s.pitch * d.elem);
       s.P = d.m ? h->alloc<char>((size_t)np * s.pitch * d.elem) : nullptr;
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;

@@ -18,7 +18,8 @@ struct DevState {
   // large power of two (see plane_pitch): power-of-two plane strides alias in the
   // memory-side cache / channel hash and cost ~20% of bandwidth at N = 2^20 (membench).
   uint64_t pitch = 0;
-  // 0: x / P are planar [rows][pitch]; kTile: tiled [ceil(N/kTile)][rows][kTile] (EKF9, KF12D)
+  // 0: x / P are planar [rows][pitch]; else the tile width W: tiled [ceil(N/W)][rows][W]
+  // (EKF9, KF12D; tile_w)
   uint32_t tile = 0;
   uint32_t model = 0;
   // estimator state: x [nx][pitch], P [np][pitch] (element type float, or double for KF12D);
@@ -160,13 +161,20 @@ struct CtrlPrm {
 // 1 KiB (fp32) between planes
 inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; }
 
-// Tiled state layout ("AoSoA"): instance i's row k at ((i / kTile) * rows + k) * kTile + i % kTile.
-// One tile = one 256-thread block, so a block's (and a wave's) rows form one contiguous span
-// and the tile base is wave-uniform.  tools/membench.hip (random data): EKF9's 54 rows at 2^22
-// 374.6 -> 353.6 us, KF12D's 90 fp64 rows 313 -> 295 us at 2^20 and 1203 -> 1165 at 2^22; the
-// 27 KF6 rows gain nothing measurable (36.3 vs 36.0 at 2^20), so KF6 / RS stay planar.  The
-// allocation (rows x plane_pitch) always covers ceil(N / kTile) tiles.
-constexpr uint32_t kTile = kBlock;
+// Tiled state layout ("AoSoA"): instance i's row k at ((i / W) * rows + k) * W + i % W, W the
+// tile width.  Block b (kBlock instances, a "chunk") owns columns (b % (W / kBlock)) * kBlock...
+// of tile b / (W / kBlock): its rows are kBlock-element runs W elements apart, its base is
+// wave-uniform.  Consecutive blocks land on different XCDs, so a wide tile has the XCDs
+// reading and writing the same DRAM rows at the same time.  tools/membench.hip `tiles` (the
+// non-temporal EKF9 pattern at 2^22 with the tick's 864-FMA compute phase, 64 KiB cap):
+// W = 256 309-313 us, 512 290-291, 1024 282-284, 2048 279-281, 4096 282-284; KF12D's 90 fp64
+// rows at 2^20 with 1280 fp64 FMAs: 256 269-270, 1024 268-269, 2048 263-265, 4096 259-260.
+// (Against planar planes the 256-wide tile already measured 374.6 -> 353.6 us for EKF9; the 27
+// KF6 rows gain nothing from tiling, so KF6 / RS stay planar.)  The allocation (rows x pitch,
+// pitch >= N rounded up to W) always covers ceil(N / W) tiles.
+template <typename T>
+constexpr uint32_t tile_w() { return sizeof(T) == 8 ? 4096u : 2048u; }  // KF12D fp64 / EKF9 fp32
+inline uint32_t tile_w_elem(uint32_t elem) { return elem == 8 ? 4096u : 2048u; }
 
 // Cache policy of the per-tick state stream.  When the state is several times the 256 MiB
 // Infinity Cache, every state byte is read once and written once per tick from HBM; loading

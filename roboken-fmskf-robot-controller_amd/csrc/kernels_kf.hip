@@ -220,16 +220,16 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
   float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n;
-  const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
+  const uint32_t ntiles = (uint32_t)((n + kBlock - 1) / kBlock);  // chunks of kBlock instances
   const uint32_t ta = blockIdx.x, tb0 = blockIdx.x + gridDim.x;
   const bool has_b = tb0 < ntiles;  // block-uniform
   const uint32_t tb = has_b ? tb0 : ta;
   const uint32_t t = threadIdx.x;
   auto slot = [&](uint32_t tile) -> uint32_t {
-    const uint64_t b0 = (uint64_t)tile * kTile;
+    const uint64_t b0 = (uint64_t)tile * kBlock;
     return b0 + t < n ? t : (uint32_t)(n - 1 - b0);
   };
-  const uint64_t ia = (uint64_t)ta * kTile + t, ib = (uint64_t)tb * kTile + t;
+  const uint64_t ia = (uint64_t)ta * kBlock + t, ib = (uint64_t)tb * kBlock + t;
   const bool live_a = ia < n, live_b = has_b && ib < n;
   const uint64_t iac = live_a ? ia : n - 1, ibc = ib < n ? ib : n - 1;
   if (PRIO) __builtin_amdgcn_s_setprio(3);
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   double x[N], P[NP];
-  const uint32_t tl = FMSKF_TILED ? kTile : 0;
+  const uint32_t tl = FMSKF_TILED ? tile_w<double>() : 0;
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = a.x[st_at(tl, pp, N, k, i)];
 #pragma unroll
@@ -505,15 +505,18 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 template <bool LIBM, bool SEQ>
 static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, bool nt, hipStream_t st) {
   if (!LIBM && s.n * 216 <= (256ull << 20)) {
-    const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
+    const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const dim3 g2((ntiles + 1) / 2);
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
     if (nt) k_ekf9p<false, SEQ, kStateNT, false, true><<<g2, kBlock, lds, st>>>(a);
     else k_ekf9p<false, SEQ, 0, false, true><<<g2, kBlock, lds, st>>>(a);
     return (int)g2.x;
   }
+  // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
+  // wants one more block per CU than the plain tick: 2^22, kbench, two passes: 331-335 us at
+  // 64 KiB (2 blocks per CU), 307-308 at 32 KiB (3), 316 uncapped
   const dim3 g = grid_for(s.n);
-  const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
+  const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9E_LDS", nt, 32u * 1024u);
   if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
   else k_ekf9t<LIBM, true, true, SEQ, 0, false, true><<<g, kBlock, lds, st>>>(a);
   return (int)g.x;
@@ -543,7 +546,7 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
       if (nt) k_ekf9t<false, true, true, SEQ, kStateNT, true><<<g, kBlock, 0, st>>>(a);
       else k_ekf9t<false, true, true, SEQ, 0, true><<<g, kBlock, 0, st>>>(a);
     } else {
-      const uint32_t ntiles = (uint32_t)((s.n + kTile - 1) / kTile);
+      const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
       const dim3 g2((ntiles + 1) / 2);
       // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);

@@ -272,8 +272,11 @@ static int launch_ens_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     else k_kf6p<4, 2, E><<<g, kBlock, lds, st>>>(a);
     return (int)g;
   }
+  // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
+  // wants a smaller cap than the plain tick: 2^24, kbench, two passes: 738 us at 48 KiB,
+  // 665-670 at 32 KiB, 680-689 at 24 KiB, 722-724 uncapped (the plain tick: 619-628)
   const dim3 g = grid_for(a.n);
-  const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6_LDS", state_nt(a.n * 108), 48u * 1024u);
+  const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6E_LDS", state_nt(a.n * 108), 32u * 1024u);
   if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g, kBlock, lds, st>>>(a);
   else k_kf6t<4, E><<<g, kBlock, lds, st>>>(a);
   return (int)g.x;

@@ -72,12 +72,12 @@ int ensemble_nblocks(uint64_t n) {
 
 // Partial: every block accumulates the shifted moment sums of its grid-stride robots and
 // writes its block record.  TILED (the EKF9 / KF12D state layout) is a compile-time choice:
-// st_at then divides by the constant kTile (shifts), not by a runtime value.
+// st_at then divides by the constant tile width (shifts), not by a runtime value.
 template <int NX, typename T, bool TILED, int R>
 __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x, uint64_t n,
                                                         uint64_t pp, const double *__restrict__ shift,
                                                         double *blocks) {
-  constexpr uint32_t tile = TILED ? kTile : 0;
+  constexpr uint32_t tile = TILED ? tile_w<T>() : 0;
   constexpr int LEN4 = EnsRec<NX>::LEN4;
   double sh[NX], v[LEN4];
   ens_load_shift<NX>(shift, sh);
@@ -260,7 +260,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_tiled_fill(T *p, uint32_t rows, uint64_t total, RowBits b) {
   const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= total) return;
-  const uint32_t k = (uint32_t)((e / kTile) % rows);
+  const uint32_t k = (uint32_t)((e / tile_w<T>()) % rows);
   p[e] = __builtin_bit_cast(T, (typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type)b.v[k]);
 }
 template <typename T, bool TO_DENSE>
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_retile(const T *src, T *dst, uint32_
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // instance
   const uint32_t k = blockIdx.y;                                    // row
   if (i >= n) return;
-  const uint64_t t = st_at(kTile, 0, rows, k, i), d = (uint64_t)k * n + i;
+  const uint64_t t = st_at(tile_w<T>(), 0, rows, k, i), d = (uint64_t)k * n + i;
   if (TO_DENSE) dst[d] = src[t];
   else dst[t] = src[d];
 }
@@ -279,7 +279,7 @@ int launch_tiled_fill(void *base, uint32_t rows, uint64_t n, const uint64_t *bit
   if (rows > 90) return (int)hipErrorInvalidValue;
   RowBits b{};
   for (uint32_t k = 0; k < rows; k++) b.v[k] = bits[k];
-  const uint64_t total = (n + kTile - 1) / kTile * kTile * rows;
+  const uint64_t w = tile_w_elem(elem), total = (n + w - 1) / w * w * rows;
   const dim3 g((unsigned)((total + kBlock - 1) / kBlock));
   if (elem == 8) k_tiled_fill<double><<<g, kBlock, 0, st>>>((double *)base, rows, total, b);
   else k_tiled_fill<float><<<g, kBlock, 0, st>>>((float *)base, rows, total, b);
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_readout(const void *xv, uint64_t n, 
                                                     float *out) {
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i0 >= n) return;
-  // row k of this instance at [k * pp + i] (planar: pp = pitch, i = i0; tiled: pp = kTile)
+  // row k of this instance at [k * pp + i] (planar: pp = pitch, i = i0; tiled: pp = the tile width)
   constexpr uint32_t rows = MODEL == 2 ? 9 : MODEL == 3 ? 12 : 6;
   const uint64_t i = tile ? st_at(tile, 0, rows, 0, i0) : i0;
   const uint64_t pp = tile ? tile : pitch;

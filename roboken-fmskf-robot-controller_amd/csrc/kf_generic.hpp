@@ -73,37 +73,41 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 
-// One tiled state array (ROWS rows, fmskf_internal.hpp st_at) as the calling block sees it:
-// the block's tile base is wave-uniform (a scalar descriptor), rows sit kTile elements apart
-// (a scalar offset per row), the lane offset is t * sizeof(T) with t the lane's slot in the
-// tile (lanes past N pass the last instance's slot).  Any N: the descriptor spans one tile.
+// One tiled state array (ROWS rows, W = tile_w<T>() wide; fmskf_internal.hpp st_at) as one
+// chunk of kBlock instances sees it (by default the calling block's own chunk): the chunk's
+// base is wave-uniform (a scalar descriptor), rows sit W elements apart (a scalar offset per
+// row), the lane offset is t * sizeof(T) with t the lane's slot in the chunk (lanes past N pass
+// the last instance's slot).  Any N: the descriptor spans the chunk's columns of one tile.
 template <typename T, int ROWS, int CP = 0>
 struct TileRows {
+  static constexpr uint32_t W = tile_w<T>(), CPT = W / kBlock;
   __amdgpu_buffer_rsrc_t r;
   uint32_t vo;
+  static __device__ __forceinline__ T *chunk_base(T *base, uint32_t c) {
+    return base + (uint64_t)(c / CPT) * ((uint64_t)ROWS * W) + (uint64_t)(c % CPT) * kBlock;
+  }
+  static constexpr uint64_t kSpan = ((uint64_t)(ROWS - 1) * W + kBlock) * sizeof(T);
   __device__ __forceinline__ TileRows(T *base, uint32_t t)
-      : r(rsrc(base + (uint64_t)blockIdx.x * (ROWS * kTile), (uint64_t)ROWS * kTile * sizeof(T))),
-        vo(t * (uint32_t)sizeof(T)) {}
-  // tile `tile` (wave-uniform) instead of the block's own
-  __device__ __forceinline__ TileRows(T *base, uint32_t tile, uint32_t t, int)
-      : r(rsrc(base + (uint64_t)tile * (ROWS * kTile), (uint64_t)ROWS * kTile * sizeof(T))),
-        vo(t * (uint32_t)sizeof(T)) {}
+      : r(rsrc(chunk_base(base, blockIdx.x), kSpan)), vo(t * (uint32_t)sizeof(T)) {}
+  // chunk `chunk` (wave-uniform) instead of the block's own
+  __device__ __forceinline__ TileRows(T *base, uint32_t chunk, uint32_t t, int)
+      : r(rsrc(chunk_base(base, chunk), kSpan)), vo(t * (uint32_t)sizeof(T)) {}
   __device__ __forceinline__ T ld(int k) const {
     if constexpr (sizeof(T) == 8)
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, vo, k * kTile * 8, CP));
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, vo, k * W * 8, CP));
     else
-      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * kTile * 4, CP));
+      return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * W * 4, CP));
   }
   __device__ __forceinline__ void st(int k, T v) const {
     if constexpr (sizeof(T) == 8)
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * kTile * 8, st_pol(CP));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, v), r, vo, k * W * 8, st_pol(CP));
     else
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * kTile * 4, st_pol(CP));
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * W * 4, st_pol(CP));
   }
 };
-// the lane's slot in its block's tile; lanes past N take the last instance's slot
+// the lane's slot in its block's chunk; lanes past N take the last instance's slot
 __device__ __forceinline__ uint32_t tile_slot(uint64_t n) {
-  const uint64_t b0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock;
   return b0 + threadIdx.x < n ? threadIdx.x : (uint32_t)(n - 1 - b0);
 }
 

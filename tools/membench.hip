@@ -275,15 +275,15 @@ __global__ __launch_bounds__(256) void k_tiled_probe(TT *st, const uint4 *raw, u
 // row) between the loads and the stores: the tick kernels' compute phase without their math
 // the KF12D shape: NS non-temporal fp64 rows per robot, FMAS fp64 FMAs (8 chains) between
 // the loads and the stores, VG extra live doubles to hold the kernel's occupancy (2 waves/SIMD)
-template <int NS, int FMAS>
+template <int NS, int FMAS, int T = 256>
 __global__ __launch_bounds__(256) void k_tiled_delay64(double *st, const uint4 *raw, uint64_t n, double sink) {
   const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= n) return;
-  double *tile = st + (v / 256) * ((uint64_t)NS * 256) + (v % 256);
+  double *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
   const uint4 r = raw[v];
   double s[NS];
 #pragma unroll
-  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * 256);
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * T);
   const double a = (double)(r.x & 0xFF) * sink + 1.0;
   double c[8];
 #pragma unroll
@@ -296,20 +296,20 @@ __global__ __launch_bounds__(256) void k_tiled_delay64(double *st, const uint4 *
 #pragma unroll
   for (int j = 1; j < 8; j++) m += c[j];
 #pragma unroll
-  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * T);
 }
 
-template <int NS, int FMAS>
+template <int NS, int FMAS, int T = 256>
 __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw, uint64_t n, float sink) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
   const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= n) return;
-  float *tile = st + (v / 256) * ((uint64_t)NS * 256) + (v % 256);
+  float *tile = st + (v / T) * ((uint64_t)NS * T) + (v % T);
   const uint4 r = raw[v];
   float s[NS];
 #pragma unroll
-  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * 256);
+  for (int k = 0; k < NS; k++) s[k] = __builtin_nontemporal_load(tile + k * T);
   const float a = __builtin_bit_cast(float, r.x | 0x3F800000u) * sink;
   float c[8];
 #pragma unroll
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void k_tiled_delay(float *st, const uint4 *raw
 #pragma unroll
   for (int j = 1; j < 8; j++) m += c[j];
 #pragma unroll
-  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * 256);
+  for (int k = 0; k < NS; k++) __builtin_nontemporal_store(s[k] + m * sink, tile + k * T);
 }
 
 // the same pattern out of place: the tile is read from src and written to dst (a ping-pong
@@ -623,6 +623,59 @@ int main(int argc, char **argv) {
         tm("kf12d_pingpong_fma1280", kb, nk, 1504, [&](int f) {
           k_tiled_oop<90, 1280, double><<<gk, 256, L>>>(f ? db : da, f ? da : db, ib, nk, 0.0);
         });
+      }
+    return 0;
+  }
+  if (argc > 3 && argv[3][0] == 't') {
+    // membench LG 1 tiles: the EKF9 non-temporal pattern at LG (and KF12D's at LG - 2) with
+    // tile widths T = 64 ... 2048 robots (a tile is NS rows of T contiguous elements), at full
+    // occupancy and at the kernels' 64 KiB cap
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t nk = n >> 2;
+    float *sb;
+    uint4 *ib;
+    CK(hipMalloc(&sb, (size_t)54 * n * 4));
+    CK(hipMalloc(&ib, (size_t)n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)54 * n, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)n * 4, 8);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, int kb, uint64_t nn, double bpi, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 20; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 20;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"lds_KiB\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)nn, name, kb, us, bpi * nn / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)(n / 256), gk = (unsigned)(nk / 256);
+    double *db = (double *)sb;
+    for (int rep = 0; rep < 2; rep++)
+      for (int kb : {0, 64}) {
+        const size_t L = (size_t)kb * 1024;
+        tm("ekf9_t64", kb, n, 448, [&] { k_tiled_probe<54, 64, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t128", kb, n, 448, [&] { k_tiled_probe<54, 128, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t256", kb, n, 448, [&] { k_tiled_probe<54, 256, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t512", kb, n, 448, [&] { k_tiled_probe<54, 512, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t2048", kb, n, 448, [&] { k_tiled_probe<54, 2048, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf12d_t256_fma1280", kb, nk, 1504, [&] { k_tiled_delay64<90, 1280, 256><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("kf12d_t1024_fma1280", kb, nk, 1504, [&] { k_tiled_delay64<90, 1280, 1024><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("kf12d_t2048_fma1280", kb, nk, 1504, [&] { k_tiled_delay64<90, 1280, 2048><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("kf12d_t4096_fma1280", kb, nk, 1504, [&] { k_tiled_delay64<90, 1280, 4096><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("ekf9_t1024_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864, 1024><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t256_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864, 256><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t512_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864, 512><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t2048_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864, 2048><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t4096_fma864", kb, n, 448, [&] { k_tiled_delay<54, 864, 4096><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("ekf9_t4096", kb, n, 448, [&] { k_tiled_probe<54, 4096, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf12d_t64", kb, nk, 1504, [&] { k_tiled_probe<90, 64, 2, double><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("kf12d_t256", kb, nk, 1504, [&] { k_tiled_probe<90, 256, 2, double><<<gk, 256, L>>>(db, ib, nk, 0.0); });
+        tm("kf12d_t1024", kb, nk, 1504, [&] { k_tiled_probe<90, 1024, 2, double><<<gk, 256, L>>>(db, ib, nk, 0.0); });
       }
     return 0;
   }
