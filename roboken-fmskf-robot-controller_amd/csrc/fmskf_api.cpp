@@ -735,7 +735,8 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.n = n;
       s.model = cfg->model;
       const uint32_t np = d.nx * (d.nx + 1) / 2;
-      s.tile = FMSKF_TILED && (cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D)
+      s.tile = (FMSKF_TILED && (cfg->model == FMSKF_MODEL_EKF9 || cfg->model == FMSKF_MODEL_KF12D)) ||
+                       (FMSKF_KF6_TILED && cfg->model == FMSKF_MODEL_KF6)
                    ? tile_w_elem(d.elem) : 0;
       // a tiled array's rows x pitch elements cover ceil(N / tile) whole tiles
       s.pitch = s.tile ? std::max(plane_pitch(n), (n + s.tile - 1) / s.tile * s.tile) : plane_pitch(n);

@@ -219,6 +219,11 @@ inline bool state_nt(uint64_t state_bytes) {
 #ifndef FMSKF_TILED
 #define FMSKF_TILED 1
 #endif
+// the KF6 state tiled like EKF9's (2048 robots per tile row) instead of planar planes at the
+// padded pitch; 0 builds the planar layout (A/B)
+#ifndef FMSKF_KF6_TILED
+#define FMSKF_KF6_TILED 1
+#endif
 __host__ __device__ inline uint64_t st_at(uint32_t tile, uint64_t pitch, uint32_t rows, uint32_t k,
                                           uint64_t i) {
   return tile ? ((i / tile) * rows + k) * tile + i % tile : k * pitch + i;

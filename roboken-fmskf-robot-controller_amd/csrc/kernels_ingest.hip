@@ -333,11 +333,7 @@ __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t 
   return o;
 }
 
-// one wheel per lane: any `present` mask (absent wheels keep their state)
-__global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
-  const uint64_t n = a.n;
-  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;  // (instance, wheel)
-  if (g >= 4 * n) return;
+__device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t g) {
   const uint64_t i = g >> 2;
   const int w = (int)(g & 3);
   if (a.present && !((a.present[i] >> w) & 1)) return;
@@ -355,6 +351,15 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
   a.rpm[g] = o.rpm;
   a.curr[g] = o.curr;
   a.head[g] = (uint8_t)o.head;
+}
+
+// one wheel per lane: any `present` mask (absent wheels keep their state).  Grid-stride: 4 N
+// lanes reach 2^32 at the 2^30-robot cap, past one dispatch's 32-bit grid size
+__global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
+  const uint64_t n = a.n;
+  for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < 4 * n;
+       g += (uint64_t)gridDim.x * kBlock)  // (instance, wheel)
+    can_lane(a, n, g);
 }
 
 // one robot per lane, every wheel present (no mask): the robot's 32 frame bytes, its four
@@ -457,8 +462,8 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
       k_can4<false><<<g, kBlock, 0, st>>>(a);
     }
   } else {
-    const dim3 g((unsigned)((4 * s.n + kBlock - 1) / kBlock));
-    k_can<<<g, kBlock, 0, st>>>(a);
+    const uint64_t blocks = (4 * s.n + kBlock - 1) / kBlock;
+    k_can<<<dim3((unsigned)(blocks < (1u << 22) ? blocks : (1u << 22))), kBlock, 0, st>>>(a);
   }
   return (int)hipGetLastError();
 }

@@ -256,12 +256,15 @@ __global__ __launch_bounds__(kBlock) void k_fill64(uint64_t *p, uint64_t bits, u
 struct RowBits {
   uint64_t v[90];
 };
+// grid-stride: the span can exceed 2^32 elements (KF6 P at 2^28 robots: 5.6e9), more work-items
+// than one dispatch's 32-bit grid size holds
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_tiled_fill(T *p, uint32_t rows, uint64_t total, RowBits b) {
-  const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= total) return;
-  const uint32_t k = (uint32_t)((e / tile_w<T>()) % rows);
-  p[e] = __builtin_bit_cast(T, (typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type)b.v[k]);
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += stride) {
+    const uint32_t k = (uint32_t)((e / tile_w<T>()) % rows);
+    p[e] = __builtin_bit_cast(T, (typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type)b.v[k]);
+  }
 }
 template <typename T, bool TO_DENSE>
 __global__ __launch_bounds__(kBlock) void k_retile(const T *src, T *dst, uint32_t rows, uint64_t n) {
@@ -280,7 +283,8 @@ int launch_tiled_fill(void *base, uint32_t rows, uint64_t n, const uint64_t *bit
   RowBits b{};
   for (uint32_t k = 0; k < rows; k++) b.v[k] = bits[k];
   const uint64_t w = tile_w_elem(elem), total = (n + w - 1) / w * w * rows;
-  const dim3 g((unsigned)((total + kBlock - 1) / kBlock));
+  const uint64_t blocks = (total + kBlock - 1) / kBlock;
+  const dim3 g((unsigned)(blocks < (1u << 20) ? blocks : (1u << 20)));
   if (elem == 8) k_tiled_fill<double><<<g, kBlock, 0, st>>>((double *)base, rows, total, b);
   else k_tiled_fill<float><<<g, kBlock, 0, st>>>((float *)base, rows, total, b);
   return (int)hipGetLastError();

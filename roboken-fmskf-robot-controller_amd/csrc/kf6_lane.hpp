@@ -86,7 +86,19 @@ __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint6
 template <class O>
 __device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg, uint64_t pp,
                                                uint32_t i, float (&x)[6], float (&P)[21]) {
-  if constexpr (O::SMALL) {
+  if constexpr (FMSKF_KF6_TILED) {
+    // tiled state (fmskf_internal.hpp st_at, 2048 robots per tile row): the tile is
+    // wave-uniform (a wave's 64 robots, the clamped ones included, lie in one 256-robot chunk),
+    // so each array is one scalar descriptor over its tile and each row a scalar offset
+    constexpr uint32_t W = tile_w<float>();
+    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane(i / W);
+    const uint32_t c = (i - tl * W) * 4u;
+    const auto rx = rsrc(xg + (uint64_t)tl * (6 * W), 6 * W * 4), rp = rsrc(Pg + (uint64_t)tl * (21 * W), 21 * W * 4);
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] = ld_f32<O::CP>(rx, c, k * W * 4);
+#pragma unroll
+    for (int k = 0; k < 21; k++) P[k] = ld_f32<O::CP>(rp, c, k * W * 4);
+  } else if constexpr (O::SMALL) {
     const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
     const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll
@@ -104,7 +116,16 @@ __device__ __forceinline__ void kf6_load_state(const float *xg, const float *Pg,
 template <class O>
 __device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t pp, uint32_t i,
                                                 const float (&x)[6], const float (&P)[21]) {
-  if constexpr (O::SMALL) {
+  if constexpr (FMSKF_KF6_TILED) {
+    constexpr uint32_t W = tile_w<float>();
+    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane(i / W);
+    const uint32_t c = (i - tl * W) * 4u;
+    const auto rx = rsrc(xg + (uint64_t)tl * (6 * W), 6 * W * 4), rp = rsrc(Pg + (uint64_t)tl * (21 * W), 21 * W * 4);
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_f32<st_pol(O::CP)>(rx, c, k * W * 4, x[k]);
+#pragma unroll
+    for (int k = 0; k < 21; k++) st_f32<st_pol(O::CP)>(rp, c, k * W * 4, P[k]);
+  } else if constexpr (O::SMALL) {
     const auto rx = rsrc(xg, pp * 24), rp = rsrc(Pg, pp * 84);
     const uint32_t ps = (uint32_t)pp * 4u;
 #pragma unroll

@@ -431,6 +431,28 @@ __global__ __launch_bounds__(256) void k_pitch_pol(float *st, const uint4 *raw, 
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * ps, SAUX);
 }
 
+// the KF6 pattern over tiled state (27 rows of T robots per tile), policy bits as k_pitch_pol
+template <int T, int LAUX, int SAUX>
+__global__ __launch_bounds__(256) void k_tiled_pol(float *st, const uint4 *raw, uint64_t n, float sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  const uint64_t b = (uint64_t)blockIdx.x;
+  float *base = st + (b / (T / 256)) * (27ull * T) + (b % (T / 256)) * 256;
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(26u * T * 4 + 1024), 0x00020000);
+  const uint32_t vo = threadIdx.x * 4u;
+  float s[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++)
+    s[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, k * T * 4, LAUX));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(raw) + v);
+  const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const float m = sink * (float)(q0 & q1 & q2 & q3 & 1);
+#pragma unroll
+  for (int k = 0; k < 27; k++)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[k] + m), r, vo, k * T * 4, SAUX);
+}
+
 // L2 pinning across launches: blocks b with b / 8 < pinb (the first pinb blocks of each XCD,
 // with blocks dealt round-robin to the 8 XCDs) load / store their state with policies PL / PS,
 // the others with SL / SS: can a state subset written back with plain stores stay in its
@@ -626,6 +648,46 @@ int main(int argc, char **argv) {
       }
     return 0;
   }
+  if (argc > 3 && argv[3][0] == 'k') {
+    // membench LG 1 kf6tiles: the KF6 state (27 fp32 rows, non-temporal) at LG, planar planes at
+    // the engine's pitch against tiles of width T, with and without a 448-FMA compute phase
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t pitch = ((n + 511) / 512) * 512 + 256;
+    float *sb;
+    uint4 *ib;
+    CK(hipMalloc(&sb, (size_t)27 * (pitch > n + 4096 ? pitch : n + 4096) * 4));
+    CK(hipMalloc(&ib, (size_t)n * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)27 * n, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ib, (uint64_t)n * 4, 8);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, int kb, auto launch) {
+      for (int w = 0; w < 3; w++) launch();
+      CK(hipEventRecord(f0));
+      for (int it = 0; it < 10; it++) launch();
+      CK(hipEventRecord(f1));
+      CK(hipEventSynchronize(f1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, f0, f1));
+      const double us = ms * 1e3 / 10;
+      printf("{\"n\": %llu, \"kernel\": \"%s\", \"lds_KiB\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+             (unsigned long long)n, name, kb, us, 232.0 * n / (us * 1e-6) / 1e9);
+    };
+    const unsigned g = (unsigned)(n / 256);
+    for (int rep = 0; rep < 2; rep++)
+      for (int kb : {48, 0}) {
+        const size_t L = (size_t)kb * 1024;
+        tm("kf6_pitch_nt", kb, [&] { k_pitch_nt<27><<<g, 256, L>>>(sb, ib, n, pitch, 0.f); });
+        tm("kf6_t256_nt", kb, [&] { k_tiled_probe<27, 256, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf6_t2048_nt", kb, [&] { k_tiled_probe<27, 2048, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf6_t4096_nt", kb, [&] { k_tiled_probe<27, 4096, 2><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf6_t256_fma448", kb, [&] { k_tiled_delay<27, 448, 256><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf6_t2048_fma448", kb, [&] { k_tiled_delay<27, 448, 2048><<<g, 256, L>>>(sb, ib, n, 0.f); });
+        tm("kf6_t4096_fma448", kb, [&] { k_tiled_delay<27, 448, 4096><<<g, 256, L>>>(sb, ib, n, 0.f); });
+      }
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 't') {
     // membench LG 1 tiles: the EKF9 non-temporal pattern at LG (and KF12D's at LG - 2) with
     // tile widths T = 64 ... 2048 robots (a tile is NS rows of T contiguous elements), at full
@@ -749,6 +811,17 @@ int main(int argc, char **argv) {
       printf("{\"n\": %llu, \"kernel\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n", (unsigned long long)n, name, us,
              232.0 * n / (us * 1e-6) / 1e9);
     };
+    if (argv[3][1] == 'l') {  // membench LG 1 planes-vs-tiles: KF6 pattern, planar vs tiled
+      for (int rep = 0; rep < 2; rep++) {
+        tm("planar_ld_plain_st_sc1", [&](const uint4 *in) { k_pitch_pol<0, 16><<<g, 256>>>(sb, in, n, pitch, 0.f); });
+        tm("t256_ld_plain_st_sc1", [&](const uint4 *in) { k_tiled_pol<256, 0, 16><<<g, 256>>>(sb, in, n, 0.f); });
+        tm("t2048_ld_plain_st_sc1", [&](const uint4 *in) { k_tiled_pol<2048, 0, 16><<<g, 256>>>(sb, in, n, 0.f); });
+        tm("t4096_ld_plain_st_sc1", [&](const uint4 *in) { k_tiled_pol<4096, 0, 16><<<g, 256>>>(sb, in, n, 0.f); });
+        tm("planar_ld_nt_st_nt", [&](const uint4 *in) { k_pitch_pol<2, 2><<<g, 256>>>(sb, in, n, pitch, 0.f); });
+        tm("t2048_ld_nt_st_nt", [&](const uint4 *in) { k_tiled_pol<2048, 2, 2><<<g, 256>>>(sb, in, n, 0.f); });
+      }
+      return 0;
+    }
     if (argv[3][1] == 'i') {  // membench LG 1 pin: the L2-pinning sweep
       for (int rep = 0; rep < 2; rep++)
         for (unsigned pb : {0u, 32u, 64u, 96u, 128u}) {
