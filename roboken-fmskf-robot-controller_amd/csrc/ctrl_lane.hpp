@@ -88,27 +88,44 @@ __device__ __forceinline__ int16_t curr_to_raw(float amp, int dir, int lim) {
   return (t > lim) ? (int16_t)lim : ((t < -lim) ? (int16_t)-lim : t);
 }
 
-// Plane access for the control state: SMALL (every array within a 4 GiB buffer window) uses
-// buffer descriptors with a 32-bit lane offset and a scalar per-plane offset; otherwise plain
-// 64-bit global addressing.
+// Plane access for the control state.  Tiled (FMSKF_CTRL_TILED, the default): the interpolator
+// and FF_PI_D arrays are [N/W][planes][W] with W = tile_w<float>() (fmskf_internal.hpp st_at),
+// one scalar descriptor over robot i's tile (wave-uniform: a wave's robots lie in one
+// 256-robot chunk) and a scalar offset per plane.  Planar: SMALL (every array within a 4 GiB
+// buffer window) uses buffer descriptors with a 32-bit lane offset and a scalar per-plane
+// offset; otherwise plain 64-bit global addressing.
 template <bool SMALL, int CP = 0>
 struct Planes {
+  static constexpr uint32_t W = tile_w<float>();
   __amdgpu_buffer_rsrc_t r;
   float *base;
   uint64_t pp;
-  __device__ __forceinline__ Planes(float *b, uint64_t pitch, int nplanes) : base(b), pp(pitch) {
-    if constexpr (SMALL) r = rsrc(b, pitch * 4 * nplanes);
+  uint32_t vo;
+  __device__ __forceinline__ Planes(float *b, uint64_t pitch, int nplanes, uint32_t i)
+      : base(b), pp(pitch), vo(i * 4u) {
+    if constexpr (FMSKF_CTRL_TILED) {
+      const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane(i / W);
+      r = rsrc(b + (uint64_t)tl * nplanes * W, (uint64_t)nplanes * W * 4);
+      vo = (i - tl * W) * 4u;
+    } else if constexpr (SMALL) {
+      r = rsrc(b, pitch * 4 * nplanes);
+    }
   }
   __device__ __forceinline__ float ld(int plane, uint32_t i) const {
-    if constexpr (SMALL)
+    if constexpr (FMSKF_CTRL_TILED)
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, plane * W * 4, CP));
+    else if constexpr (SMALL)
       return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                           r, i * 4u, (uint32_t)(plane * pp * 4), CP));
+                                           r, vo, (uint32_t)(plane * pp * 4), CP));
     else
       return base[plane * pp + i];
   }
   __device__ __forceinline__ void st(int plane, uint32_t i, float v) const {
-    if constexpr (SMALL)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, i * 4u,
+    if constexpr (FMSKF_CTRL_TILED)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, plane * W * 4,
+                                            st_pol(CP));
+    else if constexpr (SMALL)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo,
                                             (uint32_t)(plane * pp * 4), st_pol(CP));
     else
       base[plane * pp + i] = v;
@@ -125,7 +142,7 @@ struct CtrlLane {
   float pv[4][4];
 
   __device__ __forceinline__ void load(const CtrlDev &c, uint32_t i) {
-    const Planes<SMALL, CP> AX(c.ax, c.pitch, 3 * kAxF), PD(c.pid, c.pitch, 4 * kPidF);
+    const Planes<SMALL, CP> AX(c.ax, c.pitch, 3 * kAxF, i), PD(c.pid, c.pitch, 4 * kPidF, i);
     on = c.power[i];
 #pragma unroll
     for (int a = 0; a < 3; a++)
@@ -141,7 +158,7 @@ struct CtrlLane {
   // raw current targets (also stored to c.curr).
   __device__ __forceinline__ uint2 step(const CtrlDev &c, const CtrlPrm &p, uint32_t i, uint2 rw) {
     const uint64_t pp = c.pitch;
-    const Planes<SMALL, CP> AX(c.ax, pp, 3 * kAxF), PD(c.pid, pp, 4 * kPidF);
+    const Planes<SMALL, CP> AX(c.ax, pp, 3 * kAxF, i), PD(c.pid, pp, 4 * kPidF, i);
     float v[3];
 #pragma unroll
     for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);

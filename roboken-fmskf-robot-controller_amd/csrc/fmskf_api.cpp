@@ -1529,7 +1529,9 @@ void ensure_ctrl(fmskf_ctx *h) {
   if (h->ctrl_ready) return;
   CtrlDev &c = h->ctrl;
   c.n = h->s.n;
-  c.pitch = h->s.pitch;
+  // tiled interpolator / FF_PI_D arrays cover ceil(N / W) whole tiles (ctrl_lane.hpp Planes)
+  const uint64_t w = tile_w_elem(4);
+  c.pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (c.n + w - 1) / w * w) : h->s.pitch;
   c.ax = h->alloc<float>((size_t)3 * kAxF * c.pitch);
   c.pid = h->alloc<float>((size_t)4 * kPidF * c.pitch);
   c.vel_tgt = h->alloc<float>((size_t)3 * c.pitch);
@@ -1696,8 +1698,16 @@ int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *whe
     copy_planes_out(h, vel_tgt, c.vel_tgt, row, pb, 3, mem);
     copy_out(h, curr_raw, c.curr, c.n * 8, mem);
     // wheel w's field k is plane w*kPidF + k: planes of one field are kPidF planes apart
-    copy_planes_out(h, wheel_tgt, c.pid + 4 * c.pitch, row, pb * kPidF, 4, mem);
-    copy_planes_out(h, wheel_ctrl, c.pid + 5 * c.pitch, row, pb * kPidF, 4, mem);
+    const float *pid = c.pid;
+    size_t ppb = pb;
+    if (FMSKF_CTRL_TILED && (wheel_tgt || wheel_ctrl)) {  // dense [4 * kPidF][N] copy first
+      float *dense = (float *)h->stage_for((size_t)4 * kPidF * row);
+      launch_check(launch_untile(c.pid, dense, 4 * kPidF, c.n, 4, h->stream), "untile pid");
+      pid = dense;
+      ppb = row;
+    }
+    copy_planes_out(h, wheel_tgt, pid + 4 * (ppb / 4), row, ppb * kPidF, 4, mem);
+    copy_planes_out(h, wheel_ctrl, pid + 5 * (ppb / 4), row, ppb * kPidF, 4, mem);
     finish_out(h, mem);
   });
 }

@@ -224,6 +224,11 @@ inline bool state_nt(uint64_t state_bytes) {
 #ifndef FMSKF_KF6_TILED
 #define FMSKF_KF6_TILED 1
 #endif
+// the control state's interpolator and FF_PI_D arrays tiled the same way (ctrl_lane.hpp
+// Planes); 0 builds them planar at the state pitch (A/B)
+#ifndef FMSKF_CTRL_TILED
+#define FMSKF_CTRL_TILED 1
+#endif
 __host__ __device__ inline uint64_t st_at(uint32_t tile, uint64_t pitch, uint32_t rows, uint32_t k,
                                           uint64_t i) {
   return tile ? ((i / tile) * rows + k) * tile + i % tile : k * pitch + i;

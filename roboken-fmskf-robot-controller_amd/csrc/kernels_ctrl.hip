@@ -33,12 +33,16 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_set_target(CtrlDev c, const flo
 #pragma unroll
   for (int a = 0; a < 3; a++) {
     Interp s;
-    float *base = c.ax + (uint64_t)a * kAxF * pp;
+    // plane a * kAxF + k of robot i (tiled or planar, ctrl_lane.hpp Planes)
+    auto at = [&](int k) -> uint64_t {
+      const uint32_t pl = (uint32_t)(a * kAxF + k);
+      return FMSKF_CTRL_TILED ? st_at(tile_w<float>(), 0, 3 * kAxF, pl, i) : pl * pp + i;
+    };
 #pragma unroll
-    for (int k = 0; k < kAxF; k++) s.f[k] = base[k * pp + i];
+    for (int k = 0; k < kAxF; k++) s.f[k] = c.ax[at(k)];
     interp_set(s, vel[a * n + i], acl[a * n + i], jrk[a * n + i]);
 #pragma unroll
-    for (int k = 0; k < kAxF; k++) base[k * pp + i] = s.f[k];
+    for (int k = 0; k < kAxF; k++) c.ax[at(k)] = s.f[k];
   }
 }
 
