@@ -413,7 +413,7 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * n * 8, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * s.m_pitch * 8, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_dlt, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
@@ -452,7 +452,8 @@ void ensure_motors(fmskf_ctx *h) {
   s.m_rpm = h->alloc<int16_t>(4 * n);
   s.m_curr = h->alloc<int16_t>(4 * n);
   s.m_head = h->alloc<uint8_t>(4 * n);
-  s.m_sum = h->alloc<int64_t>(4 * n);
+  s.m_pitch = plane_pitch(n);
+  s.m_sum = h->alloc<int64_t>(4 * s.m_pitch);
   s.m_dlt = h->alloc<float>(4 * n);
   s.m_speed = h->alloc<float>(4 * n);
   s.m_iir_y = h->alloc<float>(4 * n);
@@ -539,6 +540,7 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
   t.rec = (const uint32_t *)in->kf6_rec;
   t.sintab = s.sintab;
   t.stride = stride;
+  t.sum_pitch = stride;
   t.n_ticks = n_ticks;
   if (t.rec && h->cfg.model != FMSKF_MODEL_KF6) fail(FMSKF_EINVAL, "kf6_rec is a KF6 input");
   if (t.rec && (t.yaw_deg || t.gyro_z || t.rpm))
@@ -572,7 +574,10 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.angle_sum, "angle_sum");
         if (!t.rpm || !t.angle_sum) ensure_motors(h);
         if (!t.rpm) t.rpm = s.m_rpm;
-        if (!t.angle_sum) t.angle_sum = s.m_sum;
+        if (!t.angle_sum) {
+          t.angle_sum = s.m_sum;
+          t.sum_pitch = s.m_pitch;
+        }
       }
       break;
     case FMSKF_MODEL_KF6:
@@ -1059,7 +1064,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
     v.push_back({s.m_head, (size_t)4 * n});
-    v.push_back({s.m_sum, (size_t)4 * n * 8});
+    v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
     for (void *p : {(void *)s.m_dlt, (void *)s.m_speed, (void *)s.m_iir_y, (void *)s.m_iir_x})
       v.push_back({p, (size_t)4 * n * 4});
   }
@@ -1226,7 +1231,7 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
-    copy_out(h, angle_sum, h->s.m_sum, 4 * n * 8, mem);
+    copy_planes_out(h, angle_sum, h->s.m_sum, n * 8, h->s.m_pitch * 8, 4, mem);
     copy_out(h, speed_radps, h->s.m_speed, 4 * n * 4, mem);
     finish_out(h, mem);
   });

@@ -41,7 +41,10 @@ struct DevState {
   int16_t *m_rpm = nullptr;    // [N][4]
   int16_t *m_curr = nullptr;   // [N][4]
   uint8_t *m_head = nullptr;   // [N][4]
-  int64_t *m_sum = nullptr;    // [4][N]
+  int64_t *m_sum = nullptr;    // [4][m_pitch]: the encoder sums the RS tick reads, at a padded
+                               // plane pitch (a power-of-two stride N aliases: RS tick 2^20
+                               // 27.5-27.8 us from [4][2^20] sums, 24.7 from [4][2^20 + 512])
+  uint64_t m_pitch = 0;
   float *m_dlt = nullptr;      // [4][N]
   float *m_speed = nullptr;    // [4][N]
   float *m_iir_y = nullptr;    // [4][N]
@@ -56,13 +59,14 @@ struct TickIn {
   const float *yaw_deg;
   const float *gyro_z;
   const int16_t *rpm;        // [N][4]
-  const int64_t *angle_sum;  // [4][N]
+  const int64_t *angle_sum;  // [4][sum_pitch]
   const int16_t *raw;        // [N][8]
   const double *z;           // [8][N]
   const uint8_t *valid;      // [N] or null
   const uint32_t *rec;       // KF6 [N] x 16-byte records {yaw, gz, rpm[4]} or null
   const float *sintab;       // 513-entry TABLE512 sine table (device)
   uint64_t stride;
+  uint64_t sum_pitch;  // plane stride of angle_sum: the caller's stride, or the ingested m_pitch
   uint32_t n_ticks;
   // fmskf_tick_ensemble: the tick kernel also writes its blocks' ensemble records of the
   // post-tick state ([LEN][grid], ens_device.hpp) against the shift vector; null otherwise

@@ -71,7 +71,8 @@ struct IsrRsArgs {
   int64_t *prev;
   const float *yaw_deg;
   const int16_t *rpm;
-  const int64_t *angle_sum;  // [4][N] (plane stride N)
+  const int64_t *angle_sum;  // [4][sum_pitch]
+  uint64_t sum_pitch;
   const float *sintab;
   uint8_t *frames;
 };
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   const uint2 rw = reinterpret_cast<const uint2 *>(a.rpm)[i];
   int64_t sum[4];
 #pragma unroll
-  for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * n + i];
+  for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * a.sum_pitch + i];
   CtrlLane<SMALL, CP> L;
   L.load(c, i);
   rs_tick1<LIBM, true, true>(s, yaw, rw, sum, a.sintab);
@@ -221,7 +222,7 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uin
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
                   const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
   if (c.n == 0) return 0;
-  const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum,
+  const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum, in.sum_pitch,
                     in.sintab, frames};
   const bool small = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   const bool nt = small && state_nt(ctrl_state_bytes(c) + s.n * 56);

@@ -279,7 +279,8 @@ struct CanArgs {
   int8_t dir[4];
   int16_t *micro, *angle, *rpm, *curr;
   uint8_t *head;
-  int64_t *sum;
+  int64_t *sum;  // [4][sum_pitch]
+  uint64_t sum_pitch;
   float *dlt, *speed, *iir_y, *iir_x;
 };
 
@@ -339,13 +340,14 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   if (a.present && !((a.present[i] >> w) & 1)) return;
   const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
   const uint64_t pw = (uint64_t)w * n + i;
+  const uint64_t ps = (uint64_t)w * a.sum_pitch + i;
   const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g], a.head[g],
-                               a.iir_y[pw], a.iir_x[pw], a.sum[pw]);
+                               a.iir_y[pw], a.iir_x[pw], a.sum[ps]);
   a.iir_y[pw] = o.iir_y;
   a.iir_x[pw] = o.iir_x;
   a.speed[pw] = o.iir_y;
   a.dlt[pw] = o.dlt;
-  a.sum[pw] = o.sum;
+  a.sum[ps] = o.sum;
   a.micro[g] = a.stamps[g];
   a.angle[g] = o.angle;
   a.rpm[g] = o.rpm;
@@ -397,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   for (int w = 0; w < 4; w++) {
     py[w] = can_ld<NT>(a.iir_y + (uint64_t)w * n + i);
     px[w] = can_ld<NT>(a.iir_x + (uint64_t)w * n + i);
-    sm[w] = can_ld<NT>(a.sum + (uint64_t)w * n + i);
+    sm[w] = can_ld<NT>(a.sum + (uint64_t)w * a.sum_pitch + i);
   }
   const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
   const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     can_st<NT>(a.iir_x + pw, o.iir_x);
     can_st<NT>(a.speed + pw, o.iir_y);
     can_st<NT>(a.dlt + pw, o.dlt);
-    can_st<NT>(a.sum + pw, o.sum);
+    can_st<NT>(a.sum + (uint64_t)w * a.sum_pitch + i, o.sum);
     na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
     nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
     nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
@@ -440,6 +442,7 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.curr = s.m_curr;
   a.head = s.m_head;
   a.sum = s.m_sum;
+  a.sum_pitch = s.m_pitch;
   a.dlt = s.m_dlt;
   a.speed = s.m_speed;
   a.iir_y = s.m_iir_y;

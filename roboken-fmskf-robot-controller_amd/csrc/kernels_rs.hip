@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
       r = reinterpret_cast<const uint2 *>(a.in.rpm)[j];
       const int64_t *sp = a.in.angle_sum + (uint64_t)t * st * 4;
 #pragma unroll
-      for (int w = 0; w < 4; w++) sum[w] = sp[w * st + i];
+      for (int w = 0; w < 4; w++) sum[w] = sp[w * a.in.sum_pitch + i];
     }
     rs_tick1<LIBM, CORR, PRED>(s, yaw, r, sum, a.in.sintab);
   }
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     yaw[r] = a.in.yaw_deg[i];
     rw[r] = reinterpret_cast<const uint2 *>(a.in.rpm)[i];
 #pragma unroll
-    for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * n + i];
+    for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * a.in.sum_pitch + i];
   }
   tv.store(wtab[WT ? threadIdx.x >> 6 : 0]);
 #pragma unroll
