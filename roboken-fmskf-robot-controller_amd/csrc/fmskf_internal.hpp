@@ -173,11 +173,12 @@ inline uint64_t plane_pitch(uint64_t n) { return ((n + 511) / 512) * 512 + 256; 
 // non-temporal EKF9 pattern at 2^22 with the tick's 864-FMA compute phase, 64 KiB cap):
 // W = 256 309-313 us, 512 290-291, 1024 282-284, 2048 279-281, 4096 282-284; KF12D's 90 fp64
 // rows at 2^20 with 1280 fp64 FMAs: 256 269-270, 1024 268-269, 2048 263-265, 4096 259-260.
-// (Against planar planes the 256-wide tile already measured 374.6 -> 353.6 us for EKF9; the 27
-// KF6 rows gain nothing from tiling, so KF6 / RS stay planar.)  The allocation (rows x pitch,
-// pitch >= N rounded up to W) always covers ceil(N / W) tiles.
+// (Against planar planes the 256-wide tile already measured 374.6 -> 353.6 us for EKF9.)  The
+// KF6 state (FMSKF_KF6_TILED) and the control state's interpolator / FF_PI_D arrays
+// (FMSKF_CTRL_TILED) use the fp32 width too; the RS state stays planar.  The allocation
+// (rows x pitch, pitch >= N rounded up to W) always covers ceil(N / W) tiles.
 template <typename T>
-constexpr uint32_t tile_w() { return sizeof(T) == 8 ? 4096u : 2048u; }  // KF12D fp64 / EKF9 fp32
+constexpr uint32_t tile_w() { return sizeof(T) == 8 ? 4096u : 2048u; }  // fp64 (KF12D) / fp32
 inline uint32_t tile_w_elem(uint32_t elem) { return elem == 8 ? 4096u : 2048u; }
 
 // Cache policy of the per-tick state stream.  When the state is several times the 256 MiB

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
 }
 
-// Two robots per lane (tiles b and b + gridDim.x of the tiled state): robot B's 54 state
+// Two robots per lane (256-robot chunks b and b + gridDim.x of the tiled state): robot B's 54 state
 // loads and its raw record are issued before robot A's update, so they stream in while A
 // computes (FMSKF_EKF9_VARIANT experiments; see launch_ekf9).  PRIO: the waves issue their
 // loads at raised priority (s_setprio 3) and compute at the base priority.
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
                                             vo, 0, 0);
     }
   };
-  // tiled layout (FMSKF_TILED): the block's tile through a scalar descriptor (without ENS
+  // tiled layout (FMSKF_TILED): the block's chunk of its tile through a scalar descriptor (without ENS
   // lanes past N returned above, so a lane's slot is its thread index)
   const uint32_t slot = ENS ? tile_slot(n) : threadIdx.x;
   const TileRows<double, N, CP> tx(a.x, slot);
