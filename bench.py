@@ -287,8 +287,8 @@ def main():
         return [float(v) for v in t.tolist()]
 
     if args.n_total > 0:  # SURVEY 8(d) cfg 4 strong scaling: the same 2^24 total at every N
-        base, rem = divmod(args.n_total, world)
-        n = base + (1 if rank < rem else 0)
+        lo, hi = fmskf.shard_span(args.n_total, world, rank)
+        n = hi - lo
         n_global = args.n_total
     else:
         n = args.n_per_gpu

@@ -481,6 +481,18 @@ def ensemble_combine(n_state: int, records) -> tuple[np.ndarray, np.ndarray]:
     return mean, cov
 
 
+def shard_span(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Rank `rank`'s contiguous robot range [lo, hi) of `n_total` over `world` ranks, the
+    remainder on the first ranks (bench.py's sharding): shards differ by at
+    most one robot and rank order is robot order, so the rank-order fold of the records is
+    the fold of the unsharded fleet."""
+    if world < 1 or not 0 <= rank < world or n_total < 0:
+        raise ValueError(f"shard_span: n_total {n_total}, world {world}, rank {rank}")
+    base, rem = divmod(n_total, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
 def comm_unique_id() -> bytes:
     """fmskf_comm_unique_id (rank 0): 128 bytes to hand to every rank's comm_init"""
     b = (C.c_uint8 * 128)()

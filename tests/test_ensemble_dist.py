@@ -1,4 +1,4 @@
-"""N > 1 path on CPU: world-size-2 gloo.
+"""N > 1 path on CPU: world-size-2 and -3 gloo.
 
 Each rank owns a contiguous shard of the robots (the bench's sharding), reduces it to the
 {count, mean, M2} record (here with the oracle: no GPU on this host), the ranks all-gather
@@ -21,13 +21,6 @@ def _free_port():
     return p
 
 
-def _shard(n, world, rank):
-    per = n // world
-    lo = rank * per
-    hi = n if rank == world - 1 else lo + per
-    return lo, hi
-
-
 def _worker(rank, world, port, n, out_dir):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -41,7 +34,7 @@ def _worker(rank, world, port, n, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rng = np.random.default_rng(1234)  # same global data on every rank
     x = (rng.normal(size=(6, n)) * np.arange(1, 7)[:, None] + 5.0).astype(np.float32)
-    lo, hi = _shard(n, world, rank)
+    lo, hi = fmskf.shard_span(n, world, rank)  # bench.py's sharding
     rec = torch.from_numpy(orc.ens_partial(np.ascontiguousarray(x[:, lo:hi])))
     gathered = [torch.zeros_like(rec) for _ in range(world)]
     dist.all_gather(gathered, rec)
@@ -53,14 +46,14 @@ def _worker(rank, world, port, n, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [10001, 65536])
-def test_ensemble_gloo_world2(tmp_path, orc, n):
+@pytest.mark.parametrize("n,world", [(10001, 2), (65536, 2), (10001, 3)])
+def test_ensemble_gloo_world2(tmp_path, orc, n, world):
     import torch.multiprocessing as mp
-    world = 2
     mp.spawn(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
     m0, c0 = np.load(tmp_path / "r0_mean.npy"), np.load(tmp_path / "r0_cov.npy")
-    m1, c1 = np.load(tmp_path / "r1_mean.npy"), np.load(tmp_path / "r1_cov.npy")
-    assert np.array_equal(m0, m1) and np.array_equal(c0, c1), "ranks disagree"
+    for r in range(1, world):
+        mr, cr = np.load(tmp_path / f"r{r}_mean.npy"), np.load(tmp_path / f"r{r}_cov.npy")
+        assert np.array_equal(m0, mr) and np.array_equal(c0, cr), f"rank {r} disagrees"
     rng = np.random.default_rng(1234)
     x = (rng.normal(size=(6, n)) * np.arange(1, 7)[:, None] + 5.0).astype(np.float32)
     ref = np.cov(x.astype(np.float64))
@@ -70,8 +63,16 @@ def test_ensemble_gloo_world2(tmp_path, orc, n):
 
 
 def test_shard_covers_all():
-    for n in (1, 7, 1 << 20):
+    """bench.py's contiguous shards: cover [0, n) in rank order, sizes differ by at most one,
+    the larger shards first (cfg 4's strong-scaling form, --n-total)"""
+    import fmskf
+    for n in (0, 1, 7, 1 << 20, (1 << 24) + 5):
         for world in (1, 2, 3, 8):
-            spans = [_shard(n, world, r) for r in range(world)]
+            spans = [fmskf.shard_span(n, world, r) for r in range(world)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+    for bad in ((5, 0, 0), (5, 2, 2), (5, 2, -1), (-1, 2, 0)):
+        with pytest.raises(ValueError):
+            fmskf.shard_span(*bad)
