@@ -180,3 +180,86 @@ def test_kf6_records_and_planes_past_2p28(orc):
         orc.kf6_tick(xo, Po, np.ascontiguousarray(ys[t]), np.ascontiguousarray(gs[t]),
                      np.ascontiguousarray(rs[t]), None, prm, nthreads=0)
     np.testing.assert_array_equal(pose_rec[:, idx].view(np.uint32), xo[:3].view(np.uint32))
+
+
+def _wt901_polls(n, stride, rng):
+    """One poll per robot at the benchmark shape (44 B = four frames 0x51 acc,
+    0x52 gyro, 0x53 angle, 0x59 quaternion per 10 ms), built vectorised: 60% clean, 15% with one
+    byte damaged (a checksum failure and the resync of wit_c_sdk.c:142-156), 15% torn (the tail
+    carried into the next poll), 10% noise with 0x55 sprinkled in."""
+    fr = np.zeros((n, 4, 11), np.uint8)
+    fr[:, :, 0] = 0x55
+    fr[:, :, 1] = np.array([0x51, 0x52, 0x53, 0x59], np.uint8)
+    fr[:, :, 2:10] = rng.integers(0, 256, (n, 4, 8), dtype=np.uint8)
+    fr[:, :, 10] = (fr[:, :, :10].sum(axis=2, dtype=np.uint32) & 0xFF).astype(np.uint8)
+    buf = np.zeros((n, stride), np.uint8)
+    buf[:, :44] = fr.reshape(n, 44)
+    lens = np.full(n, 44, np.uint32)
+    kind = rng.choice(4, n, p=[0.6, 0.15, 0.15, 0.1])
+    d = np.flatnonzero(kind == 1)
+    buf[d, rng.integers(0, 44, d.size)] ^= 0xA5
+    t = np.flatnonzero(kind == 2)
+    lens[t] = rng.integers(0, 44, t.size)
+    z = np.flatnonzero(kind == 3)
+    noise = rng.integers(0, 256, (z.size, stride), dtype=np.uint8)
+    noise[rng.random(noise.shape) < 0.2] = 0x55
+    buf[z] = noise
+    lens[z] = rng.integers(0, stride + 1, z.size)
+    return buf, lens
+
+
+def test_wt901_ingest_2p20_sampled(orc):
+    """The batched WT901 decoder at the benchmark size, 2^20 robots x 4 polls
+    of mixed clean / damaged / torn / noisy bytes at the 48-byte stride: register file, parser
+    backlog, error flag and the scaled Data page of a sample bit for bit against the oracle's
+    restatement of wit_c_sdk.c:90-198 and imu_if_wt901c.cpp:91-143."""
+    n, polls, stride = 1 << 20, 4, 48
+    rng = np.random.default_rng(2024)
+    idx = _sample(n, k=1024, seed=4)
+    orcs = [orc.Wt901(0x51) for _ in idx]
+    with Engine("kf6", n) as e:
+        for k in range(polls):
+            buf, lens = _wt901_polls(n, stride, rng)
+            e.ingest_wt901(buf, lens, latch_qinit=(k == 0))
+            for o, i in zip(orcs, idx):
+                o.update(buf[i, :lens[i]], latch_qinit=(k == 0))
+        regs, pending = e.get_imu_regs()
+        data, err = e.get_imu()
+    for o, i in zip(orcs, idx):
+        np.testing.assert_array_equal(regs[:, i], o.regs, err_msg=f"robot {i}")
+        assert pending[i] == len(o.parser) and err[i] == o.is_error, f"robot {i}"
+        np.testing.assert_array_equal(data[:, i].view(np.uint32), o.data.view(np.uint32),
+                                      err_msg=f"robot {i}")
+
+
+@pytest.mark.parametrize("n,masked", [(1 << 22, False), (1 << 20, True)])
+def test_can_ingest_large_sampled(orc, n, masked):
+    """C610 RX decode (VD_motor_if_m2006.cpp:32-72) at bench sizes: 2^22 robots takes the
+    robot-per-lane kernel with the non-temporal state, 2^20 with `present` masks the wheel-per-lane
+    kernel; a sample of robots bit for bit (angle, rpm, current, the int64 angle sum, the speed
+    IIR) after 4 ticks with out-of-range angles and equal stamps (ARM x/0 -> 0)."""
+    T = 4
+    rng = np.random.default_rng(77 + masked)
+    dirs = [1, 1, -1, -1]
+    idx = _sample(n, k=1024, seed=5)
+    motors = [[orc.M2006(d) for d in dirs] for _ in idx]
+    with Engine("rs", n) as e:
+        for t in range(T):
+            frames = rng.integers(0, 256, (n, 4, 8), dtype=np.uint8)
+            frames[:, :, 0] &= 0x1F
+            frames[rng.random((n, 4)) < 0.05, 0] |= 0x80
+            stamps = rng.integers(0, 0x8000, (n, 4)).astype(np.int16)
+            stamps[rng.random((n, 4)) < 0.05] = 1234
+            present = rng.integers(0, 16, n).astype(np.uint8) if masked else None
+            e.ingest_can(frames, stamps, present)
+            for m, i in zip(motors, idx):
+                for w in range(4):
+                    if present is None or (present[i] >> w) & 1:
+                        m[w].rx(frames[i, w], int(stamps[i, w]))
+        got = e.get_motors()
+    for m, i in zip(motors, idx):
+        for w in range(4):
+            s = m[w].s
+            assert (got["angle"][i, w], got["rpm"][i, w], got["curr"][i, w], got["angle_sum"][w, i]) == \
+                (s.angle, s.rpm, s.curr, s.angle_sum), f"robot {i} wheel {w}"
+            assert got["speed_radps"][w, i].view(np.uint32) == np.float32(s.speed_radps).view(np.uint32)
