@@ -38,10 +38,26 @@ static const float k_g0 = 9.80665f;
 /* ------------------------------------------------------------------------- */
 float orc_deg2rad(float d) { return d * k_deg2rad; } /* util_mymath.hpp:16 */
 
+/* The firmware's float -> integer casts compile to Cortex-M7 VCVT.S32.F32 / VCVT.U32.F32:
+ * truncate, saturate to the destination range, NaN -> 0.  Spelled out here because a C cast
+ * of an out-of-range float is undefined (x86 gives 0x80000000); used wherever the reference
+ * casts a float that can leave the range (util_mymath.hpp:21,30, the CMSIS table index). */
+int32_t orc_f2i32_arm(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return INT32_MAX;
+  if (f <= -2147483648.0f) return INT32_MIN;
+  return (int32_t)f;
+}
+uint32_t orc_f2u32_arm(float f) {
+  if (!(f > 0.0f)) return 0; /* NaN, negatives, -0 */
+  if (f >= 4294967296.0f) return UINT32_MAX;
+  return (uint32_t)f;
+}
+
 /* util_mymath.hpp:18-25 */
 float orc_normalize_rad_0to2pi(float d) {
   if (d < 0.0f || d >= 2.0f * ORC_PI_F) {
-    int mod = (int)(d / (2.0f * ORC_PI_F));
+    int mod = orc_f2i32_arm(d / (2.0f * ORC_PI_F));
     d -= (mod * 2.0f * ORC_PI_F);
     if (d < 0.0f) d = d + 2.0f * ORC_PI_F;
   }
@@ -51,7 +67,7 @@ float orc_normalize_rad_0to2pi(float d) {
 /* util_mymath.hpp:27-34 */
 float orc_normalize_deg_0to360(float d) {
   if (d < 0.0f || d >= 360.0f) {
-    int mod = (int)(d / (360.0f));
+    int mod = orc_f2i32_arm(d / (360.0f));
     d -= (mod * 360.0f);
     if (d < 0.0f) d = d + 360.0f;
   }
@@ -76,11 +92,11 @@ void orc_sin_table(float out[513]) {
 }
 
 static float orc_table_lookup(float in) {
-  int32_t n = (int32_t)in;
-  if (in < 0.0f) n--;
+  int32_t n = orc_f2i32_arm(in);
+  if (in < 0.0f) n = (int32_t)((uint32_t)n - 1u); /* the M7's wrapping SUB */
   in = in - (float)n;
   float findex = 512.0f * in;
-  uint16_t index = (uint16_t)findex;
+  uint16_t index = (uint16_t)orc_f2u32_arm(findex); /* VCVT.U32.F32, then UXTH */
   if (index >= 512) {
     index = 0;
     findex -= 512.0f;
@@ -888,13 +904,6 @@ float orc_pid_update(orc_pid *c, const orc_ctrl_params *p, float nowval) {
   return ctrl;
 }
 
-/* ARM VCVT.S32.F32 semantics: truncate, saturate to int32, NaN -> 0 */
-int32_t orc_f2i32_arm(float f) {
-  if (f != f) return 0;
-  if (f >= 2147483648.0f) return INT32_MAX;
-  if (f <= -2147483648.0f) return INT32_MIN;
-  return (int32_t)f;
-}
 
 /* set_CurrA_tgt: (int16_t)(A * AMPERE_TO_RAW_CURR) -- Cortex-M7: VCVT to int32 then the low
  * 16 bits; set_rawCurr_tgt: sat_curr(_tgt_cur * dir) with the int product narrowed to the

@@ -220,6 +220,7 @@ typedef struct {
 } orc_vehicle_info;
 /* ARM float -> int32 conversion (VCVT: round toward zero, saturating, NaN -> 0) */
 int32_t orc_f2i32_arm(float f);
+uint32_t orc_f2u32_arm(float f); /* VCVT.U32.F32: truncate, saturate, NaN -> 0 */
 void orc_vehicle_info_fill(orc_vehicle_info *o, float px, float py, float pth, float vx, float vy,
                            float vth, const float imu_data[16], uint8_t is_error,
                            const uint8_t floor[8], float cam_pitch, uint32_t fault);

@@ -178,6 +178,8 @@ def lib():
         L.orc_ctrl_step_batch.argtypes = [C.c_size_t, _vp, C.POINTER(CtrlParams), _i16p, _vp]
         L.orc_f2i32_arm.argtypes = [C.c_float]
         L.orc_f2i32_arm.restype = C.c_int32
+        L.orc_f2u32_arm.argtypes = [C.c_float]
+        L.orc_f2u32_arm.restype = C.c_uint32
         L.orc_vehicle_info_fill.argtypes = [C.POINTER(VehicleInfo)] + [C.c_float] * 6 + \
             [_f32p, C.c_uint8, _vp, C.c_float, C.c_uint32]
         _lib = L
@@ -459,6 +461,10 @@ def can_tx(cur):
 
 def f2i32_arm(f) -> int:
     return lib().orc_f2i32_arm(float(np.float32(f)))
+
+
+def f2u32_arm(f) -> int:
+    return lib().orc_f2u32_arm(float(np.float32(f)))
 
 
 def vehicle_info(px, py, pth, vx, vy, vth, imu_data, is_error, floor=None, cam_pitch=0.0,

@@ -218,12 +218,19 @@ static void check_ctrl(void) {
   }
   uint8_t out[8];
   for (size_t i = 0; i < n; i++) orc_can_tx(c[i].curr, out);
-  const float ext[] = {NAN, INFINITY, -INFINITY, 3e9f, -3e9f, 0.0f, -0.0f, 1e-40f, 2147483520.f};
+  /* every float -> int conversion on the path has the M7's defined semantics, so the
+   * extremes (past 2^31 turns, inf, NaN) go straight in: UBSan's float-cast-overflow and
+   * signed-overflow checks must stay silent */
+  const float ext[] = {NAN, INFINITY, -INFINITY, 3e9f, -3e9f, 0.0f, -0.0f, 1e-40f, 2147483520.f,
+                       1.5e10f, -1.5e10f, 1e20f, -1e20f, 3.4e38f, -3.4e38f};
   for (size_t k = 0; k < sizeof(ext) / sizeof(ext[0]); k++) {
     (void)orc_f2i32_arm(ext[k]);
+    (void)orc_f2u32_arm(ext[k]);
     (void)orc_curr_to_raw(ext[k], -1, 3000);
-    (void)orc_normalize_rad_0to2pi(ext[k] == ext[k] && fabsf(ext[k]) < 1e9f ? ext[k] : 1.0f);
-    (void)orc_sin(ext[k] == ext[k] && fabsf(ext[k]) < 1e6f ? ext[k] : 0.5f, 0);
+    (void)orc_normalize_rad_0to2pi(ext[k]);
+    (void)orc_normalize_deg_0to360(ext[k]);
+    (void)orc_sin(ext[k], 0);
+    (void)orc_cos(ext[k], 0);
   }
   orc_vehicle_info vi;
   float data[16];

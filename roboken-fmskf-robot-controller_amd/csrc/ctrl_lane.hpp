@@ -73,13 +73,8 @@ __device__ __forceinline__ float interp_update(Interp &s, float ts) {
   return f[IV_V];
 }
 
-// ARM VCVT.S32.F32: truncate, saturate, NaN -> 0
-__device__ __forceinline__ int32_t f2i32_arm(float f) {
-  if (f != f) return 0;
-  if (f >= 2147483648.0f) return 2147483647;
-  if (f <= -2147483648.0f) return (int32_t)0x80000000u;
-  return (int32_t)f;
-}
+// ARM VCVT.S32.F32: truncate, saturate, NaN -> 0 (fmskf_device.hpp)
+__device__ __forceinline__ int32_t f2i32_arm(float f) { return cvt_i32_arm(f); }
 
 // set_CurrA_tgt -> set_rawCurr_tgt -> sat_curr (VD_motor_if_m2006.hpp:36-37,59-60)
 __device__ __forceinline__ int16_t curr_to_raw(float amp, int dir, int lim) {

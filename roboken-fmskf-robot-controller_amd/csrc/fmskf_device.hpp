@@ -33,10 +33,25 @@ struct K {
 
 __device__ __forceinline__ float deg2rad(float d) { return d * K::deg2rad; }  // util_mymath.hpp:16
 
+// The firmware's float -> integer casts are Cortex-M7 VCVT.S32.F32 / VCVT.U32.F32: truncate,
+// saturate to the destination range, NaN -> 0.  gfx950's v_cvt_i32_f32 / v_cvt_u32_f32 do
+// exactly that, so they are issued directly: a C++ cast of an out-of-range float is undefined,
+// and these give the firmware's answer for every input (a heading past 2^31 turns, inf, NaN).
+__device__ __forceinline__ int32_t cvt_i32_arm(float f) {
+  int32_t r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+}
+__device__ __forceinline__ uint32_t cvt_u32_arm(float f) {
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+}
+
 // util_mymath.hpp:18-25
 __device__ __forceinline__ float normalize_rad_0to2pi(float d) {
   if (d < 0.0f || d >= 2.0f * FMSKF_PI_F) {
-    int mod = (int)(d / (2.0f * FMSKF_PI_F));
+    int mod = cvt_i32_arm(d / (2.0f * FMSKF_PI_F));
     d -= (mod * 2.0f * FMSKF_PI_F);
     if (d < 0.0f) d = d + 2.0f * FMSKF_PI_F;
   }
@@ -46,7 +61,7 @@ __device__ __forceinline__ float normalize_rad_0to2pi(float d) {
 // util_mymath.hpp:27-34
 __device__ __forceinline__ float normalize_deg_0to360(float d) {
   if (d < 0.0f || d >= 360.0f) {
-    int mod = (int)(d / (360.0f));
+    int mod = cvt_i32_arm(d / (360.0f));
     d -= (mod * 360.0f);
     if (d < 0.0f) d = d + 360.0f;
   }
@@ -54,13 +69,15 @@ __device__ __forceinline__ float normalize_deg_0to360(float d) {
 }
 
 // CMSIS-DSP arm_sin_f32 / arm_cos_f32 published algorithm: scale to turns, floor,
-// 512-entry table, linear interpolation.
+// 512-entry table, linear interpolation.  The floor's decrement wraps (INT_MIN - 1 on the
+// M7 is INT_MAX); the table index is VCVT.U32 then the low 16 bits (uint16_t), so it is
+// always < 513 whatever `in` is.
 __device__ __forceinline__ float table_lookup(float in, const float *__restrict__ tab) {
-  int32_t n = (int32_t)in;
-  if (in < 0.0f) n--;
+  int32_t n = cvt_i32_arm(in);
+  if (in < 0.0f) n = (int32_t)((uint32_t)n - 1u);
   in = in - (float)n;
   float findex = 512.0f * in;
-  uint32_t index = (uint16_t)findex;
+  uint32_t index = (uint16_t)cvt_u32_arm(findex);
   if (index >= 512u) {
     index = 0;
     findex -= 512.0f;

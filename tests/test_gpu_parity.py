@@ -49,6 +49,74 @@ def test_trig_table_bitexact(orc):
     bits_equal(c, co, "cos")
 
 
+# headings where the reference's float -> int casts leave the int32 range (past 2^31 turns),
+# infinities, NaN, denormals and the 2^24 float-integer edge
+EXTREME_RAD = np.float32([1.3493e10, 1.35e10, -1.35e10, 1.5e10, -1.5e10, 4e12, -4e12, 1e20, -1e20,
+                          3.4e38, -3.4e38, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 16777216.0,
+                          -16777217.0, 2147483520.0, -2147483648.0, 6.2831855, -6.2831855])
+
+
+def nan_aware_equal(a, b, what=""):
+    """bitwise equal, except that NaN only has to meet NaN (x86 and gfx950 differ in the
+    default NaN's sign bit; the firmware's value is NaN either way)"""
+    a, b = np.asarray(a), np.asarray(b)
+    na, nb = np.isnan(a), np.isnan(b)
+    assert np.array_equal(na, nb), f"{what}: NaN positions differ"
+    bits_equal(np.where(na, 0, a).astype(a.dtype), np.where(nb, 0, b).astype(a.dtype), what)
+
+
+def test_trig_table_extremes_bitexact(orc):
+    """The CMSIS table lookup with the M7's saturating VCVT (the floor of a heading past 2^31
+    turns, the uint16_t table index): every input gives the oracle's answer, and the index stays
+    inside the 513-entry table."""
+    x = np.concatenate([EXTREME_RAD, -EXTREME_RAD * np.float32(0.5)])
+    with Engine("kf6", 8, trig=TABLE) as e:
+        s, c = e.eval_trig(x)
+    so, co = orc.eval_trig(x, orc.TRIG_TABLE512)
+    nan_aware_equal(s, so, "sin")
+    nan_aware_equal(c, co, "cos")
+
+
+def test_rs_tick_extreme_headings(orc):
+    """RS tick (VD_vehicle_controller.cpp:36-51) fed IMU yaws whose radians leave the int32 turn
+    range in normalize_rad_0to2pi (util_mymath.hpp:18-25), inf and NaN: pose, velocity and
+    encoder state as the oracle gives them."""
+    with np.errstate(over="ignore"):  # rad -> deg of the largest ones overflows to inf, as wanted
+        yaw_deg = np.concatenate([EXTREME_RAD, EXTREME_RAD * np.float32(57.29578)])
+    n, T = yaw_deg.size, 3
+    tr = Trajectory(n, T, seed=41)
+    _, sums, rpm = tr.rs_inputs()
+    yaw = np.repeat(yaw_deg[None], T, 0)
+    with Engine("rs", n, trig=TABLE) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t])
+        pose = e.get_pose()
+        prev = e.get_prev_sum()
+    pos, velo, prevo = _rs_oracle(orc, n, yaw, sums, rpm, TABLE, T)
+    nan_aware_equal(np.stack(pose), pos, "pose")
+    bits_equal(prev, prevo, "prev")
+
+
+def test_kf6_tick_extreme_yaw(orc):
+    """KF6 correct + predict with IMU yaws far outside any heading (the trig of the state's
+    heading then takes the saturating table path), inf and NaN: x and P as the oracle gives
+    them, NaN meeting NaN."""
+    with np.errstate(over="ignore"):  # rad -> deg of the largest ones overflows to inf, as wanted
+        yaw_deg = np.concatenate([EXTREME_RAD, EXTREME_RAD * np.float32(57.29578)])
+    n, T = yaw_deg.size, 3
+    rng = np.random.default_rng(8)
+    yaw = np.repeat(yaw_deg[None], T, 0)
+    gz = rng.uniform(-300, 300, (T, n)).astype(np.float32)
+    rpm = rng.integers(-9000, 9000, (T, n, 4)).astype(np.int16)
+    with Engine("kf6", n, trig=TABLE) as e:
+        for t in range(T):
+            e.tick(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])
+        x, P = e.get_state()
+    xo, Po = _kf6_oracle(orc, n, yaw, gz, rpm, None, orc.TRIG_TABLE512, T)
+    nan_aware_equal(x, xo, "x")
+    nan_aware_equal(P, Po, "P")
+
+
 def test_trig_libm_close(orc):
     x = np.linspace(-10, 10, 10001).astype(np.float32)
     with Engine("kf6", 8, trig=LIBM) as e:

@@ -29,6 +29,33 @@ def test_normalize_rad(orc):
     assert 0.0 <= orc.normalize_rad_0to2pi(-20.0) < float(two_pi)
 
 
+def test_float_to_int_is_arm_vcvt(orc):
+    """The firmware's float -> int casts are Cortex-M7 VCVT (truncate, saturate, NaN -> 0);
+    x86's cvttss2si would give 0x80000000 for every out-of-range input."""
+    i32max, i32min = 2**31 - 1, -2**31
+    for f, want in ((3e9, i32max), (-3e9, i32min), (np.inf, i32max), (-np.inf, i32min),
+                    (np.nan, 0), (-2.9, -2), (2147483520.0, 2147483520), (-2147483648.0, i32min)):
+        assert orc.f2i32_arm(f) == want, f
+    for f, want in ((-1.0, 0), (np.nan, 0), (5e9, 2**32 - 1), (4294967040.0, 4294967040), (7.9, 7)):
+        assert orc.f2u32_arm(f) == want, f
+
+
+def test_normalize_rad_past_2p31_turns(orc):
+    # util_mymath.hpp:21 `mod = (int)(d / (2*PI))` saturates on the M7: 1.5e10 rad is 2.39e9
+    # turns -> mod = INT32_MAX, d -= (float)mod * 2 * PI (float arithmetic, left to right)
+    two_pi = F(2.0) * F(3.14159265358979)
+    d = F(1.5e10)
+    assert d / two_pi > 2**31
+    want = F(d - F(F(F(2**31 - 1) * F(2.0)) * F(3.14159265358979)))
+    assert orc.normalize_rad_0to2pi(float(d)) == want
+    d = F(-1.5e10)  # mod = INT32_MIN: d -= -2^32 PI, still negative, then += 2 PI
+    want = F(d - F(F(F(-2**31) * F(2.0)) * F(3.14159265358979)))
+    want = F(want + two_pi) if want < 0 else want
+    assert orc.normalize_rad_0to2pi(float(d)) == want
+    assert np.isnan(orc.normalize_rad_0to2pi(np.nan))
+    assert orc.normalize_rad_0to2pi(np.inf) == np.inf
+
+
 def test_normalize_deg(orc):
     assert orc.normalize_deg_0to360(-90.0) == F(270.0)
     assert orc.normalize_deg_0to360(725.0) == F(5.0)
