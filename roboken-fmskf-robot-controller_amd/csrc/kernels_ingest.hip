@@ -142,6 +142,12 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   ps.flags = a.flags[i];
   const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
   const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
+  // the standard 10 ms poll (0x51 acc, 0x52 gyro, 0x53 angle, 0x59 quaternion)
+  // taken by the fast path: every register updateData reads except the magnetometer's was
+  // written by exactly one of its frames, so the Data page is built from the frame words
+  // instead of reading the register file back
+  bool std4 = false;
+  uint32_t sw[4][4] = {};
   if constexpr (VEC) {
     const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
     uint4 ch[4];
@@ -179,7 +185,32 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
       for (int k = 0; k < 8; k++) w0[f] |= (uint64_t)b[k] << (8 * k);
       w1[f] = (uint64_t)b[8] | ((uint64_t)b[9] << 8) | ((uint64_t)b[10] << 16);
     }
-    if (fast) {
+    const auto ftype = [](uint64_t w) { return (uint32_t)(w >> 8) & 0xFFu; };
+    std4 = fast && nfr == 4 && ftype(w0[0]) == 0x51u && ftype(w0[1]) == 0x52u &&
+           ftype(w0[2]) == 0x53u && ftype(w0[3]) == 0x59u;
+    if (std4) {
+      // CopeWitData of the four frames with their register runs known statically
+#pragma unroll
+      for (int f = 0; f < 4; f++) {
+        sw[f][0] = (uint32_t)(w0[f] >> 16) & 0xFFFFu;
+        sw[f][1] = (uint32_t)(w0[f] >> 32) & 0xFFFFu;
+        sw[f][2] = (uint32_t)(w0[f] >> 48) & 0xFFFFu;
+        sw[f][3] = (uint32_t)w1[f] & 0xFFFFu;
+      }
+      int16_t *reg = a.reg;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        reg[(R_AX + k) * n + i] = (int16_t)sw[0][k];
+        reg[(R_GX + k) * n + i] = (int16_t)sw[1][k];
+        reg[(R_ROLL + k) * n + i] = (int16_t)sw[2][k];
+      }
+      reg[R_TEMP * n + i] = (int16_t)sw[0][3];
+      reg[R_VERSION * n + i] = (int16_t)sw[2][3];
+#pragma unroll
+      for (int k = 0; k < 4; k++) reg[(R_Q0 + k) * n + i] = (int16_t)sw[3][k];
+      ps.flags |= flags_of(R_AX, 3) | flags_of(R_TEMP, 1) | flags_of(R_GX, 3) | flags_of(R_ROLL, 3) |
+                  flags_of(R_VERSION, 1) | flags_of(R_Q0, 4);
+    } else if (fast) {
 #pragma unroll
       for (int f = 0; f < 5; f++)
         if ((uint32_t)f < nfr) ps.dispatch(w0[f], w1[f], a, i);
@@ -221,16 +252,36 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   if (!ok) return;
   // updateData, imu_if_wt901c.cpp:91-129
   float acc[3], gyr[3], mag[3], ang[3], q[4], qi[4];
+  int16_t ra[3], rg[3], rr[3], rq[4];
+  if (std4) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      ra[k] = (int16_t)sw[0][k];
+      rg[k] = (int16_t)sw[1][k];
+      rr[k] = (int16_t)sw[2][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) rq[k] = (int16_t)sw[3][k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      ra[k] = reg[(R_AX + k) * n + i];
+      rg[k] = reg[(R_GX + k) * n + i];
+      rr[k] = reg[(R_ROLL + k) * n + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    acc[k] = (float)reg[(R_AX + k) * n + i] / 32768.0f * 16.0f;
-    gyr[k] = (float)reg[(R_GX + k) * n + i] / 32768.0f * 2000.0f;
+    acc[k] = (float)ra[k] / 32768.0f * 16.0f;
+    gyr[k] = (float)rg[k] / 32768.0f * 2000.0f;
     mag[k] = (float)reg[(R_HX + k) * n + i];
-    ang[k] = (float)reg[(R_ROLL + k) * n + i] / 32768.0f * 180.0f;
+    ang[k] = (float)rr[k] / 32768.0f * 180.0f;
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    q[k] = (float)reg[(R_Q0 + k) * n + i] / 32768.0f;
+    q[k] = (float)rq[k] / 32768.0f;
     qi[k] = a.qinit[k * n + i];
   }
   float *d = a.data;
