@@ -76,3 +76,25 @@ def test_shard_covers_all():
     for bad in ((5, 0, 0), (5, 2, 2), (5, 2, -1), (-1, 2, 0)):
         with pytest.raises(ValueError):
             fmskf.shard_span(*bad)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_rank_order_fold_world_n(orc, world):
+    """The driver's 4- and 8-GPU shapes in one process: bench.py's shards of an odd fleet
+    (cfg 4's strong-scaling form), one record per rank, folded in rank order by the library's
+    host routine: the statistics of the unsharded fleet, and identical whichever rank folds
+    (every rank folds the same gathered array)."""
+    import fmskf
+    n = 8 * 4099 + 5
+    rng = np.random.default_rng(4321)
+    x = (rng.normal(size=(6, n)) * np.arange(1, 7)[:, None] - 2.0).astype(np.float32)
+    recs = np.stack([orc.ens_partial(np.ascontiguousarray(x[:, lo:hi]))
+                     for lo, hi in (fmskf.shard_span(n, world, r) for r in range(world))])
+    assert recs[:, 0].sum() == n
+    mean, cov = fmskf.ensemble_combine(6, recs)
+    m2, c2 = fmskf.ensemble_combine(6, recs.copy())
+    assert np.array_equal(mean, m2) and np.array_equal(cov, c2)
+    xd = x.astype(np.float64)
+    np.testing.assert_allclose(mean, xd.mean(axis=1), rtol=1e-12)
+    ref = np.cov(xd)
+    np.testing.assert_allclose(cov, [ref[i, j] for i in range(6) for j in range(i + 1)], rtol=1e-10)
