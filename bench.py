@@ -157,6 +157,105 @@ def secondary_configs(dev, stream, ticks: int, trig):
     return out
 
 
+# algorithmic bytes per robot of the rows either side of the tick
+PATH_BYTES = {
+    # RS tick: pos 12 r+w, prev 32 r+w, sums 32, yaw 4, rpm 8 in, vel 12 out
+    "rs_tick_2p20": 144,
+    # WT901 standard poll: row 48 + len 4, parser window / count / flags 14 r+w, error 1,
+    # 15 registers 30 w, magnetometer 6 + q_init 16 r, Data page 64 w
+    "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64,
+    # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, head, IIR y / x, int64 sum r+w;
+    # speed, dlt, rpm, curr w
+    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 4 + 4 + 2 + 2),
+    # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
+    "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
+    # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
+    # loads it once) + the 8-byte 0x200 frame
+    "isr_kf6_2p20": 232 + 369 - 8 + 8,
+}
+
+
+def path_rows(dev, stream, ticks: int, trig):
+    """The reference-semantics tick and the rows either side of the
+    tick (8(f) 1-3) at 2^20 robots, each its kernel back to back between HIP events on the
+    stream it runs on: WT901 ingest of the standard 10 ms poll, C610 CAN RX, the vehicle control
+    step and the fused KF6 firmware ISR (tick + control + 0x200 frame); kernel_ms and roofline
+    each (bytes: PATH_BYTES)."""
+    import numpy as np
+    import torch
+    import fmskf
+    from fmskf.synth import SEED, kf6_ring_torch, wt901_frame
+    n, R = 1 << 20, 4
+    yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 11, device=dev)
+    out = {}
+
+    def timed(key, run, e):
+        for k in range(3):
+            run(k)
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for k in range(ticks):
+            run(k)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / ticks
+        gbps = PATH_BYTES[key] * n / (ms * 1e-3) / 1e9
+        out[key] = {"instances": n, "kernel_ms": ms, "robots_per_s": n / (ms * 1e-3), "ticks": ticks,
+                    "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                 "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": PATH_BYTES[key]}}
+        e.close()
+
+    e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    sums = torch.cumsum(torch.randint(-20, 20, (R, 4, n), device=dev, dtype=torch.int64), 0)
+    preps = [e.prepare(yaw_deg=yaw[r], angle_sum=sums[r], rpm=rpm[r]) for r in range(R)]
+    timed("rs_tick_2p20", lambda k: e.tick_prepared(preps[k % R]), e)
+    del preps, sums
+
+    e = fmskf.Engine("kf6", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    rng = np.random.default_rng(SEED)
+    polls = []
+    for _ in range(R):
+        b = b"".join(wt901_frame(t, rng.integers(0, 65536, 4)) for t in (0x51, 0x52, 0x53, 0x59))
+        row = np.zeros(48, np.uint8)
+        row[:44] = np.frombuffer(b, np.uint8)
+        polls.append(torch.from_numpy(np.tile(row, (n, 1))).to(dev))
+    lens = torch.full((n,), 44, dtype=torch.int32, device=dev)
+    timed("wt901_ingest_2p20", lambda k: e.ingest_wt901(polls[k % R], lens), e)
+    del polls
+
+    e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    frames = [torch.from_numpy(rng.integers(0, 256, (n, 4, 8)).astype(np.uint8)).to(dev) for _ in range(R)]
+    stamps = [torch.from_numpy((np.arange(4)[None, :] * 250 + k * 1000 + np.zeros((n, 1))).astype(np.int16)).to(dev)
+              for k in range(R)]
+    timed("can_ingest_2p20", lambda k: e.ingest_can(frames[k % R], stamps[k % R]), e)
+    del frames, stamps
+
+    def driven(model):
+        en = fmskf.Engine(model, n, device=dev.index, trig=trig)
+        en.set_stream(stream)
+        en.set_power(None)
+        g = torch.Generator(device="cpu").manual_seed(7)
+        vel = torch.stack([torch.rand(n, generator=g) * 800 - 400, torch.rand(n, generator=g) * 800 - 400,
+                           torch.rand(n, generator=g) * 6 - 3]).to(dev)
+        en.set_target_vel(vel, torch.tensor([[1000.0], [1000.0], [30.0]], device=dev).expand(3, n).contiguous(),
+                          torch.tensor([[10000.0], [10000.0], [300.0]], device=dev).expand(3, n).contiguous())
+        return en
+
+    e = driven("kf6")
+    timed("control_step_2p20", lambda k: e.control(rpm[k % R]), e)
+    e = driven("kf6")
+    fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    timed("isr_kf6_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R], gyro_z_dps=gz[k % R], rpm=rpm[k % R]), e)
+    del yaw, gz, rpm, fr
+    torch.cuda.empty_cache()
+    return out
+
+
 def cfg4_shard(dev, stream, ticks: int, trig):
     """BASELINE.json configs[3] on one GPU: its 2^21-robot per-GPU shard of the 16M fleet, the
     tick alone, with the fused ensemble record (+ fold) every 16th tick and every tick (K = 16
@@ -577,6 +676,7 @@ def main():
     if not args.no_secondary and world == 1:  # single-GPU configs: one line at N=1
         torch.cuda.empty_cache()
         out["secondary"] = secondary_configs(dev, stream, args.secondary_ticks, trig)
+        out["path_rows"] = path_rows(dev, stream, max(args.secondary_ticks, 20), trig)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         y = yaw[:8, : 1 << 18].cpu().numpy()
         g = gz[:8, : 1 << 18].cpu().numpy()
