@@ -72,7 +72,42 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 // input-latency hiding of the KF6 k_kf6p, kernels_kf6.hip).
 // LTAB (TABLE512): the sine table as a wave-private LDS copy (its loads issued first, as in
 // the KF kernels) instead of gathers from the global table after the state arrives
-template <bool LIBM, bool LTAB = true>
+// tick inputs non-temporal (gfx950 `nt`), as kf6_lane.hpp reads them
+#ifndef FMSKF_IN_CPOL
+#define FMSKF_IN_CPOL 2
+#endif
+
+// POL: every plane through a scalar buffer descriptor at its block chunk (wave-uniform base
+// hb, lane offset < 256 elements, any N up to the 2^30 cap) so the loads and stores carry a
+// cache policy, as in the KF6 tick (kf6_lane.hpp): the tick inputs (read once) non-temporal,
+// the state loaded with CP and stored with st_pol(CP) (`sc1` while it fits the Infinity
+// Cache, non-temporal past it)
+template <typename T, int POL>
+__device__ __forceinline__ T ld_chunk(const T *plane, uint64_t hb, uint64_t n, uint32_t li) {
+  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
+  if constexpr (sizeof(T) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, li * 8u, 0, POL);
+    const uint32_t lo = v[0], hi = v[1];  // element copies (see kf6_load_in)
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, li * 4u, 0, POL));
+  }
+}
+template <typename T, int POL>
+__device__ __forceinline__ void st_chunk(T *plane, uint64_t hb, uint64_t n, uint32_t li, T v) {
+  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    v2u32_t w;
+    w[0] = (uint32_t)u;
+    w[1] = (uint32_t)(u >> 32);
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, li * 8u, 0, POL);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, li * 4u, 0, POL);
+  }
+}
+
+template <bool LIBM, bool LTAB = true, bool POL = true, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -86,13 +121,28 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   float yaw[2];
   uint2 rw[2];
   int64_t sum[2][4];
+  uint64_t hb[2];
+  uint32_t li[2];
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const uint64_t i = i0 + r * G < n ? i0 + r * G : n - 1;
-    yaw[r] = a.in.yaw_deg[i];
-    rw[r] = reinterpret_cast<const uint2 *>(a.in.rpm)[i];
+    if constexpr (POL) {
+      // the wave's first lane fixes its 256-robot chunk; clamped lanes (n - 1) stay inside it
+      hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
+      li[r] = (uint32_t)(i - hb[r]);
+      yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
+      const uint64_t rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm),
+                                                            hb[r], n, li[r]);
+      rw[r] = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
 #pragma unroll
-    for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * a.in.sum_pitch + i];
+      for (int w = 0; w < 4; w++)
+        sum[r][w] = ld_chunk<int64_t, FMSKF_IN_CPOL>(a.in.angle_sum + w * a.in.sum_pitch, hb[r], n, li[r]);
+    } else {
+      yaw[r] = a.in.yaw_deg[i];
+      rw[r] = reinterpret_cast<const uint2 *>(a.in.rpm)[i];
+#pragma unroll
+      for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * a.in.sum_pitch + i];
+    }
   }
   tv.store(wtab[WT ? threadIdx.x >> 6 : 0]);
 #pragma unroll
@@ -100,20 +150,36 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     const uint64_t i = i0 + r * G;
     if (i >= n) return;
     RsLane s;
-    s.px = a.x[i];
-    s.py = a.x[pp + i];
+    if constexpr (POL) {
+      s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
+      s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
+#pragma unroll
+      for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
+    } else {
+      s.px = a.x[i];
+      s.py = a.x[pp + i];
+#pragma unroll
+      for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
+    }
     s.th = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
     rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], tab);
-    a.x[i] = s.px;
-    a.x[pp + i] = s.py;
-    a.x[2 * pp + i] = s.th;
-    a.x[3 * pp + i] = s.vx;
-    a.x[4 * pp + i] = s.vy;
-    a.x[5 * pp + i] = s.vth;
+    if constexpr (POL) {
+      constexpr int SP = st_pol(CP);
+      const float xs[6] = {s.px, s.py, s.th, s.vx, s.vy, s.vth};
 #pragma unroll
-    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+      for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
+#pragma unroll
+      for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
+    } else {
+      a.x[i] = s.px;
+      a.x[pp + i] = s.py;
+      a.x[2 * pp + i] = s.th;
+      a.x[3 * pp + i] = s.vx;
+      a.x[4 * pp + i] = s.vy;
+      a.x[5 * pp + i] = s.vth;
+#pragma unroll
+      for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+    }
   }
 }
 
@@ -134,9 +200,24 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
       const char *e = getenv("FMSKF_RS_GTAB");
       return e && atoi(e) != 0;
     }();
-    if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
-    else if (gtab) k_rs2<false, false><<<g2, kBlock, lds, st>>>(a);
-    else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
+    static const bool pol = [] {  // A/B switch (FMSKF_RS_POL=0: plain global loads and stores)
+      const char *e = getenv("FMSKF_RS_POL");
+      return !e || atoi(e) != 0;
+    }();
+    const bool nt = state_nt(s.n * 124);
+    if (!pol) {
+      if (libm) k_rs2<true, true, false><<<g2, kBlock, lds, st>>>(a);
+      else if (gtab) k_rs2<false, false, false><<<g2, kBlock, lds, st>>>(a);
+      else k_rs2<false, true, false><<<g2, kBlock, lds, st>>>(a);
+    } else if (nt) {
+      if (libm) k_rs2<true, true, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+      else if (gtab) k_rs2<false, false, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+      else k_rs2<false, true, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+    } else {
+      if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
+      else if (gtab) k_rs2<false, false><<<g2, kBlock, lds, st>>>(a);
+      else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
+    }
     return (int)hipGetLastError();
   }
   if (libm) {
