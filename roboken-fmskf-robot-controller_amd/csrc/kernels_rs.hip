@@ -77,36 +77,10 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 #define FMSKF_IN_CPOL 2
 #endif
 
-// POL: every plane through a scalar buffer descriptor at its block chunk (wave-uniform base
-// hb, lane offset < 256 elements, any N up to the 2^30 cap) so the loads and stores carry a
-// cache policy, as in the KF6 tick (kf6_lane.hpp): the tick inputs (read once) non-temporal,
-// the state loaded with CP and stored with st_pol(CP) (`sc1` while it fits the Infinity
-// Cache, non-temporal past it)
-template <typename T, int POL>
-__device__ __forceinline__ T ld_chunk(const T *plane, uint64_t hb, uint64_t n, uint32_t li) {
-  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
-  if constexpr (sizeof(T) == 8) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, li * 8u, 0, POL);
-    const uint32_t lo = v[0], hi = v[1];  // element copies (see kf6_load_in)
-    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
-  } else {
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, li * 4u, 0, POL));
-  }
-}
-template <typename T, int POL>
-__device__ __forceinline__ void st_chunk(T *plane, uint64_t hb, uint64_t n, uint32_t li, T v) {
-  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
-  if constexpr (sizeof(T) == 8) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    v2u32_t w;
-    w[0] = (uint32_t)u;
-    w[1] = (uint32_t)(u >> 32);
-    __builtin_amdgcn_raw_buffer_store_b64(w, r, li * 8u, 0, POL);
-  } else {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, li * 4u, 0, POL);
-  }
-}
-
+// POL: every plane through a scalar buffer descriptor at its block chunk (ld_chunk /
+// st_chunk, kf_generic.hpp) so the loads and stores carry a cache policy, as in the KF6 tick
+// (kf6_lane.hpp): the tick inputs (read once) non-temporal, the state loaded with CP and
+// stored with st_pol(CP) (`sc1` while it fits the Infinity Cache, non-temporal past it)
 template <bool LIBM, bool LTAB = true, bool POL = true, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   extern __shared__ double occ_cap[];

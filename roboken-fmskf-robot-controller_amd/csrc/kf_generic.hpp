@@ -73,6 +73,35 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
 
+// One element of a plane at a lane of a 256-robot chunk starting at hb (wave-uniform: the
+// wave's first lane rounded down; clamped lanes stay inside the chunk), through a scalar
+// descriptor so the access carries the cache policy POL (any N up to the 2^30 cap: the lane
+// offset stays below 256 elements).
+template <typename T, int POL>
+__device__ __forceinline__ T ld_chunk(const T *plane, uint64_t hb, uint64_t n, uint32_t li) {
+  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
+  if constexpr (sizeof(T) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, li * 8u, 0, POL);
+    const uint32_t lo = v[0], hi = v[1];  // element copies (see kf6_load_in)
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, li * 4u, 0, POL));
+  }
+}
+template <typename T, int POL>
+__device__ __forceinline__ void st_chunk(T *plane, uint64_t hb, uint64_t n, uint32_t li, T v) {
+  const auto r = rsrc(plane + hb, (n - hb) * sizeof(T));
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    v2u32_t w;
+    w[0] = (uint32_t)u;
+    w[1] = (uint32_t)(u >> 32);
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, li * 8u, 0, POL);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, li * 4u, 0, POL);
+  }
+}
+
 // One tiled state array (ROWS rows, W = tile_w<T>() wide; fmskf_internal.hpp st_at) as one
 // chunk of kBlock instances sees it (by default the calling block's own chunk): the chunk's
 // base is wave-uniform (a scalar descriptor), rows sit W elements apart (a scalar offset per
