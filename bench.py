@@ -39,6 +39,35 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def launcher_cmd(argv, env) -> list[str] | None:
+    """`--gpus N > 1` without a launcher around us (no WORLD_SIZE in the environment): the
+    torch.distributed.run command that runs this same bench as N ranks, one per GPU (None when
+    no spawn is needed).  The parent never imports torch or touches a GPU; it starts the
+    launcher as a child process and exits with its status (no exec of a GPU process)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args(argv)
+    if a.gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def cpu_share() -> dict:
+    """What the CPU baseline may use on this host: the process's CPU affinity and the OpenMP
+    thread count (OMP_NUM_THREADS; the GPU pool sets 16, each GPU's share of the host)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return {"affinity_cpus": aff, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "host_cpus": os.cpu_count()}
+
+
 def cpu_model() -> str:
     """The host CPU's model string (/proc/cpuinfo, as lscpu prints it)."""
     try:
@@ -78,14 +107,50 @@ def cpu_baseline(yaw, gz, rpm, sample_s: float):
                 break
         res[label] = (n * ticks / el, ticks, el)
     v, ticks, el = res["all"]
+    share = cpu_share()
     return {
         "value": v, "unit": "steps/s", "cores": threads, "kind": "port",
+        "cores_why": f"OpenMP threads = omp_get_max_threads() = {threads} (OMP_NUM_THREADS="
+                     f"{share['omp_num_threads_env']}: the pool's per-GPU CPU share); process affinity "
+                     f"{share['affinity_cpus']} of {share['host_cpus']} host CPUs",
+        **share,
         "sample": f"{n} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick, "
                   f"oracle/fmskf_oracle.c -O3 -ffp-contract=off, OpenMP {threads} threads; "
                   f"1 thread: {n} instances x {res['one'][1]} ticks ({res['one'][2]:.1f} s)",
         "cpu_model": cpu_model(),
         "value_1core": res["one"][0],
     }
+
+
+def parity_sample(eng, applied, yaw, gz, rpm, trig, seed=0, k=2048):
+    """The bench engine's state after every tick it ran (`applied`: the ring index of each, in
+    order) against the oracle's restatement of the same sequence on k sampled robots (the first,
+    the last and k - 2 seeded random ones): bit-exact or not.  Test infrastructure used as the
+    checker after the timed regions, never inside them."""
+    import numpy as np
+    import fmskf
+    from oracle import oracle as orc
+    n = eng.n
+    rng = np.random.default_rng(1234 + seed)
+    idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, max(0, k - 2))]))
+    ti = __import__("torch").from_numpy(idx).to(yaw.device)
+    ys = yaw[:, ti].cpu().numpy()
+    gs = gz[:, ti].cpu().numpy()
+    rs = np.ascontiguousarray(rpm[:, ti].cpu().numpy())
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]),
+                         orc.TRIG_LIBM if trig == fmskf.TRIG_LIBM else orc.TRIG_TABLE512)
+    m = idx.size
+    xo = np.zeros((6, m), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], m, 1).copy()
+    for r in applied:
+        orc.kf6_tick(xo, Po, np.ascontiguousarray(ys[r]), np.ascontiguousarray(gs[r]),
+                     np.ascontiguousarray(rs[r]), None, prm, nthreads=0)
+    x, P = eng.get_state()
+    bad = ~(np.all(x[:, idx].view(np.uint32) == xo.view(np.uint32), axis=0) &
+            np.all(P[:, idx].view(np.uint32) == Po.view(np.uint32), axis=0))
+    return {"robots": int(m), "ticks": len(applied), "mismatched_robots": int(bad.sum()),
+            "bitexact": not bool(bad.any()), "against": "oracle/fmskf_oracle.c orc_kf6_tick"}
 
 
 def secondary_configs(dev, stream, ticks: int, trig):
@@ -302,6 +367,14 @@ def cfg4_shard(dev, stream, ticks: int, trig):
 
 
 def main():
+    cmd = launcher_cmd(sys.argv[1:], os.environ)
+    if cmd is not None:  # --gpus N > 1 with no launcher: run the N ranks as a child
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        print(f"bench: --gpus {cmd[4].split('=')[1]} without a launcher: {' '.join(cmd[1:9])} ...",
+              file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd, env=env).returncode)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
@@ -316,10 +389,13 @@ def main():
     ap.add_argument("--cpu-sample-s", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused multi-tick figure")
-    ap.add_argument("--gather", choices=["async", "stream", "native"], default="async",
-                    help="N > 1: torch.distributed all-gather on RCCL's stream (async) or in the tick "
-                         "stream; native: the handle's own communicator (fmskf_comm_init + "
-                         "fmskf_ensemble_stats, the path C callers bind; host-synchronous)")
+    ap.add_argument("--gather", choices=["auto", "async", "stream", "native"], default="auto",
+                    help="N > 1: native (the default with RCCL): libfmskf's own communicator "
+                         "(fmskf_comm_init), fmskf_tick_ensemble_begin / fmskf_ensemble_end -- the "
+                         "fused record, fold + ncclAllGather + copy-out on the handle's side stream "
+                         "overlapping the next ticks, the path C callers bind; async / stream: "
+                         "torch.distributed all-gather on RCCL's stream or in the tick stream "
+                         "(auto = native, or async under gloo / --same-device)")
     ap.add_argument("--ensemble", choices=["fused", "separate"], default="fused",
                     help="ensemble ticks: fmskf_tick_ensemble (the tick kernel writes the record) or "
                          "fmskf_tick + fmskf_ensemble_partial")
@@ -419,30 +495,51 @@ def main():
     ev_count = [0]
     pending = []
 
-    if args.gather == "native":
+    if args.gather == "auto":
+        args.gather = "async" if (gloo or args.same_device) else "native"
+    if args.gather == "native" and distributed:
         # the handle's own RCCL communicator: rank 0's unique id reaches the others over the
-        # torch.distributed group (or stays local at world 1)
+        # torch.distributed group (without a launcher there is no communicator: the side stream
+        # folds and copies out this GPU's record alone)
         uid = [fmskf.comm_unique_id() if rank == 0 else None]
-        if distributed:
-            dist.broadcast_object_list(uid, src=0)
+        dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0], rank, world)
     native_stats = [None]
+    native_pending = [0]
+    # ring index of every tick applied to `eng`, in order: the post-timing parity replay
+    applied = []
+
+    def tick(r, src=None):
+        eng.tick_prepared((src or prepared)[r], tick_fn)
+        applied.append(r)
+
+    def native_collect(keep):
+        """fmskf_ensemble_end of the oldest pending events until `keep` remain"""
+        while native_pending[0] > keep:
+            native_stats[0] = eng.ensemble_end()
+            native_pending[0] -= 1
 
     def ens_event(k):
         """one ensemble event after tick k: record (fused into the tick, or a separate pass),
         then this rank's share of the all-gather"""
         e = ev_count[0] % n_events
         if args.gather == "native":
-            eng.tick_prepared(prepared[k % R], tick_fn)
-            native_stats[0] = eng.ensemble_stats()
+            # fused tick + record, then fold / ncclAllGather / copy-out on the handle's side
+            # stream; the previous event's result is collected (it finished during this tick's
+            # predecessors), so one event stays in flight behind the ticks
+            eng.tick_ensemble_begin(prepared[k % R])
+            applied.append(k % R)
+            native_pending[0] += 1
+            native_collect(1)
         else:
             # without a process group the "gather" is the identity: the record is written in
             # place into its gather slot
             dst = recs[e] if distributed else gathered[e][0]
             if args.ensemble == "fused":
                 eng.tick_ensemble_prepared(prepared[k % R], dst)
+                applied.append(k % R)
             else:
-                eng.tick_prepared(prepared[k % R], tick_fn)
+                tick(k % R)
                 eng.ensemble_partial(dst)
             if distributed and (args.gather == "stream" or gloo):
                 all_gather(gathered[e].view(-1), recs[e])
@@ -454,9 +551,10 @@ def main():
         if args.ensemble_every > 0 and (k + 1) % args.ensemble_every == 0:
             ens_event(k)
         else:
-            eng.tick_prepared(prepared[k % R], tick_fn)
+            tick(k % R)
 
     def join():
+        native_collect(0)
         while pending:
             pending.pop().wait()  # the current stream waits for the collective
 
@@ -499,7 +597,7 @@ def main():
     ek1 = torch.cuda.Event(enable_timing=True)
     ek0.record(stream)
     for k in range(args.steps):
-        eng.tick_prepared(prepared[k % R], tick_fn)
+        tick(k % R)
     ek1.record(stream)
     torch.cuda.synchronize()
     tick_ms = ek0.elapsed_time(ek1)
@@ -508,7 +606,7 @@ def main():
     if args.inputs == "records":
         ek0.record(stream)
         for k in range(args.steps):
-            eng.tick_prepared(planes[k % R], tick_fn)
+            tick(k % R, planes)
         ek1.record(stream)
         torch.cuda.synchronize()
         planes_ms = ek0.elapsed_time(ek1)
@@ -529,17 +627,21 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for k in range(k1_steps):
-            if args.gather == "native":
-                eng.tick_prepared(prepared[k % R], tick_fn)
-                eng.ensemble_stats()
+            if args.gather == "native":  # begin every tick, each result collected one tick later
+                eng.tick_ensemble_begin(prepared[k % R])
+                applied.append(k % R)
+                native_pending[0] += 1
+                native_collect(1)
                 continue
             if args.ensemble == "fused":
                 eng.tick_ensemble_prepared(prepared[k % R], rec)
+                applied.append(k % R)
             else:
-                eng.tick_prepared(prepared[k % R], tick_fn)
+                tick(k % R)
                 eng.ensemble_partial(rec)
             if distributed:
                 all_gather(gathered[0].view(-1), rec)
+        native_collect(0)
         torch.cuda.synchronize()
         tb = time.perf_counter()
         k1_el = tb - ta
@@ -635,14 +737,18 @@ def main():
                          f"cfg4 strong scaling: {n_global} independent 6-state fp32 KF instances over "
                          f"{world} GPU(s)") +
                         ", fused correct+predict per tick (fmskf_tick; every ensemble_every-th tick "
-                        "fmskf_tick_ensemble, which also writes the ensemble record)",
+                        + ("fmskf_tick_ensemble_begin: the tick kernel also writes the ensemble record, "
+                           "fold + libfmskf's ncclAllGather + copy-out on a side stream, "
+                           "fmskf_ensemble_end one event later)" if args.gather == "native" else
+                           "fmskf_tick_ensemble, which also writes the ensemble record; torch "
+                           "all-gather)"),
             "instances_per_gpu": n,
             "global_instances": n_global,
             "trig": args.trig,
             "inputs": args.inputs,
             "ensemble_every": args.ensemble_every,
             "ensemble": args.ensemble,
-            "gather": args.gather if world > 1 else None,
+            "gather": args.gather,
             "parallelism": f"instance-sharded x{world}" + (
                 (", RCCL all-gather of ensemble records" if not gloo else ", gloo all-gather of ensemble records")
                 if world > 1 else "") + (" (rehearsal: every rank on cuda:0)" if args.same_device else ""),
@@ -671,13 +777,23 @@ def main():
     }
     if ens_check is not None:
         out["ensemble_check"] = ens_check
+    # post-timing parity (outside every timed region): the measured engine's state against the
+    # oracle's restatement of the same tick sequence on sampled robots, bit for bit
+    par = parity_sample(eng, applied, yaw, gz, rpm, trig, seed=rank)
+    if distributed:
+        bad, = max_over_ranks([float(par["mismatched_robots"])])
+        par["mismatched_robots_max_over_ranks"] = int(bad)
+        par["bitexact"] = bad == 0
+    out["parity_sampled"] = par
     eng.close()
     del prepared, planes, krec, many_in
     if not args.no_secondary and world == 1:  # single-GPU configs: one line at N=1
         torch.cuda.empty_cache()
         out["secondary"] = secondary_configs(dev, stream, args.secondary_ticks, trig)
         out["path_rows"] = path_rows(dev, stream, max(args.secondary_ticks, 20), trig)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baseline on rank 0 after every timed region (at N > 1 the other ranks wait at
+    # the final barrier): the same KF6 tick on a bounded 2^18-robot sample
+    if rank == 0 and not args.no_cpu_baseline:
         y = yaw[:8, : 1 << 18].cpu().numpy()
         g = gz[:8, : 1 << 18].cpu().numpy()
         r = rpm[:8, : 1 << 18].cpu().numpy()
@@ -687,6 +803,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:
+        barrier()
         dist.destroy_process_group()
 
 

@@ -241,6 +241,25 @@ int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int r
  * ncclAllGather, fold in rank order on the host -> identical on every rank, deterministic. */
 int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
 
+/* Asynchronous form of the same exchange, for callers that keep ticking while the records
+ * travel (record fused into the tick, gather on a separate stream overlapping
+ * the next tick).  Nothing blocks the host:
+ *   fmskf_tick_ensemble_begin: fmskf_tick whose kernel also writes this rank's block records
+ *     of the post-tick state (KF6, EKF9, KF12D with a positive-definite R; other models tick,
+ *     then run the stand-alone record), on the handle's stream;
+ *   fmskf_ensemble_begin: the stand-alone record of the current state (no tick);
+ *   then, on the handle's side stream: the fold, ncclAllGather over the communicator of
+ *   fmskf_comm_init (skipped without one), the copy of the gathered records to pinned host
+ *   memory.  The next tick on the handle's stream does not wait for any of it.
+ *   fmskf_ensemble_end: waits for the OLDEST pending begin and returns its mean [n] and
+ *     covariance packed [n(n+1)/2] (unbiased, rank-order fold: identical on every rank,
+ *     deterministic).  EINVAL when nothing is pending.
+ * At most two begins may be pending (EINVAL on a third).  Every rank must issue the same
+ * sequence of begins (it is a collective).  Not valid inside a graph capture. */
+int fmskf_tick_ensemble_begin(fmskf_handle h, const fmskf_tick_inputs *in);
+int fmskf_ensemble_begin(fmskf_handle h);
+int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed);
+
 /* ---- vehicle control step -------------------------- */
 /* Per-robot control state is allocated on the first call of any entry point below
  * (~250 B per robot); zero-initialised like the firmware's static objects, power off. */

@@ -121,6 +121,21 @@ struct fmskf_ctx {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   double *ens_gather = nullptr;
+  // asynchronous ensemble (fmskf_tick_ensemble_begin / fmskf_ensemble_begin / _end): two slots,
+  // each with its own block records, shift copy, record, gather buffer and pinned host copy, so
+  // the fold, the all-gather and the D2H of one event run on the side stream `ens_stream` while
+  // the next tick (which writes the other slot's block records) runs on the handle's stream
+  static constexpr int kEnsSlots = 2;
+  struct EnsSlot {
+    double *blocks = nullptr, *shift = nullptr, *rec = nullptr, *gather = nullptr;
+    double *host = nullptr;  // pinned [ranks][len]
+    size_t cap = 0;          // ranks the gather / host buffers hold
+    hipEvent_t ticked = nullptr, folded = nullptr, done = nullptr;
+    bool used = false;       // `folded` has been recorded (the slot's block records are read)
+    int ranks = 1;
+  } eslot[kEnsSlots];
+  hipStream_t ens_stream = nullptr;
+  int ens_head = 0, ens_pending = 0;
   // vehicle control state (allocated on first use) and its parameters
   CtrlDev ctrl{};
   fmskf_ctrl_params cprm{};
@@ -236,6 +251,7 @@ struct fmskf_ctx {
     return oscratch;
   }
   ~fmskf_ctx() {
+    if (ens_stream) (void)hipStreamSynchronize(ens_stream);
     if (stream) (void)hipStreamSynchronize(stream);
     else (void)hipDeviceSynchronize();
     for (void *p : allocs) (void)hipFree(p);
@@ -246,6 +262,12 @@ struct fmskf_ctx {
       if (pin_ev[k]) (void)hipEventDestroy(pin_ev[k]);
     }
     if (pin_out) (void)hipHostFree(pin_out);
+    for (EnsSlot &e : eslot) {
+      if (e.host) (void)hipHostFree(e.host);
+      for (hipEvent_t ev : {e.ticked, e.folded, e.done})
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    if (ens_stream) (void)hipStreamDestroy(ens_stream);
     destroy_comm();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -423,9 +445,18 @@ void zero_motors(fmskf_ctx *h) {
 // load_state, so successive records of one state are bitwise identical
 void ensure_shift(fmskf_ctx *h) {
   if (h->ens_shift_ok) return;
+  // a launch inside a capture is only recorded: the flag would claim a shift that no run wrote
+  // (fmskf_graph_begin takes it before capturing)
+  if (h->capturing) fail(FMSKF_EINVAL, "ensemble shift first taken inside a graph capture");
   launch_check(launch_ens_shift(h->s, (int)h->d.nx, h->d.elem == 8, h->ens_shift, h->stream),
                "ensemble shift launch");
   h->ens_shift_ok = true;
+}
+
+// the models whose tick kernel writes the ensemble block records of the state it stores
+bool fused_record(const fmskf_ctx *h) {
+  return h->cfg.model == FMSKF_MODEL_KF6 || (h->cfg.model == FMSKF_MODEL_EKF9 && h->s.tile) ||
+         (h->cfg.model == FMSKF_MODEL_KF12D && h->s.tile && h->kf12.decor);
 }
 
 void ensure_imu(fmskf_ctx *h) {
@@ -823,6 +854,7 @@ int fmskf_graph_begin(fmskf_handle h) {
     ensure_imu(h);
     ensure_motors(h);
     ensure_ctrl(h);
+    ensure_shift(h);
     hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
               "hipStreamBeginCapture");
     h->capturing = true;
@@ -1289,8 +1321,7 @@ int fmskf_tick_ensemble(fmskf_handle h, const fmskf_tick_inputs *in, double *out
     const uint32_t len = 1 + nx + nx * (nx + 1) / 2;
     double *dst = mem == FMSKF_MEM_DEVICE ? out : h->ens_out;
     ensure_shift(h);
-    if (h->cfg.model == FMSKF_MODEL_KF6 || (h->cfg.model == FMSKF_MODEL_EKF9 && h->s.tile) ||
-        (h->cfg.model == FMSKF_MODEL_KF12D && h->s.tile && h->kf12.decor)) {
+    if (fused_record(h)) {
       // one kernel: the tick writes each block's record of the state it just stored (no
       // second pass over x), then the fold
       TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
@@ -1473,6 +1504,124 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed) {
               "D2H");
     hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
     const int rc = fmskf_ensemble_combine(nx, recs.data(), (uint32_t)ranks, mean, cov_packed);
+    if (rc != FMSKF_OK) fail(rc, "ensemble combine");
+  });
+}
+
+}  // extern "C"
+
+namespace {
+
+// One asynchronous ensemble event (the record fused into the tick, the gather
+// on a separate stream overlapping the next tick).  On the handle's stream: [the tick whose
+// kernel also writes the slot's block records | the stand-alone partial], then an event.  On
+// the side stream, behind that event: the fold into the slot's record, ncclAllGather of the
+// record over the handle's communicator (when there is one), the D2H of the gathered records
+// into the slot's pinned host buffer, an event.  Nothing waits on the host.  A slot's block
+// records are rewritten only after its previous fold has read them (stream-ordered wait).
+void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
+  check_handle(h);
+  if (h->capturing) fail(FMSKF_EINVAL, "asynchronous ensemble inside a graph capture");
+  if (h->ens_pending == fmskf_ctx::kEnsSlots)
+    fail(FMSKF_EINVAL, "two ensemble results pending: call fmskf_ensemble_end first");
+  DeviceGuard g(h->cfg.device);
+  const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
+  const int ranks = h->comm ? h->world : 1;
+  if (!h->ens_stream) {
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    // the highest priority: the fold's 28-91 small blocks are dispatched as soon as CUs free up
+    // between the next tick's blocks instead of queueing behind them
+    hip_check(hipStreamCreateWithPriority(&h->ens_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
+  }
+  const int slot = (h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots;
+  fmskf_ctx::EnsSlot &S = h->eslot[slot];
+  if (!S.blocks) {
+    size_t nb = (size_t)ensemble_nblocks(h->s.n);
+    nb = std::max(nb, (size_t)((h->s.n + kBlock - 1) / kBlock));
+    S.blocks = h->alloc<double>(nb * len);
+    S.shift = h->alloc<double>(12);
+    S.rec = h->alloc<double>(91);
+    for (hipEvent_t *e : {&S.ticked, &S.folded, &S.done})
+      hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+  }
+  if ((size_t)ranks > S.cap) {
+    double *gbuf = h->alloc<double>((size_t)ranks * 91);
+    if (S.gather) h->release(S.gather);
+    S.gather = gbuf;
+    if (S.host) {
+      hip_check(hipEventSynchronize(S.done), "hipEventSynchronize");
+      hip_check(hipHostFree(S.host), "hipHostFree");
+      S.host = nullptr;
+    }
+    hip_check(hipHostMalloc((void **)&S.host, (size_t)ranks * 91 * 8, hipHostMallocDefault), "hipHostMalloc");
+    S.cap = (size_t)ranks;
+  }
+  if (S.used) hip_check(hipStreamWaitEvent(h->stream, S.folded, 0), "hipStreamWaitEvent");
+  ensure_shift(h);
+  // the slot's own shift copy: a later reset / set_state retakes the handle's shift while this
+  // slot's fold may still be queued
+  hip_check(hipMemcpyAsync(S.shift, h->ens_shift, nx * 8, hipMemcpyDeviceToDevice, h->stream), "shift copy");
+  int nb = 0;
+  if (in && fused_record(h)) {
+    TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
+    t.ens_blocks = S.blocks;
+    t.ens_shift = S.shift;
+    const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+    h->time_begin();
+    int e = 0;
+    if (h->cfg.model == FMSKF_MODEL_KF6) e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream, &nb);
+    else if (h->cfg.model == FMSKF_MODEL_EKF9) e = launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream, &nb);
+    else e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream, &nb);
+    launch_check(e, "tick kernel launch");
+    h->time_end();
+  } else {
+    if (in) run_tick(h, in, true, true, 1, h->s.n);
+    launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, S.blocks, S.shift, h->stream, &nb),
+                 "ensemble partial launch");
+  }
+  hip_check(hipEventRecord(S.ticked, h->stream), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(h->ens_stream, S.ticked, 0), "hipStreamWaitEvent");
+  launch_check(launch_ens_fold((int)nx, S.blocks, nb, S.shift, S.rec, h->ens_stream), "ensemble fold launch");
+  hip_check(hipEventRecord(S.folded, h->ens_stream), "hipEventRecord");
+  S.used = true;
+  const double *src = S.rec;
+  if (h->comm) {
+    nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
+               "ncclAllGather");
+    src = S.gather;
+  }
+  hip_check(hipMemcpyAsync(S.host, src, (size_t)ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream), "D2H");
+  hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
+  S.ranks = ranks;
+  h->ens_pending++;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fmskf_tick_ensemble_begin(fmskf_handle h, const fmskf_tick_inputs *in) {
+  return guarded([&] {
+    if (!in) fail(FMSKF_EINVAL, "null inputs");
+    ens_async_begin(h, in);
+  });
+}
+
+int fmskf_ensemble_begin(fmskf_handle h) {
+  return guarded([&] { ens_async_begin(h, nullptr); });
+}
+
+int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed) {
+  return guarded([&] {
+    check_handle(h);
+    if (h->ens_pending == 0) fail(FMSKF_EINVAL, "no ensemble pending (fmskf_*ensemble_begin)");
+    DeviceGuard g(h->cfg.device);
+    fmskf_ctx::EnsSlot &S = h->eslot[h->ens_head];
+    hip_check(hipEventSynchronize(S.done), "hipEventSynchronize");
+    h->ens_head = (h->ens_head + 1) % fmskf_ctx::kEnsSlots;
+    h->ens_pending--;
+    const int rc = fmskf_ensemble_combine(h->d.nx, S.host, (uint32_t)S.ranks, mean, cov_packed);
     if (rc != FMSKF_OK) fail(rc, "ensemble combine");
   });
 }

@@ -266,6 +266,9 @@ int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const d
                     double *out, hipStream_t st);
 int launch_ens_fold(int nx, const double *blocks, int nb, const double *shift, double *out,
                     hipStream_t st);
+// the stand-alone partial alone (no fold): *nb receives the block-record count
+int launch_ens_partial(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
+                       hipStream_t st, int *nb);
 int launch_ens_shift(const DevState &s, int nx, bool f64, double *shift, hipStream_t st);
 int ensemble_nblocks(uint64_t n);
 // vehicle control step, TX frames, VehicleInfo export (kernels_ctrl.hip)

@@ -191,6 +191,7 @@ __global__ void k_ens_shift(const T *x, uint64_t pp, uint32_t tile, double *shif
   if (k < NX) shift[k] = (double)x[st_at(tile, pp, NX, k, 0)];
 }
 
+// the stand-alone partial (block records of x); then, with `out`, the fold
 template <int NX, typename T>
 static void ens_launch(const DevState &s, double *blocks, const double *shift, double *out,
                        hipStream_t st) {
@@ -214,7 +215,7 @@ static void ens_launch(const DevState &s, double *blocks, const double *shift, d
     else if (r == 8) go(TF{}, R8{});
     else go(TF{}, R4{});
   }
-  fold_launch<NX>(blocks, nb, shift, out, st);
+  if (out) fold_launch<NX>(blocks, nb, shift, out, st);
 }
 
 int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
@@ -224,6 +225,12 @@ int launch_ensemble(const DevState &s, int nx, bool f64, double *blocks, const d
   else if (nx == 12 && f64) ens_launch<12, double>(s, blocks, shift, out, st);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
+}
+
+int launch_ens_partial(const DevState &s, int nx, bool f64, double *blocks, const double *shift,
+                       hipStream_t st, int *nb) {
+  *nb = ensemble_nblocks(s.n);
+  return launch_ensemble(s, nx, f64, blocks, shift, nullptr, st);
 }
 
 int launch_ens_fold(int nx, const double *blocks, int nb, const double *shift, double *out,

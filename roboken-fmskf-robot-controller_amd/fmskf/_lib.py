@@ -123,6 +123,9 @@ SIGNATURES = {
     "fmskf_comm_unique_id": (C.c_int, [_P]),
     "fmskf_comm_init": (C.c_int, [_H, _P, C.c_int, C.c_int]),
     "fmskf_ensemble_stats": (C.c_int, [_H, _P, _P]),
+    "fmskf_tick_ensemble_begin": (C.c_int, [_H, C.POINTER(TickInputs)]),
+    "fmskf_ensemble_begin": (C.c_int, [_H]),
+    "fmskf_ensemble_end": (C.c_int, [_H, _P, _P]),
     "fmskf_ctrl_params_init": (C.c_int, [C.POINTER(CtrlParams)]),
     "fmskf_set_ctrl_params": (C.c_int, [_H, C.POINTER(CtrlParams)]),
     "fmskf_set_power": (C.c_int, [_H, _P, C.c_uint32]),

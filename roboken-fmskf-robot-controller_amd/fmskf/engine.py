@@ -332,6 +332,30 @@ class Engine:
                                           cov.ctypes.data_as(C.c_void_p)), "ensemble_stats")
         return mean, cov
 
+    def tick_ensemble_begin(self, prepared=None, **kw):
+        """fmskf_tick_ensemble_begin: one tick whose kernel also writes this rank's ensemble
+        record; fold + all-gather + copy-out run on the handle's side stream (no host wait).
+        `prepared` (from prepare()) or tick inputs as keywords."""
+        if prepared is not None:
+            ref = prepared[2]
+        else:
+            ti, _keep = self._inputs(kw)
+            ref = C.byref(ti)
+        check(load().fmskf_tick_ensemble_begin(self.h, ref), "tick_ensemble_begin")
+
+    def ensemble_begin(self):
+        """fmskf_ensemble_begin: the stand-alone record of the current state, asynchronously"""
+        check(load().fmskf_ensemble_begin(self.h), "ensemble_begin")
+
+    def ensemble_end(self):
+        """fmskf_ensemble_end: (mean, cov packed) of the oldest pending begin"""
+        nx = self.nx
+        mean = np.empty(nx, np.float64)
+        cov = np.empty(nx * (nx + 1) // 2, np.float64)
+        check(load().fmskf_ensemble_end(self.h, mean.ctypes.data_as(C.c_void_p),
+                                        cov.ctypes.data_as(C.c_void_p)), "ensemble_end")
+        return mean, cov
+
     # ------------------------------------------------------------------ control step
     def set_ctrl_params(self, **kw):
         """FF_PI_D / interpolator / current-limit parameters (fmskf_ctrl_params); unspecified

@@ -45,39 +45,64 @@ def _i16(x):
     return np.clip(np.rint(x), -32768, 32767).astype(np.int16)
 
 
+def _robot_params(rng, n):
+    """Per-robot commanded motion: body velocity (|v| <= 400 mm/s), yaw rate, initial heading,
+    modulation phase"""
+    v = rng.uniform(-400.0, 400.0, (2, n))
+    nrm = np.maximum(1.0, np.hypot(v[0], v[1]) / 400.0)
+    v = v / nrm
+    w = rng.uniform(-np.pi, np.pi, n)
+    th0 = rng.uniform(-np.pi, np.pi, n)
+    ph = rng.uniform(0, 2 * np.pi, n)
+    return v, w, th0, ph
+
+
+def trajectory_chunks(n: int, ticks: int, chunk: int = 1000, seed: int = SEED, dt: float = 1e-3,
+                      noise: bool = True):
+    """A long trace of n robots generated `chunk` ticks at a time (memory bounded): yields
+    (t0, Trajectory of ticks t0 .. t0 + chunk - 1).  The robots' motion continues across chunks;
+    each chunk draws its sensor noise from its own seeded stream."""
+    params = _robot_params(np.random.default_rng(seed), n)
+    carry = None
+    for k, t0 in enumerate(range(0, ticks, chunk)):
+        tr = Trajectory(n, min(chunk, ticks - t0), dt=dt, noise=noise, t0=t0, params=params,
+                        carry=carry, rng=np.random.default_rng([seed, k]))
+        carry = (tr.px[-1], tr.py[-1], tr.angle_sum[-1])
+        yield t0, tr
+
+
 class Trajectory:
     """Ground truth + sensor readings of n robots over `ticks` 1 kHz ticks.
 
     Arrays are tick-major: [T, N] (and [T, N, 4] per wheel)."""
 
-    def __init__(self, n: int, ticks: int, seed: int = SEED, dt: float = 1e-3, noise: bool = True):
-        rng = np.random.default_rng(seed)
+    def __init__(self, n: int, ticks: int, seed: int = SEED, dt: float = 1e-3, noise: bool = True,
+                 t0: int = 0, params=None, carry=None, rng=None):
+        # t0 / params / carry / rng: one chunk of a longer trace (trajectory_chunks); the
+        # defaults give the whole trace at once (the committed fixtures depend on that path)
+        rng = np.random.default_rng(seed) if rng is None else rng
         self.n, self.ticks, self.dt = n, ticks, dt
-        v = rng.uniform(-400.0, 400.0, (2, n))
-        nrm = np.maximum(1.0, np.hypot(v[0], v[1]) / 400.0)
-        v = v / nrm
-        w = rng.uniform(-np.pi, np.pi, n)
-        th0 = rng.uniform(-np.pi, np.pi, n)
-        ph = rng.uniform(0, 2 * np.pi, n)
-        t = np.arange(ticks)[:, None] * dt
+        v, w, th0, ph = _robot_params(rng, n) if params is None else params
+        t = (t0 + np.arange(ticks))[:, None] * dt
         mod = 1.0 + 0.3 * np.sin(2 * np.pi * 0.5 * t + ph[None, :])
         self.vbx = v[0][None, :] * mod            # body mm/s
         self.vby = v[1][None, :] * mod
         self.w = np.broadcast_to(w[None, :], (ticks, n)).copy()   # rad/s
-        th = th0[None, :] + np.cumsum(self.w * dt, axis=0) - self.w * dt
+        th = th0[None, :] + np.cumsum(self.w * dt, axis=0) - self.w * dt + self.w * (dt * t0)
         self.th = (th + np.pi) % (2 * np.pi) - np.pi              # [-pi, pi)
         c, s = np.cos(self.th), np.sin(self.th)
         self.vx_w = (self.vbx * c - self.vby * s) * 1e-3           # world m/s
         self.vy_w = (self.vbx * s + self.vby * c) * 1e-3
-        self.px = np.cumsum(self.vx_w * dt, axis=0)
-        self.py = np.cumsum(self.vy_w * dt, axis=0)
+        px0, py0, sum0 = (0.0, 0.0, 0) if carry is None else carry
+        self.px = np.cumsum(self.vx_w * dt, axis=0) + px0
+        self.py = np.cumsum(self.vy_w * dt, axis=0) + py0
         # wheels: output rad/s -> motor rad/s -> rpm; encoder counts (motor shaft, 8192/rev)
         mdir = vdir_to_mdir(self.vbx, self.vby, self.w)            # [T, N, 4] wheel rad/s
         motor_radps = mdir * GEAR
         nz = (lambda sd, shape: rng.normal(0.0, sd, shape)) if noise else (lambda sd, shape: 0.0)
         self.rpm = _i16(motor_radps / float(RPM_TO_RADPS) + nz(2.0, motor_radps.shape))
         counts = motor_radps * dt * 8192.0 / (2 * np.pi)
-        self.angle_sum = np.cumsum(np.rint(counts + nz(2.0, counts.shape)), axis=0).astype(np.int64)
+        self.angle_sum = np.cumsum(np.rint(counts + nz(2.0, counts.shape)), axis=0).astype(np.int64) + sum0
         # IMU registers (native sensor frame; yaw == heading)
         yaw_deg = np.degrees(self.th) + nz(0.05, self.th.shape)
         self.reg_yaw = _i16(yaw_deg / 180.0 * 32768.0)

@@ -67,7 +67,7 @@ def _free_port():
 @pytest.mark.parametrize("ensemble", ["fused", "separate"])
 def test_bench_distributed_path_world1(gather, ensemble):
     if gather == "native" and ensemble == "separate":
-        pytest.skip("the native path records with fmskf_ensemble_stats itself")
+        pytest.skip("the native path records through fmskf_tick_ensemble_begin itself")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
@@ -84,6 +84,26 @@ def test_bench_distributed_path_world1(gather, ensemble):
     assert chk["cov_max_rel"] < 1e-9, chk
     assert out["nonfinite_instances"] == 0
     assert out["value"] > 1e9
+    assert out["parity_sampled"]["bitexact"], out["parity_sampled"]
+    assert out["config"]["gather"] == gather
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """`python bench.py --gpus 2` with no launcher (the driver's BENCH command form): bench.py
+    starts torch.distributed.run itself, two ranks (gloo, both on the one GPU of the test box),
+    the line reports n_gpus 2, a green ensemble check and the post-timing parity sample."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--same-device", "--steps", "20",
+           "--warmup", "5", "--n-per-gpu", str(1 << 18), "--ensemble-every", "8", "--no-fused",
+           "--no-secondary", "--check-ensemble", "--cpu-sample-s", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["global_instances"] == 2 << 18
+    chk = out["ensemble_check"]
+    assert chk["count"] == 2 << 18 and chk["mean_max_rel"] < 1e-12 and chk["cov_max_rel"] < 1e-9, chk
+    assert out["parity_sampled"]["bitexact"]
+    assert out["cpu_baseline"]["value"] > 0 and out["cpu_baseline"]["affinity_cpus"] >= 1
 
 
 @pytest.mark.parametrize("strong", [False, True])

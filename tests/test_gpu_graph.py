@@ -106,3 +106,39 @@ def test_graph_errors():
             e.graph_begin()            # null stream: capture refused
         with pytest.raises(fmskf.FmskfError):
             e.graph_launch(1)          # nothing captured
+
+
+@pytest.mark.parametrize("model", ["kf6", "ekf9"])
+def test_graph_captures_tick_ensemble(model):
+    """fmskf_tick_ensemble captured as the first record of a fresh handle: the shift vector is
+    taken by fmskf_graph_begin before the capture (a launch inside a capture would only be
+    recorded), so every replay's record equals the record of the same call made directly."""
+    import torch
+    n, T = 5003, 4
+    tr = Trajectory(n, T, seed=74)
+    st = torch.cuda.Stream()
+    if model == "kf6":
+        yaw, gz, rpm = tr.kf6_inputs()
+        src = [dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t]) for t in range(T)]
+    else:
+        raw = tr.ekf9_raw()
+        src = [dict(raw=raw[t]) for t in range(T)]
+    with torch.cuda.stream(st), Engine(model, n) as a, Engine(model, n) as b:
+        for e in (a, b):
+            e.set_stream(st)
+        dev = {k: torch.empty(v.shape, dtype=getattr(torch, str(v.dtype)), device="cuda")
+               for k, v in src[0].items()}
+        rb = torch.empty(b.ensemble_record_len(), dtype=torch.float64, device="cuda")
+        b.graph_begin()
+        b.tick_ensemble(out=rb, **dev)
+        b.graph_end()
+        for t in range(T):
+            for k, v in src[t].items():
+                dev[k].copy_(torch.from_numpy(v))
+            ra = a.tick_ensemble(**dev)
+            b.graph_launch()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(ra, rb.cpu().numpy())
+        xa, _ = a.get_state()
+        xb, _ = b.get_state()
+    np.testing.assert_array_equal(xa.view(np.uint32), xb.view(np.uint32))

@@ -41,6 +41,39 @@ def test_kf6_past_the_buffer_window(orc):
     np.testing.assert_array_equal(P[:, idx].view(np.uint32), Po.view(np.uint32))
 
 
+def test_kf6_headline_instantiation_2p20(orc):
+    """The bench's exact headline kernel: the single fused tick fed 16-byte fmskf_kf6_records at
+    exactly 2^20 robots (k_kf6p<4, 2, Opt<TABLE512, UPD, PRED, SMALL, !VALID, REC>>, two robots per
+    lane while the state fits the Infinity Cache), fed by the bench's own input generator (the
+    64-tick HBM ring of kf6_ring_torch) for 70 ticks (the ring wraps), sampled bit-exact
+    against the oracle."""
+    import torch
+    from fmskf.synth import kf6_ring_torch
+    n, R, T = 1 << 20, 64, 70
+    yaw, gz, rpm = kf6_ring_torch(n, R, seed=2024, device="cuda")
+    recs = fmskf.kf6_records(yaw, gz, rpm)
+    with Engine("kf6", n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        prepared = [e.prepare(kf6_rec=recs[r]) for r in range(R)]
+        for t in range(T):
+            e.tick_prepared(prepared[t % R])
+        x, P = e.get_state()
+        assert e.get_counters()[0] == 0
+    idx = _sample(n, seed=20)
+    ti = torch.from_numpy(idx).cuda()
+    ys, gs, rs = (a[:, ti].cpu().numpy() for a in (yaw, gz, rpm))
+    cfg = fmskf.default_config("kf6", idx.size)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
+    xo = np.zeros((6, idx.size), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], idx.size, 1).copy()
+    for t in range(T):
+        r = t % R
+        orc.kf6_tick(xo, Po, np.ascontiguousarray(ys[r]), np.ascontiguousarray(gs[r]),
+                     np.ascontiguousarray(rs[r]), None, prm, nthreads=0)
+    np.testing.assert_array_equal(x[:, idx].view(np.uint32), xo.view(np.uint32))
+    np.testing.assert_array_equal(P[:, idx].view(np.uint32), Po.view(np.uint32))
+
+
 @pytest.mark.parametrize("n", [36_000_000, 46_000_000])
 def test_control_past_the_buffer_window(orc, n):
     """36M: the 36 interpolator planes (144 B per robot) pass 4 GiB while the 24 FF_PI_D planes

@@ -72,3 +72,79 @@ def test_sharded_handles_fold_to_the_whole_fleet(model):
     packed = np.array([ref[i, j] for i in range(x.shape[0]) for j in range(i + 1)])
     np.testing.assert_allclose(cs, packed, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(ms, x.astype(np.float64).mean(axis=1), rtol=1e-12)
+
+
+def _ens_inputs(model, n, T, seed):
+    tr = Trajectory(n, T, seed=seed)
+    if model == "kf6":
+        yaw, gz, rpm = tr.kf6_inputs()
+        return lambda t: dict(yaw_deg=yaw[t], gyro_z_dps=gz[t], rpm=rpm[t])
+    if model == "ekf9":
+        raw = tr.ekf9_raw()
+        return lambda t: dict(raw=raw[t])
+    if model == "kf12d":
+        z = tr.kf12d_z()
+        return lambda t: dict(z=np.ascontiguousarray(z[t]))
+    ryaw, sums, rrpm = tr.rs_inputs()
+    return lambda t: dict(yaw_deg=ryaw[t], angle_sum=np.ascontiguousarray(sums[t]), rpm=rrpm[t])
+
+
+@pytest.mark.parametrize("model,n,every,comm", [("kf6", 70001, 1, True), ("kf6", 1 << 20, 3, False),
+                                                ("ekf9", 5001, 2, True), ("kf12d", 3001, 1, False),
+                                                ("rs", 4097, 1, True)])
+def test_async_ensemble_matches_sync(model, n, every, comm):
+    """fmskf_tick_ensemble_begin / fmskf_ensemble_end (fold + all-gather + copy-out on the side
+    stream, results collected one event late, so two are pending at every begin with every = 1)
+    against the synchronous fmskf_tick_ensemble of a twin handle on the same inputs: the states
+    stay bit-identical and every (mean, cov) equals the fold of the synchronous record bit for
+    bit, with and without a (world-1) RCCL communicator."""
+    T = 9
+    kw = _ens_inputs(model, n, T, seed=63)
+    with Engine(model, n) as a, Engine(model, n) as b:
+        if comm:
+            b.comm_init(fmskf.comm_unique_id(), 0, 1)
+        want, got, pending = [], [], 0
+        for t in range(T):
+            if (t + 1) % every == 0:
+                want.append(fmskf.ensemble_combine(a.nx, a.tick_ensemble(**kw(t))[None, :]))
+                b.tick_ensemble_begin(**kw(t))
+                pending += 1
+                if pending == 2:
+                    got.append(b.ensemble_end())
+                    pending -= 1
+            else:
+                a.tick(**kw(t))
+                b.tick(**kw(t))
+        while pending:
+            got.append(b.ensemble_end())
+            pending -= 1
+        with pytest.raises(fmskf.FmskfError):
+            b.ensemble_end()                               # nothing pending
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        # the stand-alone asynchronous record of the current state (no tick)
+        b.ensemble_begin()
+        ms, cs = b.ensemble_end()
+        mp, cp = fmskf.ensemble_combine(b.nx, b.ensemble_partial()[None, :])
+    np.testing.assert_array_equal(xa.view(np.uint8), xb.view(np.uint8))
+    if Pa is not None:
+        np.testing.assert_array_equal(Pa.view(np.uint8), Pb.view(np.uint8))
+    assert len(got) == len(want) == T // every
+    for (mw, cw), (mg, cg) in zip(want, got):
+        np.testing.assert_array_equal(mw, mg)
+        np.testing.assert_array_equal(cw, cg)
+    np.testing.assert_array_equal(ms, mp)
+    np.testing.assert_array_equal(cs, cp)
+
+
+def test_async_ensemble_limits():
+    with Engine("kf6", 1000) as e:
+        e.ensemble_begin()
+        e.ensemble_begin()
+        with pytest.raises(fmskf.FmskfError):
+            e.ensemble_begin()                              # a third pending begin
+        e.ensemble_end()
+        e.ensemble_end()
+        e.ensemble_begin()                                  # the slots are reusable
+        m, c = e.ensemble_end()
+    assert np.all(m == 0.0) and np.all(c == 0.0)            # zero state: zero moments

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Long-horizon accuracy probe (CPU only): the fp32 oracle (= the kernels' operation order)
+against the independent fp64 dense restatement (oracle/kf_ref.py), N robots x T ticks, errors
+sampled every `--every` ticks, relative per physical group as tests/test_oracle_kf_fp64.py
+judges them.  Prints the worst error per group and the tick it occurred at.
+
+  python tools/kf_accuracy.py --model ekf9 --n 1024 --ticks 60000
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")]
+
+import fmskf  # noqa: E402
+from fmskf.synth import trajectory_chunks  # noqa: E402
+from oracle import kf_ref, oracle as orc  # noqa: E402
+
+GROUPS = {6: [(0, 1), (2,), (3, 4), (5,)], 9: [(0, 1), (2,), (3, 4), (5, 6), (7, 8)]}
+
+
+def run(model, n, ticks, every, trig, chunk=1000, seed=0x464D534B):
+    cfg = fmskf.default_config(model, n)
+    nx = 6 if model == "kf6" else 9
+    npk = nx * (nx + 1) // 2
+    q = np.array(cfg.q[:npk], np.float32)
+    r = np.array(cfg.r[:(10 if nx == 6 else 21)], np.float32)
+    p0 = np.array(cfg.p0[:npk], np.float32)
+    dt32 = float(np.float32(1e-3))
+    if model == "kf6":
+        prm = orc.kf6_params(1e-3, q, r, trig)
+        ref = kf_ref.Kf6Batch(n, np.zeros(6), p0.astype(np.float64), q.astype(np.float64),
+                              r.astype(np.float64), dt32)
+    else:
+        prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
+        ref = kf_ref.Ekf9Batch(n, np.zeros(9), p0.astype(np.float64), q.astype(np.float64),
+                               r.astype(np.float64), dt32)
+    x = np.zeros((nx, n), np.float32)
+    P = np.repeat(p0[:, None], n, 1).copy()
+    worst = {}
+    scale_run = {g: np.full(n, 1e-3) for g in GROUPS[nx]}
+    t_all = 0
+    for t0, tr in trajectory_chunks(n, ticks, chunk, seed=seed):
+        if model == "kf6":
+            yaw, gz, rpm = tr.kf6_inputs()
+        else:
+            raw = tr.ekf9_raw()
+        for k in range(tr.ticks):
+            if model == "kf6":
+                z = orc.kf6_measure(yaw[k], gz[k], rpm[k], trig)
+                orc.kf6_tick(x, P, yaw[k], gz[k], rpm[k], None, prm, nthreads=8)
+            else:
+                z = orc.ekf9_measure(raw[k])
+                orc.ekf9_tick(x, P, raw[k], None, prm, nthreads=8)
+            ref.step(z.astype(np.float64))
+            t = t0 + k
+            if t % every == every - 1:
+                x64, P64 = ref.packed()
+                for g in GROUPS[nx]:
+                    fs = max(np.max(np.abs(x64[list(g)])), 1e-3)  # fleet scale of the group
+                    for kk in g:
+                        e = float(np.max(np.abs(x[kk] - x64[kk])) / fs)
+                        if e > worst.get(("fleet", kk), (0,))[0]:
+                            worst[("fleet", kk)] = (e, t, -1)
+                    sc = np.maximum(scale_run[g], np.max(np.abs(x64[list(g)]), axis=0))
+                    scale_run[g] = sc
+                    for kk in g:
+                        e = np.abs(x[kk] - x64[kk]) / sc
+                        i = int(np.argmax(e))
+                        if e[i] > worst.get(kk, (0,))[0]:
+                            worst[kk] = (float(e[i]), t, i)
+                ep = np.max(np.abs(P - P64), axis=0) / np.max(np.abs(P64), axis=0)
+                i = int(np.argmax(ep))
+                if ep[i] > worst.get("P", (0,))[0]:
+                    worst["P"] = (float(ep[i]), t, i)
+        t_all += tr.ticks
+    return worst
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", choices=["kf6", "ekf9"], default="kf6")
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--ticks", type=int, default=60000)
+    ap.add_argument("--every", type=int, default=100)
+    ap.add_argument("--trig", type=int, default=0)
+    a = ap.parse_args()
+    t = time.time()
+    w = run(a.model, a.n, a.ticks, a.every, a.trig)
+    for k, v in w.items():
+        print(f"{a.model} {k}: max rel err {v[0]:.3e} at tick {v[1]} robot {v[2]}")
+    print(f"{time.time() - t:.1f} s")
+
+
+if __name__ == "__main__":
+    main()
