@@ -224,8 +224,11 @@ def secondary_configs(dev, stream, ticks: int, trig):
 
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
-    # RS tick: pos 12 r+w, prev 32 r+w, sums 32, yaw 4, rpm 8 in, vel 12 out
+    # RS tick: pos 12 r+w, prev 32 r+w, sums 32, yaw 4, rpm 8 in, vel 12 out (the same bytes with
+    # the sums at a padded pitch, or read from the ingested motor / IMU state)
     "rs_tick_2p20": 144,
+    "rs_tick_2p20_padded_sums": 144,
+    "rs_tick_2p20_device_state": 144,
     # WT901 standard poll: row 48 + len 4, parser window / count / flags 14 r+w, error 1,
     # 15 registers 30 w, magnetometer 6 + q_init 16 r, Data page 64 w
     "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64,
@@ -253,6 +256,16 @@ def path_rows(dev, stream, ticks: int, trig):
     n, R = 1 << 20, 4
     yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 11, device=dev)
     out = {}
+    # memory-side bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same
+    # kernels at 2^20 (tools/pmc_traffic.py paths; profiles/pmc_traffic_paths.json)
+    path_traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_paths.json")
+    if os.path.exists(tpath):
+        try:
+            path_traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
+                            if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
+        except Exception:
+            path_traffic = {}
 
     def timed(key, run, e):
         for k in range(3):
@@ -269,15 +282,34 @@ def path_rows(dev, stream, ticks: int, trig):
         gbps = PATH_BYTES[key] * n / (ms * 1e-3) / 1e9
         out[key] = {"instances": n, "kernel_ms": ms, "robots_per_s": n / (ms * 1e-3), "ticks": ticks,
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                 "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": PATH_BYTES[key]}}
+                                 "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": PATH_BYTES[key],
+                                 "traffic": path_traffic.get(key)}}
         e.close()
 
     e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
     e.set_stream(stream)
-    sums = torch.cumsum(torch.randint(-20, 20, (R, 4, n), device=dev, dtype=torch.int64), 0)
-    preps = [e.prepare(yaw_deg=yaw[r], angle_sum=sums[r], rpm=rpm[r]) for r in range(R)]
+    sums = torch.cumsum(torch.randint(-20, 20, (R, 4, n + 512), device=dev, dtype=torch.int64), 0)
+    # the caller's [4][N] sum planes at the power-of-two stride N, and at a padded pitch
+    # (fmskf_tick_inputs.angle_sum_pitch = N + 512)
+    dense = sums[:, :, :n].contiguous()
+    preps = [e.prepare(yaw_deg=yaw[r], angle_sum=dense[r], rpm=rpm[r]) for r in range(R)]
     timed("rs_tick_2p20", lambda k: e.tick_prepared(preps[k % R]), e)
-    del preps, sums
+    e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    preps = [e.prepare(yaw_deg=yaw[r], angle_sum=sums[r], rpm=rpm[r]) for r in range(R)]
+    timed("rs_tick_2p20_padded_sums", lambda k: e.tick_prepared(preps[k % R]), e)
+    del preps, sums, dense
+    # the firmware pipeline's form: every input from the device-resident ingest state (yaw from
+    # the IMU Data page, sums and rpm from the motor state at its padded pitch)
+    e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
+    e.set_stream(stream)
+    e.ingest_can(torch.zeros((n, 4, 8), dtype=torch.uint8, device=dev),
+                 torch.zeros((n, 4), dtype=torch.int16, device=dev))
+    e.ingest_wt901(torch.zeros((n, 48), dtype=torch.uint8, device=dev),
+                   torch.zeros(n, dtype=torch.int32, device=dev))
+    prep0 = e.prepare()
+    timed("rs_tick_2p20_device_state", lambda k: e.tick_prepared(prep0), e)
+    del prep0
 
     e = fmskf.Engine("kf6", n, device=dev.index, trig=trig)
     e.set_stream(stream)
@@ -525,12 +557,12 @@ def main():
         e = ev_count[0] % n_events
         if args.gather == "native":
             # fused tick + record, then fold / ncclAllGather / copy-out on the handle's side
-            # stream; the previous event's result is collected (it finished during this tick's
-            # predecessors), so one event stays in flight behind the ticks
+            # stream; results are collected two events late (they finished while later ticks
+            # ran), so the host never waits behind the tick stream
             eng.tick_ensemble_begin(prepared[k % R])
             applied.append(k % R)
             native_pending[0] += 1
-            native_collect(1)
+            native_collect(2)
         else:
             # without a process group the "gather" is the identity: the record is written in
             # place into its gather slot
@@ -627,11 +659,11 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for k in range(k1_steps):
-            if args.gather == "native":  # begin every tick, each result collected one tick later
+            if args.gather == "native":  # begin every tick, each result collected two ticks later
                 eng.tick_ensemble_begin(prepared[k % R])
                 applied.append(k % R)
                 native_pending[0] += 1
-                native_collect(1)
+                native_collect(2)
                 continue
             if args.ensemble == "fused":
                 eng.tick_ensemble_prepared(prepared[k % R], rec)

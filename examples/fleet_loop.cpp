@@ -6,10 +6,18 @@
 // and predicts from the wheels, runs the wheel speed loops and sends the 0x200 current
 // frame (VD_task_main.cpp:366-372), and the ROS task publishes VehicleInfo at 60 Hz
 // (RM_task_main.cpp:772-823).  Synthetic traffic: each robot drives its wheels at a
-// constant rpm and is commanded forward at 200 mm/s.  Usage: fleet_loop [N] [ticks]
+// constant rpm and is commanded forward at 200 mm/s.  Every 16 ticks the fleet's pose
+// mean / covariance is recorded asynchronously (fmskf_ensemble_begin: fold and, across
+// processes, the RCCL all-gather on the handle's side stream) and collected two records later.
+//
+//   fleet_loop [N] [ticks]
+//   FLEET_WORLD=W FLEET_RANK=r FLEET_ID=/path/id fleet_loop ...   one process per GPU: rank 0
+//       writes the communicator id to FLEET_ID, every rank reads it (device = rank)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <thread>
 #include <vector>
 
 #include "fmskf.hpp"
@@ -30,8 +38,30 @@ static void wt901_frame(uint8_t *o, uint8_t type, int16_t w0, int16_t w1, int16_
 int main(int argc, char **argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1u << 16);
   const int ticks = argc > 2 ? atoi(argv[2]) : 1000;
+  const int world = getenv("FLEET_WORLD") ? atoi(getenv("FLEET_WORLD")) : 1;
+  const int rank = getenv("FLEET_RANK") ? atoi(getenv("FLEET_RANK")) : 0;
   try {
-    fmskf::Robots robots(FMSKF_MODEL_RS, n);
+    fmskf::Robots robots(FMSKF_MODEL_RS, n, world > 1 ? rank : 0);
+    if (world > 1) {  // the handle's RCCL communicator, its id passed through a file
+      const char *path = getenv("FLEET_ID");
+      if (!path) throw std::runtime_error("FLEET_ID must name the id file");
+      uint8_t id[FMSKF_COMM_ID_BYTES];
+      if (rank == 0) {
+        fmskf::Robots::comm_unique_id(id);
+        const std::string tmp = std::string(path) + ".tmp";
+        FILE *f = fopen(tmp.c_str(), "wb");
+        if (!f || fwrite(id, 1, sizeof(id), f) != sizeof(id)) throw std::runtime_error("cannot write FLEET_ID");
+        fclose(f);
+        rename(tmp.c_str(), path);
+      } else {
+        FILE *f = nullptr;
+        for (int k = 0; k < 600 && !(f = fopen(path, "rb")); k++)
+          std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        if (!f || fread(id, 1, sizeof(id), f) != sizeof(id)) throw std::runtime_error("cannot read FLEET_ID");
+        fclose(f);
+      }
+      robots.comm_init(id, rank, world);
+    }
     fmskf::ImuIfWt901c imu(robots);
     fmskf::MotorIfM2006 motors(robots);
     fmskf::VehicleCtrl vehicle(robots);
@@ -58,6 +88,8 @@ int main(int argc, char **argv) {
     vehicle.start();
     vehicle.set_target_vel(vel.data(), acl.data(), jrk.data());
 
+    double mean[6], cov[21];
+    int pending = 0, records = 0;
     auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < ticks; t++) {
       // CAN RX: wheel i advances (1 + i % 5) counts per tick, all wheels forward
@@ -92,6 +124,19 @@ int main(int argc, char **argv) {
       // correct + predict + wheel loops + 0x200 frames, device-resident inputs
       robots.can_tx_routine(tx.data());
       if (t % 17 == 16) fmskf::publish_vehicle_info(robots, info.data());  // ~60 Hz
+      if (t % 16 == 15) {  // the fleet's ensemble record, collected two records later
+        robots.ensemble_begin();
+        if (++pending == 3) {
+          robots.ensemble_end(mean, cov);
+          pending--;
+          records++;
+        }
+      }
+    }
+    while (pending) {
+      robots.ensemble_end(mean, cov);
+      pending--;
+      records++;
     }
     robots.sync();
     auto t1 = std::chrono::steady_clock::now();
@@ -104,6 +149,9 @@ int main(int argc, char **argv) {
     printf("robot 0: VehicleInfo pos=(%d, %d) mm imu.fault=%u  tx=[%02x %02x %02x %02x %02x %02x %02x %02x]\n",
            info[0].pos_x, info[0].pos_y, info[0].imu_fault, tx[0], tx[1], tx[2], tx[3], tx[4], tx[5],
            tx[6], tx[7]);
+    if (records)
+      printf("fleet (%d rank%s): %d ensemble records, last mean x=%.6f m th=%.6f rad, var x=%.3e\n", world,
+             world > 1 ? "s" : "", records, mean[0], mean[2], cov[0]);
   } catch (const std::exception &e) {
     fprintf(stderr, "fleet_loop: %s\n", e.what());
     return 1;

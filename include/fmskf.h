@@ -150,11 +150,15 @@ typedef struct fmskf_kf6_record {
  * device-resident value the ingest entry points produced (full pipeline). */
 typedef struct fmskf_tick_inputs {
   uint32_t mem;              /* FMSKF_MEM_HOST or FMSKF_MEM_DEVICE for all pointers below */
-  uint32_t reserved;
+  /* plane pitch of angle_sum in elements (single-tick calls; 0 = N, >= N otherwise).  A padded
+   * pitch keeps the four sum planes off a power-of-two stride, which aliases in the memory-side
+   * cache: the RS tick at 2^20 robots reads [4][2^20] sums measurably slower than [4][2^20 + 512]
+   * (fmskf_tick_many takes the plane pitch from tick_stride) */
+  uint32_t angle_sum_pitch;
   const float *yaw_deg;      /* [N] IMT::get_status_now_yaw (deg, [-180,180)); RS, KF6 */
   const float *gyro_z_dps;   /* [N] IMU_IF::Data.gyro[2] (deg/s, as published); KF6 */
   const int16_t *rpm;        /* [N][4] Status.s16_rawSpeedRpm FL,BL,BR,FR; RS, KF6 */
-  const int64_t *angle_sum;  /* [4][N] MOTOR_IF_M2006::get_rawAngleSum; RS */
+  const int64_t *angle_sum;  /* [4][angle_sum_pitch] MOTOR_IF_M2006::get_rawAngleSum; RS */
   const int16_t *raw;        /* [N][8] EKF9 words: Yaw, GZ, AX, AY registers, rpm x4 */
   const double *z;           /* [8][N] KF12D measurements */
   const uint8_t *valid;      /* [N] measurement present (0 = predict only); NULL = all */
@@ -254,7 +258,7 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
  *   fmskf_ensemble_end: waits for the OLDEST pending begin and returns its mean [n] and
  *     covariance packed [n(n+1)/2] (unbiased, rank-order fold: identical on every rank,
  *     deterministic).  EINVAL when nothing is pending.
- * At most two begins may be pending (EINVAL on a third).  Every rank must issue the same
+ * At most four begins may be pending (EINVAL on a fifth).  Every rank must issue the same
  * sequence of begins (it is a collective).  Not valid inside a graph capture. */
 int fmskf_tick_ensemble_begin(fmskf_handle h, const fmskf_tick_inputs *in);
 int fmskf_ensemble_begin(fmskf_handle h);

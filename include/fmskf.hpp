@@ -64,6 +64,24 @@ class Robots {
   void set_stream(void *hip_stream) { check(fmskf_set_stream(h_, hip_stream), "fmskf_set_stream"); }
   void sync() { check(fmskf_sync(h_), "fmskf_sync"); }
 
+  // ensemble mean / covariance over every robot of every rank: the RCCL
+  // communicator of this handle (one process per GPU; rank 0 makes the id), then asynchronous
+  // records -- the fold and the all-gather run on a side stream behind the ticks, the result is
+  // collected later (oldest first)
+  static void comm_unique_id(uint8_t id[FMSKF_COMM_ID_BYTES]) {
+    check(fmskf_comm_unique_id(id), "fmskf_comm_unique_id");
+  }
+  void comm_init(const uint8_t id[FMSKF_COMM_ID_BYTES], int rank, int world) {
+    check(fmskf_comm_init(h_, id, rank, world), "fmskf_comm_init");
+  }
+  void ensemble_begin() { check(fmskf_ensemble_begin(h_), "fmskf_ensemble_begin"); }
+  void tick_ensemble_begin(const fmskf_tick_inputs *in) {
+    check(fmskf_tick_ensemble_begin(h_, in), "fmskf_tick_ensemble_begin");
+  }
+  void ensemble_end(double *mean, double *cov_packed) {
+    check(fmskf_ensemble_end(h_, mean, cov_packed), "fmskf_ensemble_end");
+  }
+
   // VDT::can_tx_routine_intr: correct with the IMU yaw, then VEHICLE_CTRL::update (the
   // odometry / estimator time update, then the control half: interpolators, IK, FF_PI_D),
   // then M_CAN.tx_routine -- reading the device-resident IMU / motor state the ingest calls

@@ -653,21 +653,24 @@ int orc_kf12d_cinv(const double *r, double *ci) {
  * processing, Bierman 1977).  y holds the innovations of the current state: after each
  * scalar update the correction is subtracted from it.  blk: R has no base/tip cross terms,
  * so the tip rows of Cinv start at column 4 (the skipped products are exact zeros). */
+/* The decorrelated update: measurement a becomes the scalar sum_b Cinv[a][b] z_b with unit
+ * noise; exact-zero Cinv entries are skipped and every sum starts from +0 (the library's
+ * kf12d_decor_update, kernels_kf.hip) */
 static void orc_kf12d_decor_update(double *xs, double *Ps, double *y, const double *ci, int blk) {
   for (int a = 0; a < 8; a++) {
     const int b0 = (blk && a >= 4) ? 4 : 0;
     const double *c = ci + a * (a + 1) / 2;
-    double hp[12];
-    for (int j = 0; j < 12; j++) {
-      double s = c[b0] * Ps[orc_pk(k_kf12_h1[b0], j)];
-      for (int b = b0 + 1; b <= a; b++) s = fma(c[b], Ps[orc_pk(k_kf12_h1[b], j)], s);
-      hp[j] = s;
+    double hp[12], nu = 0.0;
+    for (int j = 0; j < 12; j++) hp[j] = 0.0;
+    for (int b = b0; b <= a; b++) {
+      if (c[b] == 0.0) continue;
+      for (int j = 0; j < 12; j++) hp[j] = fma(c[b], Ps[orc_pk(k_kf12_h1[b], j)], hp[j]);
+      nu = fma(c[b], y[b], nu);
     }
-    double s = c[b0] * hp[k_kf12_h1[b0]];
-    for (int b = b0 + 1; b <= a; b++) s = fma(c[b], hp[k_kf12_h1[b]], s);
+    double s = 0.0;
+    for (int b = b0; b <= a; b++)
+      if (c[b] != 0.0) s = fma(c[b], hp[k_kf12_h1[b]], s);
     s = s + 1.0;
-    double nu = c[b0] * y[b0];
-    for (int b = b0 + 1; b <= a; b++) nu = fma(c[b], y[b], nu);
     const double si = 1.0 / s;
     const double g = nu * si;
     for (int j = 0; j < 12; j++) xs[j] = fma(hp[j], g, xs[j]);
@@ -736,7 +739,7 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
     if (do_predict) {
       for (int a = 0; a < 6; a++) xs[pos[a]] = fma(prm->dt, xs[pos[a] + 3], xs[pos[a]]);
       xs[2] = orc_wrap_pi_d(xs[2]);
-      orc_kf_predict_cov_f64(12, Ps, F, pat, prm->q);
+      orc_kf_predict_cov_q_f64(12, Ps, F, pat, prm->q, 1);
     }
     for (int k = 0; k < 12; k++) x[k * n + i] = xs[k];
     for (int k = 0; k < 78; k++) P[k * n + i] = Ps[k];

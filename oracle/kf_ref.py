@@ -275,3 +275,50 @@ class Kf12dBatch:
     def packed(self):
         i, j = _tril_idx(12)
         return self.x.T.copy(), self.P[:, i, j].T.copy()
+
+
+# ----------------------------------------------------------------------------- dense C (fast)
+class DenseC:
+    """The same textbook formulas in C (oracle/kf_dense_ref.c: full matrices, LU solve, Joseph
+    update), batched over robots with OpenMP: the long-horizon reference.  model "kf6" | "ekf9";
+    q / r packed (as the engine's config), dt float; step(z [m, N] float64, valid [N] u8|None)."""
+
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            import ctypes as C
+            import os
+            import subprocess
+            here = os.path.dirname(os.path.abspath(__file__))
+            subprocess.run(["make", "-s", "libkfref.so"], cwd=here, check=True, stdout=subprocess.DEVNULL)
+            L = C.CDLL(os.path.join(here, "libkfref.so"))
+            f64 = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+            for name in ("dref_kf6_step", "dref_ekf9_step"):
+                fn = getattr(L, name)
+                fn.argtypes = [C.c_int64, f64, f64, f64, C.c_void_p, f64, f64, C.c_double]
+                fn.restype = None
+            cls._lib = L
+        return cls._lib
+
+    def __init__(self, model, n, x0, P0p, q_packed, r_packed, dt):
+        self.model, self.n, self.dt = model, n, float(dt)
+        nx, m = (6, 4) if model == "kf6" else (9, 6)
+        self.nx, self.m = nx, m
+        self.Q = np.ascontiguousarray(unpack(q_packed, nx))
+        self.R = np.ascontiguousarray(unpack(r_packed, m))
+        self.x = np.ascontiguousarray(np.tile(np.asarray(x0, float), (n, 1)))
+        self.P = np.ascontiguousarray(np.tile(unpack(P0p, nx), (n, 1, 1)))
+        self.fn = getattr(self.lib(), "dref_kf6_step" if model == "kf6" else "dref_ekf9_step")
+
+    def step(self, z, valid=None):
+        import ctypes as C
+        z = np.ascontiguousarray(z, np.float64)
+        v = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+        self.fn(self.n, self.x, self.P, z, None if v is None else v.ctypes.data_as(C.c_void_p),
+                self.Q, self.R, self.dt)
+
+    def packed(self):
+        i, j = _tril_idx(self.nx)
+        return self.x.T.copy(), self.P[:, i, j].T.copy()

@@ -35,7 +35,7 @@ def build(quiet: bool = True) -> None:
     kw = dict(cwd=HERE, check=True)
     if quiet:
         kw.update(stdout=subprocess.DEVNULL)
-    subprocess.run(["make", "-s", "liboracle.so"], **kw)
+    subprocess.run(["make", "-s", "liboracle.so", "libkfref.so"], **kw)
     if os.path.isdir("/root/reference/lib/wt901c"):
         subprocess.run(["make", "-s", "ref"], **kw)
 

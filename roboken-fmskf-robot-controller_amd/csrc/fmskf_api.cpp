@@ -121,19 +121,25 @@ struct fmskf_ctx {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   double *ens_gather = nullptr;
-  // asynchronous ensemble (fmskf_tick_ensemble_begin / fmskf_ensemble_begin / _end): two slots,
-  // each with its own block records, shift copy, record, gather buffer and pinned host copy, so
-  // the fold, the all-gather and the D2H of one event run on the side stream `ens_stream` while
-  // the next tick (which writes the other slot's block records) runs on the handle's stream
-  static constexpr int kEnsSlots = 2;
+  // asynchronous ensemble (fmskf_tick_ensemble_begin / fmskf_ensemble_begin / _end): the block
+  // records are double-buffered (the tick of event k writes buffer k % 2 while the side stream
+  // `ens_stream` folds buffer (k - 1) % 2), and up to kEnsSlots results are in flight, each
+  // with its record, gather buffer and pinned host copy, so a caller can collect results a few
+  // events late and the tick stream never waits on the host
+  static constexpr int kEnsSlots = 4;
   struct EnsSlot {
-    double *blocks = nullptr, *shift = nullptr, *rec = nullptr, *gather = nullptr;
+    double *rec = nullptr, *gather = nullptr;
     double *host = nullptr;  // pinned [ranks][len]
     size_t cap = 0;          // ranks the gather / host buffers hold
-    hipEvent_t ticked = nullptr, folded = nullptr, done = nullptr;
-    bool used = false;       // `folded` has been recorded (the slot's block records are read)
+    hipEvent_t done = nullptr;
     int ranks = 1;
   } eslot[kEnsSlots];
+  struct EnsBlocks {
+    double *blocks = nullptr;
+    hipEvent_t ticked = nullptr, folded = nullptr;
+    bool used = false;       // `folded` has been recorded
+  } eblk[2];
+  int ens_bnext = 0;
   hipStream_t ens_stream = nullptr;
   int ens_head = 0, ens_pending = 0;
   // vehicle control state (allocated on first use) and its parameters
@@ -264,9 +270,11 @@ struct fmskf_ctx {
     if (pin_out) (void)hipHostFree(pin_out);
     for (EnsSlot &e : eslot) {
       if (e.host) (void)hipHostFree(e.host);
-      for (hipEvent_t ev : {e.ticked, e.folded, e.done})
-        if (ev) (void)hipEventDestroy(ev);
+      if (e.done) (void)hipEventDestroy(e.done);
     }
+    for (EnsBlocks &b : eblk)
+      for (hipEvent_t ev : {b.ticked, b.folded})
+        if (ev) (void)hipEventDestroy(ev);
     if (ens_stream) (void)hipStreamDestroy(ens_stream);
     destroy_comm();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
@@ -283,18 +291,11 @@ void check_handle(fmskf_handle h) {
   if (!h) fail(FMSKF_EINVAL, "null handle");
 }
 
-// Small host-resident inputs / outputs (<= 1 MiB per call): FMSKF_PINNED_STAGE=0 copies every
-// host plane as its own pageable hipMemcpyAsync; 1 packs them into a pinned slot and moves it
-// with one DMA; 2 (zero-copy) lets the kernels read the packed inputs from, and write their
-// host-destined result into, the pinned slots over PCIe, with no DMA at all
-int pinned_stage() {
-  static const int v = [] {
-    const char *e = getenv("FMSKF_PINNED_STAGE");
-    const int m = e ? atoi(e) : 2;
-    return m >= 0 && m <= 2 ? m : 2;
-  }();
-  return v;
-}
+// Small host-resident inputs / outputs (<= 1 MiB per call) are zero-copy: the CPU packs the
+// call's planes into a pinned slot, the kernels read them from there and write their
+// host-destined result into the pinned output slot over PCIe, with no DMA at all.  Measured
+// against one pageable copy per plane and against a packed slot moved by one DMA (DESIGN.md
+// section 5): KF6 isr_tick at 4096 robots 60.6-63.6 / 51.5-55.1 / 31.7-34.7 us.
 
 // Host->device staging of a set of planes; returns device pointers.
 struct Stager {
@@ -312,17 +313,14 @@ struct Stager {
     size_t total = 0;
     for (auto &it : items) total += (it.second + 255) & ~size_t(255);
     size_t off = 0;
-    const int mode = pinned_stage();
-    if (total <= fmskf_ctx::kPinned && !h->capturing && mode) {  // pack into a pinned slot
+    if (total <= fmskf_ctx::kPinned && !h->capturing) {  // pack into a pinned slot, zero-copy
       char *pin = h->pinned_in();
-      char *base = mode == 2 ? (char *)fmskf_ctx::dev_ptr(pin) : (char *)h->stage_for(total);
+      char *base = (char *)fmskf_ctx::dev_ptr(pin);
       for (auto &it : items) {
         memcpy(pin + off, *it.first, it.second);
         *it.first = base + off;
         off += (it.second + 255) & ~size_t(255);
       }
-      if (mode == 1)
-        hip_check(hipMemcpyAsync(base, pin, total, hipMemcpyHostToDevice, h->stream), "stage H2D");
       return;
     }
     char *base = (char *)h->stage_for(total);
@@ -409,6 +407,7 @@ void convert_params(fmskf_ctx *h) {
   for (int a = 0; a < 4; a++)
     for (int b = 0; b <= a; b++) h->kf12.r2[a * (a + 1) / 2 + b] = c.r[(a + 4) * (a + 5) / 2 + (b + 4)];
   h->kf12.decor = kf12d_cinv(h->kf12.r, h->kf12.cinv) ? 1 : 0;
+  h->kf12.sparse = h->kf12.decor && kf12d_sparse(h->kf12.cinv, h->kf12.q) ? 1 : 0;
 }
 
 // WT901 / IMU_IF state and M2006 motor state, allocated on first use (an ingest call, a NULL
@@ -448,6 +447,9 @@ void ensure_shift(fmskf_ctx *h) {
   // a launch inside a capture is only recorded: the flag would claim a shift that no run wrote
   // (fmskf_graph_begin takes it before capturing)
   if (h->capturing) fail(FMSKF_EINVAL, "ensemble shift first taken inside a graph capture");
+  // asynchronous folds still queued on the side stream read the shift: rewrite it after them
+  for (const fmskf_ctx::EnsBlocks &b : h->eblk)
+    if (b.used) hip_check(hipStreamWaitEvent(h->stream, b.folded, 0), "hipStreamWaitEvent");
   launch_check(launch_ens_shift(h->s, (int)h->d.nx, h->d.elem == 8, h->ens_shift, h->stream),
                "ensemble shift launch");
   h->ens_shift_ok = true;
@@ -576,12 +578,17 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
   if (t.rec && h->cfg.model != FMSKF_MODEL_KF6) fail(FMSKF_EINVAL, "kf6_rec is a KF6 input");
   if (t.rec && (t.yaw_deg || t.gyro_z || t.rpm))
     fail(FMSKF_EINVAL, "kf6_rec replaces yaw_deg / gyro_z_dps / rpm: pass one or the other");
+  if (in->angle_sum_pitch) {
+    if (n_ticks != 1 || stride != n) fail(FMSKF_EINVAL, "angle_sum_pitch is for single-tick calls (tick_many: tick_stride)");
+    if (in->angle_sum_pitch < n) fail(FMSKF_EINVAL, "angle_sum_pitch < N");
+    t.sum_pitch = in->angle_sum_pitch;
+  }
   const uint64_t span = (uint64_t)(n_ticks - 1) * stride + n;  // elements per [N] plane
   Stager sg(h, in->mem);
   sg.add((const void **)&t.yaw_deg, span * 4);
   sg.add((const void **)&t.gyro_z, span * 4);
   sg.add((const void **)&t.rpm, span * 8);
-  sg.add((const void **)&t.angle_sum, ((uint64_t)(n_ticks - 1) * stride * 4 + 3 * stride + n) * 8);
+  sg.add((const void **)&t.angle_sum, ((uint64_t)(n_ticks - 1) * stride * 4 + 3 * t.sum_pitch + n) * 8);
   sg.add((const void **)&t.raw, span * 16);
   sg.add((const void **)&t.z, ((uint64_t)(n_ticks - 1) * stride * 8 + 7 * stride + n) * 8);
   sg.add((const void **)&t.valid, span);
@@ -681,8 +688,7 @@ void finish_out(fmskf_ctx *h, uint32_t mem) {
 // where a kernel writes a result of `bytes` bound for the caller's host memory: the pinned
 // output slot itself under zero-copy staging, else device scratch
 void *host_result(fmskf_ctx *h, size_t bytes) {
-  if (bytes <= fmskf_ctx::kPinned && !h->capturing && pinned_stage() == 2)
-    return fmskf_ctx::dev_ptr(h->pinned_out());
+  if (bytes <= fmskf_ctx::kPinned && !h->capturing) return fmskf_ctx::dev_ptr(h->pinned_out());
   return h->out_for(bytes);
 }
 // one device buffer to the caller's host (or device) buffer, complete on return: a small host
@@ -694,7 +700,7 @@ void copy_out_sync(fmskf_ctx *h, void *dst, const void *src, size_t bytes, uint3
     memcpy(dst, h->pin_out, bytes);
     return;
   }
-  if (mem == FMSKF_MEM_HOST && bytes <= fmskf_ctx::kPinned && !h->capturing && pinned_stage()) {
+  if (mem == FMSKF_MEM_HOST && bytes <= fmskf_ctx::kPinned && !h->capturing) {
     char *pin = h->pinned_out();
     hip_check(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
     hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
@@ -1061,12 +1067,20 @@ namespace {
 // Checkpoint sections: every per-robot device array of the handle in its device layout (planes
 // at the handle's pitch, tiles), byte for byte.  Groups: 1 estimator (x, P, RS prev sums,
 // counters), 2 IMU ingest, 4 motor ingest, 8 control (state + parameters).
-constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
+// Format 2 ('FMSKFCK2'): the header records every layout choice a section's bytes depend on
+// (estimator pitch / tile / element size, the motor sums' pitch, the control arrays' tiling
+// and pitch) and a checksum of everything after the header; a file whose layout differs from
+// this build's, or from a format-1 file (which recorded none of the control / motor layout), is
+// rejected instead of being loaded into a scrambled state.
+constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '2'};
+constexpr char kCkMagicV1[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
 struct CkHeader {
   char magic[8];
   uint32_t abi, model;
   uint64_t n, pitch;
-  uint32_t tile, elem, groups, reserved;
+  uint32_t tile, elem, groups, ctrl_tile;  // ctrl_tile: control arrays' tile width (0 = planar)
+  uint64_t m_pitch, ctrl_pitch;            // motor sum planes' pitch, control state's pitch
+  uint64_t body_bytes, checksum;           // what follows the header, and its hash
 };
 struct CkSection {
   void *dev;
@@ -1111,6 +1125,63 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
   return v;
 }
 
+// the layout fields of a header for this handle (what ensure_motors / ensure_ctrl allocate)
+void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
+  hd->abi = FMSKF_ABI_VERSION;
+  hd->model = h->cfg.model;
+  hd->n = h->s.n;
+  hd->pitch = h->s.pitch;
+  hd->tile = h->s.tile;
+  hd->elem = h->d.elem;
+  hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
+  hd->m_pitch = plane_pitch(h->s.n);
+  const uint64_t w = tile_w_elem(4);
+  hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
+}
+
+// 64-bit multiply-xor hash of a byte stream in 8-byte words (the tail zero-padded); the value
+// does not depend on how the stream is split into add() calls
+struct CkHash {
+  uint64_t h = 0x9E3779B97F4A7C15ull, len = 0;
+  unsigned char tail[8] = {};
+  size_t nt = 0;
+  static uint64_t mix(uint64_t h, uint64_t w) {
+    h = (h ^ w) * 0x100000001B3ull;
+    return h ^ (h >> 29);
+  }
+  void add(const char *p, size_t b) {
+    len += b;
+    while (nt && b) {  // finish a partial word first
+      tail[nt++] = (unsigned char)*p++;
+      b--;
+      if (nt == 8) {
+        uint64_t w;
+        memcpy(&w, tail, 8);
+        h = mix(h, w);
+        nt = 0;
+      }
+    }
+    size_t k = 0;
+    for (; k + 8 <= b; k += 8) {
+      uint64_t w;
+      memcpy(&w, p + k, 8);
+      h = mix(h, w);
+    }
+    for (; k < b; k++) tail[nt++] = (unsigned char)p[k];
+  }
+  uint64_t value() const {
+    uint64_t r = h;
+    if (nt) {
+      uint64_t w = 0;
+      memcpy(&w, tail, nt);
+      r = mix(r, w);
+    }
+    return r ^ len;
+  }
+};
+
+constexpr size_t kCkChunk = (size_t)64 << 20;  // host staging per copy: 64 MiB, a word multiple
+
 struct File {
   FILE *f = nullptr;
   File(const char *path, const char *mode) : f(fopen(path, mode)) {
@@ -1143,26 +1214,33 @@ int fmskf_save_state(fmskf_handle h, const char *path) {
     DeviceGuard g(h->cfg.device);
     CkHeader hd{};
     memcpy(hd.magic, kCkMagic, 8);
-    hd.abi = FMSKF_ABI_VERSION;
-    hd.model = h->cfg.model;
-    hd.n = h->s.n;
-    hd.pitch = h->s.pitch;
-    hd.tile = h->s.tile;
-    hd.elem = h->d.elem;
+    ck_layout(h, &hd);
     hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
     hip_check(hipStreamSynchronize(h->stream), "save sync");
     File f(path, "wb");
-    f.write(&hd, sizeof(hd));
-    f.write(&h->cfg, sizeof(h->cfg));
-    if (hd.groups & 8) f.write(&h->cprm, sizeof(h->cprm));
+    f.write(&hd, sizeof(hd));  // rewritten with the body size and checksum at the end
+    CkHash hash;
+    auto put = [&](const void *p, size_t b) {
+      f.write(p, b);
+      hash.add((const char *)p, b);
+    };
+    put(&h->cfg, sizeof(h->cfg));
+    if (hd.groups & 8) put(&h->cprm, sizeof(h->cprm));
     std::vector<char> buf;
     for (const CkSection &c : ck_sections(h, hd.groups)) {
       const uint64_t b = c.bytes;
-      f.write(&b, 8);
-      buf.resize(c.bytes);
-      hip_check(hipMemcpy(buf.data(), c.dev, c.bytes, hipMemcpyDeviceToHost), "save D2H");
-      f.write(buf.data(), c.bytes);
+      put(&b, 8);
+      for (size_t off = 0; off < c.bytes; off += kCkChunk) {  // bounded host memory
+        const size_t len = std::min(kCkChunk, c.bytes - off);
+        buf.resize(len);
+        hip_check(hipMemcpy(buf.data(), (const char *)c.dev + off, len, hipMemcpyDeviceToHost), "save D2H");
+        put(buf.data(), len);
+      }
     }
+    hd.body_bytes = hash.len;
+    hd.checksum = hash.value();
+    f.seek(0, SEEK_SET);
+    f.write(&hd, sizeof(hd));
   });
 }
 
@@ -1174,12 +1252,40 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     DeviceGuard g(h->cfg.device);
     File f(path, "rb");
     CkHeader hd{};
-    f.read(&hd, sizeof(hd));
+    f.read(&hd.magic, 8);
+    if (memcmp(hd.magic, kCkMagicV1, 8) == 0)
+      fail(FMSKF_EINVAL, "format-1 checkpoint (older build): its control / motor layout is not recorded");
     if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
-    if (hd.abi != FMSKF_ABI_VERSION || hd.model != h->cfg.model || hd.n != h->s.n ||
-        hd.pitch != h->s.pitch || hd.tile != h->s.tile || hd.elem != h->d.elem || (hd.groups & ~15u))
+    f.seek(0, SEEK_SET);
+    f.read(&hd, sizeof(hd));
+    CkHeader me{};
+    ck_layout(h, &me);
+    if (hd.abi != me.abi || hd.model != me.model || hd.n != me.n || hd.pitch != me.pitch ||
+        hd.tile != me.tile || hd.elem != me.elem || (hd.groups & ~15u))
       fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, N or layout)");
+    if ((hd.groups & 4) && hd.m_pitch != me.m_pitch) fail(FMSKF_EINVAL, "checkpoint motor layout differs");
+    if ((hd.groups & 8) && (hd.ctrl_tile != me.ctrl_tile || hd.ctrl_pitch != me.ctrl_pitch))
+      fail(FMSKF_EINVAL, "checkpoint control layout differs (tiling / pitch)");
     if (!(hd.groups & 1u)) fail(FMSKF_EINVAL, "checkpoint holds no estimator state");
+    // pass 1: the body's length and checksum, read in bounded chunks -- a truncated, extended or
+    // corrupted file is rejected before anything of the handle changes
+    const long body = f.tell();
+    f.seek(0, SEEK_END);
+    if ((uint64_t)(f.tell() - body) != hd.body_bytes)
+      fail(FMSKF_EINVAL, "checkpoint size mismatch (truncated or trailing bytes)");
+    f.seek(body, SEEK_SET);
+    std::vector<char> buf;
+    {
+      CkHash hash;
+      for (uint64_t off = 0; off < hd.body_bytes; off += kCkChunk) {
+        const size_t len = (size_t)std::min<uint64_t>(kCkChunk, hd.body_bytes - off);
+        buf.resize(len);
+        f.read(buf.data(), len);
+        hash.add(buf.data(), len);
+      }
+      if (hash.value() != hd.checksum) fail(FMSKF_EINVAL, "checkpoint checksum mismatch");
+    }
+    f.seek(body, SEEK_SET);
     fmskf_config saved;
     f.read(&saved, sizeof(saved));
     fmskf_ctrl_params cp{};
@@ -1187,35 +1293,33 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (hd.groups & 2) ensure_imu(h);
     if (hd.groups & 4) ensure_motors(h);
     if (hd.groups & 8) ensure_ctrl(h);
-    // validate every section length and the file's end before touching the handle, so a
-    // truncated or foreign file leaves the state as it was
     const std::vector<CkSection> secs = ck_sections(h, hd.groups);
-    const long body = f.tell();
+    // the section sizes follow from the (validated) layout; check them against the file's
+    // before any copy
+    const long first = f.tell();
     for (const CkSection &c : secs) {
       uint64_t b = 0;
       f.read(&b, 8);
       if (b != c.bytes) fail(FMSKF_EINVAL, "checkpoint section size mismatch");
       f.seek((long)c.bytes, SEEK_CUR);
     }
-    const long end = f.tell();
-    f.seek(0, SEEK_END);
-    if (f.tell() != end) fail(FMSKF_EINVAL, "checkpoint size mismatch (truncated or trailing bytes)");
-    f.seek(body, SEEK_SET);
-    // read every section into host memory first: a read failure leaves the handle untouched
-    std::vector<std::vector<char>> bufs(secs.size());
-    for (size_t k = 0; k < secs.size(); k++) {
-      uint64_t b = 0;
-      f.read(&b, 8);
-      bufs[k].resize(secs[k].bytes);
-      f.read(bufs[k].data(), secs[k].bytes);
-    }
+    f.seek(first, SEEK_SET);
     // groups the checkpoint does not hold were never used by the saving handle: reset them here
     if (!(hd.groups & 2) && h->s.imu_reg) zero_imu(h);
     if (!(hd.groups & 4) && h->s.m_sum) zero_motors(h);
     if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
     hip_check(hipStreamSynchronize(h->stream), "load sync");
-    for (size_t k = 0; k < secs.size(); k++)
-      hip_check(hipMemcpy(secs[k].dev, bufs[k].data(), secs[k].bytes, hipMemcpyHostToDevice), "load H2D");
+    // pass 2: stream each section to the device in bounded chunks
+    for (const CkSection &c : secs) {
+      uint64_t b = 0;
+      f.read(&b, 8);
+      for (size_t off = 0; off < c.bytes; off += kCkChunk) {
+        const size_t len = std::min(kCkChunk, c.bytes - off);
+        buf.resize(len);
+        f.read(buf.data(), len);
+        hip_check(hipMemcpy((char *)c.dev + off, buf.data(), len, hipMemcpyHostToDevice), "load H2D");
+      }
+    }
     if (hd.groups & 8) h->cprm = cp;
     h->ens_shift_ok = false;
   });
@@ -1523,7 +1627,7 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
   check_handle(h);
   if (h->capturing) fail(FMSKF_EINVAL, "asynchronous ensemble inside a graph capture");
   if (h->ens_pending == fmskf_ctx::kEnsSlots)
-    fail(FMSKF_EINVAL, "two ensemble results pending: call fmskf_ensemble_end first");
+    fail(FMSKF_EINVAL, "four ensemble results pending: call fmskf_ensemble_end first");
   DeviceGuard g(h->cfg.device);
   const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
   const int ranks = h->comm ? h->world : 1;
@@ -1534,39 +1638,36 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     // between the next tick's blocks instead of queueing behind them
     hip_check(hipStreamCreateWithPriority(&h->ens_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
   }
-  const int slot = (h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots;
-  fmskf_ctx::EnsSlot &S = h->eslot[slot];
-  if (!S.blocks) {
+  fmskf_ctx::EnsSlot &S = h->eslot[(h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots];
+  fmskf_ctx::EnsBlocks &B = h->eblk[h->ens_bnext];
+  if (!B.blocks) {
     size_t nb = (size_t)ensemble_nblocks(h->s.n);
     nb = std::max(nb, (size_t)((h->s.n + kBlock - 1) / kBlock));
-    S.blocks = h->alloc<double>(nb * len);
-    S.shift = h->alloc<double>(12);
-    S.rec = h->alloc<double>(91);
-    for (hipEvent_t *e : {&S.ticked, &S.folded, &S.done})
+    B.blocks = h->alloc<double>(nb * len);
+    for (hipEvent_t *e : {&B.ticked, &B.folded})
       hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
   }
-  if ((size_t)ranks > S.cap) {
+  if (!S.rec) {
+    S.rec = h->alloc<double>(91);
+    hip_check(hipEventCreateWithFlags(&S.done, hipEventDisableTiming), "hipEventCreate");
+  }
+  if ((size_t)ranks > S.cap) {  // the slot's previous result was consumed (or never existed)
     double *gbuf = h->alloc<double>((size_t)ranks * 91);
     if (S.gather) h->release(S.gather);
     S.gather = gbuf;
-    if (S.host) {
-      hip_check(hipEventSynchronize(S.done), "hipEventSynchronize");
-      hip_check(hipHostFree(S.host), "hipHostFree");
-      S.host = nullptr;
-    }
+    if (S.host) hip_check(hipHostFree(S.host), "hipHostFree");
+    S.host = nullptr;
     hip_check(hipHostMalloc((void **)&S.host, (size_t)ranks * 91 * 8, hipHostMallocDefault), "hipHostMalloc");
     S.cap = (size_t)ranks;
   }
-  if (S.used) hip_check(hipStreamWaitEvent(h->stream, S.folded, 0), "hipStreamWaitEvent");
+  // the block records are rewritten only after the fold that read them (two events ago)
+  if (B.used) hip_check(hipStreamWaitEvent(h->stream, B.folded, 0), "hipStreamWaitEvent");
   ensure_shift(h);
-  // the slot's own shift copy: a later reset / set_state retakes the handle's shift while this
-  // slot's fold may still be queued
-  hip_check(hipMemcpyAsync(S.shift, h->ens_shift, nx * 8, hipMemcpyDeviceToDevice, h->stream), "shift copy");
   int nb = 0;
   if (in && fused_record(h)) {
     TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
-    t.ens_blocks = S.blocks;
-    t.ens_shift = S.shift;
+    t.ens_blocks = B.blocks;
+    t.ens_shift = h->ens_shift;
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     h->time_begin();
     int e = 0;
@@ -1577,14 +1678,15 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     h->time_end();
   } else {
     if (in) run_tick(h, in, true, true, 1, h->s.n);
-    launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, S.blocks, S.shift, h->stream, &nb),
+    launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, B.blocks, h->ens_shift, h->stream, &nb),
                  "ensemble partial launch");
   }
-  hip_check(hipEventRecord(S.ticked, h->stream), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(h->ens_stream, S.ticked, 0), "hipStreamWaitEvent");
-  launch_check(launch_ens_fold((int)nx, S.blocks, nb, S.shift, S.rec, h->ens_stream), "ensemble fold launch");
-  hip_check(hipEventRecord(S.folded, h->ens_stream), "hipEventRecord");
-  S.used = true;
+  hip_check(hipEventRecord(B.ticked, h->stream), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(h->ens_stream, B.ticked, 0), "hipStreamWaitEvent");
+  launch_check(launch_ens_fold((int)nx, B.blocks, nb, h->ens_shift, S.rec, h->ens_stream), "ensemble fold launch");
+  hip_check(hipEventRecord(B.folded, h->ens_stream), "hipEventRecord");
+  B.used = true;
+  h->ens_bnext ^= 1;
   const double *src = S.rec;
   if (h->comm) {
     nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),

@@ -89,8 +89,23 @@ struct Kf12dParams {
   double r2[10];  // packed R of the arm-tip group (rows/cols 4..7), used by the sequential path
   double cinv[36];  // C^-1 of R = C C^T (packed lower), the decorrelated update's coefficients
   int decor;        // R positive definite: decorrelated scalar-sequential update
+  // the default sparsity (kf12d_sparse): C^-1 nonzero only on its diagonal and at (3,2), Q only
+  // inside the (pos, vel) pair blocks -> the kernel drops the other terms at compile time
+  int sparse;
   const double *coef;  // device copy: cinv [36] then q [78] (read by scalar loads at their use)
 };
+// true when every C^-1 entry off the diagonal and (3,2), and every Q entry between different
+// (pos, vel) pairs (pos k <-> vel k + 3; base k = 0..2, tip 6..8), is exactly zero
+inline bool kf12d_sparse(const double *cinv36, const double *q78) {
+  for (int a = 0; a < 8; a++)
+    for (int b = 0; b < a; b++)
+      if (!(a == 3 && b == 2) && cinv36[a * (a + 1) / 2 + b] != 0.0) return false;
+  auto pair = [](int s) { return s < 6 ? s % 3 : 3 + (s - 6) % 3; };
+  for (int i = 0; i < 12; i++)
+    for (int j = 0; j <= i; j++)
+      if (pair(i) != pair(j) && q78[i * (i + 1) / 2 + j] != 0.0) return false;
+  return true;
+}
 // Cinv of R = C C^T, packed lower; false when R is not positive definite.  Same operations,
 // in the same order, as the oracle's orc_kf12d_cinv (the canonical KF12D update uses it).
 inline bool kf12d_cinv(const double *r, double *ci) {

@@ -418,22 +418,14 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
 
 // one robot per lane, every wheel present (no mask): the robot's 32 frame bytes, its four
 // stamps and its [N][4] int16 / u8 state in single 16-, 8- and 4-byte accesses, and each
-// [4][N] plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines)
-template <bool NT, class T>
-__device__ __forceinline__ T can_ld(const T *p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <bool NT, class T>
-__device__ __forceinline__ void can_st(T *p, T v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-// NT: the motor state streams from HBM (past the Infinity Cache): non-temporal state accesses.
-// POL: every access through a scalar descriptor at the block's 256-robot chunk (ld_chunk /
-// st_chunk) with the KF6 tick's cache policies: the frames and stamps (read once) `nt`, the
-// state stored `sc1` while cache-resident (`nt` loads and stores when NT)
-template <bool NT, bool POL = true>
+// [4][N] plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines:
+// 2^20 57.4-57.7 -> 42.1-44.1 us, 2^22 232-239 -> 211).  Every access goes through a scalar
+// descriptor at the block's 256-robot chunk (ld_chunk / st_chunk) with the KF6 tick's cache
+// policies: the frames and stamps (read once) `nt`, the state stored `sc1` while
+// cache-resident; NT: the motor state streams from HBM (past the Infinity Cache), `nt` loads
+// and stores.  Plain global accesses measured 43.4-44.6 (2^20) and 191-195 us (2^22) against
+// 43.0-43.1 and 185-189.
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -441,49 +433,27 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   constexpr int LP = NT ? kStateNT : 0, SP = st_pol(LP), IP = 2;  // IP: inputs nt
-  const uint64_t hb = POL ? (uint64_t)(__builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1)) : 0;
+  const uint64_t hb = (uint64_t)(__builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1));
   const uint32_t li = (uint32_t)(i - hb);
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  uint4 f01, f23;
-  uint2 st;
-  u32x2 omv, oav;
-  uint32_t oh;
   float py[4], px[4];
   int64_t sm[4];
-  if constexpr (POL) {
-    const auto rf = rsrc(a.frames + hb * 32, (n - hb) * 32);
-    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u, 0, IP);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u + 16u, 0, IP);
-    f01 = make_uint4(v0[0], v0[1], v0[2], v0[3]);
-    f23 = make_uint4(v1[0], v1[1], v1[2], v1[3]);
-    const uint64_t sv = ld_chunk<uint64_t, IP>(reinterpret_cast<const uint64_t *>(a.stamps), hb, n, li);
-    st = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
-    const uint64_t mv = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.micro), hb, n, li);
-    const uint64_t av = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.angle), hb, n, li);
-    omv = u32x2{(uint32_t)mv, (uint32_t)(mv >> 32)};
-    oav = u32x2{(uint32_t)av, (uint32_t)(av >> 32)};
-    oh = ld_chunk<uint32_t, LP>(reinterpret_cast<const uint32_t *>(a.head), hb, n, li);
+  const auto rf = rsrc(a.frames + hb * 32, (n - hb) * 32);
+  const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u, 0, IP);
+  const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u + 16u, 0, IP);
+  const uint4 f01 = make_uint4(v0[0], v0[1], v0[2], v0[3]);
+  const uint4 f23 = make_uint4(v1[0], v1[1], v1[2], v1[3]);
+  const uint64_t sv = ld_chunk<uint64_t, IP>(reinterpret_cast<const uint64_t *>(a.stamps), hb, n, li);
+  const uint2 st = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
+  const uint64_t mv = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.micro), hb, n, li);
+  const uint64_t av = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.angle), hb, n, li);
+  const uint32_t oh = ld_chunk<uint32_t, LP>(reinterpret_cast<const uint32_t *>(a.head), hb, n, li);
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-      py[w] = ld_chunk<float, LP>(a.iir_y + (uint64_t)w * n, hb, n, li);
-      px[w] = ld_chunk<float, LP>(a.iir_x + (uint64_t)w * n, hb, n, li);
-      sm[w] = ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li);
-    }
-  } else {
-    f01 = reinterpret_cast<const uint4 *>(a.frames)[2 * i];
-    f23 = reinterpret_cast<const uint4 *>(a.frames)[2 * i + 1];
-    st = reinterpret_cast<const uint2 *>(a.stamps)[i];
-    omv = can_ld<NT>(reinterpret_cast<const u32x2 *>(a.micro) + i);
-    oav = can_ld<NT>(reinterpret_cast<const u32x2 *>(a.angle) + i);
-    oh = can_ld<NT>(reinterpret_cast<const uint32_t *>(a.head) + i);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      py[w] = can_ld<NT>(a.iir_y + (uint64_t)w * n + i);
-      px[w] = can_ld<NT>(a.iir_x + (uint64_t)w * n + i);
-      sm[w] = can_ld<NT>(a.sum + (uint64_t)w * a.sum_pitch + i);
-    }
+  for (int w = 0; w < 4; w++) {
+    py[w] = ld_chunk<float, LP>(a.iir_y + (uint64_t)w * n, hb, n, li);
+    px[w] = ld_chunk<float, LP>(a.iir_x + (uint64_t)w * n, hb, n, li);
+    sm[w] = ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li);
   }
-  const uint2 om = make_uint2(omv[0], omv[1]), oa = make_uint2(oav[0], oav[1]);
+  const uint2 om = make_uint2((uint32_t)mv, (uint32_t)(mv >> 32)), oa = make_uint2((uint32_t)av, (uint32_t)(av >> 32));
   const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
   const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
   uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0}, nh = 0;
@@ -493,39 +463,22 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
                                  (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
                                  (oh >> (8 * w)) & 0xFF, py[w], px[w], sm[w]);
-    const uint64_t pw = (uint64_t)w * n + i;
-    if constexpr (POL) {
-      st_chunk<float, SP>(a.iir_y + (uint64_t)w * n, hb, n, li, o.iir_y);
-      st_chunk<float, SP>(a.iir_x + (uint64_t)w * n, hb, n, li, o.iir_x);
-      st_chunk<float, SP>(a.speed + (uint64_t)w * n, hb, n, li, o.iir_y);
-      st_chunk<float, SP>(a.dlt + (uint64_t)w * n, hb, n, li, o.dlt);
-      st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li, o.sum);
-    } else {
-      can_st<NT>(a.iir_y + pw, o.iir_y);
-      can_st<NT>(a.iir_x + pw, o.iir_x);
-      can_st<NT>(a.speed + pw, o.iir_y);
-      can_st<NT>(a.dlt + pw, o.dlt);
-      can_st<NT>(a.sum + (uint64_t)w * a.sum_pitch + i, o.sum);
-    }
+    st_chunk<float, SP>(a.iir_y + (uint64_t)w * n, hb, n, li, o.iir_y);
+    st_chunk<float, SP>(a.iir_x + (uint64_t)w * n, hb, n, li, o.iir_x);
+    st_chunk<float, SP>(a.speed + (uint64_t)w * n, hb, n, li, o.iir_y);
+    st_chunk<float, SP>(a.dlt + (uint64_t)w * n, hb, n, li, o.dlt);
+    st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li, o.sum);
     na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
     nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
     nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
     nh |= o.head << (8 * w);
   }
-  if constexpr (POL) {
-    const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.micro), hb, n, li, pk(st.x, st.y));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.angle), hb, n, li, pk(na[0], na[1]));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.rpm), hb, n, li, pk(nr[0], nr[1]));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.curr), hb, n, li, pk(nc[0], nc[1]));
-    st_chunk<uint32_t, SP>(reinterpret_cast<uint32_t *>(a.head), hb, n, li, nh);
-  } else {
-    can_st<NT>(reinterpret_cast<u32x2 *>(a.micro) + i, u32x2{st.x, st.y});
-    can_st<NT>(reinterpret_cast<u32x2 *>(a.angle) + i, u32x2{na[0], na[1]});
-    can_st<NT>(reinterpret_cast<u32x2 *>(a.rpm) + i, u32x2{nr[0], nr[1]});
-    can_st<NT>(reinterpret_cast<u32x2 *>(a.curr) + i, u32x2{nc[0], nc[1]});
-    can_st<NT>(reinterpret_cast<uint32_t *>(a.head) + i, nh);
-  }
+  const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
+  st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.micro), hb, n, li, pk(st.x, st.y));
+  st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.angle), hb, n, li, pk(na[0], na[1]));
+  st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.rpm), hb, n, li, pk(nr[0], nr[1]));
+  st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.curr), hb, n, li, pk(nc[0], nc[1]));
+  st_chunk<uint32_t, SP>(reinterpret_cast<uint32_t *>(a.head), hb, n, li, nh);
 }
 
 int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
@@ -548,27 +501,17 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.iir_y = s.m_iir_y;
   a.iir_x = s.m_iir_x;
   // every wheel present and the caller's frames / stamps aligned for the wide loads: one robot
-  // per lane (FMSKF_CAN_WHEEL=1 keeps the wheel-per-lane kernel, for A/B)
-  static const bool wheel = [] {
-    const char *e = getenv("FMSKF_CAN_WHEEL");
-    return e && atoi(e) != 0;
-  }();
-  if (!present && !wheel && ((uintptr_t)frames & 15) == 0 && ((uintptr_t)stamps & 7) == 0) {
+  // per lane; a `present` mask or unaligned buffers: one wheel per lane
+  if (!present && ((uintptr_t)frames & 15) == 0 && ((uintptr_t)stamps & 7) == 0) {
     const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
     // 132 B of motor state per robot.  Non-temporal with 2 blocks per CU once it is well past
     // the Infinity Cache; measured (kbench, two passes): 2^22 plain 191.6-192.8 us, nt
     // 183.9-187.2, nt + 64 KiB cap 176.7-179.8; at 2^21 (277 MB) plain 83.3-85.1, nt 87.5-87.9
-    static const bool pol = [] {  // A/B switch (FMSKF_CAN_POL=0: plain global accesses)
-      const char *e = getenv("FMSKF_CAN_POL");
-      return !e || atoi(e) != 0;
-    }();
     if (state_nt(s.n * 66)) {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
-      if (pol) k_can4<true><<<g, kBlock, lds, st>>>(a);
-      else k_can4<true, false><<<g, kBlock, lds, st>>>(a);
+      k_can4<true><<<g, kBlock, lds, st>>>(a);
     } else {
-      if (pol) k_can4<false><<<g, kBlock, 0, st>>>(a);
-      else k_can4<false, false><<<g, kBlock, 0, st>>>(a);
+      k_can4<false><<<g, kBlock, 0, st>>>(a);
     }
   } else {
     const uint64_t blocks = (4 * s.n + kBlock - 1) / kBlock;

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
 // ENS: the record epilogue of fmskf_tick_ensemble (ens_device.hpp)
-template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool PRIO = false, bool ENS = false>
+template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -167,7 +167,6 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
-  if (PRIO) __builtin_amdgcn_s_setprio(3);
   WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
   const TileRows<float, N, CP> tx(a.x, tile_slot(n));
   const TileRows<float, NP, CP> tp(a.P, tile_slot(n));
@@ -184,7 +183,6 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
   const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
-  if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P);
   if (live) {
@@ -212,9 +210,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 
 // Two robots per lane (256-robot chunks b and b + gridDim.x of the tiled state): robot B's 54 state
 // loads and its raw record are issued before robot A's update, so they stream in while A
-// computes (FMSKF_EKF9_VARIANT experiments; see launch_ekf9).  PRIO: the waves issue their
-// loads at raised priority (s_setprio 3) and compute at the base priority.
-template <bool LIBM, bool SEQ, int CP, bool PRIO, bool ENS = false>
+// computes (see launch_ekf9).
+template <bool LIBM, bool SEQ, int CP, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -232,7 +229,6 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   const uint64_t ia = (uint64_t)ta * kBlock + t, ib = (uint64_t)tb * kBlock + t;
   const bool live_a = ia < n, live_b = has_b && ib < n;
   const uint64_t iac = live_a ? ia : n - 1, ibc = ib < n ? ib : n - 1;
-  if (PRIO) __builtin_amdgcn_s_setprio(3);
   WaveTable<LIBM> tv(a.in.sintab);
   const TileRows<float, N, CP> txa(a.x, ta, slot(ta), 0), txb(a.x, tb, slot(tb), 0);
   const TileRows<float, NP, CP> tpa(a.P, ta, slot(ta), 0), tpb(a.P, tb, slot(tb), 0);
@@ -249,7 +245,6 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   for (int k = 0; k < N; k++) xb[k] = txb.ld(k);
 #pragma unroll
   for (int k = 0; k < NP; k++) Pb[k] = tpb.ld(k);
-  if (PRIO) __builtin_amdgcn_s_setprio(0);
   tv.store(stab);
   ekf9_tick1<LIBM, true, true, SEQ>(a, ra, ha, stab, xa, Pa);
   if (live_a) {
@@ -295,6 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = a.P[st_at(tl, pp, NP, k, i)];
   const double dt = a.prm.dt;
+  const auto fdt = [&](int, int) { return dt; };
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t base = (uint64_t)t * a.in.stride * M;
     if (UPD) {
@@ -325,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12d(KfArgs<MdKF12D, Kf12dParams> a
         x[p] = dfma(dt, x[p + 3], x[p]);
       }
       x[2] = wrap_pi(x[2]);
-      kf_predict_cov<MdKF12D>(P, [&](int, int) { return dt; }, a.prm.q);
+      kf_predict_cov<MdKF12D, decltype(fdt), double, 12, 78, true>(P, fdt, a.prm.q);
     }
   }
 #pragma unroll
@@ -354,28 +350,54 @@ __device__ __forceinline__ kparam_ptr opaque_param(const double *p) {
   return (kparam_ptr)v;
 }
 
-template <bool BLK>
+// Exact-zero coefficients are skipped (the canonical order of the oracle's
+// orc_kf12d_decor_update: a zero C^-1 entry contributes nothing, every sum starts from +0, and
+// fma(c, p, +0) = c p up to the sign of a zero).  C^-1 of the default R (diagonal but for the
+// two wheel velocities) is mostly exact zeros: 11 of the 20 off-diagonal entries the update
+// reads, each a 12-wide dfma row of HP plus the innovation term.  SP (the host checked that
+// every C^-1 entry off the diagonal and (3,2), and every Q entry outside the (pos, vel) pair
+// blocks, is zero): those terms are dropped at compile time; the entries that may be nonzero
+// are added through a select (the same bits as skipping a zero), as every entry is when !SP.
+// Measured: runtime branches on the scalar coefficient instead of selects took the kernel to
+// 256 VGPRs (1 wave per SIMD) and were not kept.
+__device__ __forceinline__ constexpr bool kf12_cinv_sp(int a, int b) { return a == b || (a == 3 && b == 2); }
+__device__ __forceinline__ double fma_nz(double c, double p, double acc) {
+  const double v = dfma(c, p, acc);
+  return c != 0.0 ? v : acc;
+}
+
+template <bool BLK, bool SP>
 __device__ __forceinline__ void kf12d_decor_update(double (&x)[12], double (&P)[78], double (&y)[8],
                                                    const double *ci) {
 #pragma unroll
   for (int a = 0; a < 8; a++) {
     const int b0 = (BLK && a >= 4) ? 4 : 0;
     const kparam_ptr c = opaque_param(ci + a * (a + 1) / 2);
+    // the diagonal of C^-1 is 1 / C[a][a] > 0 (R positive definite): a plain fma; the other
+    // entries through fma_nz (or, under SP, dropped where the host found them zero)
+    auto term = [&](int b, double p, double acc) -> double {
+      return b == a ? dfma(c[b], p, acc) : fma_nz(c[b], p, acc);
+    };
+    // constant trip counts (b over 0..7, filtered): every index stays compile-time after
+    // unrolling (a b0..a loop left P indexed at run time, in scratch)
+    auto used = [&](int b) { return b >= b0 && b <= a && (!SP || kf12_cinv_sp(a, b)); };
     double hp[12];
 #pragma unroll
     for (int j = 0; j < 12; j++) {
-      double s = c[b0] * P[pk(MdKF12D::h1(b0), j)];
+      double s = 0.0;
 #pragma unroll
-      for (int b = b0 + 1; b <= a; b++) s = dfma(c[b], P[pk(MdKF12D::h1(b), j)], s);
+      for (int b = 0; b < 8; b++)
+        if (used(b)) s = term(b, P[pk(MdKF12D::h1(b), j)], s);
       hp[j] = s;
     }
-    double s = c[b0] * hp[MdKF12D::h1(b0)];
+    double s = 0.0, nu = 0.0;
 #pragma unroll
-    for (int b = b0 + 1; b <= a; b++) s = dfma(c[b], hp[MdKF12D::h1(b)], s);
+    for (int b = 0; b < 8; b++)
+      if (used(b)) s = term(b, hp[MdKF12D::h1(b)], s);
     s = s + 1.0;
-    double nu = c[b0] * y[b0];
 #pragma unroll
-    for (int b = b0 + 1; b <= a; b++) nu = dfma(c[b], y[b], nu);
+    for (int b = 0; b < 8; b++)
+      if (used(b)) nu = term(b, y[b], nu);
     const double si = 1.0 / s;
     const double g = nu * si;
 #pragma unroll
@@ -393,20 +415,30 @@ __device__ __forceinline__ void kf12d_decor_update(double (&x)[12], double (&P)[
 
 // P <- F P F^T + Q with F = I + dt (pos <- vel): every 2x2 block {p_k, v_k} x {p_l, v_l} maps
 // from its own four entries (a b / c d): pp = (a + dt c) + dt (b + dt d), vp = c + dt d,
-// pv = b + dt d, vv = d; bit-identical to the generic T = F P, T F^T form (kf_predict_cov)
+// pv = b + dt d, vv = d; bit-identical to the generic T = F P, T F^T form (kf_predict_cov).
+// Exactly-zero Q entries are not added (kf_predict_cov's SKIPQ); SP: the blocks k != l have
+// no Q at all (checked on the host)
+template <bool SP>
 __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, const double *Q) {
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     const kparam_ptr q = opaque_param(Q);
 #pragma unroll
     for (int l = 0; l <= k; l++) {
+      const bool hasq = !SP || k == l;
+      auto addq = [&](double v, int e) -> double {
+        if (!hasq) return v;
+        const double qe = q[e];
+        const double w = v + qe;
+        return qe != 0.0 ? w : v;
+      };
       const int pk_ = kf12_pos(k), vk = pk_ + 3, pl = kf12_pos(l), vl = pl + 3;
       const double a = P[pk(pk_, pl)], b = P[pk(pk_, vl)], c = P[pk(vk, pl)], d = P[pk(vk, vl)];
       const double t01 = dfma(dt, d, b);
-      P[pk(pk_, pl)] = dfma(dt, t01, dfma(dt, c, a)) + q[pk(pk_, pl)];
-      P[pk(vk, pl)] = dfma(dt, d, c) + q[pk(vk, pl)];
-      if (k != l) P[pk(pk_, vl)] = t01 + q[pk(pk_, vl)];
-      P[pk(vk, vl)] = d + q[pk(vk, vl)];
+      P[pk(pk_, pl)] = addq(dfma(dt, t01, dfma(dt, c, a)), pk(pk_, pl));
+      P[pk(vk, pl)] = addq(dfma(dt, d, c), pk(vk, pl));
+      if (k != l) P[pk(pk_, vl)] = addq(t01, pk(pk_, vl));
+      P[pk(vk, vl)] = addq(d, pk(vk, vl));
     }
   }
 }
@@ -416,7 +448,7 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 // and a scalar plane offset; otherwise one descriptor per plane (n < 2^29 lanes of 8 bytes).
 // ENS: the record epilogue of fmskf_tick_ensemble; every lane then stays to the block
 // reduction (lanes past N tick instance N-1, a clamped index, and store nothing)
-template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool PRIO = false, bool ENS = false>
+template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool ENS = false, bool SP = false>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
   const uint64_t n = a.n, pp = a.pitch;
@@ -449,12 +481,10 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   const uint32_t slot = ENS ? tile_slot(n) : threadIdx.x;
   const TileRows<double, N, CP> tx(a.x, slot);
   const TileRows<double, NP, CP> tp(a.P, slot);
-  if (PRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
 #pragma unroll
   for (int k = 0; k < NP; k++) P[k] = FMSKF_TILED ? tp.ld(k) : ld(rp, a.P, k);
-  if (PRIO) __builtin_amdgcn_s_setprio(0);
   const double dt = a.prm.dt;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     if (UPD) {
@@ -464,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 #pragma unroll
         for (int q = 0; q < M; q++) y[q] = z[q * a.in.stride + i] - x[MdKF12D::h1(q)];
         y[0] = wrap_innov(y[0]);
-        kf12d_decor_update<BLK>(x, P, y, a.prm.coef);
+        kf12d_decor_update<BLK, SP>(x, P, y, a.prm.coef);
       }
     }
     if (PRED) {
@@ -474,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
         x[p] = dfma(dt, x[p + 3], x[p]);
       }
       x[2] = wrap_pi(x[2]);
-      kf12d_predict_cov(P, dt, a.prm.coef + 36);
+      kf12d_predict_cov<SP>(P, dt, a.prm.coef + 36);
     }
   }
   asm volatile("" : "+s"(ps));  // the store offsets are recomputed here, not held from the loads
@@ -508,8 +538,8 @@ static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const dim3 g2((ntiles + 1) / 2);
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) k_ekf9p<false, SEQ, kStateNT, false, true><<<g2, kBlock, lds, st>>>(a);
-    else k_ekf9p<false, SEQ, 0, false, true><<<g2, kBlock, lds, st>>>(a);
+    if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, SEQ, 0, true><<<g2, kBlock, lds, st>>>(a);
     return (int)g2.x;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
@@ -517,8 +547,8 @@ static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &
   // 64 KiB (2 blocks per CU), 307-308 at 32 KiB (3), 316 uncapped
   const dim3 g = grid_for(s.n);
   const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9E_LDS", nt, 32u * 1024u);
-  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
-  else k_ekf9t<LIBM, true, true, SEQ, 0, false, true><<<g, kBlock, lds, st>>>(a);
+  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, true><<<g, kBlock, lds, st>>>(a);
+  else k_ekf9t<LIBM, true, true, SEQ, 0, true><<<g, kBlock, lds, st>>>(a);
   return (int)g.x;
 }
 
@@ -530,31 +560,24 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
     *ens_nb = libm ? launch_ekf9_ens<true, SEQ>(a, s, nt, st) : launch_ekf9_ens<false, SEQ>(a, s, nt, st);
     return (int)hipGetLastError();
   }
-  // Single-tick kernel choice (FMSKF_EKF9_VARIANT, read once, forces one): 0 (default) two
-  // robots per lane (k_ekf9p) while the 216-byte state fits the 256 MiB Infinity Cache, else
-  // one per lane (k_ekf9t); 1 k_ekf9t with a raised-priority load phase; 2 k_ekf9p; 3 k_ekf9p
-  // with the raised-priority load phase; 4 k_ekf9t.  Measured (kbench, one box, two passes):
-  // 2^20: k_ekf9t 74.8-74.9 us, 1: 71.2-71.3, 2: 71.2-71.9, 3: 73.7-73.9;
-  // 2^22 (HBM): k_ekf9t 336-338, 1: 342, 2: 339, 3: 342-343.
+  // Single-tick kernel: two robots per lane (k_ekf9p) while the 216-byte state fits the 256 MiB
+  // Infinity Cache, else one per lane (k_ekf9t); FMSKF_EKF9_VARIANT (read once) forces one of
+  // them, 2 = k_ekf9p, 4 = k_ekf9t (the tests' cross-check at small N).  Measured (kbench, one
+  // box, two passes): 2^20 k_ekf9t 74.8-74.9 us, k_ekf9p 71.2-71.9; 2^22 (HBM) k_ekf9t 336-338,
+  // k_ekf9p 339.  A raised-priority load phase (s_setprio 3 while issuing the loads) measured
+  // 71.2-73.9 at 2^20 and 342-343 at 2^22 and was removed.
   static const int var = [] {
     const char *e = getenv("FMSKF_EKF9_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  const int v = var == 0 ? (s.n * 216 <= (256ull << 20) ? 2 : 4) : var;
-  if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v >= 1 && v <= 3) {
-    if (v == 1) {
-      if (nt) k_ekf9t<false, true, true, SEQ, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<false, true, true, SEQ, 0, true><<<g, kBlock, 0, st>>>(a);
-    } else {
-      const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
-      const dim3 g2((ntiles + 1) / 2);
-      // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
-      const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-      if (v == 2 && nt) k_ekf9p<false, SEQ, kStateNT, false><<<g2, kBlock, lds, st>>>(a);
-      else if (v == 2) k_ekf9p<false, SEQ, 0, false><<<g2, kBlock, lds, st>>>(a);
-      else if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
-      else k_ekf9p<false, SEQ, 0, true><<<g2, kBlock, lds, st>>>(a);
-    }
+  const int v = var == 2 || var == 4 ? var : (s.n * 216 <= (256ull << 20) ? 2 : 4);
+  if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v == 2) {
+    const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
+    const dim3 g2((ntiles + 1) / 2);
+    // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
+    if (nt) k_ekf9p<false, SEQ, kStateNT><<<g2, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, SEQ, 0><<<g2, kBlock, lds, st>>>(a);
     return (int)hipGetLastError();
   }
   // predict-only launches run no update: one (SEQ = false) instantiation serves both
@@ -606,32 +629,31 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
   const dim3 g = grid_for(s.n);
   const bool small = FMSKF_TILED || s.pitch * 8 * 78 < 0xFFFFFFFFull;  // tiled: any N
   const bool nt = FMSKF_TILED && state_nt(s.n * 90 * 8);
+  const bool sp = p.sparse != 0;
   if (in.ens_blocks) {
     // fused tick + record (fmskf_tick_ensemble): the default kernel (decorrelated update,
     // tiled state) with the record epilogue; one record per tick block
     if (!FMSKF_TILED || !p.decor || !ens_nb || !upd || !pred || in.n_ticks != 1) return (int)hipErrorInvalidValue;
     const bool blk = kf12d_sequential(p.r);
-    if (blk && nt) k_kf12s<true, true, true, true, kStateNT, false, true><<<g, kBlock, 0, st>>>(a);
-    else if (blk) k_kf12s<true, true, true, true, 0, false, true><<<g, kBlock, 0, st>>>(a);
-    else if (nt) k_kf12s<false, true, true, true, kStateNT, false, true><<<g, kBlock, 0, st>>>(a);
-    else k_kf12s<false, true, true, true, 0, false, true><<<g, kBlock, 0, st>>>(a);
+    if (sp && nt) k_kf12s<true, true, true, true, kStateNT, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (sp) k_kf12s<true, true, true, true, 0, true, true><<<g, kBlock, 0, st>>>(a);
+    else if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+    else if (blk) k_kf12s<true, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+    else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
+    else k_kf12s<false, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
     *ens_nb = (int)g.x;
     return (int)hipGetLastError();
   }
   if (p.decor) {
-    const bool blk = kf12d_sequential(p.r);
-    static const int var = [] {  // FMSKF_KF12D_VARIANT=1: raised-priority load phase
-      const char *e = getenv("FMSKF_KF12D_VARIANT");
-      return e ? atoi(e) : 0;
-    }();
-    if (var == 1 && FMSKF_TILED && upd && pred && in.n_ticks == 1) {
-      if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-      else if (blk) k_kf12s<true, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
-      else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-      else k_kf12s<false, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF12D_LDS", nt, 0u);
+    // SP (the default R and Q: sparse C^-1 and Q, checked on the host) implies BLK; tiled
+    // state, so SMALL holds for any N
+    if (sp && small && upd && pred) {
+      if (nt) k_kf12s<true, true, true, true, kStateNT, false, true><<<g, kBlock, lds, st>>>(a);
+      else k_kf12s<true, true, true, true, 0, false, true><<<g, kBlock, lds, st>>>(a);
       return (int)hipGetLastError();
     }
-    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF12D_LDS", nt, 0u);
+    const bool blk = kf12d_sequential(p.r);
 #define KF12S(B, S)                                                          \
   if (upd && pred && nt) k_kf12s<B, true, true, S, kStateNT><<<g, kBlock, lds, st>>>(a); \
   else if (upd && pred) k_kf12s<B, true, true, S><<<g, kBlock, lds, st>>>(a); \

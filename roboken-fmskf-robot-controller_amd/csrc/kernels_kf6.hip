@@ -17,9 +17,7 @@
 //    addresses every plane, so the loop needs almost no scalar or vector address math;
 //  * whether a validity mask exists is a compile-time choice (no conditional load whose
 //    merge would force a full vmcnt(0) drain);
-//  * tick_many loads the inputs of tick t+1 before computing tick t; the double-buffered
-//    persistent variant loads the next instance's state + inputs before computing the
-//    current one (two register sets, loop unrolled by two: no loop-carried copies).
+//  * tick_many loads the inputs of tick t+1 before computing tick t.
 #include "ens_device.hpp"
 #include "kf6_lane.hpp"
 
@@ -142,64 +140,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   if constexpr (O::ENS) ens_epilogue<6, R>(a.in, xs, lv);
 }
 
-// Persistent, explicitly double-buffered: two register sets A/B, loop unrolled by two (no
-// loop-carried copies); while set A is computed and stored, set B's loads are in flight
-// (vmcnt is in-order: B's 30 loads + A's 27 stores stay within the 63-deep counter).
-// Loads use clamped indices (always in bounds); the loop condition is block-uniform.
-// Single-tick launches only.
-template <int WPE, class O>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6db(
-    KfArgs<MdKF6, Kf6Params> a) {
-  __shared__ float stab[O::LIBM ? 1 : 513];
-  const uint64_t n = a.n;
-  const uint32_t nn = (uint32_t)n, last = nn - 1u;
-  const uint32_t gs = gridDim.x * kBlock;
-  uint32_t ba = blockIdx.x * kBlock;  // block base of set A
-  const uint32_t t = threadIdx.x;
-  float xa[6], Pa[21], xb[6], Pb[21];
-  Kf6In ma, mb;
-  {
-    const uint32_t i = min(ba + t, last);
-    kf6_load_state<O>(a.x, a.P, a.pitch, i, xa, Pa);
-    if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, i);
-  }
-  stage_table<O::LIBM>(stab, a.in.sintab);
-  for (;;) {
-    const uint32_t bb = ba + gs;
-    if (bb < nn) {
-      const uint32_t i = min(bb + t, last);
-      kf6_load_state<O>(a.x, a.P, a.pitch, i, xb, Pb);
-      if (O::UPD) mb = kf6_load_in<O>(a.in, n, 0, i);
-    }
-    kf6_tick1<O>(ma, stab, a.prm, xa, Pa);
-    if (ba + t < nn) kf6_store_state<O>(a.x, a.P, a.pitch, ba + t, xa, Pa);
-    nan_guard(xa, Pa, a.counters, ba + t < nn);
-    if (bb >= nn) break;
-    const uint32_t bn = bb + gs;
-    if (bn < nn) {
-      const uint32_t i = min(bn + t, last);
-      kf6_load_state<O>(a.x, a.P, a.pitch, i, xa, Pa);
-      if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, i);
-    }
-    kf6_tick1<O>(mb, stab, a.prm, xb, Pb);
-    if (bb + t < nn) kf6_store_state<O>(a.x, a.P, a.pitch, bb + t, xb, Pb);
-    nan_guard(xb, Pb, a.counters, bb + t < nn);
-    if (bn >= nn) break;
-    ba = bn;
-  }
-}
-
 // Variant (FMSKF_KF6_VARIANT, read once) for single-tick launches; default 0:
 //   0: k_kf6p with 2 robots per lane while 124 B x N fits the Infinity Cache, else 15
 //   15: one instance per lane, grid = N/256, straight-line single-tick kernel (k_kf6t)
-//   12 / 13 / 14: k_kf6p with 2 / 3 / 4 robots per lane
-//   3: the same through the tick-loop kernel (k_kf6, as tick_many uses)
-//   1: double-buffered persistent, 2 blocks/CU   2: same, 3 blocks/CU
-//   4: same at <= 128 VGPRs, 4 blocks/CU          5: same, 8 blocks/CU
+//   12: k_kf6p with 2 robots per lane at any N
+// (the tests force 12 / 15 at small N to check both kernels).  Measured and removed: 3 or 4
+// robots per lane (38.0 us at 2^20 against 37.4-38.6 for 2), the single tick through the
+// tick-loop kernel, and persistent double-buffered kernels at 2-8 blocks per CU (5-20% slower).
 static int kf6_variant() {
   static int v = [] {
     const char *e = getenv("FMSKF_KF6_VARIANT");
-    return e ? atoi(e) : 0;
+    const int x = e ? atoi(e) : 0;
+    return x == 12 || x == 15 ? x : 0;
   }();
   return v;
 }
@@ -207,27 +159,15 @@ static int kf6_variant() {
 template <class O>
 static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
   const int v = a.in.n_ticks == 1 ? kf6_variant() : 0;
-  if (v == 1 || v == 2 || v == 4 || v == 5) {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t g = (uint64_t)cus * (v == 1 ? 2 : v == 2 ? 3 : v == 4 ? 4 : 8);
-    const uint64_t need = (a.n + kBlock - 1) / kBlock;
-    const unsigned grid = (unsigned)(g < need ? g : need);
-    if (v <= 2) k_kf6db<2, O><<<grid, kBlock, 0, st>>>(a);
-    else k_kf6db<4, O><<<grid, kBlock, 0, st>>>(a);
-  } else if (a.in.n_ticks == 1 && v >= 12 && v <= 14) {
-    const int R = v - 10;
-    const unsigned g = (unsigned)((a.n + (uint64_t)R * kBlock - 1) / ((uint64_t)R * kBlock));
+  if (a.in.n_ticks == 1 && v == 12) {
+    const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     if constexpr (O::UPD && O::PRED) {
-      if (R == 2 && state_nt(a.n * 108)) {
+      if (state_nt(a.n * 108)) {
         k_kf6p<4, 2, WithNT<O>><<<g, kBlock, 0, st>>>(a);
         return;
       }
     }
-    if (R == 2) k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
-    else if (R == 3) k_kf6p<4, 3, O><<<g, kBlock, 0, st>>>(a);
-    else k_kf6p<4, 4, O><<<g, kBlock, 0, st>>>(a);
+    k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
   } else if (a.in.n_ticks == 1 && v == 0 && a.n * 124 <= (256ull << 20)) {
     // state + one tick's inputs resident in the 256 MiB Infinity Cache: two robots per lane,
     // both robots' inputs loaded up front, one wave round (2^20: 39.7 -> 37.4-38.1 us,

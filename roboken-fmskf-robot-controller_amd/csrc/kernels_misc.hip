@@ -48,19 +48,11 @@ constexpr int ens_r() { return NX >= 12 ? 2 : 8; }
 constexpr int kEnsMaxBlocks = 2048;
 
 // robots per lane of the stand-alone partial: sizes the partial's grid, hence the block-record
-// count the fold reads.  FMSKF_ENS_R 2 | 4 | 8 forces it; by default 8 while n <= 2^21 (a
-// small grid: half the block records for the fold), else 4.  Measured (rocprof, one box):
-// KF6 2^20 partial + fold 6.35 + 4.42 us with 4 -> 5.86 + 2.77 with 8; EKF9 2^20 10.66 + 4.30
-// -> 9.71 + 4.47; at 2^22 8 is neutral (KF6 18.9 / 18.7) or slower (EKF9 27.6 -> 31.0)
-static int ens_rpl(uint64_t n) {
-  static const int forced = [] {
-    const char *e = getenv("FMSKF_ENS_R");
-    const int v = e ? atoi(e) : 0;
-    return v == 2 || v == 4 || v == 8 ? v : 0;
-  }();
-  if (forced) return forced;
-  return n <= (2ull << 20) ? 8 : 4;
-}
+// count the fold reads: 8 while n <= 2^21 (a small grid: half the block records for the
+// fold), else 4.  Measured (rocprof, one box): KF6 2^20 partial + fold 6.35 + 4.42 us with 4
+// -> 5.86 + 2.77 with 8; EKF9 2^20 10.66 + 4.30 -> 9.71 + 4.47; at 2^22 8 is neutral (KF6
+// 18.9 / 18.7) or slower (EKF9 27.6 -> 31.0)
+static int ens_rpl(uint64_t n) { return n <= (2ull << 20) ? 8 : 4; }
 
 int ensemble_nblocks(uint64_t n) {
   const uint64_t per = (uint64_t)kBlock * ens_rpl(n);
@@ -155,33 +147,20 @@ __global__ __launch_bounds__(FT) void k_ens_fold(const double *__restrict__ bloc
   }
 }
 
-// fold block size (FMSKF_ENS_FOLD_THREADS 256 | 512 | 1024; default 1024: 2 record loads per
-// row per thread at 2^20).  KF6 record at 2^20 (partial + fold, back to back): 8.9 us with 256,
-// 8.4 / 11.5 with 512, 8.3 with 1024; EKF9 13.8-15.5 / 13.3-13.4 / 13.2-13.9; a record every
-// tick in the bench: 2.46-2.48e10 steps/s with either (kbench, bench, two passes)
-static int fold_threads() {
-  static const int t = [] {
-    const char *e = getenv("FMSKF_ENS_FOLD_THREADS");
-    const int v = e ? atoi(e) : 1024;
-    return v == 256 || v == 512 ? v : 1024;
-  }();
-  return t;
-}
-template <int NX, int FT>
-static void fold_launch_ft(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
+// fold block size 1024: 2 record loads per row per thread at 2^20.  KF6 record at 2^20
+// (partial + fold, back to back): 8.9 us with 256 threads, 8.4 / 11.5 with 512, 8.3 with 1024;
+// EKF9 13.8-15.5 / 13.3-13.4 / 13.2-13.9; a record every tick in the bench: 2.46-2.48e10
+// steps/s with either (kbench, bench, two passes)
+constexpr int kFoldThreads = 1024;
+template <int NX>
+static void fold_launch(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
+  constexpr int FT = kFoldThreads;
   const int per = (nb + FT - 1) / FT;  // record loads per row per thread
   const dim3 g(EnsRec<NX>::LEN);
   if (per <= 1) k_ens_fold<NX, FT, 1><<<g, FT, 0, st>>>(blocks, nb, shift, out);
   else if (per <= 2) k_ens_fold<NX, FT, 2><<<g, FT, 0, st>>>(blocks, nb, shift, out);
   else if (per <= 4) k_ens_fold<NX, FT, 4><<<g, FT, 0, st>>>(blocks, nb, shift, out);
   else k_ens_fold<NX, FT, 8><<<g, FT, 0, st>>>(blocks, nb, shift, out);
-}
-template <int NX>
-static void fold_launch(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
-  const int ft = fold_threads();
-  if (ft == 1024) fold_launch_ft<NX, 1024>(blocks, nb, shift, out, st);
-  else if (ft == 512) fold_launch_ft<NX, 512>(blocks, nb, shift, out, st);
-  else fold_launch_ft<NX, 256>(blocks, nb, shift, out, st);
 }
 
 // the shift vector: robot 0's state

@@ -69,23 +69,22 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 // Fused correct + predict, one tick, two robots per lane (i and i + G): the tick inputs of
 // both robots (yaw, rpm, the four encoder sums: 44 B, fresh every tick) are loaded first, so
 // the second robot's arrive while the first one's state is read, stepped and written (the
-// input-latency hiding of the KF6 k_kf6p, kernels_kf6.hip).
-// LTAB (TABLE512): the sine table as a wave-private LDS copy (its loads issued first, as in
-// the KF kernels) instead of gathers from the global table after the state arrives
-// tick inputs non-temporal (gfx950 `nt`), as kf6_lane.hpp reads them
+// input-latency hiding of the KF6 k_kf6p, kernels_kf6.hip).  TABLE512: the sine table as a
+// wave-private LDS copy, its loads issued first, as in the KF kernels (global gathers after
+// the state arrives measured 26.8-27.7 against 26.5-27.3 us at 2^20).
+// Every plane goes through a scalar buffer descriptor at its block chunk (ld_chunk /
+// st_chunk, kf_generic.hpp) so the loads and stores carry a cache policy, as in the KF6 tick
+// (kf6_lane.hpp): the tick inputs (read once) non-temporal, the state loaded with CP and
+// stored with st_pol(CP) (`sc1` while it fits the Infinity Cache, non-temporal past it);
+// plain global accesses measured 27.0-27.5 (2^20) and 417 us (2^24) against 26.7 and 398-404.
 #ifndef FMSKF_IN_CPOL
 #define FMSKF_IN_CPOL 2
 #endif
-
-// POL: every plane through a scalar buffer descriptor at its block chunk (ld_chunk /
-// st_chunk, kf_generic.hpp) so the loads and stores carry a cache policy, as in the KF6 tick
-// (kf6_lane.hpp): the tick inputs (read once) non-temporal, the state loaded with CP and
-// stored with st_pol(CP) (`sc1` while it fits the Infinity Cache, non-temporal past it)
-template <bool LIBM, bool LTAB = true, bool POL = true, int CP = 0>
+template <bool LIBM, int CP = 0>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
-  constexpr bool WT = !LIBM && LTAB;
+  constexpr bool WT = !LIBM;
   __shared__ float wtab[WT ? kBlock / 64 : 1][WT ? kWaveTab : 1];
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t G = (uint64_t)gridDim.x * kBlock;
@@ -100,23 +99,16 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
 #pragma unroll
   for (int r = 0; r < 2; r++) {
     const uint64_t i = i0 + r * G < n ? i0 + r * G : n - 1;
-    if constexpr (POL) {
-      // the wave's first lane fixes its 256-robot chunk; clamped lanes (n - 1) stay inside it
-      hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
-      li[r] = (uint32_t)(i - hb[r]);
-      yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
-      const uint64_t rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm),
-                                                            hb[r], n, li[r]);
-      rw[r] = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
+    // the wave's first lane fixes its 256-robot chunk; clamped lanes (n - 1) stay inside it
+    hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
+    li[r] = (uint32_t)(i - hb[r]);
+    yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
+    const uint64_t rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm),
+                                                          hb[r], n, li[r]);
+    rw[r] = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
 #pragma unroll
-      for (int w = 0; w < 4; w++)
-        sum[r][w] = ld_chunk<int64_t, FMSKF_IN_CPOL>(a.in.angle_sum + w * a.in.sum_pitch, hb[r], n, li[r]);
-    } else {
-      yaw[r] = a.in.yaw_deg[i];
-      rw[r] = reinterpret_cast<const uint2 *>(a.in.rpm)[i];
-#pragma unroll
-      for (int w = 0; w < 4; w++) sum[r][w] = a.in.angle_sum[w * a.in.sum_pitch + i];
-    }
+    for (int w = 0; w < 4; w++)
+      sum[r][w] = ld_chunk<int64_t, FMSKF_IN_CPOL>(a.in.angle_sum + w * a.in.sum_pitch, hb[r], n, li[r]);
   }
   tv.store(wtab[WT ? threadIdx.x >> 6 : 0]);
 #pragma unroll
@@ -124,36 +116,18 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     const uint64_t i = i0 + r * G;
     if (i >= n) return;
     RsLane s;
-    if constexpr (POL) {
-      s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
-      s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
+    s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
+    s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
 #pragma unroll
-      for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
-    } else {
-      s.px = a.x[i];
-      s.py = a.x[pp + i];
-#pragma unroll
-      for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
-    }
+    for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
     s.th = 0.f;
     rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], tab);
-    if constexpr (POL) {
-      constexpr int SP = st_pol(CP);
-      const float xs[6] = {s.px, s.py, s.th, s.vx, s.vy, s.vth};
+    constexpr int SP = st_pol(CP);
+    const float xs[6] = {s.px, s.py, s.th, s.vx, s.vy, s.vth};
 #pragma unroll
-      for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
+    for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
 #pragma unroll
-      for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
-    } else {
-      a.x[i] = s.px;
-      a.x[pp + i] = s.py;
-      a.x[2 * pp + i] = s.th;
-      a.x[3 * pp + i] = s.vx;
-      a.x[4 * pp + i] = s.vy;
-      a.x[5 * pp + i] = s.vth;
-#pragma unroll
-      for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
-    }
+    for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
   }
 }
 
@@ -170,26 +144,11 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
     // past the Infinity Cache: 2 blocks per CU (64 KiB of dynamic LDS).  2^24, kbench, two
     // passes: 436.7-448.2 us uncapped, 429-430 at 48 KiB, 418.5-424.5 at 64 KiB
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_RS_LDS", state_nt(s.n * 124), 64u * 1024u);
-    static const bool gtab = [] {  // A/B switch (FMSKF_RS_GTAB=1: the global sine table)
-      const char *e = getenv("FMSKF_RS_GTAB");
-      return e && atoi(e) != 0;
-    }();
-    static const bool pol = [] {  // A/B switch (FMSKF_RS_POL=0: plain global loads and stores)
-      const char *e = getenv("FMSKF_RS_POL");
-      return !e || atoi(e) != 0;
-    }();
-    const bool nt = state_nt(s.n * 124);
-    if (!pol) {
-      if (libm) k_rs2<true, true, false><<<g2, kBlock, lds, st>>>(a);
-      else if (gtab) k_rs2<false, false, false><<<g2, kBlock, lds, st>>>(a);
-      else k_rs2<false, true, false><<<g2, kBlock, lds, st>>>(a);
-    } else if (nt) {
-      if (libm) k_rs2<true, true, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
-      else if (gtab) k_rs2<false, false, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
-      else k_rs2<false, true, true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+    if (state_nt(s.n * 124)) {
+      if (libm) k_rs2<true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+      else k_rs2<false, kStateNT><<<g2, kBlock, lds, st>>>(a);
     } else {
       if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
-      else if (gtab) k_rs2<false, false><<<g2, kBlock, lds, st>>>(a);
       else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
     }
     return (int)hipGetLastError();

@@ -271,8 +271,10 @@ __device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], 
 }
 
 // P <- F P F^T + Q, F = I + Fv(i,k) on the compile-time pattern Md::pat
+// SKIPQ: an exactly-zero Q entry is not added (a wave-uniform branch on the kernel-argument Q;
+// the canonical KF12D order, oracle orc_kf12d_tick: t + 0 only differs from t for t = -0)
 template <class Md, class FV, typename T = typename Md::T, int N = Md::N,
-          int NP = Md::N *(Md::N + 1) / 2>
+          int NP = Md::N *(Md::N + 1) / 2, bool SKIPQ = false>
 __device__ __forceinline__ void kf_predict_cov(T (&P)[NP], const FV &fv, const T *Q) {
   T Tm[N][N];
 #pragma unroll
@@ -294,7 +296,8 @@ __device__ __forceinline__ void kf_predict_cov(T (&P)[NP], const FV &fv, const T
 #pragma unroll
       for (int k = 0; k < N; k++)
         if (Md::pat(j, k)) t = dfma<T>(fv(j, k), Tm[i][k], t);
-      P[pk(i, j)] = t + Q[pk(i, j)];
+      if (!SKIPQ || Q[pk(i, j)] != T(0)) t = t + Q[pk(i, j)];
+      P[pk(i, j)] = t;
     }
   }
 }

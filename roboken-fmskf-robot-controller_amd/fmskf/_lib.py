@@ -56,7 +56,7 @@ class Config(C.Structure):
 class TickInputs(C.Structure):
     _fields_ = [
         ("mem", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("angle_sum_pitch", C.c_uint32),
         ("yaw_deg", C.c_void_p),
         ("gyro_z_dps", C.c_void_p),
         ("rpm", C.c_void_p),

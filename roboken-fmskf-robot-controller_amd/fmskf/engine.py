@@ -202,6 +202,11 @@ class Engine:
             if v is not None:
                 # the C ABI takes bare pointers: check extents here, before the kernel reads
                 need = ((int(n_ticks) - 1) * int(stride) + self.n) * _PER_TICK[name]
+                nd = v.dim() if _is_torch(v) else np.ndim(v)
+                if name == "angle_sum" and n_ticks == 1 and nd == 2 and v.shape[0] == 4 \
+                        and v.shape[1] > self.n:
+                    ti.angle_sum_pitch = int(v.shape[1])  # padded [4][pitch] planes
+                    need = 3 * int(v.shape[1]) + self.n
                 have = v.numel() if _is_torch(v) else np.size(v)
                 if have < need:
                     raise ValueError(f"{name}: {have} elements, {n_ticks} tick(s) need {need}")

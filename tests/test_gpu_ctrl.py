@@ -378,13 +378,17 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
     with Engine(model, n + 1) as d:
         with pytest.raises(fmskf.FmskfError):
             d.load_state(ck)
-    # a truncated file, or one with trailing bytes, is rejected before any copy: the handle
-    # keeps its state
+    # a truncated file, one with trailing bytes, one with a flipped byte in the middle (the
+    # checksum) or a format-1 file (no recorded control / motor layout) is rejected before any
+    # copy: the handle keeps its state
     blob = ck.read_bytes()
+    mid = len(blob) // 2
+    flipped = blob[:mid] + bytes([blob[mid] ^ 0x40]) + blob[mid + 1:]
+    v1 = b"FMSKFCK1" + blob[8:]
     with Engine(model, n) as e:
         e.load_state(ck)
         before = readout(e)
-        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0")):
+        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1)):
             bad = tmp_path / name
             bad.write_bytes(data)
             with pytest.raises(fmskf.FmskfError):

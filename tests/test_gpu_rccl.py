@@ -94,7 +94,7 @@ def _ens_inputs(model, n, T, seed):
                                                 ("rs", 4097, 1, True)])
 def test_async_ensemble_matches_sync(model, n, every, comm):
     """fmskf_tick_ensemble_begin / fmskf_ensemble_end (fold + all-gather + copy-out on the side
-    stream, results collected one event late, so two are pending at every begin with every = 1)
+    stream, results collected two events late, so three are pending at every begin with every = 1)
     against the synchronous fmskf_tick_ensemble of a twin handle on the same inputs: the states
     stay bit-identical and every (mean, cov) equals the fold of the synchronous record bit for
     bit, with and without a (world-1) RCCL communicator."""
@@ -109,7 +109,7 @@ def test_async_ensemble_matches_sync(model, n, every, comm):
                 want.append(fmskf.ensemble_combine(a.nx, a.tick_ensemble(**kw(t))[None, :]))
                 b.tick_ensemble_begin(**kw(t))
                 pending += 1
-                if pending == 2:
+                if pending == 3:
                     got.append(b.ensemble_end())
                     pending -= 1
             else:
@@ -139,12 +139,36 @@ def test_async_ensemble_matches_sync(model, n, every, comm):
 
 def test_async_ensemble_limits():
     with Engine("kf6", 1000) as e:
-        e.ensemble_begin()
-        e.ensemble_begin()
+        for _ in range(4):
+            e.ensemble_begin()
         with pytest.raises(fmskf.FmskfError):
-            e.ensemble_begin()                              # a third pending begin
-        e.ensemble_end()
-        e.ensemble_end()
+            e.ensemble_begin()                              # a fifth pending begin
+        for _ in range(4):
+            e.ensemble_end()
         e.ensemble_begin()                                  # the slots are reusable
         m, c = e.ensemble_end()
     assert np.all(m == 0.0) and np.all(c == 0.0)            # zero state: zero moments
+
+
+def test_async_ensemble_across_reset():
+    """Results begun before a reset fold with the shift of the state they recorded: the reset
+    retakes the shift only after the pending folds (stream-ordered), so the pending result and
+    the next one both equal the synchronous records of the same states."""
+    n = 3001
+    rng = np.random.default_rng(8)
+    with Engine("ekf9", n) as a, Engine("ekf9", n) as b:
+        x1 = (rng.normal(size=(9, n)) + 2.0).astype(np.float32)
+        for e in (a, b):
+            e.set_state(x1, None)
+        b.ensemble_begin()
+        want1 = fmskf.ensemble_combine(9, a.ensemble_partial()[None, :])
+        x2 = (rng.normal(size=(9, n)) * 3.0 - 1.0).astype(np.float32)
+        for e in (a, b):
+            e.reset()
+            e.set_state(x2, None)
+        b.ensemble_begin()
+        want2 = fmskf.ensemble_combine(9, a.ensemble_partial()[None, :])
+        got1, got2 = b.ensemble_end(), b.ensemble_end()
+    for w, g in ((want1, got1), (want2, got2)):
+        np.testing.assert_array_equal(w[0], g[0])
+        np.testing.assert_array_equal(w[1], g[1])

@@ -1,13 +1,14 @@
 """fp32 KF restatement (oracle, = kernel op order) vs the independent fp64 dense
 restatement of the north-star formulas (oracle/kf_ref.py).
 
-Tolerance (north star: "within 1e-5 rel fp32 on state/covariance"), per run of
-T ticks over several instances, relative per physical quantity:
-    max|x_k - x64_k| / max_{j in group(k)} |x64_j|  <= 1e-5
+Tolerance (north star: "within 1e-5 rel fp32 on state/covariance"), after T ticks of a
+small fleet, relative per physical quantity over the fleet (as tests/test_oracle_kf_long.py,
+which runs the 60 000-tick horizon):
+    max_i |x_k,i - x64_k,i| / max_{i, j in group(k)} |x64_j,i|  <= 1e-5
         groups = components sharing a unit (positions, heading, velocities, rates,
         accelerations): a weakly observable component such as the EKF9 gyro bias is
         judged against the rate it biases, not against its own near-zero value
-    max|P - P64| / max|P64|  <= 1e-5   over the packed covariance
+    max|P - P64| / max|P64|  <= 1e-5   over each robot's packed covariance
 The measurement vector z is taken from the fp32 frontend so that only the filter
 arithmetic is compared here.
 """
@@ -25,20 +26,14 @@ GROUPS = {
     6: [(0, 1), (2,), (3, 4), (5,)],
     9: [(0, 1), (2,), (3, 4), (5, 6), (7, 8)],
 }
-# EKF9 rate group (omega, gyro bias): only their sum is measured directly, the split is
-# conditioned at cond(P) ~ 1e7; the fp32 split error peaks near 2e-5 of |omega| during the
-# transient (0.4 % of the bias' own sigma).  Documented looser bound for that group only.
-GROUP_TOL = {(9, (5, 6)): 5e-5}
-
-
 def _check(x32, P32, x64, P64):
+    """x [n, N], P [np, N] of N robots, fp32 against fp64"""
     for grp in GROUPS[x64.shape[0]]:
-        scale = max(max(np.abs(x64[k]).max() for k in grp), 1e-3)
-        tol = GROUP_TOL.get((x64.shape[0], grp), TOL)
+        scale = max(np.abs(x64[list(grp)]).max(), 1e-30)
         for k in grp:
             err = np.abs(x32[k] - x64[k]).max() / scale
-            assert err <= tol, f"state {k}: {err}"
-    assert np.abs(P32 - P64).max() / np.abs(P64).max() <= TOL
+            assert err <= TOL, f"state {k}: {err}"
+    assert (np.abs(P32 - P64).max(axis=0) / np.abs(P64).max(axis=0)).max() <= TOL
 
 
 @pytest.mark.parametrize("trig", [0, 1])
@@ -60,11 +55,10 @@ def test_kf6_fp32_vs_fp64(orc, trig):
         v = np.full(n, valid[t], np.uint8)
         orc.kf6_tick(x, P, yaw[t], gz[t], rpm[t], v, prm)
     zs = np.stack(zs)
-    for i in range(n):
-        x64, P64 = kf_ref.kf6_run(np.zeros(6), p0.astype(np.float64), zs[:, :, i].astype(np.float64),
-                                  q.astype(np.float64), r.astype(np.float64),
-                                  float(np.float32(1e-3)), valid=valid)[-1]
-        _check(x[:, i], P[:, i], x64, P64)
+    res = [kf_ref.kf6_run(np.zeros(6), p0.astype(np.float64), zs[:, :, i].astype(np.float64),
+                          q.astype(np.float64), r.astype(np.float64), float(np.float32(1e-3)),
+                          valid=valid)[-1] for i in range(n)]
+    _check(x, P, np.stack([a for a, _ in res], 1), np.stack([b for _, b in res], 1))
 
 
 # diagonal R: the canonical EKF9 update is the sequential scalar one; correlated: the joint LDL^T
@@ -85,11 +79,10 @@ def test_ekf9_fp32_vs_fp64(orc, terms):
         zs.append(orc.ekf9_measure(raw[t]))
         orc.ekf9_tick(x, P, raw[t], None, prm)
     zs = np.stack(zs)
-    for i in range(n):
-        x64, P64 = kf_ref.ekf9_run(np.zeros(9), p0.astype(np.float64), zs[:, :, i].astype(np.float64),
-                                   q.astype(np.float64), r.astype(np.float64),
-                                   float(np.float32(1e-3)))[-1]
-        _check(x[:, i], P[:, i], x64, P64)
+    res = [kf_ref.ekf9_run(np.zeros(9), p0.astype(np.float64), zs[:, :, i].astype(np.float64),
+                           q.astype(np.float64), r.astype(np.float64), float(np.float32(1e-3)))[-1]
+           for i in range(n)]
+    _check(x, P, np.stack([a for a, _ in res], 1), np.stack([b for _, b in res], 1))
 
 
 def _r_with(r, terms):
@@ -128,7 +121,10 @@ def test_kf12d_cinv_matches_numpy(orc):
                               "groups_semidefinite"])
 def test_kf12d_oracle_vs_dense(orc, terms):
     """fp64 restatement vs dense fp64 (every update path): only the order of operations
-    differs -> 1e-10."""
+    differs -> 1e-12 (BASELINE.json configs[4]'s tolerance; measured 2e-14 - 2e-13).  An
+    indefinite R is no covariance (the joint fallback still inverts S = H P H^T + R, which its
+    negative direction leaves ill-conditioned): measured 1.7e-11, held to 1e-10."""
+    tol = 1e-10 if terms == {(4, 0): 1e-5, (7, 3): -2e-5} else 1e-12
     T, n = 200, 4
     tr = Trajectory(n, T, seed=13)
     z = tr.kf12d_z()
@@ -143,8 +139,8 @@ def test_kf12d_oracle_vs_dense(orc, terms):
     for i in range(n):
         x64, P64 = kf_ref.kf12d_run(np.zeros(12), p0, z[:, :, i], q, r, 1e-3)[-1]
         for k in range(12):
-            assert np.abs(x[k, i] - x64[k]) <= 1e-10 * max(np.abs(x64[k]), 1e-3)
-        assert np.abs(P[:, i] - P64).max() <= 1e-10 * np.abs(P64).max()
+            assert np.abs(x[k, i] - x64[k]) <= tol * max(np.abs(x64[k]), 1e-3)
+        assert np.abs(P[:, i] - P64).max() <= tol * np.abs(P64).max()
 
 
 def test_kf6_tracks_truth(orc):

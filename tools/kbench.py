@@ -59,7 +59,8 @@ def main():
         preps = [e.prepare(yaw_deg=yaw[r], gyro_z_dps=gz[r], rpm=rpm[r]) for r in range(R)]
         many = dict(yaw_deg=yaw, gyro_z_dps=gz, rpm=rpm)
     elif args.model == "rs":
-        sums = torch.cumsum(torch.randint(-20, 20, (R, 4, n), device=dev, dtype=torch.int64), 0)
+        # --pad: the [4][N] encoder-sum planes at a padded pitch (fmskf_tick_inputs.angle_sum_pitch)
+        sums = torch.cumsum(torch.randint(-20, 20, (R, 4, n + args.pad), device=dev, dtype=torch.int64), 0)
         preps = [e.prepare(yaw_deg=yaw[r], angle_sum=sums[r], rpm=rpm[r]) for r in range(R)]
         many = dict(yaw_deg=yaw, angle_sum=sums, rpm=rpm)
     elif args.model == "ekf9":

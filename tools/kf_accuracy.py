@@ -35,12 +35,12 @@ def run(model, n, ticks, every, trig, chunk=1000, seed=0x464D534B):
     dt32 = float(np.float32(1e-3))
     if model == "kf6":
         prm = orc.kf6_params(1e-3, q, r, trig)
-        ref = kf_ref.Kf6Batch(n, np.zeros(6), p0.astype(np.float64), q.astype(np.float64),
-                              r.astype(np.float64), dt32)
+        ref = kf_ref.DenseC("kf6", n, np.zeros(6), p0.astype(np.float64), q.astype(np.float64),
+                            r.astype(np.float64), dt32)
     else:
         prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
-        ref = kf_ref.Ekf9Batch(n, np.zeros(9), p0.astype(np.float64), q.astype(np.float64),
-                               r.astype(np.float64), dt32)
+        ref = kf_ref.DenseC("ekf9", n, np.zeros(9), p0.astype(np.float64), q.astype(np.float64),
+                            r.astype(np.float64), dt32)
     x = np.zeros((nx, n), np.float32)
     P = np.repeat(p0[:, None], n, 1).copy()
     worst = {}

@@ -9,6 +9,7 @@ give the correction factors, applied to the tick kernel's readings.
 
   python tools/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json] [records|planes]
   python tools/pmc_traffic.py secondary gpurun_out [profiles/pmc_traffic_secondary.json]
+  python tools/pmc_traffic.py paths gpurun_out [profiles/pmc_traffic_paths.json]
 """
 import csv
 import glob
@@ -75,7 +76,54 @@ def secondary(root, out):
     return 0
 
 
+# The rows either side of the tick at 2^20 (bench path_rows): (bench key, kernel substring,
+# kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
+# written (56); WT901 standard poll: row, len, parser window / count / flags, magnetometer,
+# q_init read (88), parser state, error, 15 registers, Data page written (109); CAN RX, four
+# wheels: frame, stamp, micro, angle, head, IIR y / x, sum read (124), those state fields plus
+# speed, dlt, rpm, curr written (132).  The counters are corrected with the KF6 calibration of
+# profiles/pmc_traffic.json (the same streaming dword / 8- / 16-byte lane accesses: FETCH_SIZE
+# counts half, WRITE_SIZE exact).
+PATHS = [
+    ("rs_tick_2p20", "k_rs2", 84, 56),
+    ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
+    ("wt901_ingest_2p20", "k_wt901", 88, 109),
+    ("can_ingest_2p20", "k_can4", 124, 132),
+]
+
+
+def paths(root, out, calib="profiles/pmc_traffic.json"):
+    """profiles/pmc_traffic_paths.json: memory-side bytes per launch of the path-row kernels at
+    2^20 (gpurun_out/pmc_path_{key}_{FETCH,WRITE}_SIZE, tools/kbench.py runs)."""
+    cj = json.load(open(calib))
+    fac = {c: cj[c]["calibration_factor"] for c in ("FETCH_SIZE", "WRITE_SIZE")}
+    n = 1 << 20
+    res = {"unit": "bytes per launch", "n_instances": n,
+           "calibration": f"{calib} (KF6 pattern): FETCH x {fac['FETCH_SIZE']:.4f}, WRITE x {fac['WRITE_SIZE']:.4f}"}
+    for key, ksub, rd, wr in PATHS:
+        ent = {"kernel": ksub}
+        for c, algo in (("FETCH_SIZE", rd * n), ("WRITE_SIZE", wr * n)):
+            kv = read(os.path.join(root, f"pmc_path_{key}_{c}"), ksub)
+            if not kv:
+                print(f"missing data for {key} {c}")
+                return 1
+            k = sorted(kv)[len(kv) // 2] * 1024.0
+            ent[c] = {"raw_bytes": k, "calibrated_bytes": k * fac[c], "kernel_algorithmic_bytes": algo,
+                      "over_algorithmic": k * fac[c] / algo}
+        ent["hbm_bytes_per_launch"] = ent["FETCH_SIZE"]["calibrated_bytes"] + ent["WRITE_SIZE"]["calibrated_bytes"]
+        ent["algorithmic_bytes_per_launch"] = (rd + wr) * n
+        ent["traffic_over_algorithmic"] = ent["hbm_bytes_per_launch"] / ent["algorithmic_bytes_per_launch"]
+        res[key] = ent
+    print(json.dumps(res, indent=1))
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+    return 0
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "paths":
+        return paths(sys.argv[2] if len(sys.argv) > 2 else "gpurun_out",
+                     sys.argv[3] if len(sys.argv) > 3 else None)
     if len(sys.argv) > 1 and sys.argv[1] == "secondary":
         return secondary(sys.argv[2] if len(sys.argv) > 2 else "gpurun_out",
                          sys.argv[3] if len(sys.argv) > 3 else None)

@@ -1,0 +1,43 @@
+#!/usr/bin/env bash
+# Round-3 GPU session: parity tests, the driver's bench command, its rocprofv3 kernel trace,
+# and FETCH_SIZE / WRITE_SIZE passes (one counter per run) of the path-row kernels at 2^20.
+# Each GPU step has its own limit; a crash / abort / timeout (rc not in {0,1}) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+STEPS="${STEPS:-tests bench prof pmc}"
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 6 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!!! $name rc=$rc: stopping"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -rf ${PYTEST_K:-} ;;
+    bench) run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+             python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc)   for c in FETCH_SIZE WRITE_SIZE; do
+             run pmc_path_rs_tick_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_rs_tick_2p20_$c" -o run -- \
+               python tools/kbench.py --model rs --ticks 30
+             run pmc_path_rs_tick_2p20_padded_sums_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_rs_tick_2p20_padded_sums_$c" -o run -- \
+               python tools/kbench.py --model rs --pad 512 --ticks 30
+             run pmc_path_wt901_ingest_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_wt901_ingest_2p20_$c" -o run -- \
+               python tools/kbench.py --op wt901 --ticks 30
+             run pmc_path_can_ingest_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_can_ingest_2p20_$c" -o run -- \
+               python tools/kbench.py --op can --ticks 30
+           done ;;
+    kb)    i=0; IFS=';' read -ra KBL <<< "${KB_LIST:-}"; for a in "${KBL[@]}"; do
+             i=$((i+1)); run kb$i 240 python tools/kbench.py $a
+           done ;;
+  esac
+done
+echo "=== session done"
