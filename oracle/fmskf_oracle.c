@@ -503,7 +503,7 @@ void orc_kf6_tick(size_t n, float *x, float *P, const float *yaw_deg, const floa
       y[1] = z[1] - xs[5];
       y[2] = z[2] - xs[3];
       y[3] = z[3] - xs[4];
-      orc_kf_update_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r);
+      orc_kf_update_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r, NULL, -1);
     }
     if (do_predict) {
       xs[0] = fmaf(prm->dt, xs[3], xs[0]);
@@ -567,19 +567,21 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
     size_t i = (size_t)ii;
     float xs[9], Ps[45];
     for (int k = 0; k < 9; k++) xs[k] = x[k * n + i];
+    float lo = x[9 * n + i];  /* row 9: the compensated heading's low part */
     for (int k = 0; k < 45; k++) Ps[k] = P[k * n + i];
     if (do_update && (!valid || valid[i])) {
       float z[6], y[6];
       orc_ekf9_meas1(raw + i * 8, z);
-      y[0] = orc_wrap_innov_f(z[0] - xs[2]);
+      y[0] = orc_wrap_innov_f((z[0] - xs[2]) - lo);
       y[1] = z[1] - (xs[5] + xs[6]);
       y[2] = z[2] - xs[7];
       y[3] = z[3] - xs[8];
       y[4] = z[4] - xs[3];
       y[5] = z[5] - xs[4];
       /* canonical order: sequential scalar updates for a diagonal R, else the joint LDL^T */
-      if (rdiag) orc_kf_update_seq_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
-      else orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r);
+      if (rdiag) orc_kf_update_seq_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2);
+      else orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2);
+      orc_th_norm_f32(&xs[2], &lo);
     }
     if (do_predict) {
       float dt = prm->dt;
@@ -600,12 +602,22 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
       F[4][8] = dt;
       xs[0] = xs[0] + vwx * dt;
       xs[1] = xs[1] + vwy * dt;
-      xs[2] = orc_wrap_pi_f(xs[2] + xs[5] * dt);
+      orc_th_add_f32(&xs[2], &lo, xs[5] * dt);
+      /* wrap of the compensated heading: hi -/+ fp32(2 pi) is exact, the rest of 2 pi to lo */
+      if (xs[2] >= ORC_PI_F) {
+        xs[2] = xs[2] - 2.0f * ORC_PI_F;
+        lo = lo + 1.7484555e-7f;
+      } else if (xs[2] < -ORC_PI_F) {
+        xs[2] = xs[2] + 2.0f * ORC_PI_F;
+        lo = lo - 1.7484555e-7f;
+      }
+      orc_th_norm_f32(&xs[2], &lo);
       xs[3] = xs[3] + xs[7] * dt;
       xs[4] = xs[4] + xs[8] * dt;
       orc_kf_predict_cov_f32(9, Ps, F, pat, prm->q);
     }
     for (int k = 0; k < 9; k++) x[k * n + i] = xs[k];
+    x[9 * n + i] = lo;
     for (int k = 0; k < 45; k++) P[k * n + i] = Ps[k];
   }
 }
@@ -727,13 +739,13 @@ void orc_kf12d_tick(size_t n, double *x, double *P, const double *z, const uint8
       } else if (seq) {
         for (int a = 0; a < 4; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
         y[0] = orc_wrap_innov_d(y[0]);
-        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1, k_kf12_h2, y, r1);
+        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1, k_kf12_h2, y, r1, NULL, -1);
         for (int a = 0; a < 4; a++) y[a] = z[(a + 4) * n + i] - xs[k_kf12_h1[a + 4]];
-        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1 + 4, k_kf12_h2 + 4, y, r2);
+        orc_kf_update_f64(12, 4, xs, Ps, k_kf12_h1 + 4, k_kf12_h2 + 4, y, r2, NULL, -1);
       } else {
         for (int a = 0; a < 8; a++) y[a] = z[a * n + i] - xs[k_kf12_h1[a]];
         y[0] = orc_wrap_innov_d(y[0]);
-        orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r);
+        orc_kf_update_f64(12, 8, xs, Ps, k_kf12_h1, k_kf12_h2, y, prm->r, NULL, -1);
       }
     }
     if (do_predict) {

@@ -124,7 +124,8 @@ typedef struct {
   float r[21];        /* (theta, omega_gyro, ax, ay, vbx, vby) packed */
   int   trig;
 } orc_ekf9_params;
-/* x [9][n], P [45][n], raw [n][8] int16 words (yaw, gz, ax, ay, rpm FL BL BR FR) */
+/* x [10][n] (the 9 states, then the compensated heading's low part), P [45][n], raw [n][8]
+ * int16 words (yaw, gz, ax, ay, rpm FL BL BR FR) */
 void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8_t *valid,
                    const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads);
 void orc_ekf9_measure(size_t n, const int16_t *raw, float *z /*[6][n]*/);

@@ -329,6 +329,10 @@ def ekf9_params(dt, q_packed, r_packed, trig=TRIG_TABLE512):
 
 
 def ekf9_tick(x, P, raw, valid, prm, do_update=True, do_predict=True, nthreads=1):
+    """x [10, n]: the 9 states and, in row 9, the compensated heading's low part (zero at start;
+    the library keeps it as a hidden row: its x[2] is row 2 here, bit for bit)"""
+    if x.shape[0] != 10:
+        raise ValueError("ekf9_tick: x needs 10 rows (row 9: the heading's low part)")
     n = x.shape[1]
     lib().orc_ekf9_tick(n, x, P, _ptr(raw), _ptr(valid), C.byref(prm), int(do_update),
                         int(do_predict), nthreads)

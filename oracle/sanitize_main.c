@@ -142,7 +142,7 @@ static void check_kf(void) {
   }
   orc_kf6_measure(n, yaw, gz, rpm, z, 0);
 
-  float *x9 = xmalloc(9 * n * 4), *P9 = xmalloc(45 * n * 4);
+  float *x9 = xmalloc(10 * n * 4), *P9 = xmalloc(45 * n * 4); /* row 9: the heading low part */
   int16_t *raw = xmalloc(n * 16);
   orc_ekf9_params p9;
   memset(&p9, 0, sizeof(p9));

@@ -539,6 +539,7 @@ void do_reset(fmskf_ctx *h) {
     }
   }
   if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * pp * 8, st), "reset prev");
+  if (s.thlo) hip_check(hipMemsetAsync(s.thlo, 0, n * 4, st), "reset heading low part");
   if (s.imu_reg) zero_imu(h);
   if (s.m_sum) zero_motors(h);
   if (h->ctrl_ready) {  // the control objects are static in the firmware too: zero, power off
@@ -785,6 +786,8 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.x = h->alloc<char>((size_t)d.nx * s.pitch * d.elem);
       s.P = d.m ? h->alloc<char>((size_t)np * s.pitch * d.elem) : nullptr;
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
+      // EKF9: the compensated heading's hidden low part (kf_generic.hpp th_add), one float a robot
+      s.thlo = cfg->model == FMSKF_MODEL_EKF9 ? h->alloc<float>(n) : nullptr;
       // the WT901 / motor ingest state (~470 B per robot) is allocated on first use
       // (ensure_imu / ensure_motors): a handle fed tick inputs by the caller holds only x, P
       s.counters = h->alloc<unsigned long long>(8);
@@ -1056,6 +1059,8 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
       if (p_packed) copy_planes_in(h, h->s.P, p_packed, row, pb, np, mem);
     }
     if (x) h->ens_shift_ok = false;
+    // a heading set from outside is exact as given: its compensation term restarts at zero
+    if (x && h->s.thlo) hip_check(hipMemsetAsync(h->s.thlo, 0, n * 4, h->stream), "heading low part");
     finish_out(h, mem);
   });
 }
@@ -1095,6 +1100,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.x, (size_t)d.nx * pp * d.elem});
     if (s.P) v.push_back({s.P, (size_t)d.nx * (d.nx + 1) / 2 * pp * d.elem});
     if (s.prev_sum) v.push_back({s.prev_sum, (size_t)4 * pp * 8});
+    if (s.thlo) v.push_back({s.thlo, (size_t)n * 4});
     v.push_back({s.counters, 8 * 8});
   }
   if (groups & 2) {

@@ -123,6 +123,17 @@ __device__ __forceinline__ float wrap_innov(float a) {
   else if (a < -FMSKF_PI_F) a = a + 2.0f * FMSKF_PI_F;
   return a;
 }
+// wrap_pi of a compensated angle hi + lo: hi -/+ fp32(2 pi) is exact (Sterbenz), the rest of
+// 2 pi (2 pi - 6.28318548f = -1.7484555e-7) goes to lo
+__device__ __forceinline__ void wrap_pi_c(float &hi, float &lo) {
+  if (hi >= FMSKF_PI_F) {
+    hi = hi - 2.0f * FMSKF_PI_F;
+    lo = lo + 1.7484555e-7f;
+  } else if (hi < -FMSKF_PI_F) {
+    hi = hi + 2.0f * FMSKF_PI_F;
+    lo = lo - 1.7484555e-7f;
+  }
+}
 __device__ __forceinline__ double wrap_pi(double a) {
   if (a >= FMSKF_PI_D) a = a - 2.0 * FMSKF_PI_D;
   else if (a < -FMSKF_PI_D) a = a + 2.0 * FMSKF_PI_D;

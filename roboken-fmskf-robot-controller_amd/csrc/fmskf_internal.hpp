@@ -27,6 +27,7 @@ struct DevState {
   void *x = nullptr;
   void *P = nullptr;
   int64_t *prev_sum = nullptr;  // RS: s64_rawAngleSumPrev [4][N]
+  float *thlo = nullptr;        // EKF9: the heading's low part [N] (compensated heading)
   // WT901 / IMU_IF_WT901C
   int16_t *imu_reg = nullptr;     // sReg [0x90][N]
   uint32_t *imu_parser = nullptr; // parser window [3][N] (bytes 0..11, little-endian)
@@ -81,7 +82,12 @@ struct KfParams {
   T r[MP];
 };
 using Kf6Params = KfParams<float, 21, 10>;
-using Ekf9Params = KfParams<float, 45, 21>;
+struct Ekf9Params {
+  float dt;
+  float q[45];
+  float r[21];
+  float *thlo;  // [N] the compensated heading's low part (a hidden state row; th_add)
+};
 struct Kf12dParams {
   double dt;
   double q[78];

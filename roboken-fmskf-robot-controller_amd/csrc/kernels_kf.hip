@@ -14,8 +14,9 @@
 
 namespace fmskf {
 
-// EKF9 z from raw WT901 registers (imu_if_wt901c.cpp:96-99,107-113) + wheel rpm
-__device__ __forceinline__ void ekf9_innov(const uint4 w, const float (&x)[9], float (&y)[6]) {
+// EKF9 z from raw WT901 registers (imu_if_wt901c.cpp:96-99,107-113) + wheel rpm; the heading
+// innovation against the compensated heading x[2] + lo
+__device__ __forceinline__ void ekf9_innov(const uint4 w, const float (&x)[9], float lo, float (&y)[6]) {
   int16_t a[4], r[4];
   unpack4(make_uint2(w.x, w.y), a);
   unpack4(make_uint2(w.z, w.w), r);
@@ -28,7 +29,7 @@ __device__ __forceinline__ void ekf9_innov(const uint4 w, const float (&x)[9], f
                vth);
   const float z0 = deg2rad(yaw), z1 = deg2rad(gz), z2 = ax * K::g0, z3 = ay * K::g0;
   const float z4 = vx * 0.001f, z5 = vy * 0.001f;
-  y[0] = wrap_innov(z0 - x[2]);
+  y[0] = wrap_innov((z0 - x[2]) - lo);
   y[1] = z1 - (x[5] + x[6]);
   y[2] = z2 - x[7];
   y[3] = z3 - x[8];
@@ -53,16 +54,18 @@ __device__ __forceinline__ uint4 ekf9_raw_at(const int16_t *raw, uint64_t i) {
 
 // one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
 // SEQ: R is diagonal -> the sequential scalar update (kf_update_seq), else the joint LDL^T one
+// lo: the compensated heading's low part (th_add, kf_generic.hpp)
 template <bool LIBM, bool UPD, bool PRED, bool SEQ>
 __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, const uint4 raw,
                                            bool have, const float *stab, float (&x)[9],
-                                           float (&P)[45]) {
+                                           float (&P)[45], float &lo) {
   const float dt = a.prm.dt;
   if (UPD && have) {
     float y[6];
-    ekf9_innov(raw, x, y);
-    if constexpr (SEQ) kf_update_seq<MdEKF9>(x, P, y, a.prm.r);
-    else kf_update<MdEKF9>(x, P, y, a.prm.r);
+    ekf9_innov(raw, x, lo, y);
+    if constexpr (SEQ) kf_update_seq<MdEKF9, 2>(x, P, y, a.prm.r, &lo);
+    else kf_update<MdEKF9, 2>(x, P, y, a.prm.r, &lo);
+    th_norm(x[2], lo);
   }
   if (PRED) {
     // f(x): mecanum body velocity rotated into the world frame (the reference's
@@ -75,7 +78,9 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
     const float f12 = vwx * dt, f13 = s * dt, f14 = c * dt;
     x[0] = x[0] + vwx * dt;
     x[1] = x[1] + vwy * dt;
-    x[2] = wrap_pi(x[2] + x[5] * dt);
+    th_add(x[2], lo, x[5] * dt);
+    wrap_pi_c(x[2], lo);
+    th_norm(x[2], lo);
     x[3] = x[3] + x[7] * dt;
     x[4] = x[4] + x[8] * dt;
     auto fv = [&](int r, int k) -> float {
@@ -123,6 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 #pragma unroll
     for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
   }
+  float lo = a.prm.thlo[ic];
   uint4 ra = raw_at(0), rb;
   bool ha = have_at(0), hb;
   for (uint32_t t = 0; t < T; t += 2) {
@@ -130,15 +136,16 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
       rb = raw_at(t + 1);
       hb = have_at(t + 1);
     }
-    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, ra, ha, stab, x, P);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, ra, ha, stab, x, P, lo);
     if (t + 1 >= T) break;
     if (t + 2 < T) {
       ra = raw_at(t + 2);
       ha = have_at(t + 2);
     }
-    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, rb, hb, stab, x, P);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, rb, hb, stab, x, P, lo);
   }
   if (live) {
+    a.prm.thlo[i] = lo;
     if constexpr (FMSKF_TILED) {
 #pragma unroll
       for (int k = 0; k < N; k++) tx.st(k, x[k]);
@@ -183,9 +190,13 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
   const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
+  const uint64_t hb0 = (uint64_t)blockIdx.x * kBlock;
+  const uint32_t sl = tile_slot(n);
+  float lo = ld_chunk<float, CP>(a.prm.thlo, hb0, n, sl);
   tv.store(stab);
-  ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P);
+  ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P, lo);
   if (live) {
+    st_chunk<float, st_pol(CP)>(a.prm.thlo, hb0, n, sl, lo);
     if constexpr (FMSKF_TILED) {
 #pragma unroll
       for (int k = 0; k < N; k++) tx.st(k, x[k]);
@@ -245,9 +256,12 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   for (int k = 0; k < N; k++) xb[k] = txb.ld(k);
 #pragma unroll
   for (int k = 0; k < NP; k++) Pb[k] = tpb.ld(k);
+  float loa = ld_chunk<float, CP>(a.prm.thlo, (uint64_t)ta * kBlock, n, slot(ta));
+  float lob = ld_chunk<float, CP>(a.prm.thlo, (uint64_t)tb * kBlock, n, slot(tb));
   tv.store(stab);
-  ekf9_tick1<LIBM, true, true, SEQ>(a, ra, ha, stab, xa, Pa);
+  ekf9_tick1<LIBM, true, true, SEQ>(a, ra, ha, stab, xa, Pa, loa);
   if (live_a) {
+    st_chunk<float, st_pol(CP)>(a.prm.thlo, (uint64_t)ta * kBlock, n, slot(ta), loa);
 #pragma unroll
     for (int k = 0; k < N; k++) txa.st(k, xa[k]);
 #pragma unroll
@@ -259,8 +273,9 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = xa[k];
   }
-  ekf9_tick1<LIBM, true, true, SEQ>(a, rb, hb, stab, xb, Pb);
+  ekf9_tick1<LIBM, true, true, SEQ>(a, rb, hb, stab, xb, Pb, lob);
   if (live_b) {
+    st_chunk<float, st_pol(CP)>(a.prm.thlo, (uint64_t)tb * kBlock, n, slot(tb), lob);
 #pragma unroll
     for (int k = 0; k < N; k++) txb.st(k, xb[k]);
 #pragma unroll
@@ -534,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 // epilogue; returns the grid (= the number of block records)
 template <bool LIBM, bool SEQ>
 static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, bool nt, hipStream_t st) {
-  if (!LIBM && s.n * 216 <= (256ull << 20)) {
+  if (!LIBM && s.n * 220 <= (256ull << 20)) {
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const dim3 g2((ntiles + 1) / 2);
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
@@ -570,7 +585,7 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
     const char *e = getenv("FMSKF_EKF9_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  const int v = var == 2 || var == 4 ? var : (s.n * 216 <= (256ull << 20) ? 2 : 4);
+  const int v = var == 2 || var == 4 ? var : (s.n * 220 <= (256ull << 20) ? 2 : 4);
   if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v == 2) {
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const dim3 g2((ntiles + 1) / 2);
@@ -614,7 +629,9 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
 int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool libm, bool upd,
                 bool pred, hipStream_t st, int *ens_nb) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
-  const bool nt = FMSKF_TILED && state_nt(s.n * 54 * 4);
+  a.prm.thlo = s.thlo;
+  if (!s.thlo) return (int)hipErrorInvalidValue;
+  const bool nt = FMSKF_TILED && state_nt(s.n * 55 * 4);
   if (in.ens_blocks && (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1))
     return (int)hipErrorInvalidValue;
   // canonical update order (oracle orc_ekf9_tick): sequential scalar updates when R is

@@ -152,11 +152,37 @@ struct KfArgs {
 };
 
 // ---------------------------------------------------------------------------
-// generic update / covariance predict (fully unrolled -> registers only)
+// compensated heading (EKF9): the heading is kept as hi + lo, hi the fp32 state row and lo a
+// hidden row of the rounding errors of every addition to it (TwoSum), renormalised once per
+// update and once per predict.  The EKF9's rate split is inferred from heading differences over
+// dt, so plain fp32 rounding of the heading (up to 2.4e-7 rad) is amplified by 1/dt into the
+// omega / gyro-bias split; with the lo row the split stays within 7e-7 of the float64 filter
+// (1.3e-5 without) -- tests/test_oracle_kf_long.py.  Canonical order of the oracle's th_add /
+// th_norm (oracle/orc_kf_generic.inc).
 // ---------------------------------------------------------------------------
-template <class Md, typename T = typename Md::T, int N = Md::N, int M = Md::M,
+template <typename T>
+__device__ __forceinline__ void th_add(T &hi, T &lo, T d) {
+  const T s = hi + d;
+  const T bp = s - hi;
+  const T e = (hi - (s - bp)) + (d - bp);
+  hi = s;
+  lo = lo + e;
+}
+template <typename T>
+__device__ __forceinline__ void th_norm(T &hi, T &lo) {
+  const T s = hi + lo;
+  lo = lo - (s - hi);
+  hi = s;
+}
+
+// ---------------------------------------------------------------------------
+// generic update / covariance predict (fully unrolled -> registers only)
+// CI >= 0: state CI is compensated (x[CI] + *lo, th_add instead of the plain addition)
+// ---------------------------------------------------------------------------
+template <class Md, int CI = -1, typename T = typename Md::T, int N = Md::N, int M = Md::M,
           int NP = Md::N *(Md::N + 1) / 2>
-__device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M], const T *R) {
+__device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M], const T *R,
+                                          T *lo = nullptr) {
   T HP[M][N];
 #pragma unroll
   for (int a = 0; a < M; a++) {
@@ -216,7 +242,8 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
     T t = HP[0][j] * vw[0];
 #pragma unroll
     for (int a = 1; a < M; a++) t = dfma<T>(HP[a][j], vw[a], t);
-    x[j] = x[j] + t;
+    if (j == CI) th_add(x[j], *lo, t);
+    else x[j] = x[j] + t;
   }
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -236,9 +263,10 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
 // of P, or the sum of two), s = H_a hp + r_aa, g = y_a / s, x += hp g, P -= (hp / s) hp^T.
 // About 2/3 of the LDL^T form's VALU (EKF9: no 6x9 U / V matrices, no forward substitution).
 // Canonical order of oracle orc_kf_update_seq.
-template <class Md, typename T = typename Md::T, int N = Md::N, int M = Md::M,
+template <class Md, int CI = -1, typename T = typename Md::T, int N = Md::N, int M = Md::M,
           int NP = Md::N *(Md::N + 1) / 2>
-__device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], const T *R) {
+__device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], const T *R,
+                                              T *lo = nullptr) {
 #pragma unroll
   for (int a = 0; a < M; a++) {
     T hp[N];
@@ -254,7 +282,10 @@ __device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], 
     const T si = (T)1 / s;
     const T g = y[a] * si;
 #pragma unroll
-    for (int j = 0; j < N; j++) x[j] = dfma<T>(hp[j], g, x[j]);
+    for (int j = 0; j < N; j++) {
+      if (j == CI) th_add(x[j], *lo, hp[j] * g);
+      else x[j] = dfma<T>(hp[j], g, x[j]);
+    }
 #pragma unroll
     for (int b = a + 1; b < M; b++) {
       T h = hp[Md::h1(b)];

@@ -20,11 +20,11 @@ pytestmark = pytest.mark.gpu
 def _ekf9_oracle(orc, n, raw):
     cfg = fmskf.default_config("ekf9", n)
     prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
-    x = np.zeros((9, n), np.float32)
+    x = np.zeros((10, n), np.float32)  # row 9: the heading's low part
     P = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
     for t in range(raw.shape[0]):
         orc.ekf9_tick(x, P, raw[t], None, prm, nthreads=0)
-    return x, P
+    return np.ascontiguousarray(x[:9]), P
 
 
 def test_two_handles_two_streams_interleaved(orc):

@@ -72,7 +72,7 @@ def test_ekf9_fp32_vs_fp64(orc, terms):
     r = _r_with(np.array(cfg.r[:21]), terms).astype(np.float32)
     p0 = np.array(cfg.p0[:45], np.float32)
     prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
-    x = np.zeros((9, n), np.float32)
+    x = np.zeros((10, n), np.float32)  # row 9: the heading's low part
     P = np.repeat(p0[:, None], n, 1).copy()
     zs = []
     for t in range(T):

@@ -15,12 +15,11 @@ quantity's vector across robots): for state k in group g,
 momentary value), and for the covariance, per robot, max |P32 - P64| / max |P64|.
 
 North-star bar 1e-5.  Measured over 60 000 ticks:
-* every observable state (heading, velocities, yaw rate, accelerations): <= 1.2e-6 at every
-  sampled tick;
-* the EKF9 rate split (omega, gyro bias): only their sum is measured, the split is inferred
-  from heading differences over dt = 1 ms, so the heading's fp32 rounding (up to 2.4e-7 rad) is
-  amplified by 1/dt into the split while the gains are large: 1.3e-5 in the first 200 ticks,
-  <= 6.5e-6 after;
+* every observable state (heading, velocities, yaw rate, gyro bias, accelerations) within 1e-5
+  at every sampled tick.  The EKF9's rate split (omega, gyro bias) is inferred from heading
+  differences over dt = 1 ms: a plain fp32 heading's rounding (up to 2.4e-7 rad) is amplified by
+  1/dt into the split (1.3e-5 in the first 200 ticks); the compensated heading (a hidden fp32
+  low-part row, kf_generic.hpp th_add) holds it below 1e-6;
 * the open-loop integrals -- positions and their variance, which no measurement observes:
   every x += v dt rounds (a random walk, the same drift the firmware's fp32 odometry has,
   VD_vehicle_controller.cpp:50-51), and the position variance (1 m^2 from P0) grows by process
@@ -60,7 +59,7 @@ def run_long(orc, model, n=N_LONG, ticks=T_LONG, every=EVERY, seed=0x464D534B ^ 
         prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
     ref = kf_ref.DenseC(model, n, np.zeros(nx), p0.astype(np.float64), q.astype(np.float64),
                         r.astype(np.float64), float(np.float32(1e-3)))
-    x = np.zeros((nx, n), np.float32)
+    x = np.zeros((nx + (nx == 9), n), np.float32)  # EKF9: row 9 the heading's low part
     P = np.repeat(p0[:, None], n, 1).copy()
     rng = np.random.default_rng(seed)
     samples, gerr, perr = [], {g: [] for g in GROUPS[nx]}, []
@@ -118,11 +117,7 @@ def test_kf6_60000_ticks_1024_robots_vs_fp64(orc):
 @pytest.mark.slow
 def test_ekf9_60000_ticks_1024_robots_vs_fp64(orc):
     samples, gerr, perr = run_long(orc, "ekf9")
-    # the rate split's transient (ticks < 200): the heading's rounding over dt, see the docstring
-    late = samples >= 200
-    assert gerr["rate"][late].max() <= TOL, gerr["rate"][late].max()
-    assert gerr["rate"].max() <= 1.5 * TOL, gerr["rate"].max()
-    _assert_long("ekf9", samples, gerr, perr, ("th", "vel", "acc"))
+    _assert_long("ekf9", samples, gerr, perr, ("th", "vel", "rate", "acc"))
 
 
 @pytest.mark.parametrize("model", ["kf6", "ekf9"])

@@ -1,5 +1,9 @@
-"""Copy the profiling session's outputs (tools/profile_session.sh, PROF_ALL=1) from gpurun_out/
-into profiles/ under a round prefix:  python tools/collect_profiles.py r1"""
+"""Copy the profiling session's outputs from gpurun_out/ into profiles/ under a round prefix:
+    python tools/collect_profiles.py r3 [--pmc-kf6] [--secondary]
+always: bench.log / prof.log lines, the rocprofv3 kernel / domain stats and the fmskf kernel trace
+of the driver's command, and the path-row PMC passes (pmc_path_*, tools/r3_session.sh) when
+present; --pmc-kf6: the headline kernel's FETCH / WRITE passes and their calibration pattern
+(tools/profile_session.sh); --secondary: the HBM-regime PMC passes and the prof_* kernel stats"""
 import csv
 import glob
 import json
@@ -24,6 +28,8 @@ def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
     if not tag.isidentifier():  # a round prefix such as r2, never an option
         raise SystemExit(__doc__)
+    pmc_kf6 = "--pmc-kf6" in sys.argv
+    secondary = "--secondary" in sys.argv
     json.dump(last_json(os.path.join(G, "bench.log")), open(os.path.join(P, f"{tag}_bench.json"), "w"), indent=1)
     json.dump(last_json(os.path.join(G, "prof.log")), open(os.path.join(P, f"{tag}_prof_bench_line.json"), "w"),
               indent=1)
@@ -39,14 +45,30 @@ def main():
         for row in r:
             if "fmskf::" in row[col]:
                 w.writerow(row)
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        for kind in ("kf6", "pat"):
-            src = glob.glob(os.path.join(G, f"pmc_{kind}_{c}", "**", "*counter_collection.csv"), recursive=True)[0]
-            shutil.copy(src, os.path.join(P, f"{tag}_pmc_{'kf6' if kind == 'kf6' else 'pattern'}_{c}.csv"))
-    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), G,
-                    os.path.join(P, "pmc_traffic.json"), "records"], check=True, stdout=subprocess.DEVNULL)
+    if pmc_kf6:
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            for kind in ("kf6", "pat"):
+                src = glob.glob(os.path.join(G, f"pmc_{kind}_{c}", "**", "*counter_collection.csv"), recursive=True)[0]
+                shutil.copy(src, os.path.join(P, f"{tag}_pmc_{'kf6' if kind == 'kf6' else 'pattern'}_{c}.csv"))
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), G,
+                        os.path.join(P, "pmc_traffic.json"), "records"], check=True, stdout=subprocess.DEVNULL)
+    # the rows either side of the tick (r3_session.sh pmc): calibrated traffic + the counter rows
+    if glob.glob(os.path.join(G, "pmc_path_*")):
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "paths", G,
+                        os.path.join(P, "pmc_traffic_paths.json")], check=True, stdout=subprocess.DEVNULL)
+        for d in sorted(glob.glob(os.path.join(G, "pmc_path_*"))):
+            f = os.path.join(d, "run_counter_collection.csv")
+            if not os.path.isdir(d) or not os.path.exists(f):
+                continue
+            rows_in = list(csv.reader(open(f)))
+            col = rows_in[0].index("Kernel_Name")
+            keep = [r for r in rows_in[1:] if "fmskf::" in r[col]]
+            with open(os.path.join(P, f"{tag}_{os.path.basename(d)}.csv"), "w", newline="") as fo:
+                w = csv.writer(fo)
+                w.writerow(rows_in[0])
+                w.writerows(keep)
     # HBM-regime bench lines (profile_session.sh PMC_SEC=1): calibrated traffic + the counter rows
-    if glob.glob(os.path.join(G, "pmc_sec_*")):
+    if secondary and glob.glob(os.path.join(G, "pmc_sec_*")):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "secondary", G,
                         os.path.join(P, "pmc_traffic_secondary.json")], check=True, stdout=subprocess.DEVNULL)
         for d in sorted(glob.glob(os.path.join(G, "pmc_sec_*"))):
@@ -61,7 +83,7 @@ def main():
                 w.writerow(rows_in[0])
                 w.writerows(keep)
     rows = []
-    for d in sorted(glob.glob(os.path.join(G, "prof_*"))):
+    for d in sorted(glob.glob(os.path.join(G, "prof_*")) if secondary else []):
         if not os.path.isdir(d):
             continue
         f = glob.glob(os.path.join(d, "*kernel_stats.csv"))
@@ -70,10 +92,11 @@ def main():
         for r in csv.DictReader(open(f[0])):
             if "fmskf::" in r["Name"]:
                 rows.append([os.path.basename(d)[5:], r["Name"], r["Calls"], r["AverageNs"], r["MinNs"], r["MaxNs"]])
-    with open(os.path.join(P, f"{tag}_secondary_kernel_stats.csv"), "w", newline="") as fo:
-        w = csv.writer(fo)
-        w.writerow(["workload", "kernel", "calls", "avg_ns", "min_ns", "max_ns"])
-        w.writerows(rows)
+    if rows:
+        with open(os.path.join(P, f"{tag}_secondary_kernel_stats.csv"), "w", newline="") as fo:
+            w = csv.writer(fo)
+            w.writerow(["workload", "kernel", "calls", "avg_ns", "min_ns", "max_ns"])
+            w.writerows(rows)
     print(f"profiles/{tag}_* refreshed: {len(rows)} secondary kernel rows")
 
 

@@ -41,7 +41,7 @@ def run(model, n, ticks, every, trig, chunk=1000, seed=0x464D534B):
         prm = orc.ekf9_params(1e-3, q, r, orc.TRIG_LIBM)
         ref = kf_ref.DenseC("ekf9", n, np.zeros(9), p0.astype(np.float64), q.astype(np.float64),
                             r.astype(np.float64), dt32)
-    x = np.zeros((nx, n), np.float32)
+    x = np.zeros((nx + (nx == 9), n), np.float32)  # EKF9: row 9 the heading's low part
     P = np.repeat(p0[:, None], n, 1).copy()
     worst = {}
     scale_run = {g: np.full(n, 1e-3) for g in GROUPS[nx]}
