@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
     ap.add_argument("--packed", action="store_true", help="KF6: fmskf_kf6_record inputs")
     ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
@@ -87,7 +87,7 @@ def main():
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
-    tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op in ("ensemble", "tick_ensemble") else args.op))
+    tick = getattr(fmskf.load(), "fmskf_" + ("tick" if args.op in ("ensemble", "tick_ensemble", "ens_async") else args.op))
     for k in range(20):
         e.tick_prepared(preps[k % R], tick)
     torch.cuda.synchronize()
@@ -104,6 +104,46 @@ def main():
         ms = ev0.elapsed_time(ev1) / args.ticks
         print(json.dumps({"model": args.model, "n": n, "op": "tick_ensemble", "ms_per_tick": ms,
                           "steps_per_s": n / (ms * 1e-3)}), flush=True)
+        return
+    if args.op == "ens_async":  # a record every tick: plain ticks, sync fused record, async begin/end
+        import time
+        rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
+        res = {"model": args.model, "n": n, "op": "ens_async"}
+
+        def loop(kind, ticks):
+            pend = 0
+            for k in range(ticks):
+                if kind == "tick":
+                    e.tick_prepared(preps[k % R], tick)
+                elif kind == "sync":
+                    e.tick_ensemble_prepared(preps[k % R], rec)
+                else:
+                    e.tick_ensemble_begin(preps[k % R])
+                    pend += 1
+                    if pend == 3:
+                        e.ensemble_end()
+                        pend -= 1
+            while pend:
+                e.ensemble_end()
+                pend -= 1
+        for kind in ("tick", "sync", "async", "tick", "sync", "async"):
+            loop(kind, 8)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            loop(kind, args.ticks)
+            torch.cuda.synchronize()
+            res[kind + "_us"] = min(res.get(kind + "_us", 1e9), (time.perf_counter() - t0) * 1e6 / args.ticks)
+        # host-side cost alone: the calls without waiting for the GPU (submission rate)
+        t0 = time.perf_counter()
+        for k in range(64):
+            e.tick_ensemble_begin(preps[k % R])
+            if k >= 2:
+                e.ensemble_end()
+        res["async_submit_us"] = (time.perf_counter() - t0) * 1e6 / 64
+        e.ensemble_end()
+        e.ensemble_end()
+        torch.cuda.synchronize()
+        print(json.dumps(res), flush=True)
         return
     if args.op == "ensemble":  # the ensemble record reduction alone (partial + fold)
         rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
