@@ -171,7 +171,9 @@ def secondary_configs(dev, stream, ticks: int, trig):
                            if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
         except Exception:
             sec_traffic = {}
-    specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 448), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504),
+    # EKF9: 448 algorithmic bytes + the compensated heading's low-part row read
+    # and written (8 B)
+    specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 456), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504),
              ("cfg2_kf6_2p24", "kf6", 1 << 24, 232)]
     R = 4
     for key, model, n, bps in specs:

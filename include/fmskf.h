@@ -216,7 +216,12 @@ int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
 /* Record layout: {count, mean[n], M2 packed[n(n+1)/2]} in fp64 (28 doubles for n=6).
  * fmskf_ensemble_partial writes this rank's record; ranks all-gather the records
  * (RCCL over xGMI, one process per GPU) and fmskf_ensemble_combine folds them in
- * rank order -> deterministic.  `out` may be host or device per mem. */
+ * rank order -> deterministic.  `out` may be host or device per mem.
+ * The moment sums are accumulated about a shift vector: robot 0's state when the first
+ * record after create / reset / set_state / load_state (or fmskf_graph_begin) is taken.  It
+ * stays pinned until the next of those calls, so successive records of one state are bitwise
+ * identical; M2 loses relative precision only if the fleet drifts many standard deviations
+ * away from that snapshot (reset or set_state takes a new one). */
 int fmskf_ensemble_record_len(fmskf_handle h, uint32_t *len);
 int fmskf_ensemble_partial(fmskf_handle h, double *out, uint32_t mem);
 /* fmskf_tick, then this rank's record of the post-tick state (as fmskf_ensemble_partial) in

@@ -121,25 +121,23 @@ struct fmskf_ctx {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   double *ens_gather = nullptr;
-  // asynchronous ensemble (fmskf_tick_ensemble_begin / fmskf_ensemble_begin / _end): the block
-  // records are double-buffered (the tick of event k writes buffer k % 2 while the side stream
-  // `ens_stream` folds buffer (k - 1) % 2), and up to kEnsSlots results are in flight, each
-  // with its record, gather buffer and pinned host copy, so a caller can collect results a few
-  // events late and the tick stream never waits on the host
+  // asynchronous ensemble (fmskf_tick_ensemble_begin / fmskf_ensemble_begin / _end): up to
+  // kEnsSlots events in flight, each slot with its own block records, record, gather buffer and
+  // pinned host copy.  A slot is reused only after fmskf_ensemble_end consumed it (its `done`
+  // event, behind the fold, was waited for), so the tick that rewrites a slot's block records
+  // needs no stream wait; the side stream `ens_stream` folds event k while the tick stream runs
+  // ticks k + 1, k + 2, ...
   static constexpr int kEnsSlots = 4;
   struct EnsSlot {
-    double *rec = nullptr, *gather = nullptr;
+    double *blocks = nullptr, *rec = nullptr, *gather = nullptr;
     double *host = nullptr;  // pinned [ranks][len]
+    double *host_dev = nullptr;  // the device's address of `host` (the fold writes it over PCIe)
     size_t cap = 0;          // ranks the gather / host buffers hold
     hipEvent_t done = nullptr;
+    bool used = false;       // `done` has been recorded
     int ranks = 1;
   } eslot[kEnsSlots];
-  struct EnsBlocks {
-    double *blocks = nullptr;
-    hipEvent_t ticked = nullptr, folded = nullptr;
-    bool used = false;       // `folded` has been recorded
-  } eblk[2];
-  int ens_bnext = 0;
+  hipEvent_t ens_ticked = nullptr;  // the tick stream's point the side stream waits for
   hipStream_t ens_stream = nullptr;
   int ens_head = 0, ens_pending = 0;
   // vehicle control state (allocated on first use) and its parameters
@@ -272,9 +270,7 @@ struct fmskf_ctx {
       if (e.host) (void)hipHostFree(e.host);
       if (e.done) (void)hipEventDestroy(e.done);
     }
-    for (EnsBlocks &b : eblk)
-      for (hipEvent_t ev : {b.ticked, b.folded})
-        if (ev) (void)hipEventDestroy(ev);
+    if (ens_ticked) (void)hipEventDestroy(ens_ticked);
     if (ens_stream) (void)hipStreamDestroy(ens_stream);
     destroy_comm();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
@@ -448,8 +444,9 @@ void ensure_shift(fmskf_ctx *h) {
   // (fmskf_graph_begin takes it before capturing)
   if (h->capturing) fail(FMSKF_EINVAL, "ensemble shift first taken inside a graph capture");
   // asynchronous folds still queued on the side stream read the shift: rewrite it after them
-  for (const fmskf_ctx::EnsBlocks &b : h->eblk)
-    if (b.used) hip_check(hipStreamWaitEvent(h->stream, b.folded, 0), "hipStreamWaitEvent");
+  for (int k = 0; k < h->ens_pending; k++)
+    hip_check(hipStreamWaitEvent(h->stream, h->eslot[(h->ens_head + k) % fmskf_ctx::kEnsSlots].done, 0),
+              "hipStreamWaitEvent");
   launch_check(launch_ens_shift(h->s, (int)h->d.nx, h->d.elem == 8, h->ens_shift, h->stream),
                "ensemble shift launch");
   h->ens_shift_ok = true;
@@ -1569,6 +1566,8 @@ int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int r
   return guarded([&] {
     check_handle(h);
     if (!id || world < 1 || rank < 0 || rank >= world) fail(FMSKF_EINVAL, "bad rank / world / id");
+    // a pending asynchronous result may still be gathered over the old communicator
+    if (h->ens_pending) fail(FMSKF_EINVAL, "collect the pending ensemble results (fmskf_ensemble_end) first");
     const RcclApi &a = need_rccl();
     DeviceGuard g(h->cfg.device);
     h->destroy_comm();
@@ -1643,17 +1642,13 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     // the highest priority: the fold's 28-91 small blocks are dispatched as soon as CUs free up
     // between the next tick's blocks instead of queueing behind them
     hip_check(hipStreamCreateWithPriority(&h->ens_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
+    hip_check(hipEventCreateWithFlags(&h->ens_ticked, hipEventDisableTiming), "hipEventCreate");
   }
   fmskf_ctx::EnsSlot &S = h->eslot[(h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots];
-  fmskf_ctx::EnsBlocks &B = h->eblk[h->ens_bnext];
-  if (!B.blocks) {
+  if (!S.blocks) {
     size_t nb = (size_t)ensemble_nblocks(h->s.n);
     nb = std::max(nb, (size_t)((h->s.n + kBlock - 1) / kBlock));
-    B.blocks = h->alloc<double>(nb * len);
-    for (hipEvent_t *e : {&B.ticked, &B.folded})
-      hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
-  }
-  if (!S.rec) {
+    S.blocks = h->alloc<double>(nb * len);
     S.rec = h->alloc<double>(91);
     hip_check(hipEventCreateWithFlags(&S.done, hipEventDisableTiming), "hipEventCreate");
   }
@@ -1664,15 +1659,14 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     if (S.host) hip_check(hipHostFree(S.host), "hipHostFree");
     S.host = nullptr;
     hip_check(hipHostMalloc((void **)&S.host, (size_t)ranks * 91 * 8, hipHostMallocDefault), "hipHostMalloc");
+    S.host_dev = (double *)fmskf_ctx::dev_ptr(S.host);
     S.cap = (size_t)ranks;
   }
-  // the block records are rewritten only after the fold that read them (two events ago)
-  if (B.used) hip_check(hipStreamWaitEvent(h->stream, B.folded, 0), "hipStreamWaitEvent");
   ensure_shift(h);
   int nb = 0;
   if (in && fused_record(h)) {
     TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
-    t.ens_blocks = B.blocks;
+    t.ens_blocks = S.blocks;
     t.ens_shift = h->ens_shift;
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     h->time_begin();
@@ -1684,23 +1678,23 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     h->time_end();
   } else {
     if (in) run_tick(h, in, true, true, 1, h->s.n);
-    launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, B.blocks, h->ens_shift, h->stream, &nb),
+    launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, S.blocks, h->ens_shift, h->stream, &nb),
                  "ensemble partial launch");
   }
-  hip_check(hipEventRecord(B.ticked, h->stream), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(h->ens_stream, B.ticked, 0), "hipStreamWaitEvent");
-  launch_check(launch_ens_fold((int)nx, B.blocks, nb, h->ens_shift, S.rec, h->ens_stream), "ensemble fold launch");
-  hip_check(hipEventRecord(B.folded, h->ens_stream), "hipEventRecord");
-  B.used = true;
-  h->ens_bnext ^= 1;
-  const double *src = S.rec;
-  if (h->comm) {
+  hip_check(hipEventRecord(h->ens_ticked, h->stream), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(h->ens_stream, h->ens_ticked, 0), "hipStreamWaitEvent");
+  if (h->comm) {  // fold on the device, all-gather over xGMI, one copy of the gathered records
+    launch_check(launch_ens_fold((int)nx, S.blocks, nb, h->ens_shift, S.rec, h->ens_stream), "ensemble fold launch");
     nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
                "ncclAllGather");
-    src = S.gather;
+    hip_check(hipMemcpyAsync(S.host, S.gather, (size_t)ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream),
+              "D2H");
+  } else {  // one GPU: the fold writes the record straight into the pinned host slot
+    launch_check(launch_ens_fold((int)nx, S.blocks, nb, h->ens_shift, S.host_dev, h->ens_stream),
+                 "ensemble fold launch");
   }
-  hip_check(hipMemcpyAsync(S.host, src, (size_t)ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream), "D2H");
   hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
+  S.used = true;
   S.ranks = ranks;
   h->ens_pending++;
 }

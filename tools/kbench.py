@@ -13,7 +13,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")]
 
-BYTES = {"kf6": 232, "rs": 144, "ekf9": 448, "kf12d": 1504}
+BYTES = {"kf6": 232, "rs": 144, "ekf9": 456, "kf12d": 1504}  # EKF9: + the heading low-part row
 
 
 def main():
