@@ -130,11 +130,11 @@ __device__ __forceinline__ void ens_load_shift(const double *shift, double (&sh)
 
 // Block record (element-major [LEN][nblocks], so the fold reads one element coalesced)
 template <int NX>
-__device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], double *blocks) {
+__device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], double *blocks, uint32_t nblocks) {
   __shared__ double red[4 * EnsRec<NX>::LEN4];
   const double s = block_reduce<EnsRec<NX>::LEN4>(v, red);
   if (threadIdx.x < EnsRec<NX>::LEN)
-    blocks[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+    blocks[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = s;
 }
 
 // The tick kernels' record epilogue (fmskf_tick_ensemble): the R robots this lane ticked
@@ -148,7 +148,94 @@ __device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][
 #pragma unroll
   for (int r = 0; r < R; r++)
     if (live[r]) ens_add<NX>(v, xs[r], sh);
-  ens_block_write<NX>(v, in.ens_blocks);
+  ens_block_write<NX>(v, in.ens_blocks, in.ens_grid);
+}
+
+// Fold of record element k: sum, over the nb block records, the count row, the two S1 rows
+// the element needs and its own row, then convert: count; mean = s + S1 / c; M2 = S2 - S1 S1^T
+// / c.  The summation order is fixed at kFoldLanes partial sums (lane L adds blocks L,
+// L + kFoldLanes, ... ascending, then the block_reduce tree over kFoldLanes / 64 waves), and a
+// 256-thread block plays kFoldLanes / 256 lanes per thread, so the stand-alone fold kernel and
+// the fold blocks a tick kernel carries (ens_fold_carried) give bitwise the same record.  A row
+// summed by several elements gets bitwise the same total in each, so the record is
+// consistent.  U: passes of kFoldLanes blocks whose loads are in flight together.
+constexpr uint32_t kFoldLanes = 1024;
+template <int NX, int U>
+__device__ __forceinline__ void ens_fold_block(const double *__restrict__ blocks, uint32_t nb,
+                                               const double *__restrict__ shift, double *out, uint32_t k) {
+  constexpr int J = kFoldLanes / kBlock;
+  uint32_t ra = k, rb = k;
+  if (k > (uint32_t)NX) {
+    uint32_t p = 0, q = k - 1 - NX;
+    while (q > p) q -= ++p;
+    ra = 1 + p;
+    rb = 1 + q;
+  }
+  const double *rows[4] = {blocks, blocks + (uint64_t)ra * nb, blocks + (uint64_t)rb * nb,
+                           blocks + (uint64_t)k * nb};
+  double v[J][4];
+#pragma unroll
+  for (int j = 0; j < J; j++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) v[j][c] = 0.0;
+  for (uint32_t b = threadIdx.x; b < nb; b += U * kFoldLanes) {
+    double l[U][J][4];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        const uint32_t bi = b + u * kFoldLanes + j * kBlock;
+        const uint32_t bc = bi < nb ? bi : b;
+#pragma unroll
+        for (int c = 0; c < 4; c++) l[u][j][c] = rows[c][bc];
+      }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < J; j++)
+        if (b + u * kFoldLanes + j * kBlock < nb) {
+#pragma unroll
+          for (int c = 0; c < 4; c++) v[j][c] = v[j][c] + l[u][j][c];
+        }
+  }
+  // block_reduce<4, kFoldLanes>'s tree: lane-level part per played wave, then the waves in order
+  __shared__ double red[kFoldLanes / 64 * 4];
+  __shared__ double tot[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < J; j++) {
+    const double w0 = halve32(v[j][0], v[j][2]), w1 = halve32(v[j][1], v[j][3]);
+    const double s = row_sum(halve16(w0, w1));
+    if ((lane & 15) == 0) red[(j * (kBlock / 64) + wave) * 4 + (lane >> 4)] = s;
+  }
+  lds_barrier();
+  const int t = threadIdx.x;
+  if (t < 4) {
+    double s = red[t];
+#pragma unroll
+    for (int wv = 1; wv < (int)(kFoldLanes / 64); wv++) s = s + red[wv * 4 + t];
+    tot[t] = s;
+  }
+  lds_barrier();
+  if (t == 0) {
+    const double c = tot[0];
+    double r;
+    if (k == 0) r = c;
+    else if (k <= (uint32_t)NX) r = shift[k - 1] + (c > 0.0 ? tot[3] / c : 0.0);
+    else r = c > 0.0 ? tot[3] - tot[1] * tot[2] / c : 0.0;
+    out[k] = r;
+  }
+}
+
+// The fold blocks a fused tick kernel carries past its ens_grid tick blocks
+// (fmskf_tick_ensemble_begin): blocks ens_grid .. ens_grid + LEN - 1 fold the PREVIOUS event's
+// block records (complete: that event's kernel ran earlier on the stream) into in.fold_out, in
+// the shadow of this tick's blocks instead of a launch of their own.  True on those blocks.
+template <int NX>
+__device__ __forceinline__ bool ens_fold_carried(const TickIn &in) {
+  if (blockIdx.x < in.ens_grid) return false;
+  ens_fold_block<NX, 1>(in.fold_blocks, in.fold_nb, in.ens_shift, in.fold_out, blockIdx.x - in.ens_grid);
+  return true;
 }
 
 }  // namespace fmskf

@@ -37,6 +37,12 @@ void hip_check(hipError_t e, const char *what) {
 }
 void launch_check(int e, const char *what) { hip_check((hipError_t)e, what); }
 
+// The events the library records only to order its own work or to tell the host that the GPU
+// is done with a pinned host buffer: no system-scope release.  That release writes back and
+// invalidates the L2 behind each recorded event before the next kernel starts; the host reads
+// nothing behind these events but pinned host memory that kernels and copies write over PCIe.
+constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventDisableSystemFence;
+
 template <class F>
 int guarded(F &&f) {
   try {
@@ -125,8 +131,10 @@ struct fmskf_ctx {
   // kEnsSlots events in flight, each slot with its own block records, record, gather buffer and
   // pinned host copy.  A slot is reused only after fmskf_ensemble_end consumed it (its `done`
   // event, behind the fold, was waited for), so the tick that rewrites a slot's block records
-  // needs no stream wait; the side stream `ens_stream` folds event k while the tick stream runs
-  // ticks k + 1, k + 2, ...
+  // needs no stream wait.  Event k's fold rides in the next event's tick kernel (extra blocks
+  // past its tick blocks: ens_fold_carried), or runs stand-alone when no such kernel comes
+  // first (ens_flush); with a communicator the side stream `ens_stream` all-gathers it while
+  // the tick stream runs on.
   static constexpr int kEnsSlots = 4;
   struct EnsSlot {
     double *blocks = nullptr, *rec = nullptr, *gather = nullptr;
@@ -134,12 +142,13 @@ struct fmskf_ctx {
     double *host_dev = nullptr;  // the device's address of `host` (the fold writes it over PCIe)
     size_t cap = 0;          // ranks the gather / host buffers hold
     hipEvent_t done = nullptr;
-    bool used = false;       // `done` has been recorded
+    int nb = 0;              // the event's block records
     int ranks = 1;
   } eslot[kEnsSlots];
   hipEvent_t ens_ticked = nullptr;  // the tick stream's point the side stream waits for
   hipStream_t ens_stream = nullptr;
   int ens_head = 0, ens_pending = 0;
+  int ens_carry = -1;  // the newest event's slot while its fold is not queued yet
   // vehicle control state (allocated on first use) and its parameters
   CtrlDev ctrl{};
   fmskf_ctrl_params cprm{};
@@ -222,7 +231,7 @@ struct fmskf_ctx {
     pin_slot ^= 1;
     if (!pin_in[slot]) {
       hip_check(hipHostMalloc(&pin_in[slot], kPinned, hipHostMallocDefault), "hipHostMalloc");
-      hip_check(hipEventCreateWithFlags(&pin_ev[slot], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&pin_ev[slot], kSyncEvent), "hipEventCreate");
     } else {
       hip_check(hipEventSynchronize(pin_ev[slot]), "hipEventSynchronize");
     }
@@ -436,6 +445,27 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
 }
+// ---- asynchronous ensemble: queueing a slot's fold ----------------------------------------
+// The fold of slot S is queued on the handle's stream (carried by a tick kernel, or
+// stand-alone): with a communicator the side stream all-gathers the record over xGMI and copies
+// the gathered records into the slot's pinned buffer behind it; on one GPU the fold wrote the
+// pinned buffer itself.  Then the slot's `done` event.
+double *ens_fold_dst(const fmskf_ctx *h, const fmskf_ctx::EnsSlot &S) { return h->comm ? S.rec : S.host_dev; }
+void ens_gather_async(fmskf_ctx *h, fmskf_ctx::EnsSlot &S);  // with the RCCL entry points below
+void ens_fold_queued(fmskf_ctx *h, fmskf_ctx::EnsSlot &S) {
+  if (h->comm) ens_gather_async(h, S);
+  else hip_check(hipEventRecord(S.done, h->stream), "hipEventRecord");
+  h->ens_carry = -1;
+}
+// the stand-alone fold of the newest event, when no tick kernel carried it
+void ens_flush(fmskf_ctx *h) {
+  if (h->ens_carry < 0) return;
+  fmskf_ctx::EnsSlot &S = h->eslot[h->ens_carry];
+  launch_check(launch_ens_fold((int)h->d.nx, S.blocks, S.nb, h->ens_shift, ens_fold_dst(h, S), h->stream),
+               "ensemble fold launch");
+  ens_fold_queued(h, S);
+}
+
 // the ensemble shift vector: robot 0's state, taken once per create / reset / set_state /
 // load_state, so successive records of one state are bitwise identical
 void ensure_shift(fmskf_ctx *h) {
@@ -443,10 +473,9 @@ void ensure_shift(fmskf_ctx *h) {
   // a launch inside a capture is only recorded: the flag would claim a shift that no run wrote
   // (fmskf_graph_begin takes it before capturing)
   if (h->capturing) fail(FMSKF_EINVAL, "ensemble shift first taken inside a graph capture");
-  // asynchronous folds still queued on the side stream read the shift: rewrite it after them
-  for (int k = 0; k < h->ens_pending; k++)
-    hip_check(hipStreamWaitEvent(h->stream, h->eslot[(h->ens_head + k) % fmskf_ctx::kEnsSlots].done, 0),
-              "hipStreamWaitEvent");
+  // a pending fold reads the shift its event's records were taken against: queue it first
+  // (stream order then keeps it ahead of the rewrite)
+  ens_flush(h);
   launch_check(launch_ens_shift(h->s, (int)h->d.nx, h->d.elem == 8, h->ens_shift, h->stream),
                "ensemble shift launch");
   h->ens_shift_ok = true;
@@ -1541,6 +1570,25 @@ void nccl_check(ncclResult_t r, const char *what) {
   if (r != ncclSuccess) fail(FMSKF_ERCCL, std::string(what) + ": " + rccl().error_string(r));
 }
 
+// behind the fold queued on the tick stream, on the side stream: ncclAllGather of the slot's
+// record over the handle's communicator, one D2H of the gathered records, the slot's event
+void ens_gather_async(fmskf_ctx *h, fmskf_ctx::EnsSlot &S) {
+  if (!h->ens_stream) {
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    hip_check(hipStreamCreateWithPriority(&h->ens_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
+    hip_check(hipEventCreateWithFlags(&h->ens_ticked, kSyncEvent), "hipEventCreate");
+  }
+  const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
+  hip_check(hipEventRecord(h->ens_ticked, h->stream), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(h->ens_stream, h->ens_ticked, 0), "hipStreamWaitEvent");
+  nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
+             "ncclAllGather");
+  hip_check(hipMemcpyAsync(S.host, S.gather, (size_t)S.ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream),
+            "D2H");
+  hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
+}
+
 }  // namespace
 
 void fmskf_ctx::destroy_comm() {
@@ -1621,13 +1669,18 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed) {
 
 namespace {
 
-// One asynchronous ensemble event (the record fused into the tick, the gather
-// on a separate stream overlapping the next tick).  On the handle's stream: [the tick whose
-// kernel also writes the slot's block records | the stand-alone partial], then an event.  On
-// the side stream, behind that event: the fold into the slot's record, ncclAllGather of the
-// record over the handle's communicator (when there is one), the D2H of the gathered records
-// into the slot's pinned host buffer, an event.  Nothing waits on the host.  A slot's block
-// records are rewritten only after its previous fold has read them (stream-ordered wait).
+// One asynchronous ensemble event (the record fused into the tick, the fold
+// and the gather off the tick's critical path).  On the handle's stream: the tick whose kernel
+// writes the slot's block records and, in LEN blocks past its tick blocks, folds the PREVIOUS
+// event's records (ens_fold_carried) | the stand-alone partial.  The previous event's fold is
+// then queued: its `done` event (one GPU: the fold wrote the pinned host slot itself) or, with
+// a communicator, the all-gather and D2H on the side stream.  This event's own fold waits for
+// the next event's tick kernel, or for fmskf_ensemble_end / a shift rewrite (ens_flush).
+// Nothing waits on the host.  Folds of more than kCarryMax block records (the one-robot-per-
+// lane kernels past the Infinity Cache) run stand-alone: a carried fold block's passes over
+// them would outlast the tick blocks it hides behind.
+constexpr int kCarryMax = 8192;
+
 void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
   check_handle(h);
   if (h->capturing) fail(FMSKF_EINVAL, "asynchronous ensemble inside a graph capture");
@@ -1636,21 +1689,14 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
   DeviceGuard g(h->cfg.device);
   const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
   const int ranks = h->comm ? h->world : 1;
-  if (!h->ens_stream) {
-    int lo = 0, hi = 0;
-    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-    // the highest priority: the fold's 28-91 small blocks are dispatched as soon as CUs free up
-    // between the next tick's blocks instead of queueing behind them
-    hip_check(hipStreamCreateWithPriority(&h->ens_stream, hipStreamNonBlocking, hi), "hipStreamCreate");
-    hip_check(hipEventCreateWithFlags(&h->ens_ticked, hipEventDisableTiming), "hipEventCreate");
-  }
-  fmskf_ctx::EnsSlot &S = h->eslot[(h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots];
+  const int si = (h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots;
+  fmskf_ctx::EnsSlot &S = h->eslot[si];
   if (!S.blocks) {
     size_t nb = (size_t)ensemble_nblocks(h->s.n);
     nb = std::max(nb, (size_t)((h->s.n + kBlock - 1) / kBlock));
     S.blocks = h->alloc<double>(nb * len);
     S.rec = h->alloc<double>(91);
-    hip_check(hipEventCreateWithFlags(&S.done, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&S.done, kSyncEvent), "hipEventCreate");
   }
   if ((size_t)ranks > S.cap) {  // the slot's previous result was consumed (or never existed)
     double *gbuf = h->alloc<double>((size_t)ranks * 91);
@@ -1662,12 +1708,22 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     S.host_dev = (double *)fmskf_ctx::dev_ptr(S.host);
     S.cap = (size_t)ranks;
   }
-  ensure_shift(h);
+  ensure_shift(h);  // queues the previous event's fold first if it rewrites the shift
   int nb = 0;
   if (in && fused_record(h)) {
     TickIn t = resolve_inputs(h, in, true, true, 1, h->s.n);
     t.ens_blocks = S.blocks;
     t.ens_shift = h->ens_shift;
+    fmskf_ctx::EnsSlot *C = h->ens_carry >= 0 ? &h->eslot[h->ens_carry] : nullptr;
+    if (C && C->nb > kCarryMax) {
+      ens_flush(h);
+      C = nullptr;
+    }
+    if (C) {
+      t.fold_blocks = C->blocks;
+      t.fold_nb = (uint32_t)C->nb;
+      t.fold_out = ens_fold_dst(h, *C);
+    }
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     h->time_begin();
     int e = 0;
@@ -1676,26 +1732,16 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     else e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream, &nb);
     launch_check(e, "tick kernel launch");
     h->time_end();
+    if (C) ens_fold_queued(h, *C);
   } else {
+    ens_flush(h);
     if (in) run_tick(h, in, true, true, 1, h->s.n);
     launch_check(launch_ens_partial(h->s, (int)nx, h->d.elem == 8, S.blocks, h->ens_shift, h->stream, &nb),
                  "ensemble partial launch");
   }
-  hip_check(hipEventRecord(h->ens_ticked, h->stream), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(h->ens_stream, h->ens_ticked, 0), "hipStreamWaitEvent");
-  if (h->comm) {  // fold on the device, all-gather over xGMI, one copy of the gathered records
-    launch_check(launch_ens_fold((int)nx, S.blocks, nb, h->ens_shift, S.rec, h->ens_stream), "ensemble fold launch");
-    nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
-               "ncclAllGather");
-    hip_check(hipMemcpyAsync(S.host, S.gather, (size_t)ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream),
-              "D2H");
-  } else {  // one GPU: the fold writes the record straight into the pinned host slot
-    launch_check(launch_ens_fold((int)nx, S.blocks, nb, h->ens_shift, S.host_dev, h->ens_stream),
-                 "ensemble fold launch");
-  }
-  hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
-  S.used = true;
+  S.nb = nb;
   S.ranks = ranks;
+  h->ens_carry = si;
   h->ens_pending++;
 }
 
@@ -1720,6 +1766,10 @@ int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed) {
     if (h->ens_pending == 0) fail(FMSKF_EINVAL, "no ensemble pending (fmskf_*ensemble_begin)");
     DeviceGuard g(h->cfg.device);
     fmskf_ctx::EnsSlot &S = h->eslot[h->ens_head];
+    if (h->ens_carry == h->ens_head) {  // no later tick kernel carried its fold: queue it now
+      if (h->capturing) fail(FMSKF_EINVAL, "the newest ensemble result collected inside a graph capture");
+      ens_flush(h);
+    }
     hip_check(hipEventSynchronize(S.done), "hipEventSynchronize");
     h->ens_head = (h->ens_head + 1) % fmskf_ctx::kEnsSlots;
     h->ens_pending--;

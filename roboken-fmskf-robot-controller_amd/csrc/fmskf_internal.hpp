@@ -73,6 +73,12 @@ struct TickIn {
   // post-tick state ([LEN][grid], ens_device.hpp) against the shift vector; null otherwise
   double *ens_blocks;
   const double *ens_shift;
+  uint32_t ens_grid;  // the tick blocks (= block records); set by the launcher
+  // fmskf_tick_ensemble_begin: the previous event's block records ([LEN][fold_nb]), folded by
+  // LEN extra blocks of this tick's grid into fold_out (ens_fold_carried); null otherwise
+  uint32_t fold_nb;
+  const double *fold_blocks;
+  double *fold_out;
 };
 
 template <typename T, int NP, int MP>

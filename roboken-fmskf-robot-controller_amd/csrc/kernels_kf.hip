@@ -167,6 +167,9 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
+  if constexpr (ENS) {
+    if (ens_fold_carried<9>(a.in)) return;
+  }
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
   float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n, pp = a.pitch;
@@ -219,17 +222,20 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
 }
 
-// Two robots per lane (256-robot chunks b and b + gridDim.x of the tiled state): robot B's 54 state
-// loads and its raw record are issued before robot A's update, so they stream in while A
-// computes (see launch_ekf9).
+// Two robots per lane (256-robot chunks b and b + G of the tiled state, G the tick blocks):
+// robot B's 54 state loads and its raw record are issued before robot A's update, so they
+// stream in while A computes (see launch_ekf9).
 template <bool LIBM, bool SEQ, int CP, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
+  if constexpr (ENS) {
+    if (ens_fold_carried<9>(a.in)) return;
+  }
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
   float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n;
   const uint32_t ntiles = (uint32_t)((n + kBlock - 1) / kBlock);  // chunks of kBlock instances
-  const uint32_t ta = blockIdx.x, tb0 = blockIdx.x + gridDim.x;
+  const uint32_t ta = blockIdx.x, tb0 = blockIdx.x + (ENS ? a.in.ens_grid : gridDim.x);
   const bool has_b = tb0 < ntiles;  // block-uniform
   const uint32_t tb = has_b ? tb0 : ta;
   const uint32_t t = threadIdx.x;
@@ -466,6 +472,9 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool ENS = false, bool SP = false>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
+  if constexpr (ENS) {
+    if (ens_fold_carried<12>(a.in)) return;
+  }
   const uint64_t n = a.n, pp = a.pitch;
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = i0 < n;
@@ -546,25 +555,29 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 }
 
 // fused tick + record (fmskf_tick_ensemble): the default single-tick kernel with the record
-// epilogue; returns the grid (= the number of block records)
+// epilogue (and the carried fold blocks past the tick blocks when in.fold_blocks is set);
+// returns the tick grid (= the number of block records)
 template <bool LIBM, bool SEQ>
-static int launch_ekf9_ens(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, bool nt, hipStream_t st) {
+static int launch_ekf9_ens(KfArgs<MdEKF9, Ekf9Params> a, const DevState &s, bool nt, hipStream_t st) {
+  const unsigned carry = a.in.fold_blocks ? (unsigned)EnsRec<9>::LEN : 0u;
   if (!LIBM && s.n * 220 <= (256ull << 20)) {
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
-    const dim3 g2((ntiles + 1) / 2);
+    const unsigned g2 = (ntiles + 1) / 2;
+    a.in.ens_grid = g2;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
-    else k_ekf9p<false, SEQ, 0, true><<<g2, kBlock, lds, st>>>(a);
-    return (int)g2.x;
+    if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2 + carry, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, SEQ, 0, true><<<g2 + carry, kBlock, lds, st>>>(a);
+    return (int)g2;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
   // wants one more block per CU than the plain tick: 2^22, kbench, two passes: 331-335 us at
   // 64 KiB (2 blocks per CU), 307-308 at 32 KiB (3), 316 uncapped
-  const dim3 g = grid_for(s.n);
+  const unsigned g = grid_for(s.n).x;
+  a.in.ens_grid = g;
   const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9E_LDS", nt, 32u * 1024u);
-  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, true><<<g, kBlock, lds, st>>>(a);
-  else k_ekf9t<LIBM, true, true, SEQ, 0, true><<<g, kBlock, lds, st>>>(a);
-  return (int)g.x;
+  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, true><<<g + carry, kBlock, lds, st>>>(a);
+  else k_ekf9t<LIBM, true, true, SEQ, 0, true><<<g + carry, kBlock, lds, st>>>(a);
+  return (int)g;
 }
 
 template <bool SEQ>
@@ -632,7 +645,8 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
   a.prm.thlo = s.thlo;
   if (!s.thlo) return (int)hipErrorInvalidValue;
   const bool nt = FMSKF_TILED && state_nt(s.n * 55 * 4);
-  if (in.ens_blocks && (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1))
+  if ((in.ens_blocks && (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1)) ||
+      (in.fold_blocks && !in.ens_blocks))
     return (int)hipErrorInvalidValue;
   // canonical update order (oracle orc_ekf9_tick): sequential scalar updates when R is
   // diagonal, the joint LDL^T update otherwise
@@ -647,17 +661,20 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
   const bool small = FMSKF_TILED || s.pitch * 8 * 78 < 0xFFFFFFFFull;  // tiled: any N
   const bool nt = FMSKF_TILED && state_nt(s.n * 90 * 8);
   const bool sp = p.sparse != 0;
+  if (in.fold_blocks && !in.ens_blocks) return (int)hipErrorInvalidValue;
   if (in.ens_blocks) {
     // fused tick + record (fmskf_tick_ensemble): the default kernel (decorrelated update,
     // tiled state) with the record epilogue; one record per tick block
     if (!FMSKF_TILED || !p.decor || !ens_nb || !upd || !pred || in.n_ticks != 1) return (int)hipErrorInvalidValue;
     const bool blk = kf12d_sequential(p.r);
-    if (sp && nt) k_kf12s<true, true, true, true, kStateNT, true, true><<<g, kBlock, 0, st>>>(a);
-    else if (sp) k_kf12s<true, true, true, true, 0, true, true><<<g, kBlock, 0, st>>>(a);
-    else if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-    else if (blk) k_kf12s<true, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
-    else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<g, kBlock, 0, st>>>(a);
-    else k_kf12s<false, true, true, true, 0, true><<<g, kBlock, 0, st>>>(a);
+    a.in.ens_grid = g.x;
+    const dim3 ge(g.x + (in.fold_blocks ? (unsigned)EnsRec<12>::LEN : 0u));  // + the carried fold
+    if (sp && nt) k_kf12s<true, true, true, true, kStateNT, true, true><<<ge, kBlock, 0, st>>>(a);
+    else if (sp) k_kf12s<true, true, true, true, 0, true, true><<<ge, kBlock, 0, st>>>(a);
+    else if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<ge, kBlock, 0, st>>>(a);
+    else if (blk) k_kf12s<true, true, true, true, 0, true><<<ge, kBlock, 0, st>>>(a);
+    else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<ge, kBlock, 0, st>>>(a);
+    else k_kf12s<false, true, true, true, 0, true><<<ge, kBlock, 0, st>>>(a);
     *ens_nb = (int)g.x;
     return (int)hipGetLastError();
   }

@@ -75,6 +75,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 template <int WPE, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6t(
     KfArgs<MdKF6, Kf6Params> a) {
+  if constexpr (O::ENS) {
+    if (ens_fold_carried<6>(a.in)) return;
+  }
   const uint64_t n = a.n;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
@@ -101,15 +104,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   }
 }
 
-// R robots per lane (i, i + G, ..., G = the grid's lane count), the tick inputs of all R
+// R robots per lane (i, i + G, ..., G = the tick blocks' lane count), the tick inputs of all R
 // loaded up front: robot r's inputs (fresh from HBM) arrive while robots 0..r-1 are loaded,
 // computed and stored; one register set for the state, 1/R of the grid.
 template <int WPE, int R, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6p(
     KfArgs<MdKF6, Kf6Params> a) {
+  if constexpr (O::ENS) {
+    if (ens_fold_carried<6>(a.in)) return;
+  }
   const uint64_t n = a.n;
   const uint32_t nn = (uint32_t)n, last = nn - 1u;
-  const uint32_t G = gridDim.x * kBlock;
+  const uint32_t G = (O::ENS ? a.in.ens_grid : gridDim.x) * kBlock;
   const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x;
   float x[6], P[21];
   __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
@@ -201,25 +207,29 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
 }
 
 // fused tick + ensemble record (fmskf_tick_ensemble): the kernel launch_o picks by default,
-// with the record epilogue; returns the grid (= the number of block records)
+// with the record epilogue (and the carried fold blocks past the tick blocks when
+// in.fold_blocks is set); returns the tick grid (= the number of block records)
 template <class O>
-static int launch_ens_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
+static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   using E = WithEns<O>;
+  const unsigned carry = a.in.fold_blocks ? (unsigned)EnsRec<6>::LEN : 0u;
   if (a.n * 124 <= (256ull << 20)) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
+    a.in.ens_grid = g;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
-    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g, kBlock, lds, st>>>(a);
-    else k_kf6p<4, 2, E><<<g, kBlock, lds, st>>>(a);
+    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g + carry, kBlock, lds, st>>>(a);
+    else k_kf6p<4, 2, E><<<g + carry, kBlock, lds, st>>>(a);
     return (int)g;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
   // wants a smaller cap than the plain tick: 2^24, kbench, two passes: 738 us at 48 KiB,
   // 665-670 at 32 KiB, 680-689 at 24 KiB, 722-724 uncapped (the plain tick: 619-628)
-  const dim3 g = grid_for(a.n);
+  const unsigned g = grid_for(a.n).x;
+  a.in.ens_grid = g;
   const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6E_LDS", state_nt(a.n * 108), 32u * 1024u);
-  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g, kBlock, lds, st>>>(a);
-  else k_kf6t<4, E><<<g, kBlock, lds, st>>>(a);
-  return (int)g.x;
+  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g + carry, kBlock, lds, st>>>(a);
+  else k_kf6t<4, E><<<g + carry, kBlock, lds, st>>>(a);
+  return (int)g;
 }
 
 template <class O>
@@ -257,7 +267,7 @@ int launch_kf6(const DevState &s, const TickIn &in, const Kf6Params &p, bool lib
   const bool small = s.pitch * 84 < 0xFFFFFFFFull;
   const bool valid = upd && in.valid != nullptr;
   int *nb = in.ens_blocks && upd && pred && in.n_ticks == 1 ? ens_nb : nullptr;
-  if (in.ens_blocks && !nb) return (int)hipErrorInvalidValue;
+  if ((in.ens_blocks && !nb) || (in.fold_blocks && !in.ens_blocks)) return (int)hipErrorInvalidValue;
   if (libm) {
     if (upd && pred) launch_lup<true, true, true>(a, small, valid, st, nb);
     else if (upd) launch_lup<true, true, false>(a, small, valid, st, nullptr);

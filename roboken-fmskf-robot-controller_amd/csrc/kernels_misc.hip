@@ -88,79 +88,26 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
     for (int u = 0; u < R; u++)
       if (i0 + u * stride < n) ens_add<NX>(v, xv[u], sh);
   }
-  ens_block_write<NX>(v, blocks);
+  ens_block_write<NX>(v, blocks, gridDim.x);
 }
 
-// Fold: one block per record element k.  Block k sums, over the nb block records in a fixed
-// order (thread t: blocks t, t + 256, ... ascending; then block_reduce), the count row, the
-// two S1 rows its element needs and its own row, then converts: count; mean = s + S1 / c;
-// M2 = S2 - S1 S1^T / c.  A row summed by several blocks gets bitwise the same total in each
-// (same per-thread order, same reduction tree), so the record is consistent.  LEN blocks in
-// parallel, each one load round trip at 2^20: the round-1 one-block fold was 4.2-10 us.
-template <int NX, int FT, int U>
-__global__ __launch_bounds__(FT) void k_ens_fold(const double *__restrict__ blocks, int nb,
-                                                 const double *__restrict__ shift, double *out) {
-  const int k = blockIdx.x;
-  int ra = k, rb = k;
-  if (k > NX) {
-    int p = 0, q = k - 1 - NX;
-    while (q > p) q -= ++p;
-    ra = 1 + p;
-    rb = 1 + q;
-  }
-  const double *r0 = blocks, *r1 = blocks + (uint64_t)ra * nb, *r2 = blocks + (uint64_t)rb * nb,
-               *r3 = blocks + (uint64_t)k * nb;
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-  // U strides per row in flight per pass (the launcher sizes U to the record count, so one
-  // pass usually covers it), the ragged last pass predicated: one load round trip per pass;
-  // thread t adds blocks t, t + FT, ... in ascending order either way
-  for (int b = threadIdx.x; b < nb; b += U * FT) {
-    double l[U][4];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const bool in = b + u * FT < nb;
-      const int bi = in ? b + u * FT : b;
-      l[u][0] = r0[bi];
-      l[u][1] = r1[bi];
-      l[u][2] = r2[bi];
-      l[u][3] = r3[bi];
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (b + u * FT < nb) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) v[j] = v[j] + l[u][j];
-      }
-  }
-  __shared__ double red[FT / 64 * 4];
-  __shared__ double tot[4];
-  const double s = block_reduce<4, FT>(v, red);
-  if (threadIdx.x < 4) tot[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double c = tot[0];
-    double r;
-    if (k == 0) r = c;
-    else if (k <= NX) r = shift[k - 1] + (c > 0.0 ? tot[3] / c : 0.0);
-    else r = c > 0.0 ? tot[3] - tot[1] * tot[2] / c : 0.0;
-    out[k] = r;
-  }
+// Fold: one block per record element (ens_fold_block: kFoldLanes partial sums, so this kernel
+// and the fold blocks a tick kernel carries agree bitwise), LEN blocks in parallel, each one
+// load round trip per U passes.  Round 1's one-block fold was 4.2-10 us at 2^20; KF6 record
+// at 2^20 (partial + fold back to back) 8.3-8.9 us with 256-1024 threads per block.
+template <int NX, int U>
+__global__ __launch_bounds__(kBlock) void k_ens_fold(const double *__restrict__ blocks, int nb,
+                                                     const double *__restrict__ shift, double *out) {
+  ens_fold_block<NX, U>(blocks, (uint32_t)nb, shift, out, blockIdx.x);
 }
 
-// fold block size 1024: 2 record loads per row per thread at 2^20.  KF6 record at 2^20
-// (partial + fold, back to back): 8.9 us with 256 threads, 8.4 / 11.5 with 512, 8.3 with 1024;
-// EKF9 13.8-15.5 / 13.3-13.4 / 13.2-13.9; a record every tick in the bench: 2.46-2.48e10
-// steps/s with either (kbench, bench, two passes)
-constexpr int kFoldThreads = 1024;
 template <int NX>
 static void fold_launch(const double *blocks, int nb, const double *shift, double *out, hipStream_t st) {
-  constexpr int FT = kFoldThreads;
-  const int per = (nb + FT - 1) / FT;  // record loads per row per thread
+  const int per = (nb + (int)kFoldLanes - 1) / (int)kFoldLanes;  // passes of kFoldLanes records
   const dim3 g(EnsRec<NX>::LEN);
-  if (per <= 1) k_ens_fold<NX, FT, 1><<<g, FT, 0, st>>>(blocks, nb, shift, out);
-  else if (per <= 2) k_ens_fold<NX, FT, 2><<<g, FT, 0, st>>>(blocks, nb, shift, out);
-  else if (per <= 4) k_ens_fold<NX, FT, 4><<<g, FT, 0, st>>>(blocks, nb, shift, out);
-  else k_ens_fold<NX, FT, 8><<<g, FT, 0, st>>>(blocks, nb, shift, out);
+  if (per <= 1) k_ens_fold<NX, 1><<<g, kBlock, 0, st>>>(blocks, nb, shift, out);
+  else if (per <= 2) k_ens_fold<NX, 2><<<g, kBlock, 0, st>>>(blocks, nb, shift, out);
+  else k_ens_fold<NX, 4><<<g, kBlock, 0, st>>>(blocks, nb, shift, out);
 }
 
 // the shift vector: robot 0's state

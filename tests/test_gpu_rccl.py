@@ -90,14 +90,17 @@ def _ens_inputs(model, n, T, seed):
 
 
 @pytest.mark.parametrize("model,n,every,comm", [("kf6", 70001, 1, True), ("kf6", 1 << 20, 3, False),
+                                                ("kf6", (1 << 21) + 200_000, 2, False),
                                                 ("ekf9", 5001, 2, True), ("kf12d", 3001, 1, False),
                                                 ("rs", 4097, 1, True)])
 def test_async_ensemble_matches_sync(model, n, every, comm):
-    """fmskf_tick_ensemble_begin / fmskf_ensemble_end (fold + all-gather + copy-out on the side
-    stream, results collected two events late, so three are pending at every begin with every = 1)
-    against the synchronous fmskf_tick_ensemble of a twin handle on the same inputs: the states
-    stay bit-identical and every (mean, cov) equals the fold of the synchronous record bit for
-    bit, with and without a (world-1) RCCL communicator."""
+    """fmskf_tick_ensemble_begin / fmskf_ensemble_end (event k's fold carried by the blocks past
+    event k + 1's tick blocks, or stand-alone for the last event, the non-fused RS record and
+    the 8974-record fold of the one-robot-per-lane KF6 kernel past the Infinity Cache; the
+    all-gather and copy-out on the side stream; results collected two events late, so three are
+    pending at every begin with every = 1) against the synchronous fmskf_tick_ensemble of a twin
+    handle on the same inputs: the states stay bit-identical and every (mean, cov) equals the
+    fold of the synchronous record bit for bit, with and without a (world-1) RCCL communicator."""
     T = 9
     kw = _ens_inputs(model, n, T, seed=63)
     with Engine(model, n) as a, Engine(model, n) as b:
@@ -151,9 +154,9 @@ def test_async_ensemble_limits():
 
 
 def test_async_ensemble_across_reset():
-    """Results begun before a reset fold with the shift of the state they recorded: the reset
-    retakes the shift only after the pending folds (stream-ordered), so the pending result and
-    the next one both equal the synchronous records of the same states."""
+    """Results begun before a reset fold with the shift of the state they recorded: retaking
+    the shift first queues the pending fold (stream-ordered ahead of the rewrite), so the
+    pending result and the next one both equal the synchronous records of the same states."""
     n = 3001
     rng = np.random.default_rng(8)
     with Engine("ekf9", n) as a, Engine("ekf9", n) as b:

@@ -110,11 +110,18 @@ def main():
         rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
         res = {"model": args.model, "n": n, "op": "ens_async"}
 
+        evs = [torch.cuda.Event() for _ in range(4)]  # hipEventDisableTiming, system-scope release
+
         def loop(kind, ticks):
             pend = 0
             for k in range(ticks):
                 if kind == "tick":
                     e.tick_prepared(preps[k % R], tick)
+                elif kind == "tick_ev":  # the cost of a system-scope event behind every tick
+                    e.tick_prepared(preps[k % R], tick)
+                    evs[k % 4].record(st)
+                    if k >= 2:
+                        evs[(k - 2) % 4].synchronize()
                 elif kind == "sync":
                     e.tick_ensemble_prepared(preps[k % R], rec)
                 else:
@@ -126,23 +133,32 @@ def main():
             while pend:
                 e.ensemble_end()
                 pend -= 1
-        for kind in ("tick", "sync", "async", "tick", "sync", "async"):
+        for kind in ("tick", "tick_ev", "sync", "async") * 2:
             loop(kind, 8)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             loop(kind, args.ticks)
             torch.cuda.synchronize()
             res[kind + "_us"] = min(res.get(kind + "_us", 1e9), (time.perf_counter() - t0) * 1e6 / args.ticks)
-        # host-side cost alone: the calls without waiting for the GPU (submission rate)
-        t0 = time.perf_counter()
-        for k in range(64):
-            e.tick_ensemble_begin(preps[k % R])
-            if k >= 2:
+        # the bench's K = 16 region shape: 20 ticks, one event at tick 10, its result collected
+        # at the end (end() then synchronize, or synchronize then end()), against 20 plain ticks
+        def region(kind):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(20):
+                if kind != "plain" and k == 10:
+                    e.tick_ensemble_begin(preps[k % R])
+                else:
+                    e.tick_prepared(preps[k % R], tick)
+            if kind == "end_first":
                 e.ensemble_end()
-        res["async_submit_us"] = (time.perf_counter() - t0) * 1e6 / 64
-        e.ensemble_end()
-        e.ensemble_end()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            if kind == "sync_first":
+                e.ensemble_end()
+            return (time.perf_counter() - t0) * 1e6 / 20
+        for kind in ("plain", "end_first", "sync_first"):
+            ts = sorted(region(kind) for _ in range(9))
+            res["region20_" + kind + "_us"] = [round(ts[0], 2), round(ts[4], 2)]
         print(json.dumps(res), flush=True)
         return
     if args.op == "ensemble":  # the ensemble record reduction alone (partial + fold)

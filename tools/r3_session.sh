@@ -21,7 +21,8 @@ run() {
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -rf ${PYTEST_K:-} ;;
+    tests) if [ -n "${PYTEST_K:-}" ]; then KARGS=(-k "$PYTEST_K"); else KARGS=(); fi
+           run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -rf "${KARGS[@]}" ;;
     bench) run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
              python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
