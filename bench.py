@@ -598,6 +598,14 @@ def main():
     # first launch: ~2 ms for the ensemble kernels, measured inside the timed region in round 1)
     if args.ensemble_every > 0 and (args.warmup < args.ensemble_every or args.warmup == 0):
         ens_event(args.warmup)
+    if args.ensemble_every > 0 and args.gather == "native":
+        # the handle's four result slots each come into use once before the timed region
+        # (first record / wait of a slot's events), collected both ways: two events late and
+        # the newest one by itself (its fold stand-alone)
+        for j in range(5):
+            ens_event(args.warmup + 1 + j)
+        join()
+        ens_event(args.warmup + 6)
     join()
     torch.cuda.synchronize()
     barrier()
@@ -607,11 +615,17 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
+    t_sub = time.perf_counter()
     join()
+    t_join = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    # where the host spent the timed region (diagnostic): submitting the K steps, collecting
+    # the pending ensemble results, the final synchronise
+    host_split = {"submit_ms": (t_sub - t0) * 1e3, "join_ms": (t_join - t_sub) * 1e3,
+                  "sync_ms": (t1 - t_join) * 1e3}
     # the same K-step sequence once more between HIP events on the tick stream: the GPU-side
     # duration of the timed region's work (diagnostic; `value` is the wall clock above)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -803,6 +817,7 @@ def main():
             "timed_region_ms_per_step": region_ms / args.steps,
             "kernel_ms_plane_inputs": planes_ms / args.steps,
         },
+        "timed_region_host": host_split,
         "cpu_baseline": None,
         "fused_replay": fused,
         "ensemble_every_1": k1,

@@ -132,9 +132,9 @@ struct fmskf_ctx {
   // pinned host copy.  A slot is reused only after fmskf_ensemble_end consumed it (its `done`
   // event, behind the fold, was waited for), so the tick that rewrites a slot's block records
   // needs no stream wait.  Event k's fold rides in the next event's tick kernel (extra blocks
-  // past its tick blocks: ens_fold_carried), or runs stand-alone when no such kernel comes
-  // first (ens_flush); with a communicator the side stream `ens_stream` all-gathers it while
-  // the tick stream runs on.
+  // past its tick blocks: ens_fold_carried), or runs stand-alone when a plain tick or a result
+  // request comes first (ens_flush); with a communicator the side stream `ens_stream`
+  // all-gathers it while the tick stream runs on.
   static constexpr int kEnsSlots = 4;
   struct EnsSlot {
     double *blocks = nullptr, *rec = nullptr, *gather = nullptr;
@@ -672,6 +672,11 @@ void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, ui
   check_handle(h);
   DeviceGuard g(h->cfg.device);
   TickIn t = resolve_inputs(h, in, upd, pred, n_ticks, stride);
+  // a plain tick after an asynchronous ensemble event: the event's fold runs stand-alone
+  // ahead of it (a record every K > 1 ticks gets its result one fold after its tick; only the
+  // next ensemble tick's kernel carries it).  Not inside a capture: the replay would fold
+  // whatever the slot holds then
+  if (!h->capturing) ens_flush(h);
   const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
   h->time_begin();
   int e = 0;
@@ -1675,7 +1680,8 @@ namespace {
 // event's records (ens_fold_carried) | the stand-alone partial.  The previous event's fold is
 // then queued: its `done` event (one GPU: the fold wrote the pinned host slot itself) or, with
 // a communicator, the all-gather and D2H on the side stream.  This event's own fold waits for
-// the next event's tick kernel, or for fmskf_ensemble_end / a shift rewrite (ens_flush).
+// the next event's tick kernel, or runs stand-alone ahead of a plain tick, at
+// fmskf_ensemble_end or before a shift rewrite (ens_flush).
 // Nothing waits on the host.  Folds of more than kCarryMax block records (the one-robot-per-
 // lane kernels past the Infinity Cache) run stand-alone: a carried fold block's passes over
 // them would outlast the tick blocks it hides behind.

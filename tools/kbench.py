@@ -111,6 +111,12 @@ def main():
         res = {"model": args.model, "n": n, "op": "ens_async"}
 
         evs = [torch.cuda.Event() for _ in range(4)]  # hipEventDisableTiming, system-scope release
+        import ctypes  # the library's kind of event: hipEventDisableTiming | hipEventDisableSystemFence
+        hip = ctypes.CDLL("libamdhip64.so")
+        nf = [ctypes.c_void_p() for _ in range(4)]
+        for v in nf:
+            assert hip.hipEventCreateWithFlags(ctypes.byref(v), ctypes.c_uint(0x2 | 0x20000000)) == 0
+        sp = ctypes.c_void_p(st.cuda_stream)
 
         def loop(kind, ticks):
             pend = 0
@@ -122,18 +128,28 @@ def main():
                     evs[k % 4].record(st)
                     if k >= 2:
                         evs[(k - 2) % 4].synchronize()
+                elif kind == "tick_ev3":  # the same, collected three ticks late
+                    e.tick_prepared(preps[k % R], tick)
+                    evs[k % 4].record(st)
+                    if k >= 3:
+                        evs[(k - 3) % 4].synchronize()
+                elif kind == "tick_evnf":  # an event without the system-scope release per tick
+                    e.tick_prepared(preps[k % R], tick)
+                    hip.hipEventRecord(nf[k % 4], sp)
+                    if k >= 2:
+                        hip.hipEventSynchronize(nf[(k - 2) % 4])
                 elif kind == "sync":
                     e.tick_ensemble_prepared(preps[k % R], rec)
-                else:
+                else:  # async: results collected two (async) or three (async3) events late
                     e.tick_ensemble_begin(preps[k % R])
                     pend += 1
-                    if pend == 3:
+                    if pend == (4 if kind == "async3" else 3):
                         e.ensemble_end()
                         pend -= 1
             while pend:
                 e.ensemble_end()
                 pend -= 1
-        for kind in ("tick", "tick_ev", "sync", "async") * 2:
+        for kind in ("tick", "tick_ev", "tick_ev3", "tick_evnf", "sync", "async", "async3") * 2:
             loop(kind, 8)
             torch.cuda.synchronize()
             t0 = time.perf_counter()

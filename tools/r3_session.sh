@@ -36,6 +36,13 @@ for s in $STEPS; do
              run pmc_path_can_ingest_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_can_ingest_2p20_$c" -o run -- \
                python tools/kbench.py --op can --ticks 30
            done ;;
+    sq)    # one pass of wave-state counters per path-row kernel (7 SQ + 1 GRBM: within one pass)
+           SQC="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"
+           run sq_kf6 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_kf6" -o run -- python tools/kbench.py --packed --ticks 30
+           run sq_rs 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_rs" -o run -- python tools/kbench.py --model rs --pad 512 --ticks 30
+           run sq_wt901 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_wt901" -o run -- python tools/kbench.py --op wt901 --ticks 30
+           run sq_can 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_can" -o run -- python tools/kbench.py --op can --ticks 30
+           ;;
     kb)    i=0; IFS=';' read -ra KBL <<< "${KB_LIST:-}"; for a in "${KBL[@]}"; do
              i=$((i+1)); run kb$i 240 python tools/kbench.py $a
            done ;;
