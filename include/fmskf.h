@@ -257,9 +257,11 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
  *     of the post-tick state (KF6, EKF9, KF12D with a positive-definite R; other models tick,
  *     then run the stand-alone record), on the handle's stream;
  *   fmskf_ensemble_begin: the stand-alone record of the current state (no tick);
- *   then, on the handle's side stream: the fold, ncclAllGather over the communicator of
- *   fmskf_comm_init (skipped without one), the copy of the gathered records to pinned host
- *   memory.  The next tick on the handle's stream does not wait for any of it.
+ *   the record's fold rides in the next begin's tick kernel (extra blocks past its tick
+ *   blocks), or runs ahead of the next fmskf_tick, or at fmskf_ensemble_end when nothing
+ *   came first; with a communicator of fmskf_comm_init, ncclAllGather and the copy of the
+ *   gathered records to pinned host memory then run on the handle's side stream.  No tick on
+ *   the handle's stream waits for the gather, and no call waits on the host.
  *   fmskf_ensemble_end: waits for the OLDEST pending begin and returns its mean [n] and
  *     covariance packed [n(n+1)/2] (unbiased, rank-order fold: identical on every rank,
  *     deterministic).  EINVAL when nothing is pending.

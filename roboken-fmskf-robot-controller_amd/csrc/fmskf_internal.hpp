@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace fmskf {
@@ -79,7 +80,18 @@ struct TickIn {
   uint32_t fold_nb;
   const double *fold_blocks;
   double *fold_out;
+  // host side only (never read by a kernel): the event the fused ENS launch attaches to the
+  // kernel's own completion signal (launch_signal), or null
+  hipEvent_t ens_done;
 };
+
+// k<<<g, kBlock, lds, st>>>(a); with `done`, the dispatch's own completion signal records the
+// event (hipExtLaunchKernelGGL), so no marker packet follows the kernel on the stream
+template <typename A>
+inline void launch_signal(void (*k)(A), dim3 g, unsigned lds, hipStream_t st, hipEvent_t done, const A &a) {
+  if (done) hipExtLaunchKernelGGL(k, g, dim3(kBlock), lds, st, nullptr, done, 0u, a);
+  else k<<<g, kBlock, lds, st>>>(a);
+}
 
 template <typename T, int NP, int MP>
 struct KfParams {

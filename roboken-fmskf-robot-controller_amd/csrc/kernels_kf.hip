@@ -565,8 +565,8 @@ static int launch_ekf9_ens(KfArgs<MdEKF9, Ekf9Params> a, const DevState &s, bool
     const unsigned g2 = (ntiles + 1) / 2;
     a.in.ens_grid = g2;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) k_ekf9p<false, SEQ, kStateNT, true><<<g2 + carry, kBlock, lds, st>>>(a);
-    else k_ekf9p<false, SEQ, 0, true><<<g2 + carry, kBlock, lds, st>>>(a);
+    if (nt) launch_signal(k_ekf9p<false, SEQ, kStateNT, true>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
+    else launch_signal(k_ekf9p<false, SEQ, 0, true>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
     return (int)g2;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
@@ -575,8 +575,8 @@ static int launch_ekf9_ens(KfArgs<MdEKF9, Ekf9Params> a, const DevState &s, bool
   const unsigned g = grid_for(s.n).x;
   a.in.ens_grid = g;
   const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9E_LDS", nt, 32u * 1024u);
-  if (nt) k_ekf9t<LIBM, true, true, SEQ, kStateNT, true><<<g + carry, kBlock, lds, st>>>(a);
-  else k_ekf9t<LIBM, true, true, SEQ, 0, true><<<g + carry, kBlock, lds, st>>>(a);
+  if (nt) launch_signal(k_ekf9t<LIBM, true, true, SEQ, kStateNT, true>, dim3(g + carry), lds, st, a.in.ens_done, a);
+  else launch_signal(k_ekf9t<LIBM, true, true, SEQ, 0, true>, dim3(g + carry), lds, st, a.in.ens_done, a);
   return (int)g;
 }
 
@@ -669,12 +669,13 @@ int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool
     const bool blk = kf12d_sequential(p.r);
     a.in.ens_grid = g.x;
     const dim3 ge(g.x + (in.fold_blocks ? (unsigned)EnsRec<12>::LEN : 0u));  // + the carried fold
-    if (sp && nt) k_kf12s<true, true, true, true, kStateNT, true, true><<<ge, kBlock, 0, st>>>(a);
-    else if (sp) k_kf12s<true, true, true, true, 0, true, true><<<ge, kBlock, 0, st>>>(a);
-    else if (blk && nt) k_kf12s<true, true, true, true, kStateNT, true><<<ge, kBlock, 0, st>>>(a);
-    else if (blk) k_kf12s<true, true, true, true, 0, true><<<ge, kBlock, 0, st>>>(a);
-    else if (nt) k_kf12s<false, true, true, true, kStateNT, true><<<ge, kBlock, 0, st>>>(a);
-    else k_kf12s<false, true, true, true, 0, true><<<ge, kBlock, 0, st>>>(a);
+    const hipEvent_t ev = in.ens_done;
+    if (sp && nt) launch_signal(k_kf12s<true, true, true, true, kStateNT, true, true>, ge, 0, st, ev, a);
+    else if (sp) launch_signal(k_kf12s<true, true, true, true, 0, true, true>, ge, 0, st, ev, a);
+    else if (blk && nt) launch_signal(k_kf12s<true, true, true, true, kStateNT, true>, ge, 0, st, ev, a);
+    else if (blk) launch_signal(k_kf12s<true, true, true, true, 0, true>, ge, 0, st, ev, a);
+    else if (nt) launch_signal(k_kf12s<false, true, true, true, kStateNT, true>, ge, 0, st, ev, a);
+    else launch_signal(k_kf12s<false, true, true, true, 0, true>, ge, 0, st, ev, a);
     *ens_nb = (int)g.x;
     return (int)hipGetLastError();
   }

@@ -217,8 +217,8 @@ static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     a.in.ens_grid = g;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
-    if (state_nt(a.n * 108)) k_kf6p<4, 2, WithNT<E>><<<g + carry, kBlock, lds, st>>>(a);
-    else k_kf6p<4, 2, E><<<g + carry, kBlock, lds, st>>>(a);
+    if (state_nt(a.n * 108)) launch_signal(k_kf6p<4, 2, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
+    else launch_signal(k_kf6p<4, 2, E>, dim3(g + carry), lds, st, a.in.ens_done, a);
     return (int)g;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
@@ -227,8 +227,8 @@ static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   const unsigned g = grid_for(a.n).x;
   a.in.ens_grid = g;
   const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6E_LDS", state_nt(a.n * 108), 32u * 1024u);
-  if (state_nt(a.n * 108)) k_kf6t<4, WithNT<E>><<<g + carry, kBlock, lds, st>>>(a);
-  else k_kf6t<4, E><<<g + carry, kBlock, lds, st>>>(a);
+  if (state_nt(a.n * 108)) launch_signal(k_kf6t<4, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
+  else launch_signal(k_kf6t<4, E>, dim3(g + carry), lds, st, a.in.ens_done, a);
   return (int)g;
 }
 
