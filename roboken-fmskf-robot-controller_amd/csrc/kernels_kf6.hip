@@ -180,8 +180,14 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     // 2^21: 75.9 -> 71.5; at 2^24, HBM-bound, it is 3% slower than one robot per lane)
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     // 32 KiB of dynamic LDS: at most 5 blocks per CU.  kbench, records, two passes: 2^20
-    // 38.2-38.5 -> 37.2-37.3 us (24 KiB 37.6-37.7, 40 KiB 37.4-37.5); 2^21 71.6-71.8 -> 70.5-70.9
-    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
+    // 38.2-38.5 -> 37.2-37.3 us (24 KiB 37.6-37.7, 40 KiB 37.4-37.5); 2^21 71.6-71.8 -> 70.5-70.9.
+    // Records fed while state + inputs fill at most half the cache (2^20 robots): 48 KiB, 3
+    // blocks per CU (round 3, kbench, three alternating passes on one box: 32 KiB 36.99-37.14 us,
+    // 48 KiB 36.67-36.93, 64 KiB 36.61-36.97, 80 KiB 44.0, uncapped 38.0).  Plane inputs and
+    // 2^21 records stay at 32 KiB (48 KiB: 2^20 planes 37.49 -> 37.72-38.07, 2^21 records
+    // 68.3-68.4 -> 69.0, 2^21 planes 69.5-69.7 -> 71.2-71.4)
+    const bool rec_half = a.in.rec != nullptr && a.n * 124 <= (128ull << 20);
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, rec_half ? 48u * 1024u : 32u * 1024u);
     if constexpr (O::UPD && O::PRED) {
       if (state_nt(a.n * 108)) {  // only when forced: this branch's state fits the cache
         k_kf6p<4, 2, WithNT<O>><<<g, kBlock, lds, st>>>(a);
