@@ -67,6 +67,37 @@ def main():
                 w = csv.writer(fo)
                 w.writerow(rows_in[0])
                 w.writerows(keep)
+    # wave-state counters of the path-row kernels (r3_session.sh sq) and their per-kernel summary
+    sq = []
+    for d in sorted(glob.glob(os.path.join(G, "sq_*"))):
+        f = os.path.join(d, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        rows_in = list(csv.reader(open(f)))
+        hdr = rows_in[0]
+        col, cn, cv = hdr.index("Kernel_Name"), hdr.index("Counter_Name"), hdr.index("Counter_Value")
+        keep = [r for r in rows_in[1:] if "fmskf::" in r[col]]
+        with open(os.path.join(P, f"{tag}_{os.path.basename(d)}.csv"), "w", newline="") as fo:
+            w = csv.writer(fo)
+            w.writerow(hdr)
+            w.writerows(keep)
+        tot, calls = {}, {}
+        for r in keep:
+            k = (r[col], r[cn])
+            tot[k] = tot.get(k, 0.0) + float(r[cv])
+            calls[k] = calls.get(k, 0) + 1
+        for name in sorted({k[0] for k in tot}):
+            if calls.get((name, "SQ_WAVES"), 0) < 5:  # warm-up launches of other kernels
+                continue
+            a = {c: tot[(name, c)] / calls[(name, c)] for (nm, c) in tot if nm == name}
+            wc = a["SQ_WAVE_CYCLES"]
+            sq.append({"run": os.path.basename(d), "kernel": name, "launches": calls[(name, "SQ_WAVES")],
+                       "waves": a["SQ_WAVES"], "valu_per_wave": a["SQ_INSTS_VALU"] / a["SQ_WAVES"],
+                       "salu_per_wave": a["SQ_INSTS_SALU"] / a["SQ_WAVES"],
+                       "wait_frac": a["SQ_WAIT_ANY"] / wc, "issue_wait_frac": a["SQ_WAIT_INST_ANY"] / wc,
+                       "active_frac": a["SQ_ACTIVE_INST_ANY"] / wc})
+    if sq:
+        json.dump(sq, open(os.path.join(P, f"{tag}_sq_summary.json"), "w"), indent=1)
     # HBM-regime bench lines (profile_session.sh PMC_SEC=1): calibrated traffic + the counter rows
     if secondary and glob.glob(os.path.join(G, "pmc_sec_*")):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "secondary", G,
