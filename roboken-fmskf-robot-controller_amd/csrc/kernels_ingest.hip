@@ -131,6 +131,13 @@ struct Wt901Parser {
 // VEC: the poll buffer rows are 16-byte aligned and at most 64 bytes (the 44-byte standard
 // poll in a 48-byte row): the lane's whole row is fetched with up to four 16-byte loads
 // issued before any byte is parsed, instead of one dependent byte load per parser step.
+// One IMU per lane.  Measured and not kept (round 3, kbench at 2^20 standard polls, one box
+// each): two IMUs per lane with the second one's parser state and poll row loaded before the
+// first is parsed (as k_kf6p does), 38.1 us against 34.9; the register file as pair planes
+// (registers 2k, 2k + 1 in one dword, so 5 of the poll's 15 register stores become dword
+// pairs), 38.7-38.9 against 35-36: the remaining single-register stores then half-fill the
+// lines they touch; the magnetometer / q_init loads issued with the poll instead of after the
+// parse, neutral.
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   const uint64_t n = a.n;

@@ -183,6 +183,12 @@ def test_fleet_loop_cpp_host_program():
     x0 = float(lines[1].split("x=")[1].split()[0])
     assert 0.0 < x0 < 1.0          # driven forward for 0.2 s
     assert "imu.fault=0" in lines[2]
+    # the asynchronous ensemble every 16 ticks (fmskf_ensemble_begin / _end, two results late):
+    # 12 records, the fleet mean of x between the slowest and fastest robots' x
+    assert lines[3].startswith("fleet (1 rank): 12 ensemble records"), lines[3]
+    mx = float(lines[3].split("mean x=")[1].split()[0])
+    vx = float(lines[3].split("var x=")[1].split()[0])
+    assert 0.0 < mx < 1.0 and vx > 0.0
 
 
 def test_reset_zeroes_control_state():
