@@ -142,3 +142,36 @@ def test_graph_captures_tick_ensemble(model):
         xa, _ = a.get_state()
         xb, _ = b.get_state()
     np.testing.assert_array_equal(xa.view(np.uint32), xb.view(np.uint32))
+
+
+def test_async_ensemble_pending_across_capture():
+    """A pending asynchronous result whose fold has not been queued yet (the newest event) stays
+    pending across a capture: plain ticks captured in the graph do not fold it (the replay would
+    fold whatever the slot holds then), fmskf_ensemble_end refuses inside the capture, and after
+    it the result equals the synchronous record of the same state, bit for bit."""
+    import torch
+    n, T = 4099, 3
+    tr = Trajectory(n, T, seed=75)
+    yaw, gz, rpm = tr.kf6_inputs()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st), Engine("kf6", n) as a, Engine("kf6", n) as b:
+        for e in (a, b):
+            e.set_stream(st)
+        want = fmskf.ensemble_combine(6, a.tick_ensemble(yaw_deg=yaw[0], gyro_z_dps=gz[0], rpm=rpm[0])[None, :])
+        b.tick_ensemble_begin(yaw_deg=yaw[0], gyro_z_dps=gz[0], rpm=rpm[0])
+        dev = [torch.from_numpy(np.ascontiguousarray(v[1])).cuda() for v in (yaw, gz, rpm)]
+        torch.cuda.synchronize()
+        b.graph_begin()
+        b.tick(yaw_deg=dev[0], gyro_z_dps=dev[1], rpm=dev[2])
+        with pytest.raises(fmskf.FmskfError):
+            b.ensemble_end()                      # the newest fold would be captured, not run
+        b.graph_end()
+        got = b.ensemble_end()
+        b.graph_launch()
+        a.tick(yaw_deg=yaw[1], gyro_z_dps=gz[1], rpm=rpm[1])
+        torch.cuda.synchronize()
+        xa, _ = a.get_state()
+        xb, _ = b.get_state()
+    np.testing.assert_array_equal(want[0], got[0])
+    np.testing.assert_array_equal(want[1], got[1])
+    np.testing.assert_array_equal(xa.view(np.uint32), xb.view(np.uint32))
