@@ -426,7 +426,8 @@ def main():
     ap.add_argument("--gather", choices=["auto", "async", "stream", "native"], default="auto",
                     help="N > 1: native (the default with RCCL): libfmskf's own communicator "
                          "(fmskf_comm_init), fmskf_tick_ensemble_begin / fmskf_ensemble_end -- the "
-                         "fused record, fold + ncclAllGather + copy-out on the handle's side stream "
+                         "fused record, its fold carried by the next record's tick kernel (or run ahead of "
+                         "the next plain tick), ncclAllGather + copy-out on the handle's side stream "
                          "overlapping the next ticks, the path C callers bind; async / stream: "
                          "torch.distributed all-gather on RCCL's stream or in the tick stream "
                          "(auto = native, or async under gloo / --same-device)")
@@ -533,8 +534,8 @@ def main():
         args.gather = "async" if (gloo or args.same_device) else "native"
     if args.gather == "native" and distributed:
         # the handle's own RCCL communicator: rank 0's unique id reaches the others over the
-        # torch.distributed group (without a launcher there is no communicator: the side stream
-        # folds and copies out this GPU's record alone)
+        # torch.distributed group (without a launcher there is no communicator: the fold writes
+        # this GPU's record straight into the handle's pinned result slot)
         uid = [fmskf.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0], rank, world)
@@ -558,9 +559,10 @@ def main():
         then this rank's share of the all-gather"""
         e = ev_count[0] % n_events
         if args.gather == "native":
-            # fused tick + record, then fold / ncclAllGather / copy-out on the handle's side
-            # stream; results are collected two events late (they finished while later ticks
-            # ran), so the host never waits behind the tick stream
+            # fused tick + record; its fold rides in the next record's tick kernel (or runs ahead
+            # of the next plain tick), the all-gather and copy-out on the handle's side stream;
+            # results are collected two events late (they finished while later ticks ran), so
+            # the host never waits behind the tick stream
             eng.tick_ensemble_begin(prepared[k % R])
             applied.append(k % R)
             native_pending[0] += 1
@@ -786,8 +788,8 @@ def main():
                          f"{world} GPU(s)") +
                         ", fused correct+predict per tick (fmskf_tick; every ensemble_every-th tick "
                         + ("fmskf_tick_ensemble_begin: the tick kernel also writes the ensemble record, "
-                           "fold + libfmskf's ncclAllGather + copy-out on a side stream, "
-                           "fmskf_ensemble_end one event later)" if args.gather == "native" else
+                           "its fold carried by the next tick, libfmskf's ncclAllGather + copy-out on a side "
+                           "stream, fmskf_ensemble_end two events later)" if args.gather == "native" else
                            "fmskf_tick_ensemble, which also writes the ensemble record; torch "
                            "all-gather)"),
             "instances_per_gpu": n,
