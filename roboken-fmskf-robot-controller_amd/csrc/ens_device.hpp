@@ -130,17 +130,20 @@ __device__ __forceinline__ void ens_load_shift(const double *shift, double (&sh)
 
 // Block record (element-major [LEN][nblocks], so the fold reads one element coalesced)
 template <int NX>
-__device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], double *blocks, uint32_t nblocks) {
+__device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], double *blocks, uint32_t nblocks,
+                                                uint32_t bid) {
   __shared__ double red[4 * EnsRec<NX>::LEN4];
   const double s = block_reduce<EnsRec<NX>::LEN4>(v, red);
   if (threadIdx.x < EnsRec<NX>::LEN)
-    blocks[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = s;
+    blocks[(uint64_t)threadIdx.x * nblocks + bid] = s;
 }
 
 // The tick kernels' record epilogue (fmskf_tick_ensemble): the R robots this lane ticked
-// (live ones only), reduced over the block into its record of the post-tick state
+// (live ones only), reduced over the block into its record of the post-tick state; bid: the
+// block's tick block index (its record's column)
 template <int NX, int R, typename T>
-__device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][NX], const bool (&live)[R]) {
+__device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][NX], const bool (&live)[R],
+                                             uint32_t bid) {
   double sh[NX], v[EnsRec<NX>::LEN4];
   ens_load_shift<NX>(in.ens_shift, sh);
 #pragma unroll
@@ -148,7 +151,7 @@ __device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][
 #pragma unroll
   for (int r = 0; r < R; r++)
     if (live[r]) ens_add<NX>(v, xs[r], sh);
-  ens_block_write<NX>(v, in.ens_blocks, in.ens_grid);
+  ens_block_write<NX>(v, in.ens_blocks, in.ens_grid, bid);
 }
 
 // Fold of record element k: sum, over the nb block records, the count row, the two S1 rows
@@ -238,6 +241,22 @@ __device__ __forceinline__ bool ens_fold_carried(const TickIn &in) {
   if (blockIdx.x < in.ens_grid) return false;
   ens_fold_block<NX, 1>(in.fold_blocks, in.fold_nb, in.ens_shift, in.fold_out, blockIdx.x - in.ens_grid);
   return true;
+}
+// The same with the fold blocks FIRST in the grid (the KF6 kernels, whose tick blocks address
+// their robots through `bid` alone): dispatched first, the fold blocks' load round trips
+// overlap the tick blocks' instead of extending the grid's tail (at 2^21 robots a fold block
+// makes 4 passes over 4096 records).  bid: this block's tick block index.
+template <int NX>
+__device__ __forceinline__ bool ens_fold_front(const TickIn &in, uint32_t &bid) {
+  constexpr uint32_t L = EnsRec<NX>::LEN;
+  bid = blockIdx.x;
+  if (!in.fold_blocks) return false;
+  if (blockIdx.x < L) {
+    ens_fold_block<NX, 1>(in.fold_blocks, in.fold_nb, in.ens_shift, in.fold_out, blockIdx.x);
+    return true;
+  }
+  bid = blockIdx.x - L;
+  return false;
 }
 
 }  // namespace fmskf

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    ens_epilogue<9, 1>(a.in, xs, lv);
+    ens_epilogue<9, 1>(a.in, xs, lv, blockIdx.x);
   }
 }
 
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[1][k] = xb[k];
     const bool lv[2] = {live_a, live_b};
-    ens_epilogue<9, 2>(a.in, xs, lv);
+    ens_epilogue<9, 2>(a.in, xs, lv, blockIdx.x);
   }
 }
 
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    ens_epilogue<12, 1>(a.in, xs, lv);
+    ens_epilogue<12, 1>(a.in, xs, lv, blockIdx.x);
   }
 }
 

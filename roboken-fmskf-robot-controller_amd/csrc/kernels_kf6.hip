@@ -75,11 +75,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 template <int WPE, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6t(
     KfArgs<MdKF6, Kf6Params> a) {
+  uint32_t bid = blockIdx.x;
   if constexpr (O::ENS) {
-    if (ens_fold_carried<6>(a.in)) return;
+    if (ens_fold_front<6>(a.in, bid)) return;
   }
   const uint64_t n = a.n;
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = bid * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
   const uint32_t ic = live ? i : (uint32_t)n - 1u;
   float x[6], P[21];
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 #pragma unroll
     for (int k = 0; k < 6; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    ens_epilogue<6, 1>(a.in, xs, lv);
+    ens_epilogue<6, 1>(a.in, xs, lv, bid);
   }
 }
 
@@ -110,13 +111,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
 template <int WPE, int R, class O>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_kf6p(
     KfArgs<MdKF6, Kf6Params> a) {
+  uint32_t bid = blockIdx.x;
   if constexpr (O::ENS) {
-    if (ens_fold_carried<6>(a.in)) return;
+    if (ens_fold_front<6>(a.in, bid)) return;
   }
   const uint64_t n = a.n;
   const uint32_t nn = (uint32_t)n, last = nn - 1u;
   const uint32_t G = (O::ENS ? a.in.ens_grid : gridDim.x) * kBlock;
-  const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i0 = bid * kBlock + threadIdx.x;
   float x[6], P[21];
   __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
   float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
     }
     lv[r] = live;
   }
-  if constexpr (O::ENS) ens_epilogue<6, R>(a.in, xs, lv);
+  if constexpr (O::ENS) ens_epilogue<6, R>(a.in, xs, lv, bid);
 }
 
 // Variant (FMSKF_KF6_VARIANT, read once) for single-tick launches; default 0:

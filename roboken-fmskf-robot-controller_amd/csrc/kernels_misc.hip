@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_ens_partial(const T *__restrict__ x,
     for (int u = 0; u < R; u++)
       if (i0 + u * stride < n) ens_add<NX>(v, xv[u], sh);
   }
-  ens_block_write<NX>(v, blocks, gridDim.x);
+  ens_block_write<NX>(v, blocks, gridDim.x, blockIdx.x);
 }
 
 // Fold: one block per record element (ens_fold_block: kFoldLanes partial sums, so this kernel
