@@ -357,9 +357,10 @@ def path_rows(dev, stream, ticks: int, trig):
 
 def cfg4_shard(dev, stream, ticks: int, trig):
     """BASELINE.json configs[3] on one GPU: its 2^21-robot per-GPU shard of the 16M fleet, the
-    tick alone, with the fused ensemble record (+ fold) every 16th tick and every tick (K = 16
-    and K = 1, SURVEY.md 8(d) cfg 4); HIP events on the tick stream, no collective (that is the
-    N > 1 bench run's).  Fed the SoA input planes: the record-fed kernel instantiation stays the
+    tick alone, with the asynchronous ensemble record every 16th tick and every tick (K = 16
+    and K = 1, SURVEY.md 8(d) cfg 4: fmskf_tick_ensemble_begin, each result collected two
+    events late, as the headline does); HIP events on the tick stream, no collective (that is
+    the N > 1 bench run's).  Fed the SoA input planes: the record-fed kernel instantiation stays the
     headline's alone, so a rocprofv3 --stats summary of the bench keeps its 2^20 average."""
     import torch
     import fmskf
@@ -372,11 +373,18 @@ def cfg4_shard(dev, stream, ticks: int, trig):
     out_rec = torch.empty(e.ensemble_record_len(), dtype=torch.float64, device=dev)
 
     def run(every):
+        pending = 0
         for k in range(ticks):
             if every and (k + 1) % every == 0:
-                e.tick_ensemble_prepared(preps[k % R], out_rec)
+                e.tick_ensemble_begin(preps[k % R])
+                pending += 1
+                if pending == 3:
+                    e.ensemble_end()
+                    pending -= 1
             else:
                 e.tick_prepared(preps[k % R])
+        for _ in range(pending):
+            e.ensemble_end()
 
     res = {"instances": n, "ticks": ticks, "inputs": "planes"}
     for label, every in (("tick_only", 0), ("ensemble_every_16", 16), ("ensemble_every_1", 1)):
@@ -393,6 +401,7 @@ def cfg4_shard(dev, stream, ticks: int, trig):
     gbps = 232 * n / (res["tick_only"]["ms_per_step"] * 1e-3) / 1e9
     res["roofline"] = {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                        "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": 232}
+    e.ensemble_partial(out_rec)  # the record of the final state (sanity: every robot counted)
     res["ensemble_count"] = float(out_rec[0].item())
     e.close()
     del preps, yaw, gz, rpm
