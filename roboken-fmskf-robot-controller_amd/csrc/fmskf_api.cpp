@@ -1686,9 +1686,9 @@ namespace {
 // a communicator, the all-gather and D2H on the side stream.  This event's own fold waits for
 // the next event's tick kernel, or runs stand-alone ahead of a plain tick, at
 // fmskf_ensemble_end or before a shift rewrite (ens_flush).
-// Nothing waits on the host.  Folds of more than kCarryMax block records (the one-robot-per-
-// lane kernels past the Infinity Cache) run stand-alone: a carried fold block's passes over
-// them would outlast the tick blocks it hides behind.
+// Nothing waits on the host.  Folds of more than kCarryMax block records (the EKF9 one-robot-
+// per-lane kernel past the Infinity Cache) run stand-alone: a fold block carried at the end of
+// the grid would outlast the tick blocks it hides behind (the KF6 kernels carry theirs first).
 constexpr int kCarryMax = 8192;
 
 void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
@@ -1727,7 +1727,9 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     t.ens_blocks = S.blocks;
     t.ens_shift = h->ens_shift;
     fmskf_ctx::EnsSlot *C = h->ens_carry >= 0 ? &h->eslot[h->ens_carry] : nullptr;
-    if (C && C->nb > kCarryMax) {
+    // the KF6 kernels take their fold blocks first in the grid (ens_fold_front): any record
+    // count hides behind their tick blocks
+    if (C && C->nb > kCarryMax && h->cfg.model != FMSKF_MODEL_KF6) {
       ens_flush(h);
       C = nullptr;
     }
