@@ -159,7 +159,7 @@ __device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][
 // / c.  The summation order is fixed at kFoldLanes partial sums (lane L adds blocks L,
 // L + kFoldLanes, ... ascending, then the block_reduce tree over kFoldLanes / 64 waves), and a
 // 256-thread block plays kFoldLanes / 256 lanes per thread, so the stand-alone fold kernel and
-// the fold blocks a tick kernel carries (ens_fold_carried) give bitwise the same record.  A row
+// the fold blocks a tick kernel carries (ens_fold_front) give bitwise the same record.  A row
 // summed by several elements gets bitwise the same total in each, so the record is
 // consistent.  U: passes of kFoldLanes blocks whose loads are in flight together.
 constexpr uint32_t kFoldLanes = 1024;
@@ -232,20 +232,12 @@ __device__ __forceinline__ void ens_fold_block(const double *__restrict__ blocks
   }
 }
 
-// The fold blocks a fused tick kernel carries past its ens_grid tick blocks
-// (fmskf_tick_ensemble_begin): blocks ens_grid .. ens_grid + LEN - 1 fold the PREVIOUS event's
-// block records (complete: that event's kernel ran earlier on the stream) into in.fold_out, in
-// the shadow of this tick's blocks instead of a launch of their own.  True on those blocks.
-template <int NX>
-__device__ __forceinline__ bool ens_fold_carried(const TickIn &in) {
-  if (blockIdx.x < in.ens_grid) return false;
-  ens_fold_block<NX, 1>(in.fold_blocks, in.fold_nb, in.ens_shift, in.fold_out, blockIdx.x - in.ens_grid);
-  return true;
-}
-// The same with the fold blocks FIRST in the grid (the KF6 kernels, whose tick blocks address
-// their robots through `bid` alone): dispatched first, the fold blocks' load round trips
-// overlap the tick blocks' instead of extending the grid's tail (at 2^21 robots a fold block
-// makes 4 passes over 4096 records).  bid: this block's tick block index.
+// The fold blocks a fused tick kernel carries (fmskf_tick_ensemble_begin): blocks 0 .. LEN - 1
+// of its grid fold the PREVIOUS event's block records (complete: that event's kernel ran
+// earlier on the stream) into in.fold_out, in the shadow of this tick's blocks instead of a
+// launch of their own.  They come FIRST in the grid: dispatched first, their load round trips
+// overlap the tick blocks' instead of extending the grid's tail (a fold block makes one pass
+// per 1024 records: 64 at 2^24 KF6 robots).  bid: this block's tick block index.
 template <int NX>
 __device__ __forceinline__ bool ens_fold_front(const TickIn &in, uint32_t &bid) {
   constexpr uint32_t L = EnsRec<NX>::LEN;

@@ -132,7 +132,7 @@ struct fmskf_ctx {
   // pinned host copy.  A slot is reused only after fmskf_ensemble_end consumed it (its `done`
   // event, behind the fold, was waited for), so the tick that rewrites a slot's block records
   // needs no stream wait.  Event k's fold rides in the next event's tick kernel (extra blocks
-  // past its tick blocks: ens_fold_carried), or runs stand-alone when a plain tick or a result
+  // ahead of its tick blocks: ens_fold_front), or runs stand-alone when a plain tick or a result
   // request comes first (ens_flush); with a communicator the side stream `ens_stream`
   // all-gathers it while the tick stream runs on.
   static constexpr int kEnsSlots = 4;
@@ -1680,16 +1680,13 @@ namespace {
 
 // One asynchronous ensemble event (the record fused into the tick, the fold
 // and the gather off the tick's critical path).  On the handle's stream: the tick whose kernel
-// writes the slot's block records and, in LEN blocks past its tick blocks, folds the PREVIOUS
-// event's records (ens_fold_carried) | the stand-alone partial.  The previous event's fold is
+// writes the slot's block records and, in LEN blocks ahead of its tick blocks, folds the
+// PREVIOUS event's records (ens_fold_front) | the stand-alone partial.  The previous event's fold is
 // then queued: its `done` event (one GPU: the fold wrote the pinned host slot itself) or, with
 // a communicator, the all-gather and D2H on the side stream.  This event's own fold waits for
 // the next event's tick kernel, or runs stand-alone ahead of a plain tick, at
 // fmskf_ensemble_end or before a shift rewrite (ens_flush).
-// Nothing waits on the host.  Folds of more than kCarryMax block records (the EKF9 one-robot-
-// per-lane kernel past the Infinity Cache) run stand-alone: a fold block carried at the end of
-// the grid would outlast the tick blocks it hides behind (the KF6 kernels carry theirs first).
-constexpr int kCarryMax = 8192;
+// Nothing waits on the host.
 
 void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
   check_handle(h);
@@ -1727,12 +1724,6 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     t.ens_blocks = S.blocks;
     t.ens_shift = h->ens_shift;
     fmskf_ctx::EnsSlot *C = h->ens_carry >= 0 ? &h->eslot[h->ens_carry] : nullptr;
-    // the KF6 kernels take their fold blocks first in the grid (ens_fold_front): any record
-    // count hides behind their tick blocks
-    if (C && C->nb > kCarryMax && h->cfg.model != FMSKF_MODEL_KF6) {
-      ens_flush(h);
-      C = nullptr;
-    }
     if (C) {
       t.fold_blocks = C->blocks;
       t.fold_nb = (uint32_t)C->nb;

@@ -76,7 +76,8 @@ struct TickIn {
   const double *ens_shift;
   uint32_t ens_grid;  // the tick blocks (= block records); set by the launcher
   // fmskf_tick_ensemble_begin: the previous event's block records ([LEN][fold_nb]), folded by
-  // LEN extra blocks of this tick's grid into fold_out (ens_fold_carried); null otherwise
+  // LEN extra blocks at the front of this tick's grid into fold_out (ens_fold_front); null
+  // otherwise
   uint32_t fold_nb;
   const double *fold_blocks;
   double *fold_out;

@@ -167,19 +167,21 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
+  uint32_t bid = blockIdx.x;  // the tick block (the carried fold blocks come first)
   if constexpr (ENS) {
-    if (ens_fold_carried<9>(a.in)) return;
+    if (ens_fold_front<9>(a.in, bid)) return;
   }
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
   float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n, pp = a.pitch;
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t i = (uint64_t)bid * kBlock + threadIdx.x;
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
   float x[N], P[NP];
   WaveTable<LIBM> tv(a.in.sintab);  // wave-private table copy, loads issued first
-  const TileRows<float, N, CP> tx(a.x, tile_slot(n));
-  const TileRows<float, NP, CP> tp(a.P, tile_slot(n));
+  const uint32_t sl = tile_slot(n, bid);
+  const TileRows<float, N, CP> tx(a.x, bid, sl, 0);
+  const TileRows<float, NP, CP> tp(a.P, bid, sl, 0);
   if constexpr (FMSKF_TILED) {
 #pragma unroll
     for (int k = 0; k < N; k++) x[k] = tx.ld(k);
@@ -193,8 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   }
   const bool have = a.in.valid == nullptr || a.in.valid[ic];
   const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
-  const uint64_t hb0 = (uint64_t)blockIdx.x * kBlock;
-  const uint32_t sl = tile_slot(n);
+  const uint64_t hb0 = (uint64_t)bid * kBlock;
   float lo = ld_chunk<float, CP>(a.prm.thlo, hb0, n, sl);
   tv.store(stab);
   ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P, lo);
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    ens_epilogue<9, 1>(a.in, xs, lv, blockIdx.x);
+    ens_epilogue<9, 1>(a.in, xs, lv, bid);
   }
 }
 
@@ -228,14 +229,15 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 template <bool LIBM, bool SEQ, int CP, bool ENS = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
+  uint32_t bid = blockIdx.x;  // the tick block (the carried fold blocks come first)
   if constexpr (ENS) {
-    if (ens_fold_carried<9>(a.in)) return;
+    if (ens_fold_front<9>(a.in, bid)) return;
   }
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
   float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
   const uint64_t n = a.n;
   const uint32_t ntiles = (uint32_t)((n + kBlock - 1) / kBlock);  // chunks of kBlock instances
-  const uint32_t ta = blockIdx.x, tb0 = blockIdx.x + (ENS ? a.in.ens_grid : gridDim.x);
+  const uint32_t ta = bid, tb0 = bid + (ENS ? a.in.ens_grid : gridDim.x);
   const bool has_b = tb0 < ntiles;  // block-uniform
   const uint32_t tb = has_b ? tb0 : ta;
   const uint32_t t = threadIdx.x;
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[1][k] = xb[k];
     const bool lv[2] = {live_a, live_b};
-    ens_epilogue<9, 2>(a.in, xs, lv, blockIdx.x);
+    ens_epilogue<9, 2>(a.in, xs, lv, bid);
   }
 }
 
@@ -472,11 +474,12 @@ __device__ __forceinline__ void kf12d_predict_cov(double (&P)[78], double dt, co
 template <bool BLK, bool UPD, bool PRED, bool SMALL, int CP = 0, bool ENS = false, bool SP = false>
 __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a) {
   constexpr int N = 12, NP = 78, M = 8;
+  uint32_t bid = blockIdx.x;  // the tick block (the carried fold blocks come first)
   if constexpr (ENS) {
-    if (ens_fold_carried<12>(a.in)) return;
+    if (ens_fold_front<12>(a.in, bid)) return;
   }
   const uint64_t n = a.n, pp = a.pitch;
-  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t i0 = (uint64_t)bid * kBlock + threadIdx.x;
   const bool live = i0 < n;
   if (!ENS && !live) return;
   const uint64_t i = live ? i0 : n - 1;
@@ -502,9 +505,9 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
   };
   // tiled layout (FMSKF_TILED): the block's chunk of its tile through a scalar descriptor (without ENS
   // lanes past N returned above, so a lane's slot is its thread index)
-  const uint32_t slot = ENS ? tile_slot(n) : threadIdx.x;
-  const TileRows<double, N, CP> tx(a.x, slot);
-  const TileRows<double, NP, CP> tp(a.P, slot);
+  const uint32_t slot = ENS ? tile_slot(n, bid) : threadIdx.x;
+  const TileRows<double, N, CP> tx(a.x, bid, slot, 0);
+  const TileRows<double, NP, CP> tp(a.P, bid, slot, 0);
 #pragma unroll
   for (int k = 0; k < N; k++) x[k] = FMSKF_TILED ? tx.ld(k) : ld(rx, a.x, k);
 #pragma unroll
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
-    ens_epilogue<12, 1>(a.in, xs, lv, blockIdx.x);
+    ens_epilogue<12, 1>(a.in, xs, lv, bid);
   }
 }
 

@@ -134,11 +134,13 @@ struct TileRows {
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, k * W * 4, st_pol(CP));
   }
 };
-// the lane's slot in its block's chunk; lanes past N take the last instance's slot
-__device__ __forceinline__ uint32_t tile_slot(uint64_t n) {
-  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock;
+// the lane's slot in chunk `bid` (by default its block's); lanes past N take the last
+// instance's slot
+__device__ __forceinline__ uint32_t tile_slot(uint64_t n, uint32_t bid) {
+  const uint64_t b0 = (uint64_t)bid * kBlock;
   return b0 + threadIdx.x < n ? threadIdx.x : (uint32_t)(n - 1 - b0);
 }
+__device__ __forceinline__ uint32_t tile_slot(uint64_t n) { return tile_slot(n, blockIdx.x); }
 
 template <class Md, typename Prm>
 struct KfArgs {
