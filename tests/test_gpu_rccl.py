@@ -95,12 +95,11 @@ def _ens_inputs(model, n, T, seed):
                                                 ("ekf9", 5001, 2, True), ("kf12d", 3001, 1, False),
                                                 ("rs", 4097, 1, True)])
 def test_async_ensemble_matches_sync(model, n, every, comm):
-    """fmskf_tick_ensemble_begin / fmskf_ensemble_end (event k's fold carried by extra blocks of
-    event k + 1's tick kernel -- first in the KF6 grid, including the 8974-record fold of the
-    one-robot-per-lane KF6 kernel past the Infinity Cache, last in the EKF9 / KF12D grids -- or
-    stand-alone: ahead of a plain tick, for the last event, for the non-fused RS record and for
-    the 8583-record EKF9 fold past the Infinity Cache; the all-gather and copy-out on the side
-    stream; results collected two events late, so three are
+    """fmskf_tick_ensemble_begin / fmskf_ensemble_end (event k's fold carried by extra blocks at
+    the front of event k + 1's tick grid -- including the 8974-record KF6 and 8583-record EKF9
+    folds of the one-robot-per-lane kernels past the Infinity Cache -- or stand-alone: ahead of
+    a plain tick, for the last event and for the non-fused RS record; the all-gather and
+    copy-out on the side stream; results collected two events late, so three are
     pending at every begin with every = 1) against the synchronous fmskf_tick_ensemble of a twin
     handle on the same inputs: the states stay bit-identical and every (mean, cov) equals the
     fold of the synchronous record bit for bit, with and without a (world-1) RCCL communicator."""
