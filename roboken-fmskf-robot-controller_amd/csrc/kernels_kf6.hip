@@ -215,8 +215,10 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
 }
 
 // fused tick + ensemble record (fmskf_tick_ensemble): the kernel launch_o picks by default,
-// with the record epilogue (and the carried fold blocks past the tick blocks when
-// in.fold_blocks is set); returns the tick grid (= the number of block records)
+// with the record epilogue (and the carried fold blocks ahead of the tick blocks when
+// in.fold_blocks is set); returns the tick grid (= the number of block records).  Four robots
+// per lane (half the block reductions per robot) measured slower: K = 1 at 2^20 40.8-41.0 us
+// per tick against 38.6-39.0 (kbench, two alternating passes)
 template <class O>
 static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   using E = WithEns<O>;
