@@ -808,6 +808,9 @@ def main():
             "ensemble_every": args.ensemble_every,
             "ensemble": args.ensemble,
             "gather": args.gather,
+            # the library libfmskf's communicator resolves (a rehearsal names its stand-in)
+            "rccl_library": (os.environ.get("FMSKF_RCCL_LIBRARY") or "librccl.so.1")
+            if args.gather == "native" and distributed else None,
             "parallelism": f"instance-sharded x{world}" + (
                 (", RCCL all-gather of ensemble records" if not gloo else ", gloo all-gather of ensemble records")
                 if world > 1 else "") + (" (rehearsal: every rank on cuda:0)" if args.same_device else ""),

@@ -12,7 +12,8 @@
 //
 //   fleet_loop [N] [ticks]
 //   FLEET_WORLD=W FLEET_RANK=r FLEET_ID=/path/id fleet_loop ...   one process per GPU: rank 0
-//       writes the communicator id to FLEET_ID, every rank reads it (device = rank)
+//       writes the communicator id to FLEET_ID, every rank reads it (device = rank, or
+//       FLEET_DEVICE)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,7 +42,8 @@ int main(int argc, char **argv) {
   const int world = getenv("FLEET_WORLD") ? atoi(getenv("FLEET_WORLD")) : 1;
   const int rank = getenv("FLEET_RANK") ? atoi(getenv("FLEET_RANK")) : 0;
   try {
-    fmskf::Robots robots(FMSKF_MODEL_RS, n, world > 1 ? rank : 0);
+    const int device = getenv("FLEET_DEVICE") ? atoi(getenv("FLEET_DEVICE")) : (world > 1 ? rank : 0);
+    fmskf::Robots robots(FMSKF_MODEL_RS, n, device);
     if (world > 1) {  // the handle's RCCL communicator, its id passed through a file
       const char *path = getenv("FLEET_ID");
       if (!path) throw std::runtime_error("FLEET_ID must name the id file");

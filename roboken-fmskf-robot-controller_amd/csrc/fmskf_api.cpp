@@ -1551,8 +1551,16 @@ struct RcclApi {
 const RcclApi &rccl() {
   static RcclApi api = [] {
     RcclApi a;
-    void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    // FMSKF_RCCL_LIBRARY names another RCCL build (or the tests' one-GPU loopback stand-in,
+    // tests/native/loopback_rccl.cpp); it is used alone, without falling back
+    const char *alt = getenv("FMSKF_RCCL_LIBRARY");
+    void *lib = nullptr;
+    if (alt && *alt) {
+      lib = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!lib) {
       a.why = std::string("cannot load librccl.so.1: ") + dlerror();
       return a;

@@ -106,14 +106,20 @@ def test_bench_spawns_ranks_without_launcher():
     assert out["cpu_baseline"]["value"] > 0 and out["cpu_baseline"]["affinity_cpus"] >= 1
 
 
-@pytest.mark.parametrize("strong", [False, True])
-def test_bench_world2_rehearsal_same_gpu(strong):
+@pytest.mark.parametrize("strong,gather", [(False, "async"), (True, "async"), (False, "native"), (True, "native")])
+def test_bench_world2_rehearsal_same_gpu(strong, gather, tmp_path):
     """bench.py's N > 1 code path with two ranks (torch.distributed.run, gloo, both ranks on the
     one GPU of the test box; RCCL refuses two ranks on one device): per-rank shards with their
     own seeds, fused records all-gathered every 8 ticks, max-over-ranks timing, the whole-job
     count, and every rank's gathered records folding to the statistics of the stand-alone
-    records.  strong: cfg 4's strong-scaling form (--n-total, an odd total split unevenly)."""
+    records.  strong: cfg 4's strong-scaling form (--n-total, an odd total split unevenly).
+    native: the driver's default at N > 1 -- libfmskf's own communicator (comm id broadcast over
+    the process group, fmskf_tick_ensemble_begin / fmskf_ensemble_end) -- with the loopback
+    stand-in for RCCL (tests/native/loopback_rccl.cpp, FMSKF_RCCL_LIBRARY)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    if gather == "native":
+        env.update(FMSKF_RCCL_LIBRARY=os.path.join(ROOT, "build", "libloopback_rccl.so"),
+                   LOOPBACK_RCCL_DIR=str(tmp_path))
     n = 1 << 18
     total = 2 * n + 3 if strong else 2 * n
     size = ["--n-total", str(total)] if strong else ["--n-per-gpu", str(n)]
@@ -121,7 +127,7 @@ def test_bench_world2_rehearsal_same_gpu(strong):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
            "--steps", "32", "--warmup", "4", "--ensemble-every", "8", *size,
            "--no-cpu-baseline", "--no-fused", "--no-secondary", "--backend", "gloo", "--same-device",
-           "--check-ensemble"]
+           "--check-ensemble", "--gather", gather]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -133,3 +139,4 @@ def test_bench_world2_rehearsal_same_gpu(strong):
     assert chk["cov_max_rel"] < 1e-9, chk
     assert out["ensemble"]["count"] == total
     assert out["nonfinite_instances"] == 0
+    assert out["config"]["gather"] == gather
