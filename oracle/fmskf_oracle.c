@@ -10,6 +10,8 @@
 #include "fmskf_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -74,15 +76,23 @@ float orc_normalize_deg_0to360(float d) {
   return d;
 }
 
-/* CMSIS-DSP arm_sin_f32 / arm_cos_f32 (third-party, absent from the image):
- * published algorithm = 512-entry sine table over [0, 2pi] plus linear
- * interpolation.  Table entries computed as (float)sin(2*pi*i/512). */
+/* CMSIS-DSP arm_sin_f32 / arm_cos_f32 (third-party, absent from the image; called at
+ * util_mymath.hpp:44-45): published algorithm = 512-entry sine table over [0, 2pi] plus
+ * linear interpolation.  The table is CMSIS-DSP's sinTable_f32 (arm_common_tables.c), which
+ * ships sin(2*pi*i/512) as decimal literals with 8 digits after the point ("0.01227154f",
+ * "-0.00000000f" for i = 512): each entry is that literal, i.e. the value rounded to 8
+ * decimals and then to float.  62 of the 513 entries differ by 1-2 ulp from
+ * (float)sin(2*pi*i/512), and entry 512 is -0.0f instead of -2.4e-16f. */
 static float g_sintab[513];
 static int g_tab_ready = 0;
 
 static void orc_init_tab(void) {
   if (g_tab_ready) return;
-  for (int i = 0; i <= 512; i++) g_sintab[i] = (float)sin(2.0 * 3.14159265358979323846 * (double)i / 512.0);
+  for (int i = 0; i <= 512; i++) {
+    char lit[32];
+    snprintf(lit, sizeof(lit), "%.8f", sin(2.0 * 3.14159265358979323846 * (double)i / 512.0));
+    g_sintab[i] = strtof(lit, NULL);
+  }
   g_tab_ready = 1;
 }
 

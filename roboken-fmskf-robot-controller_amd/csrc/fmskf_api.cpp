@@ -12,6 +12,7 @@
 #include <math.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -838,8 +839,14 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
         h->ens_shift = h->alloc<double>(12);
       }
       h->readout = h->alloc<float>(6 * n);
+      // TABLE512: CMSIS-DSP's sinTable_f32, sin(2 pi i / 512) published as 8-decimal literals
+      // (arm_common_tables.c; the firmware's arm_sin_f32 / arm_cos_f32, util_mymath.hpp:44-45)
       float tab[513];
-      for (int i = 0; i <= 512; i++) tab[i] = (float)sin(2.0 * 3.14159265358979323846 * (double)i / 512.0);
+      for (int i = 0; i <= 512; i++) {
+        char lit[32];
+        snprintf(lit, sizeof(lit), "%.8f", sin(2.0 * 3.14159265358979323846 * (double)i / 512.0));
+        tab[i] = strtof(lit, nullptr);
+      }
       hip_check(hipMemcpy(s.sintab, tab, sizeof(tab), hipMemcpyHostToDevice), "sintab upload");
       hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
       hip_check(hipEventCreate(&h->ev1), "hipEventCreate");

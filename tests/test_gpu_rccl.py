@@ -2,7 +2,8 @@
 communicator owned by the handle.  One GPU on the test box -> world size 1: the record goes
 through ncclAllGather on the handle's stream and must fold to exactly what the host combine
 of the device partial gives; without a communicator the same call covers this handle alone.
-(N > 1 is exercised by bench.py under torch.distributed at round end.)"""
+(World > 1 on one GPU: tests/test_gpu_rccl_multirank.py, through the loopback stand-in; RCCL
+itself at N > 1: bench.py on the driver's node.)"""
 import numpy as np
 import pytest
 

@@ -64,7 +64,18 @@ def test_normalize_deg(orc):
 
 def test_table512_trig(orc):
     tab = orc.sin_table()
-    assert tab[0] == 0.0 and tab[128] == F(1.0) and tab[512] == F(np.sin(2 * np.pi))
+    # CMSIS-DSP sinTable_f32 (arm_common_tables.c) publishes its entries as 8-decimal literals;
+    # its first twelve, the peak and the closing -0.00000000f
+    cmsis = ["0.00000000", "0.01227154", "0.02454123", "0.03680722", "0.04906767", "0.06132074",
+             "0.07356456", "0.08579731", "0.09801714", "0.11022221", "0.12241068", "0.13458071"]
+    np.testing.assert_array_equal(tab[:12], np.array([F(float(v)) for v in cmsis]))
+    assert tab[128] == F(1.0) and tab[256] == 0.0 and tab[384] == F(-1.0)
+    assert tab[512] == 0.0 and np.signbit(tab[512])
+    # every entry is sin(2 pi i / 512) rounded to 8 decimals, then to float: 62 of them differ
+    # by 1-2 ulp from (float)sin(2 pi i / 512)
+    lit = np.array([F(float(f"{np.sin(2 * np.pi * i / 512):.8f}")) for i in range(513)])
+    np.testing.assert_array_equal(tab, lit)
+    assert int((tab != np.sin(2 * np.pi * np.arange(513) / 512).astype(np.float32)).sum()) == 62
     # exact at table nodes: x = 2*pi*k/512 -> in = k/512 up to rounding
     x = np.linspace(-10, 10, 20001).astype(np.float32)
     s, c = orc.eval_trig(x, orc.TRIG_TABLE512)
