@@ -136,3 +136,43 @@ def test_c_struct_layouts_match_python_mirror(tmp_path):
     assert got == [16, 8, C.sizeof(_lib.TickInputs), _lib.TickInputs.kf6_rec.offset,
                    C.sizeof(_lib.VehicleInfo)]
     assert KF6_RECORD_DTYPE.itemsize == 16 and KF6_RECORD_DTYPE.fields["rpm"][1] == 8
+
+
+def _rccl_subprocess(env_extra, tmp_path):
+    """fmskf_comm_unique_id in a fresh process (the RCCL library is resolved once per process)"""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import fmskf\n"
+            "try:\n    print('ID', fmskf.comm_unique_id().rstrip(b'\\0').decode())\n"
+            "except fmskf.FmskfError as e:\n    print('ERR', e)\n"
+            % os.path.join(ROOT, "roboken-fmskf-robot-controller_amd"))
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def test_rccl_library_override_loopback(tmp_path):
+    """FMSKF_RCCL_LIBRARY: fmskf_comm_unique_id comes from the named library (here the tests'
+    loopback stand-in, whose id is a fresh directory under LOOPBACK_RCCL_DIR); no GPU needed"""
+    lb = os.path.join(ROOT, "build", "libloopback_rccl.so")
+    assert os.path.exists(lb), "build() makes build/libloopback_rccl.so"
+    out = _rccl_subprocess({"FMSKF_RCCL_LIBRARY": lb, "LOOPBACK_RCCL_DIR": str(tmp_path)}, tmp_path)
+    assert out.startswith("ID " + str(tmp_path) + "/loopback_rccl."), out
+    assert os.path.isdir(out[3:])
+
+
+def test_rccl_library_override_missing_fails_loudly(tmp_path):
+    """a named RCCL library that cannot be loaded is an FMSKF_ERCCL error naming it, with no
+    fallback to the system RCCL"""
+    out = _rccl_subprocess({"FMSKF_RCCL_LIBRARY": str(tmp_path / "nope.so")}, tmp_path)
+    assert out.startswith("ERR") and "nope.so" in out, out
+
+
+def test_loopback_exports_the_rccl_entry_points():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "build", "libloopback_rccl.so")],
+                         capture_output=True, text=True, check=True).stdout
+    names = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert {"ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclAllGather",
+            "ncclGetErrorString"} <= names
