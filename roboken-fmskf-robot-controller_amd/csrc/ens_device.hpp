@@ -140,7 +140,10 @@ __device__ __forceinline__ void ens_block_write(double (&v)[EnsRec<NX>::LEN4], d
 
 // The tick kernels' record epilogue (fmskf_tick_ensemble): the R robots this lane ticked
 // (live ones only), reduced over the block into its record of the post-tick state; bid: the
-// block's tick block index (its record's column)
+// block's tick block index (its record's column).  Measured and not kept (kbench ens_async, two
+// alternating passes, one box): a record per wave (the lane-level tree only, no LDS and no block
+// barrier; four times the records for the fold), KF6 2^20 async 39.5-40.1 us per tick against
+// 39.0-39.3, EKF9 2^22 323-325 against 305, KF6 2^24 675-676 against 617.
 template <int NX, int R, typename T>
 __device__ __forceinline__ void ens_epilogue(const TickIn &in, const T (&xs)[R][NX], const bool (&live)[R],
                                              uint32_t bid) {
