@@ -1,0 +1,106 @@
+"""BASELINE configs[0]'s full horizon at fleet size on the GPU: 60 000 ticks (60 s at 1 kHz) of
+8192 KF6 robots through the bench's kernel form (k_kf6p, 16-byte fmskf_kf6_records, here with a
+validity mask: one tick in 13 without a measurement), of 4096 EKF9 robots (k_ekf9p, raw IMU +
+wheel records, compensated heading) and of 1024 KF12D fp64 robots (k_kf12s, cfg 5's model).  The inputs are one 1000-tick trajectory
+(fmskf.synth.Trajectory), device-resident, replayed 60 times with a fresh validity mask per pass
+(each replay restarts the measured motion: the filters also take the jump).  The state and the
+covariance equal the oracle's (oracle/fmskf_oracle.c) bit for bit at every 1000th tick (KF12D:
+within cfg 5's 1e-12, relative to each state's fleet scale): no rounding difference is allowed to
+appear and compound over the horizon.  (The cfg 1 trace in
+tests/test_oracle_frozen.py is one robot over the same horizon; tests/test_oracle_kf_long.py
+holds the oracle itself against float64 over it.)"""
+import numpy as np
+import pytest
+
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+
+pytestmark = pytest.mark.gpu
+
+T_LONG = 60000
+CHUNK = 1000
+
+
+def _bits(a, b, what, t):
+    ai, bi = a.view(np.uint32), b.view(np.uint32)
+    if not np.array_equal(ai, bi):
+        bad = np.argwhere(ai != bi)
+        raise AssertionError(f"{what} differs at tick {t}: {bad.shape[0]} entries, first {bad[0].tolist()}")
+
+
+def test_kf6_records_masked_60000_ticks(orc):
+    import torch
+    n = 8192
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]), orc.TRIG_TABLE512)
+    xo = np.zeros((6, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    rng = np.random.default_rng(1313)
+    with Engine("kf6", n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        yaw, gz, rpm = Trajectory(n, CHUNK, seed=0x464D534B ^ 7).kf6_inputs()
+        rec_d = torch.from_numpy(fmskf.kf6_records(yaw, gz, rpm).view(np.int32).reshape(CHUNK, n, 4)).cuda()
+        for t0 in range(0, T_LONG, CHUNK):
+            valid = (rng.random((CHUNK, n)) > 1.0 / 13).astype(np.uint8)
+            val_d = torch.from_numpy(valid).cuda()
+            for k in range(CHUNK):
+                e.tick(kf6_rec=rec_d[k], valid=val_d[k])
+                orc.kf6_tick(xo, Po, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=0)
+            x, P = e.get_state()
+            t = t0 + CHUNK - 1
+            _bits(x, xo, "x", t)
+            _bits(P, Po, "P", t)
+        assert e.get_counters()[0] == 0
+    assert np.isfinite(xo).all() and np.abs(xo[:2]).max() > 1.0  # the robots went somewhere
+
+
+def test_ekf9_masked_60000_ticks(orc):
+    import torch
+    n = 4096
+    cfg = fmskf.default_config("ekf9", n)
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((10, n), np.float32)  # row 9: the heading's low part
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    rng = np.random.default_rng(99)
+    with Engine("ekf9", n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        raw = Trajectory(n, CHUNK, seed=0x464D534B ^ 9).ekf9_raw()
+        raw_d = torch.from_numpy(raw).cuda()
+        for t0 in range(0, T_LONG, CHUNK):
+            valid = (rng.random((CHUNK, n)) > 1.0 / 13).astype(np.uint8)
+            val_d = torch.from_numpy(valid).cuda()
+            for k in range(CHUNK):
+                e.tick(raw=raw_d[k], valid=val_d[k])
+                orc.ekf9_tick(xo, Po, raw[k], valid[k], prm, nthreads=0)
+            x, P = e.get_state()
+            t = t0 + CHUNK - 1
+            _bits(x, xo[:9], "x", t)
+            _bits(P, Po, "P", t)
+        assert e.get_counters()[0] == 0
+
+
+def test_kf12d_60000_ticks(orc):
+    import torch
+    n = 1024
+    cfg = fmskf.default_config("kf12d", n)
+    prm = orc.kf12d_params(cfg.dt, np.array(cfg.q[:78]), np.array(cfg.r[:36]))
+    xo = np.zeros((12, n))
+    Po = np.repeat(np.array(cfg.p0[:78])[:, None], n, 1).copy()
+    worst = 0.0
+    with Engine("kf12d", n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        z = Trajectory(n, CHUNK, seed=0x464D534B ^ 12).kf12d_z()
+        z_d = torch.from_numpy(z).cuda()
+        for t0 in range(0, T_LONG, CHUNK):
+            for k in range(CHUNK):
+                e.tick(z=z_d[k])
+                orc.kf12d_tick(xo, Po, z[k], None, prm, nthreads=0)
+            x, P = e.get_state()
+            scale = np.maximum(np.abs(xo).max(axis=1, keepdims=True), 1e-3)
+            ex = float((np.abs(x - xo) / scale).max())
+            ep = float((np.abs(P - Po) / max(np.abs(Po).max(), 1e-3)).max())
+            assert ex <= 1e-12 and ep <= 1e-12, (t0 + CHUNK - 1, ex, ep)
+            worst = max(worst, ex, ep)
+        assert e.get_counters()[0] == 0
+    print(f"kf12d 60000 ticks x {n}: max relative difference {worst:.3e}")
