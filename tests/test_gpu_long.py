@@ -104,3 +104,51 @@ def test_kf12d_60000_ticks(orc):
             worst = max(worst, ex, ep)
         assert e.get_counters()[0] == 0
     print(f"kf12d 60000 ticks x {n}: max relative difference {worst:.3e}")
+
+
+def test_isr_kf6_control_60000_ticks(orc):
+    """The firmware ISR over the same horizon (fmskf_isr_tick: the KF6 tick, the wheel speed
+    loops and the 0x200 frame in one kernel, k_isr_kf6), 2048 robots fed records with a
+    validity mask, power and target-velocity events every few seconds: the estimator state, the
+    FF_PI_D outputs, the current targets and the frame bytes equal the oracle's (kf6_tick +
+    the control batch + can_tx) at every 1000th tick."""
+    n = 2048
+    rng = np.random.default_rng(4242)
+    cfg = fmskf.default_config("kf6", n)
+    prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]), orc.TRIG_TABLE512)
+    xo = np.zeros((6, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    ref = orc.CtrlBatch(n)
+    yaw, gz, rpm = Trajectory(n, CHUNK, seed=0x464D534B ^ 11).kf6_inputs()
+    rec = fmskf.kf6_records(yaw, gz, rpm)
+    with Engine("kf6", n) as e:
+        for t0 in range(0, T_LONG, CHUNK):
+            valid = (rng.random((CHUNK, n)) > 1.0 / 13).astype(np.uint8)
+            if t0 % 6000 == 0:  # new targets (C_ACCEL / JERK_MAX_MOVE, VD_task_main.cpp:29-38)
+                vel = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                                rng.uniform(-6 * np.pi, 6 * np.pi, n)]).astype(np.float32)
+                acl = np.array([[1000.0], [1000.0], [30.0]], np.float32).repeat(n, 1)
+                jrk = np.array([[10000.0], [10000.0], [300.0]], np.float32).repeat(n, 1)
+                e.set_target_vel(vel, acl, jrk)
+                ref.set_target_vel(vel, acl, jrk)
+            if t0 % 9000 == 0:  # power: most robots on, some off, changing every 9 s
+                on = (rng.random(n) < 0.85).astype(np.uint8)
+                e.set_power(on)
+                ref.set_power(on)
+            for k in range(CHUNK):
+                last = k == CHUNK - 1
+                fr = e.isr_tick(frames=last, kf6_rec=rec[k], valid=valid[k])
+                orc.kf6_tick(xo, Po, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=0)
+                ref.step(rpm[k])
+            t = t0 + CHUNK - 1
+            x, P = e.get_state()
+            _bits(x, xo, "x", t)
+            _bits(P, Po, "P", t)
+            g = e.get_ctrl()
+            cur = ref.curr()
+            np.testing.assert_array_equal(g["curr"], cur, err_msg=f"currents at tick {t}")
+            _bits(g["wheel_ctrl"], ref.wheel("ctrl"), "FF_PI_D output", t)
+            _bits(g["vel_tgt"], ref.vel_tgt(), "velocity target", t)
+            np.testing.assert_array_equal(fr, orc.can_tx(cur), err_msg=f"0x200 frames at tick {t}")
+        assert e.get_counters()[0] == 0
+    assert np.abs(cur).max() > 0  # the loops drove the wheels
