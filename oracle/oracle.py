@@ -144,6 +144,10 @@ def lib():
         L.orc_wt901_is_com_comp.restype = C.c_int
         L.orc_m2006_reset.argtypes = [C.POINTER(M2006State), C.c_int]
         L.orc_m2006_rx.argtypes = [C.POINTER(M2006State), _u8p, C.c_int16]
+        L.orc_wt901_update_batch.argtypes = [C.c_size_t, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+        L.orc_wt901_update_batch.restype = None
+        L.orc_can_ingest_batch.argtypes = [C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_can_ingest_batch.restype = None
         L.orc_rs_tick.argtypes = [C.c_size_t, _f32p, _f32p, _i64p, _vp, _i64p, _i16p,
                                   C.c_int, C.c_int, C.c_int]
         L.orc_kf6_tick.argtypes = [C.c_size_t, _f32p, _f32p, _vp, _vp, _vp, _vp,
@@ -280,6 +284,72 @@ class M2006:
     def rx(self, frame, micro: int):
         f = np.ascontiguousarray(np.frombuffer(bytes(frame), np.uint8))
         lib().orc_m2006_rx(C.byref(self.s), f, int(np.int16(micro)))
+
+
+def _struct_view(arr, cls):
+    """numpy structured view of a ctypes array of `cls`, laid out from the ctypes field offsets"""
+    names, formats, offsets = [], [], []
+    for name, ct in cls._fields_:
+        base, shape = ct, ()
+        while hasattr(base, "_length_"):
+            shape += (base._length_,)
+            base = base._type_
+        names.append(name)
+        formats.append((np.dtype(base), shape) if shape else np.dtype(base))
+        offsets.append(getattr(cls, name).offset)
+    dt = np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": C.sizeof(cls)})
+    return np.frombuffer(arr, dtype=dt)
+
+
+class Wt901Batch:
+    """n IMU_IF_WT901C instances updated by one C call per poll (orc_wt901_update_batch, the
+    per-instance orc_wt901_update in a loop)."""
+
+    def __init__(self, n: int, read_reg_index: int = 0x51):
+        self.n = n
+        self.s = (Wt901State * n)()
+        for i in range(n):
+            lib().orc_wt901_reset(C.byref(self.s[i]), read_reg_index)
+
+    def update(self, buf, lens, latch_qinit: bool = False):
+        """buf [n][stride] uint8 rows, lens [n]: one poll per instance"""
+        buf = np.ascontiguousarray(buf, np.uint8)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        assert buf.shape[0] == self.n and lens.shape == (self.n,)
+        lib().orc_wt901_update_batch(self.n, C.cast(self.s, C.c_void_p), buf.ctypes.data_as(C.c_void_p),
+                                     buf.shape[1], lens.ctypes.data_as(C.c_void_p), int(latch_qinit))
+
+    @property
+    def data(self):
+        """[16][n] Data pages"""
+        return np.ascontiguousarray(_struct_view(self.s, Wt901State)["data"].T)
+
+    @property
+    def is_error(self):
+        return _struct_view(self.s, Wt901State)["is_error"].copy()
+
+
+class MotorBatch:
+    """n robots' four MOTOR_IF_M2006 instances fed by one C call per tick (orc_can_ingest_batch)."""
+
+    def __init__(self, n: int, dirs=(1, 1, -1, -1)):
+        self.n = n
+        self.m = (M2006State * (4 * n))()
+        for i in range(n):
+            for w in range(4):
+                lib().orc_m2006_reset(C.byref(self.m[4 * i + w]), int(dirs[w]))
+
+    def rx(self, frames, stamps):
+        """frames [n][4][8] uint8, stamps [n][4] int16, every wheel present"""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        stamps = np.ascontiguousarray(stamps, np.int16)
+        assert frames.shape == (self.n, 4, 8) and stamps.shape == (self.n, 4)
+        lib().orc_can_ingest_batch(self.n, C.cast(self.m, C.c_void_p), frames.ctypes.data_as(C.c_void_p),
+                                   stamps.ctypes.data_as(C.c_void_p), None)
+
+    def field(self, name):
+        """[n][4] of one M2006 field"""
+        return _struct_view(self.m, M2006State)[name].reshape(self.n, 4).copy()
 
 
 # ----------------------------------------------------------------------------- RS tick

@@ -158,6 +158,29 @@ class Trajectory:
                 wt901_frame(0x53, [0, 0, yaw, 0x1234]) +
                 wt901_frame(0x59, q))
 
+    def wt901_poll_rows(self, tick: int, stride: int = 48):
+        """wt901_poll_bytes for every robot at once: ([N, stride] uint8 rows, [N] uint32 lengths)."""
+        n = self.n
+        yaw = self.reg_yaw[tick].astype(np.int64)
+        half = np.radians(yaw / 32768.0 * 180.0) / 2.0
+        z = np.zeros(n, np.int64)
+        words = [(0x51, [self.reg_ax[tick].astype(np.int64), self.reg_ay[tick].astype(np.int64), z + 2048, z + 2500]),
+                 (0x52, [z, z, self.reg_gz[tick].astype(np.int64), z]),
+                 (0x53, [z, z, yaw, z + 0x1234]),
+                 (0x59, [np.rint(np.cos(half) * 32767).astype(np.int64), z, z,
+                         np.rint(np.sin(half) * 32767).astype(np.int64)])]
+        rows = np.zeros((n, stride), np.uint8)
+        for f, (ftype, w) in enumerate(words):
+            fr = rows[:, 11 * f: 11 * f + 11]
+            fr[:, 0] = 0x55
+            fr[:, 1] = ftype
+            for k, v in enumerate(w):
+                u = v & 0xFFFF
+                fr[:, 2 + 2 * k] = (u & 0xFF).astype(np.uint8)
+                fr[:, 3 + 2 * k] = (u >> 8).astype(np.uint8)
+            fr[:, 10] = (fr[:, :10].astype(np.int64).sum(axis=1) & 0xFF).astype(np.uint8)
+        return rows, np.full(n, 44, np.uint32)
+
     def can_frames(self, tick: int):
         """([N,4,8] uint8 C610 payloads, [N,4] int16 stamps) for one 1 ms tick."""
         n = self.n

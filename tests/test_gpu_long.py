@@ -152,3 +152,71 @@ def test_isr_kf6_control_60000_ticks(orc):
             np.testing.assert_array_equal(fr, orc.can_tx(cur), err_msg=f"0x200 frames at tick {t}")
         assert e.get_counters()[0] == 0
     assert np.abs(cur).max() > 0  # the loops drove the wheels
+
+
+@pytest.mark.parametrize("model", ["rs", "kf6"])
+def test_firmware_pipeline_60000_ticks(orc, model):
+    """The firmware's whole per-tick path for a fleet over the same horizon, device-resident:
+    four C610 frames per robot every tick (fmskf_ingest_can, MOTOR_IF_M2006::rx_callback), a
+    44-byte WT901 poll every 10 ticks (fmskf_ingest_wt901: WitSerialDataIn, CopeWitData,
+    isComComp, updateData), and the tick on the ingested state (NULL planes: the yaw / gyro
+    page, the wheel rpm and angle sums).  2048 robots; the RS model is the reference's own
+    integrator (VD_vehicle_controller.cpp:36-51).  Against the batched oracle (the same
+    restatements as tests/cfg1_trace.py's one robot): pose / state, covariance, the previous
+    angle sums, the Data page and the motor state bit for bit at every 1000th tick."""
+    import torch
+    n = 2048
+    tr = Trajectory(n, CHUNK, seed=0x464D534B ^ 21)
+    frames = np.stack([tr.can_frames(k)[0] for k in range(CHUNK)])          # [T, N, 4, 8]
+    polls = [tr.wt901_poll_rows(k) for k in range(0, CHUNK, 10)]
+    frames_d = torch.from_numpy(frames).cuda()
+    polls_d = [(torch.from_numpy(r).cuda(), torch.from_numpy(ln).cuda()) for r, ln in polls]
+    wb, mb = orc.Wt901Batch(n), orc.MotorBatch(n)
+    if model == "rs":
+        pos, vel = np.zeros((3, n), np.float32), np.zeros((3, n), np.float32)
+        prev = np.zeros((4, n), np.int64)
+    else:
+        cfg = fmskf.default_config("kf6", n)
+        prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]), orc.TRIG_TABLE512)
+        xo = np.zeros((6, n), np.float32)
+        Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    with Engine(model, n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        for t0 in range(0, T_LONG, CHUNK):
+            g = t0 + np.arange(CHUNK)
+            stamps = (((g[:, None, None] + 1) * 1000 + np.arange(4)[None, None, :] * 7) & 0x7FFF).astype(np.int16)
+            stamps = np.ascontiguousarray(np.broadcast_to(stamps, (CHUNK, n, 4)))
+            stamps_d = torch.from_numpy(stamps).cuda()
+            for k in range(CHUNK):
+                t = t0 + k
+                e.ingest_can(frames_d[k], stamps_d[k])
+                mb.rx(frames[k], stamps[k])
+                if k % 10 == 0:
+                    rows_d, lens_d = polls_d[k // 10]
+                    e.ingest_wt901(rows_d, lens_d, latch_qinit=(t == 0))
+                    wb.update(*polls[k // 10], latch_qinit=(t == 0))
+                e.tick()
+                d = wb.data
+                rpm = mb.field("rpm")
+                if model == "rs":
+                    sums = np.ascontiguousarray(mb.field("angle_sum").T)
+                    orc.rs_tick(pos, vel, prev, np.ascontiguousarray(d[11]), sums, rpm)
+                else:
+                    orc.kf6_tick(xo, Po, np.ascontiguousarray(d[11]), np.ascontiguousarray(d[5]), rpm, None, prm,
+                                 nthreads=0)
+            t = t0 + CHUNK - 1
+            x, P = e.get_state()
+            if model == "rs":
+                _bits(x[:3], pos, "pose", t)
+                _bits(x[3:], vel, "velocity", t)
+                np.testing.assert_array_equal(e.get_prev_sum(), prev, err_msg=f"previous sums at tick {t}")
+            else:
+                _bits(x, xo, "x", t)
+                _bits(P, Po, "P", t)
+            data, err = e.get_imu()
+            _bits(data, wb.data, "Data page", t)
+            np.testing.assert_array_equal(err, wb.is_error, err_msg=f"IMU error flags at tick {t}")
+            m = e.get_motors()
+            np.testing.assert_array_equal(m["angle_sum"], mb.field("angle_sum").T, err_msg=f"angle sums at tick {t}")
+            np.testing.assert_array_equal(m["rpm"], mb.field("rpm"), err_msg=f"rpm at tick {t}")
+        assert e.get_counters()[0] == 0
