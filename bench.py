@@ -242,6 +242,10 @@ PATH_BYTES = {
     # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
     # loads it once) + the 8-byte 0x200 frame
     "isr_kf6_2p20": 232 + 369 - 8 + 8,
+    # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
+    # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
+    # the WT901 poll
+    "firmware_loop_kf6_2p20": 256 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
 }
 
 
@@ -332,7 +336,6 @@ def path_rows(dev, stream, ticks: int, trig):
     stamps = [torch.from_numpy((np.arange(4)[None, :] * 250 + k * 1000 + np.zeros((n, 1))).astype(np.int16)).to(dev)
               for k in range(R)]
     timed("can_ingest_2p20", lambda k: e.ingest_can(frames[k % R], stamps[k % R]), e)
-    del frames, stamps
 
     def driven(model):
         en = fmskf.Engine(model, n, device=dev.index, trig=trig)
@@ -350,7 +353,21 @@ def path_rows(dev, stream, ticks: int, trig):
     e = driven("kf6")
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     timed("isr_kf6_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R], gyro_z_dps=gz[k % R], rpm=rpm[k % R]), e)
-    del yaw, gz, rpm, fr
+    # the whole firmware loop (VDT::can_tx_routine_intr with the CAN RX and IMU tasks feeding it):
+    # four C610 frames per robot every tick, a WT901 poll every 10th tick, the fused ISR on the
+    # ingested state; time per tick over a multiple of 10 ticks
+    e = driven("kf6")
+    poll = torch.from_numpy(np.tile(np.frombuffer(b"".join(
+        wt901_frame(t, rng.integers(0, 65536, 4)) for t in (0x51, 0x52, 0x53, 0x59)) + bytes(4), np.uint8),
+        (n, 1))).to(dev)
+
+    def loop(k):
+        e.ingest_can(frames[k % R], stamps[k % R])
+        if k % 10 == 0:
+            e.ingest_wt901(poll, lens, latch_qinit=(k == 0))
+        e.isr_tick(out=fr)
+    timed("firmware_loop_kf6_2p20", loop, e)
+    del yaw, gz, rpm, fr, frames, stamps, poll
     torch.cuda.empty_cache()
     return out
 
@@ -853,7 +870,7 @@ def main():
     if not args.no_secondary and world == 1:  # single-GPU configs: one line at N=1
         torch.cuda.empty_cache()
         out["secondary"] = secondary_configs(dev, stream, args.secondary_ticks, trig)
-        out["path_rows"] = path_rows(dev, stream, max(args.secondary_ticks, 20), trig)
+        out["path_rows"] = path_rows(dev, stream, -(-max(args.secondary_ticks, 20) // 10) * 10, trig)
     # the CPU baseline on rank 0 after every timed region (at N > 1 the other ranks wait at
     # the final barrier): the same KF6 tick on a bounded 2^18-robot sample
     if rank == 0 and not args.no_cpu_baseline:
