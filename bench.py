@@ -235,8 +235,8 @@ PATH_BYTES = {
     # 15 registers 30 w, magnetometer 6 + q_init 16 r, Data page 64 w
     "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, head, IIR y / x, int64 sum r+w;
-    # speed, dlt, rpm, curr w
-    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 4 + 4 + 2 + 2),
+    # rpm, curr w (the speed is the IIR state y; the unread dlt is not kept)
+    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2),
     # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
     "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
     # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
@@ -245,7 +245,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 256 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
+    "firmware_loop_kf6_2p20": 224 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
 }
 
 

@@ -441,8 +441,6 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_sum, 0, 4 * s.m_pitch * 8, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_dlt, 0, 4 * n * 4, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_speed, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
 }
@@ -518,8 +516,6 @@ void ensure_motors(fmskf_ctx *h) {
   s.m_head = h->alloc<uint8_t>(4 * n);
   s.m_pitch = plane_pitch(n);
   s.m_sum = h->alloc<int64_t>(4 * s.m_pitch);
-  s.m_dlt = h->alloc<float>(4 * n);
-  s.m_speed = h->alloc<float>(4 * n);
   s.m_iir_y = h->alloc<float>(4 * n);
   s.m_iir_x = h->alloc<float>(4 * n);
   zero_motors(h);
@@ -1118,9 +1114,11 @@ namespace {
 // (estimator pitch / tile / element size, the motor sums' pitch, the control arrays' tiling
 // and pitch) and a checksum of everything after the header; a file whose layout differs from
 // this build's, or from a format-1 file (which recorded none of the control / motor layout), is
-// rejected instead of being loaded into a scrambled state.
-constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '2'};
+// rejected instead of being loaded into a scrambled state.  Format 3 ('FMSKFCK3'): the motor
+// group without the dlt and speed planes (no longer kept); format-2 files are rejected.
+constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '3'};
 constexpr char kCkMagicV1[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
+constexpr char kCkMagicV2[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '2'};
 struct CkHeader {
   char magic[8];
   uint32_t abi, model;
@@ -1159,7 +1157,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
       v.push_back({p, (size_t)4 * n * 2});
     v.push_back({s.m_head, (size_t)4 * n});
     v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
-    for (void *p : {(void *)s.m_dlt, (void *)s.m_speed, (void *)s.m_iir_y, (void *)s.m_iir_x})
+    for (void *p : {(void *)s.m_iir_y, (void *)s.m_iir_x})
       v.push_back({p, (size_t)4 * n * 4});
   }
   if (groups & 8) {
@@ -1303,6 +1301,8 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     f.read(&hd.magic, 8);
     if (memcmp(hd.magic, kCkMagicV1, 8) == 0)
       fail(FMSKF_EINVAL, "format-1 checkpoint (older build): its control / motor layout is not recorded");
+    if (memcmp(hd.magic, kCkMagicV2, 8) == 0)
+      fail(FMSKF_EINVAL, "format-2 checkpoint (older build): its motor group holds the dlt / speed planes this build no longer keeps");
     if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
     f.seek(0, SEEK_SET);
     f.read(&hd, sizeof(hd));
@@ -1416,7 +1416,8 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
     copy_planes_out(h, angle_sum, h->s.m_sum, n * 8, h->s.m_pitch * 8, 4, mem);
-    copy_out(h, speed_radps, h->s.m_speed, 4 * n * 4, mem);
+    // Status::flt_SpeedRadPS is the IIR1 output, i.e. its state y (VD_motor_if_m2006.cpp:63)
+    copy_out(h, speed_radps, h->s.m_iir_y, 4 * n * 4, mem);
     finish_out(h, mem);
   });
 }

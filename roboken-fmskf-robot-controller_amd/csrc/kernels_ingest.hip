@@ -340,7 +340,7 @@ struct CanArgs {
   uint8_t *head;
   int64_t *sum;  // [4][sum_pitch]
   uint64_t sum_pitch;
-  float *dlt, *speed, *iir_y, *iir_x;
+  float *iir_y, *iir_x;  // UTIL::IIR1 state; y is also Status::flt_SpeedRadPS
 };
 
 __device__ __forceinline__ int16_t s16_of(uint32_t h, uint32_t l) { return (int16_t)((h << 8) | l); }
@@ -359,7 +359,7 @@ __device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
 struct CanWheel {
   int16_t angle, rpm, curr;
   uint32_t head;
-  float iir_y, iir_x, dlt;
+  float iir_y, iir_x;
   int64_t sum;
 };
 __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t micro, int dir,
@@ -386,7 +386,8 @@ __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t 
   const float x = (float)sdiv_arm(num, usec_dlt) / (float)K::raw_per_rot;
   o.iir_y = 0.8f * py + 0.1f * x + 0.1f * pxv;  // UTIL::IIR1::update, util_iir.hpp:39-45
   o.iir_x = x;
-  o.dlt = (float)(new_angle - old_angle) * K::out_rad_per_raw * K::gear_ratio_inv;
+  // Status::flt_dltOutAngle_rad (VD_motor_if_m2006.cpp:64) is not kept: nothing reads it, in the reference
+  // (VD_vehicle_controller.cpp:11-33 reads s16_rawSpeedRpm) or through the ABI
   int16_t d = (int16_t)(new_angle - old_angle);
   d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
   o.sum = sum + d;
@@ -404,8 +405,6 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
                                a.iir_y[pw], a.iir_x[pw], a.sum[ps]);
   a.iir_y[pw] = o.iir_y;
   a.iir_x[pw] = o.iir_x;
-  a.speed[pw] = o.iir_y;
-  a.dlt[pw] = o.dlt;
   a.sum[ps] = o.sum;
   a.micro[g] = a.stamps[g];
   a.angle[g] = o.angle;
@@ -472,8 +471,6 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
                                  (oh >> (8 * w)) & 0xFF, py[w], px[w], sm[w]);
     st_chunk<float, SP>(a.iir_y + (uint64_t)w * n, hb, n, li, o.iir_y);
     st_chunk<float, SP>(a.iir_x + (uint64_t)w * n, hb, n, li, o.iir_x);
-    st_chunk<float, SP>(a.speed + (uint64_t)w * n, hb, n, li, o.iir_y);
-    st_chunk<float, SP>(a.dlt + (uint64_t)w * n, hb, n, li, o.dlt);
     st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li, o.sum);
     na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
     nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
@@ -503,8 +500,6 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.head = s.m_head;
   a.sum = s.m_sum;
   a.sum_pitch = s.m_pitch;
-  a.dlt = s.m_dlt;
-  a.speed = s.m_speed;
   a.iir_y = s.m_iir_y;
   a.iir_x = s.m_iir_x;
   // every wheel present and the caller's frames / stamps aligned for the wide loads: one robot

@@ -385,16 +385,18 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
         with pytest.raises(fmskf.FmskfError):
             d.load_state(ck)
     # a truncated file, one with trailing bytes, one with a flipped byte in the middle (the
-    # checksum) or a format-1 file (no recorded control / motor layout) is rejected before any
+    # checksum), a format-1 file (no recorded control / motor layout) or a format-2 one (motor
+    # planes no longer kept) is rejected before any
     # copy: the handle keeps its state
     blob = ck.read_bytes()
     mid = len(blob) // 2
     flipped = blob[:mid] + bytes([blob[mid] ^ 0x40]) + blob[mid + 1:]
     v1 = b"FMSKFCK1" + blob[8:]
+    v2 = b"FMSKFCK2" + blob[8:]  # format 2 kept the dlt / speed motor planes
     with Engine(model, n) as e:
         e.load_state(ck)
         before = readout(e)
-        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1)):
+        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2)):
             bad = tmp_path / name
             bad.write_bytes(data)
             with pytest.raises(fmskf.FmskfError):

@@ -333,8 +333,8 @@ def bench_io(args, e, n, R, dev, rpm, st):
                for k in range(4)]
         run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
         # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), head 1, IIR y / x (4 + 4) and
-        # the int64 sum read and written; speed, dlt (4 + 4), rpm, curr (2 + 2) written
-        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 4 + 4 + 2 + 2)
+        # the int64 sum read and written; rpm, curr (2 + 2) written
+        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2)
     for k in range(10):
         run(k)
     torch.cuda.synchronize()

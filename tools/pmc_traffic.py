@@ -81,14 +81,14 @@ def secondary(root, out):
 # written (56); WT901 standard poll: row, len, parser window / count / flags, magnetometer,
 # q_init read (88), parser state, error, 15 registers, Data page written (109); CAN RX, four
 # wheels: frame, stamp, micro, angle, head, IIR y / x, sum read (124), those state fields plus
-# speed, dlt, rpm, curr written (132).  The counters are corrected with the KF6 calibration of
+# rpm, curr written (100).  The counters are corrected with the KF6 calibration of
 # profiles/pmc_traffic.json (the same streaming dword / 8- / 16-byte lane accesses: FETCH_SIZE
 # counts half, WRITE_SIZE exact).
 PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 88, 109),
-    ("can_ingest_2p20", "k_can4", 124, 132),
+    ("can_ingest_2p20", "k_can4", 124, 100),
 ]
 
 
