@@ -29,6 +29,21 @@ def _bits(a, b, what, t):
         raise AssertionError(f"{what} differs at tick {t}: {bad.shape[0]} entries, first {bad[0].tolist()}")
 
 
+def _moments(got, want, t):
+    """the fused asynchronous ensemble record (the shift taken once, at the first record, while
+    the fleet drifts for 60 s) against the oracle's two-pass moments of the same state: each mean
+    within 1e-12 of max(|mean|, its standard deviation), each covariance entry within 1e-9 of
+    sqrt(var_p var_q) (an entry near zero is judged against its variables' scale)"""
+    (mg, cg), (mw, cw) = got, want
+    nx = mw.size
+    var = np.array([cw[p * (p + 1) // 2 + p] for p in range(nx)])
+    sd = np.sqrt(np.maximum(var, 0.0))
+    em = float(np.max(np.abs(mg - mw) / np.maximum(np.maximum(np.abs(mw), sd), 1e-300)))
+    scale = np.array([sd[p] * sd[q] for p in range(nx) for q in range(p + 1)])
+    ec = float(np.max(np.abs(cg - cw) / np.maximum(scale, 1e-300)))
+    assert em <= 1e-12 and ec <= 1e-9, (t, em, ec)
+
+
 def test_kf6_records_masked_60000_ticks(orc):
     import torch
     n = 8192
@@ -45,12 +60,16 @@ def test_kf6_records_masked_60000_ticks(orc):
             valid = (rng.random((CHUNK, n)) > 1.0 / 13).astype(np.uint8)
             val_d = torch.from_numpy(valid).cuda()
             for k in range(CHUNK):
-                e.tick(kf6_rec=rec_d[k], valid=val_d[k])
+                if k == CHUNK - 1:  # the chunk's last tick also records the fleet's moments
+                    e.tick_ensemble_begin(kf6_rec=rec_d[k], valid=val_d[k])
+                else:
+                    e.tick(kf6_rec=rec_d[k], valid=val_d[k])
                 orc.kf6_tick(xo, Po, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=0)
             x, P = e.get_state()
             t = t0 + CHUNK - 1
             _bits(x, xo, "x", t)
             _bits(P, Po, "P", t)
+            _moments(e.ensemble_end(), orc.ens_finalize(6, orc.ens_partial(xo)), t)
         assert e.get_counters()[0] == 0
     assert np.isfinite(xo).all() and np.abs(xo[:2]).max() > 1.0  # the robots went somewhere
 
@@ -71,12 +90,16 @@ def test_ekf9_masked_60000_ticks(orc):
             valid = (rng.random((CHUNK, n)) > 1.0 / 13).astype(np.uint8)
             val_d = torch.from_numpy(valid).cuda()
             for k in range(CHUNK):
-                e.tick(raw=raw_d[k], valid=val_d[k])
+                if k == CHUNK - 1:
+                    e.tick_ensemble_begin(raw=raw_d[k], valid=val_d[k])
+                else:
+                    e.tick(raw=raw_d[k], valid=val_d[k])
                 orc.ekf9_tick(xo, Po, raw[k], valid[k], prm, nthreads=0)
             x, P = e.get_state()
             t = t0 + CHUNK - 1
             _bits(x, xo[:9], "x", t)
             _bits(P, Po, "P", t)
+            _moments(e.ensemble_end(), orc.ens_finalize(9, orc.ens_partial(np.ascontiguousarray(xo[:9]))), t)
         assert e.get_counters()[0] == 0
 
 
