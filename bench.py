@@ -703,7 +703,9 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for k in range(k1_steps):
-            if args.gather == "native":  # begin every tick, each result collected two ticks later
+            # begin every tick, each result collected two ticks later (three: the same 2.68-2.69e10,
+            # three alternating pairs on one box)
+            if args.gather == "native":
                 eng.tick_ensemble_begin(prepared[k % R])
                 applied.append(k % R)
                 native_pending[0] += 1
