@@ -171,13 +171,16 @@ def secondary_configs(dev, stream, ticks: int, trig):
                            if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
         except Exception:
             sec_traffic = {}
-    # EKF9: 448 algorithmic bytes + the compensated heading's low-part row read
-    # and written (8 B)
-    specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 456), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504),
-             ("cfg2_kf6_2p24", "kf6", 1 << 24, 232)]
+    # algorithmic bytes per robot-tick as SURVEY.md 8(d) prices them (x and P read and written +
+    # the inputs): EKF9 448 (its compensated heading's hidden low-part row, 8 B more read and
+    # written, is reported beside it as `bytes_with_hidden_rows`), KF12D 1504, KF6 232; the KF6
+    # with FMSKF_CFG_COMP_POS (the position low parts: 5 rows read and written) 272
+    specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 448, 456, 0), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504, None, 0),
+             ("cfg2_kf6_2p24", "kf6", 1 << 24, 232, None, 0),
+             ("cfg2_kf6_comp_pos_2p20", "kf6", 1 << 20, 272, None, fmskf.CFG_COMP_POS)]
     R = 4
-    for key, model, n, bps in specs:
-        e = fmskf.Engine(model, n, device=dev.index, trig=trig)
+    for key, model, n, bps, bps_hidden, flags in specs:
+        e = fmskf.Engine(model, n, device=dev.index, trig=trig, flags=flags)
         e.set_stream(stream)
         yaw, gz, rpm = kf6_ring_torch(n, R, seed=SEED ^ 7, device=dev)
         if model == "kf6":
@@ -220,23 +223,31 @@ def secondary_configs(dev, stream, ticks: int, trig):
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                  "frac": gbps / HBM_PEAK_GBPS, "traffic": sec_traffic.get(key),
                                  "bytes_per_step": bps}}
+        if flags:
+            out[key]["config_flags"] = "FMSKF_CFG_COMP_POS"
+        if bps_hidden:
+            g2 = bps_hidden * n / (ms * 1e-3) / 1e9
+            out[key]["roofline"]["bytes_with_hidden_rows"] = {"bytes_per_step": bps_hidden, "achieved": g2,
+                                                              "frac": g2 / HBM_PEAK_GBPS}
     out["cfg4_shard_kf6_2p21"] = cfg4_shard(dev, stream, max(ticks, 32), trig)
     return out
 
 
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
-    # RS tick: pos 12 r+w, prev 32 r+w, sums 32, yaw 4, rpm 8 in, vel 12 out (the same bytes with
-    # the sums at a padded pitch, or read from the ingested motor / IMU state)
-    "rs_tick_2p20": 144,
-    "rs_tick_2p20_padded_sums": 144,
-    "rs_tick_2p20_device_state": 144,
+    # RS tick: pos (x, y) 8 r + (x, y, th) 12 w -- theta is overwritten by the correct, so it is
+    # never read --, prev 32 r+w, sums 32, yaw 4, rpm 8 in, vel 12 out (the same bytes with the
+    # sums at a padded pitch, or read from the ingested motor / IMU state)
+    "rs_tick_2p20": 140,
+    "rs_tick_2p20_padded_sums": 140,
+    "rs_tick_2p20_device_state": 140,
     # WT901 standard poll: row 48 + len 4, parser window / count / flags 14 r+w, error 1,
     # 15 registers 30 w, magnetometer 6 + q_init 16 r, Data page 64 w
     "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, head, IIR y / x, int64 sum r+w;
-    # rpm, curr w (the speed is the IIR state y; the unread dlt is not kept)
-    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2),
+    # rpm, curr and the previous angle w (the speed is the IIR state y; Status's dlt is formed at
+    # readout from the angle and the previous one)
+    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2 + 2),
     # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
     "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
     # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
@@ -245,7 +256,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 224 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
+    "firmware_loop_kf6_2p20": 232 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
 }
 
 
@@ -473,6 +484,11 @@ def main():
                          "record of the same state (reported as ensemble_check)")
     ap.add_argument("--inputs", choices=["records", "planes"], default="records",
                     help="16-byte fmskf_kf6_record per robot (one load per lane) or yaw/gyro/rpm planes")
+    ap.add_argument("--cfg4-16m", action="store_true",
+                    help="also run BASELINE configs[3] (2^24 robots over the ranks) at world 1 "
+                         "(at world > 1 it always runs, reported as cfg4_16M)")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4_16M block")
+    ap.add_argument("--cfg4-steps", type=int, default=64)
     args = ap.parse_args()
 
     import numpy as np
@@ -558,6 +574,7 @@ def main():
 
     if args.gather == "auto":
         args.gather = "async" if (gloo or args.same_device) else "native"
+    rccl = None
     if args.gather == "native" and distributed:
         # the handle's own RCCL communicator: rank 0's unique id reaches the others over the
         # torch.distributed group (without a launcher there is no communicator: the fold writes
@@ -565,6 +582,13 @@ def main():
         uid = [fmskf.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0], rank, world)
+        # what RCCL itself reports (ncclCommCount / ncclCommUserRank), from every rank: a
+        # one-rank communicator inside an N-process job would show here
+        cw, cr = eng.comm_info()
+        seen = [None] * world
+        dist.all_gather_object(seen, (cw, cr))
+        rccl = {"ranks": cw, "user_ranks": sorted(r for _, r in seen), "sizes": sorted({w for w, _ in seen}),
+                "library": fmskf.rccl_library()}
     native_stats = [None]
     native_pending = [0]
     # ring index of every tick applied to `eng`, in order: the post-timing parity replay
@@ -575,9 +599,10 @@ def main():
         applied.append(r)
 
     def native_collect(keep):
-        """fmskf_ensemble_end of the oldest pending events until `keep` remain"""
+        """fmskf_ensemble_end_count of the oldest pending events until `keep` remain (the robots
+        the gathered records count and how many records were folded are kept with the result)"""
         while native_pending[0] > keep:
-            native_stats[0] = eng.ensemble_end()
+            native_stats[0] = eng.ensemble_end_count()
             native_pending[0] -= 1
 
     def ens_event(k):
@@ -614,6 +639,75 @@ def main():
             ens_event(k)
         else:
             tick(k % R)
+
+    def run_cfg4_16m():
+        n_total = 1 << 24
+        lo4, hi4 = fmskf.shard_span(n_total, world, rank)
+        n4, R4 = hi4 - lo4, 8
+        e4 = fmskf.Engine("kf6", n4, device=local, trig=trig)
+        e4.set_stream(stream)
+        y4, g4, r4 = kf6_ring_torch(n4, R4, seed=SEED ^ 0x16 ^ (rank << 8), device=dev)
+        rec4 = fmskf.kf6_records(y4, g4, r4)
+        del y4, g4, r4
+        p4 = [e4.prepare(kf6_rec=rec4[r]) for r in range(R4)]
+        native4 = args.gather == "native"
+        info = None
+        if native4 and distributed:
+            uid4 = [fmskf.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid4, src=0)
+            e4.comm_init(uid4[0], rank, world)
+            info = e4.comm_info()
+        rb = torch.empty(e4.ensemble_record_len(), dtype=torch.float64, device=dev)
+        gb = torch.empty(world, e4.ensemble_record_len(), dtype=torch.float64, device=dev)
+        pend, last = [0], [None]
+
+        def collect(keep):
+            while pend[0] > keep:
+                last[0] = e4.ensemble_end_count()
+                pend[0] -= 1
+
+        def run(every, ticks):
+            for k in range(ticks):
+                if (k + 1) % every:
+                    e4.tick_prepared(p4[k % R4])
+                elif native4:
+                    e4.tick_ensemble_begin(p4[k % R4])
+                    pend[0] += 1
+                    collect(2)
+                else:
+                    e4.tick_ensemble_prepared(p4[k % R4], rb)
+                    if distributed:
+                        all_gather(gb.view(-1), rb)
+                    else:
+                        gb[0].copy_(rb)
+            collect(0)
+
+        res = {"instances_total": n_total, "instances_this_rank": n4, "n_gpus": world, "scaling": "strong",
+               "inputs": "records", "gather": args.gather}
+        for label, every in (("ensemble_every_16", 16), ("ensemble_every_1", 1)):
+            run(every, 2 * every + 6)  # warm-up: every kernel and result slot of this sequence
+            torch.cuda.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            run(every, args.cfg4_steps)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - ta
+            barrier()
+            if distributed:
+                el = max_over_ranks([el])[0]
+            res[label] = {"steps_per_s": n_total * args.cfg4_steps / el, "ms_per_step": el * 1e3 / args.cfg4_steps,
+                          "ticks": args.cfg4_steps}
+        if native4:
+            res["gathered_count"], res["records_folded"] = last[0][2], last[0][3]
+        else:
+            res["gathered_count"], res["records_folded"] = float(gb[:, 0].sum().item()), world
+        if info is not None:
+            res["rccl_ranks"], res["rccl_rank"] = info
+        e4.close()
+        del p4, rec4, rb, gb
+        torch.cuda.empty_cache()
+        return res
 
     def join():
         native_collect(0)
@@ -728,12 +822,21 @@ def main():
         k1 = {"steps_per_s": n_global * k1_steps / k1_el, "ms_per_step": k1_el * 1e3 / k1_steps,
               "ticks": k1_steps}
 
+    # BASELINE configs[3] in the same invocation (SURVEY.md 8(d) cfg 4): 2^24 robots over the
+    # ranks (contiguous shards, strong scaling), records, the ensemble record every 16th tick and
+    # every tick, each result gathered over the ranks -- libfmskf's own communicator in the
+    # native path -- and collected two events late; wall clock between barriers, max over ranks
+    cfg4 = None
+    if (world > 1 or args.cfg4_16m) and not args.no_cfg4:
+        cfg4 = run_cfg4_16m()
+
     # ensemble sanity (outside the timed region): fold the last gathered records in rank order
     last = gathered[(ev_count[0] - 1) % n_events].cpu().numpy() if ev_count[0] else None
     ens = None
     if args.gather == "native" and native_stats[0] is not None:
-        mean, cov = native_stats[0]
-        ens = {"count": float(n_global), "mean_theta": float(mean[2]), "var_vx": float(cov[9])}
+        # the count is the gathered records' own (the sum of their count rows), not n_global
+        mean, cov, cnt, nrec = native_stats[0]
+        ens = {"count": cnt, "records_folded": nrec, "mean_theta": float(mean[2]), "var_vx": float(cov[9])}
     elif last is not None:
         mean, cov = fmskf.ensemble_combine(6, last)
         ens = {"count": float(last[:, 0].sum()), "mean_theta": float(mean[2]),
@@ -758,7 +861,7 @@ def main():
             allown[0].copy_(own)
         mr, cr = fmskf.ensemble_combine(6, allown.cpu().numpy())
         if args.gather == "native":
-            mg, cg = native_stats[0]
+            mg, cg = native_stats[0][:2]
         else:
             mg, cg = fmskf.ensemble_combine(6, gathered[e].cpu().numpy())
         import numpy as np
@@ -828,8 +931,7 @@ def main():
             "ensemble": args.ensemble,
             "gather": args.gather,
             # the library libfmskf's communicator resolves (a rehearsal names its stand-in)
-            "rccl_library": (os.environ.get("FMSKF_RCCL_LIBRARY") or "librccl.so.1")
-            if args.gather == "native" and distributed else None,
+            "rccl_library": rccl["library"] if rccl is not None else None,
             "parallelism": f"instance-sharded x{world}" + (
                 (", RCCL all-gather of ensemble records" if not gloo else ", gloo all-gather of ensemble records")
                 if world > 1 else "") + (" (rehearsal: every rank on cuda:0)" if args.same_device else ""),
@@ -859,6 +961,12 @@ def main():
     }
     if ens_check is not None:
         out["ensemble_check"] = ens_check
+    if rccl is not None:
+        # the communicator libfmskf's asynchronous exchange ran over, as RCCL reports it
+        out["rccl_ranks"] = rccl["ranks"]
+        out["rccl"] = rccl
+    if cfg4 is not None:
+        out["cfg4_16M"] = cfg4
     # post-timing parity (outside every timed region): the measured engine's state against the
     # oracle's restatement of the same tick sequence on sampled robots, bit for bit
     par = parity_sample(eng, applied, yaw, gz, rpm, trig, seed=rank)

@@ -63,6 +63,9 @@ int main(int argc, char **argv) {
         fclose(f);
       }
       robots.comm_init(id, rank, world);
+      int cw = 0, cr = -1;
+      robots.comm_info(&cw, &cr);  // what RCCL itself reports
+      if (cw != world || cr != rank) throw std::runtime_error("communicator size / rank differ from FLEET_*");
     }
     fmskf::ImuIfWt901c imu(robots);
     fmskf::MotorIfM2006 motors(robots);
@@ -90,7 +93,8 @@ int main(int argc, char **argv) {
     vehicle.start();
     vehicle.set_target_vel(vel.data(), acl.data(), jrk.data());
 
-    double mean[6], cov[21];
+    double mean[6], cov[21], counted = 0.0;
+    uint32_t folded = 0;
     int pending = 0, records = 0;
     auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < ticks; t++) {
@@ -129,14 +133,14 @@ int main(int argc, char **argv) {
       if (t % 16 == 15) {  // the fleet's ensemble record, collected two records later
         robots.ensemble_begin();
         if (++pending == 3) {
-          robots.ensemble_end(mean, cov);
+          robots.ensemble_end(mean, cov, &counted, &folded);
           pending--;
           records++;
         }
       }
     }
     while (pending) {
-      robots.ensemble_end(mean, cov);
+      robots.ensemble_end(mean, cov, &counted, &folded);
       pending--;
       records++;
     }
@@ -152,8 +156,14 @@ int main(int argc, char **argv) {
            info[0].pos_x, info[0].pos_y, info[0].imu_fault, tx[0], tx[1], tx[2], tx[3], tx[4], tx[5],
            tx[6], tx[7]);
     if (records)
-      printf("fleet (%d rank%s): %d ensemble records, last mean x=%.6f m th=%.6f rad, var x=%.3e\n", world,
-             world > 1 ? "s" : "", records, mean[0], mean[2], cov[0]);
+      printf("fleet (%d rank%s): %d ensemble records, last mean x=%.6f m th=%.6f rad, var x=%.3e, %.0f robots in "
+             "%u records\n",
+             world, world > 1 ? "s" : "", records, mean[0], mean[2], cov[0], counted, folded);
+    // MOTOR_IF_M2006::get_status_latest of robot 0's front-left wheel
+    std::vector<int16_t> mus(n * 4), ang(n * 4);
+    std::vector<float> dlt(n * 4), spd(n * 4);
+    motors.get_status_latest(mus.data(), ang.data(), nullptr, nullptr, dlt.data(), spd.data());
+    printf("robot 0 FL: microsec_id=%d angle=%d dlt=%.7e rad speed=%.4f rad/s\n", mus[0], ang[0], dlt[0], spd[0]);
   } catch (const std::exception &e) {
     fprintf(stderr, "fleet_loop: %s\n", e.what());
     return 1;

@@ -47,7 +47,9 @@
 extern "C" {
 #endif
 
-#define FMSKF_ABI_VERSION 2u
+/* 3: fmskf_tick_inputs.angle_sum_pitch (the former unchecked `reserved` word), fmskf_config.flags,
+ * the asynchronous ensemble entry points, fmskf_comm_info, fmskf_get_motor_status */
+#define FMSKF_ABI_VERSION 3u
 
 /* ---- status codes (every entry point returns one) ------------------------ */
 #define FMSKF_OK 0
@@ -95,7 +97,17 @@ typedef struct fmskf_config {
   double p0[78];
   int8_t motor_dir[4];   /* FL, BL, BR, FR: +1 / -1 (VD_task_main.cpp:75-78) */
   uint32_t imu_read_reg; /* register index for 0x5F REGVALUE frames; init() leaves q0 = 0x51 */
+  uint32_t flags;        /* FMSKF_CFG_* (0 = the defaults) */
+  uint32_t reserved;     /* must be 0 */
 } fmskf_config;
+
+/* KF6: carry the open-loop integrals -- px, py and the position block of P (P[0][0], P[1][0],
+ * P[1][1]) -- as compensated fp32 pairs (hi + lo; every addition to them a TwoSum), so that
+ * they track the float64 filter over long horizons (60 s at 1 kHz within 1e-5, where plain
+ * fp32 drifts to 2e-5 / 6e-5).  fmskf_get_state returns hi (hi + lo rounded is hi); the lo
+ * parts are readable through fmskf_get_state_lo.  +40 B per robot-tick (232 -> 272).  Off by
+ * default: the plain fp32 filter is the headline. */
+#define FMSKF_CFG_COMP_POS 1u
 
 /* Fill defaults for `model` with `n` instances (dt = 1 ms, TABLE512, reference motor
  * directions, model-specific Q/R/P0).  Pure host function (no GPU needed). */
@@ -186,9 +198,19 @@ int fmskf_get_pose(fmskf_handle h, float *x, float *y, float *th, uint32_t mem);
 /* VEHICLE_CTRL::get_vehicle_vel_mmps_latest (body frame mm/s, mm/s, rad/s) */
 int fmskf_get_vel(fmskf_handle h, float *vx, float *vy, float *vth, uint32_t mem);
 /* Full model state: x [n][N] and P packed [n(n+1)/2][N] in the model's element type
- * (float, or double for KF12D); RS: x = (x, y, th, vx, vy, vth) floats, P unused. */
+ * (float, or double for KF12D); RS: x = (x, y, th, vx, vy, vth) floats, P unused.
+ * Hidden compensation rows are not part of x / P: EKF9's heading low part and, with
+ * FMSKF_CFG_COMP_POS, KF6's position low parts.  get_state returns the hi rows; set_state
+ * restarts every low part at 0, so a get_state / set_state round trip is exact only up to the
+ * low parts (fmskf_get_state_lo / fmskf_set_state_lo carry them; fmskf_save_state /
+ * fmskf_load_state keep everything). */
 int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem);
 int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_t mem);
+/* The hidden low-part rows [rows][N] float: EKF9 1 row (heading); KF6 with FMSKF_CFG_COMP_POS
+ * 5 rows (px, py, P[0][0], P[1][0], P[1][1]); *rows receives the count (0: the model keeps none,
+ * and lo may be NULL).  set_state_lo after set_state restores a handle bit for bit. */
+int fmskf_get_state_lo(fmskf_handle h, float *lo, uint32_t *rows, uint32_t mem);
+int fmskf_set_state_lo(fmskf_handle h, const float *lo, uint32_t mem);
 /* RS: the int64 s64_rawAngleSumPrev [4][N] (VD_vehicle_controller.hpp:75) */
 int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem);
 /* Checkpoint / resume: every per-robot array of the handle (estimator state,
@@ -209,6 +231,13 @@ int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t
  * speed_radps [4][N] float (MOTOR_IF_M2006::Status + s64_rawAngleSum) */
 int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr,
                      int64_t *angle_sum, float *speed_radps, uint32_t mem);
+/* MOTOR_IF_M2006::get_status_latest (VD_motor_if_m2006.hpp:23-30,47-50) for every wheel of every
+ * robot, [N][4] each (FL, BL, BR, FR): s16_microsec_id, s16_rawAngle, s16_rawSpeedRpm,
+ * s16_rawCurr, flt_dltOutAngle_rad (VD_motor_if_m2006.cpp:64: the unwrapped raw angle step of
+ * the last frame x OUT_RAD_PER_RAW_ANGLE x GEAR_RATIO_INV, formed at readout from the last two
+ * angles), flt_SpeedRadPS.  Any pointer may be NULL. */
+int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle, int16_t *rpm,
+                           int16_t *curr, float *dlt_out_angle_rad, float *speed_radps, uint32_t mem);
 /* counters: [0] = instances whose state went non-finite (NaN/Inf guard) */
 int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
 
@@ -245,6 +274,14 @@ int fmskf_ensemble_combine(uint32_t n_state, const double *records, uint32_t n_r
 #define FMSKF_COMM_ID_BYTES 128
 int fmskf_comm_unique_id(uint8_t id[FMSKF_COMM_ID_BYTES]);
 int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int rank, int world);
+/* The handle's communicator as RCCL itself reports it (ncclCommCount, ncclCommUserRank);
+ * EINVAL when the handle has none. */
+int fmskf_comm_info(fmskf_handle h, int *world, int *rank);
+/* The file the RCCL entry points were resolved from (dladdr of ncclAllGather; "" before the
+ * first communicator call or when RCCL cannot be loaded).  FMSKF_RCCL_LIBRARY may name another
+ * file only if it exports `fmskf_rccl_stand_in` (the tests' one-GPU loopback): a deployed
+ * controller cannot have its collective swapped by the environment. */
+const char *fmskf_rccl_library(void);
 /* mean [n], cov packed [n(n+1)/2] (unbiased) over every robot of every rank (the ranks of
  * fmskf_comm_init; without a communicator, this handle's robots): device partial record,
  * ncclAllGather, fold in rank order on the host -> identical on every rank, deterministic. */
@@ -270,6 +307,11 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
 int fmskf_tick_ensemble_begin(fmskf_handle h, const fmskf_tick_inputs *in);
 int fmskf_ensemble_begin(fmskf_handle h);
 int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed);
+/* fmskf_ensemble_end that also returns the robots the gathered records count (the sum of their
+ * count rows) and how many records were folded (the communicator's size; 1 without one).  Any
+ * pointer may be NULL. */
+int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, double *count,
+                             uint32_t *n_records);
 
 /* ---- vehicle control step -------------------------- */
 /* Per-robot control state is allocated on the first call of any entry point below

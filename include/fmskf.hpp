@@ -6,8 +6,8 @@
 //   IMT::IMU_IF_WT901C::update / isError / getDataLatest    fmskf::ImuIfWt901c
 //     (src/Imu/imu_if_wt901c.hpp:8-42)
 //   IMT::get_status_now_yaw (src/Imu/imu_task_main.cpp:102)  ImuIfWt901c::getYawDate
-//   VDT::MOTOR_IF_M2006::rx_callback / get_rawAngleSum        fmskf::MotorIfM2006
-//     (src/VehicleDrive/VD_motor_if_m2006.hpp:42,53)
+//   VDT::MOTOR_IF_M2006::rx_callback / get_rawAngleSum /     fmskf::MotorIfM2006
+//     get_status_latest (src/VehicleDrive/VD_motor_if_m2006.hpp:23-30,42,47-50,53)
 //   VDT::VEHICLE_CTRL::set_now_yaw_world / update /          fmskf::VehicleCtrl
 //     get_vehicle_pos_m_latest / get_vehicle_vel_mmps_latest
 //     (src/VehicleDrive/VD_vehicle_controller.hpp:52-61)
@@ -81,6 +81,12 @@ class Robots {
   void ensemble_end(double *mean, double *cov_packed) {
     check(fmskf_ensemble_end(h_, mean, cov_packed), "fmskf_ensemble_end");
   }
+  // the same, with the robots the gathered records count and how many records were folded
+  void ensemble_end(double *mean, double *cov_packed, double *count, uint32_t *n_records) {
+    check(fmskf_ensemble_end_count(h_, mean, cov_packed, count, n_records), "fmskf_ensemble_end_count");
+  }
+  // the communicator's size and this rank, as RCCL reports them
+  void comm_info(int *world, int *rank) { check(fmskf_comm_info(h_, world, rank), "fmskf_comm_info"); }
 
   // VDT::can_tx_routine_intr: correct with the IMU yaw, then VEHICLE_CTRL::update (the
   // odometry / estimator time update, then the control half: interpolators, IK, FF_PI_D),
@@ -132,6 +138,14 @@ class MotorIfM2006 {
   // get_rawAngleSum: [4][N]
   void get_rawAngleSum(int64_t *sum, uint32_t mem = FMSKF_MEM_HOST) {
     check(fmskf_get_motors(r_.handle(), nullptr, nullptr, nullptr, sum, nullptr, mem), "get_rawAngleSum");
+  }
+  // get_status_latest for every wheel (Status, VD_motor_if_m2006.hpp:23-30): [N][4] each of
+  // s16_microsec_id, s16_rawAngle, s16_rawSpeedRpm, s16_rawCurr, flt_dltOutAngle_rad,
+  // flt_SpeedRadPS; any pointer may be NULL
+  void get_status_latest(int16_t *microsec_id, int16_t *angle, int16_t *rpm, int16_t *curr, float *dlt_out_angle_rad,
+                         float *speed_radps, uint32_t mem = FMSKF_MEM_HOST) {
+    check(fmskf_get_motor_status(r_.handle(), microsec_id, angle, rpm, curr, dlt_out_angle_rad, speed_radps, mem),
+          "get_status_latest");
   }
   // get_rawCurr_tgt: [N][4] (FL, BL, BR, FR), what tx_routine packs
   void get_rawCurr_tgt(int16_t *curr, uint32_t mem = FMSKF_MEM_HOST) {

@@ -114,6 +114,10 @@ void orc_kf6_tick(size_t n, float *x, float *P, const float *yaw_deg, const floa
                   const int16_t *rpm, const uint8_t *valid, const orc_kf6_params *prm,
                   int do_update, int do_predict, int nthreads);
 /* measurement frontend only: z [4][n] */
+/* KF6 with FMSKF_CFG_COMP_POS: lo [5][n] = low parts of px, py, P00, P10, P11 */
+void orc_kf6_tick_comp(size_t n, float *x, float *P, float *lo, const float *yaw_deg,
+                       const float *gyro_z_dps, const int16_t *rpm, const uint8_t *valid,
+                       const orc_kf6_params *prm, int do_update, int do_predict, int nthreads);
 void orc_kf6_measure(size_t n, const float *yaw_deg, const float *gyro_z_dps,
                      const int16_t *rpm, float *z, int trig);
 

@@ -152,6 +152,8 @@ def lib():
                                   C.c_int, C.c_int, C.c_int]
         L.orc_kf6_tick.argtypes = [C.c_size_t, _f32p, _f32p, _vp, _vp, _vp, _vp,
                                    C.POINTER(Kf6Params), C.c_int, C.c_int, C.c_int]
+        L.orc_kf6_tick_comp.argtypes = [C.c_size_t, _f32p, _f32p, _f32p, _vp, _vp, _vp, _vp,
+                                        C.POINTER(Kf6Params), C.c_int, C.c_int, C.c_int]
         L.orc_kf6_measure.argtypes = [C.c_size_t, _f32p, _f32p, _i16p, _f32p, C.c_int]
         L.orc_ekf9_tick.argtypes = [C.c_size_t, _f32p, _f32p, _vp, _vp,
                                     C.POINTER(Ekf9Params), C.c_int, C.c_int, C.c_int]
@@ -377,6 +379,15 @@ def kf6_tick(x, P, yaw, gz, rpm, valid, prm, do_update=True, do_predict=True, nt
     n = x.shape[1]
     lib().orc_kf6_tick(n, x, P, _ptr(yaw), _ptr(gz), _ptr(rpm), _ptr(valid), C.byref(prm),
                        int(do_update), int(do_predict), nthreads)
+
+
+def kf6_tick_comp(x, P, lo, yaw, gz, rpm, valid, prm, do_update=True, do_predict=True, nthreads=1):
+    """KF6 with compensated positions (FMSKF_CFG_COMP_POS): lo [5][n] float32, the low parts of
+    px, py, P00, P10, P11 (oracle/fmskf_oracle.c orc_kf6_tick_comp)"""
+    n = x.shape[1]
+    assert lo.shape == (5, n) and lo.dtype == np.float32 and lo.flags.c_contiguous
+    lib().orc_kf6_tick_comp(n, x, P, lo, _ptr(yaw), _ptr(gz), _ptr(rpm), _ptr(valid), C.byref(prm),
+                            int(do_update), int(do_predict), nthreads)
 
 
 def kf6_measure(yaw, gz, rpm, trig=TRIG_TABLE512):

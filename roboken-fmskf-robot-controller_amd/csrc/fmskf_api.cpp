@@ -437,6 +437,7 @@ void zero_motors(fmskf_ctx *h) {
   hipStream_t st = h->stream;
   hip_check(hipMemsetAsync(s.m_micro, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_angle, 0, 4 * n * 2, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_prev, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
@@ -511,6 +512,7 @@ void ensure_motors(fmskf_ctx *h) {
   const uint64_t n = s.n;
   s.m_micro = h->alloc<int16_t>(4 * n);
   s.m_angle = h->alloc<int16_t>(4 * n);
+  s.m_prev = h->alloc<int16_t>(4 * n);
   s.m_rpm = h->alloc<int16_t>(4 * n);
   s.m_curr = h->alloc<int16_t>(4 * n);
   s.m_head = h->alloc<uint8_t>(4 * n);
@@ -567,6 +569,7 @@ void do_reset(fmskf_ctx *h) {
   }
   if (s.prev_sum) hip_check(hipMemsetAsync(s.prev_sum, 0, 4 * pp * 8, st), "reset prev");
   if (s.thlo) hip_check(hipMemsetAsync(s.thlo, 0, n * 4, st), "reset heading low part");
+  if (s.xlo) hip_check(hipMemsetAsync(s.xlo, 0, (size_t)kKf6LoRows * pp * 4, st), "reset position low parts");
   if (s.imu_reg) zero_imu(h);
   if (s.m_sum) zero_motors(h);
   if (h->ctrl_ready) {  // the control objects are static in the firmware too: zero, power off
@@ -795,6 +798,9 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
     if (cfg->trig > FMSKF_TRIG_LIBM) fail(FMSKF_EINVAL, "bad trig policy");
     if (!(cfg->dt > 0.0) || !isfinite(cfg->dt)) fail(FMSKF_EINVAL, "dt must be > 0");
     if (cfg->imu_read_reg + 4 > 0x90) fail(FMSKF_EINVAL, "imu_read_reg out of range");
+    if ((cfg->flags & ~FMSKF_CFG_COMP_POS) || cfg->reserved) fail(FMSKF_EINVAL, "unknown config flags");
+    if ((cfg->flags & FMSKF_CFG_COMP_POS) && cfg->model != FMSKF_MODEL_KF6)
+      fail(FMSKF_ENOTSUP, "FMSKF_CFG_COMP_POS is a KF6 mode");
     for (int w = 0; w < 4; w++)
       if (cfg->motor_dir[w] != 1 && cfg->motor_dir[w] != -1) fail(FMSKF_EINVAL, "motor_dir must be +-1");
     int ndev = 0;
@@ -820,6 +826,9 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
       // EKF9: the compensated heading's hidden low part (kf_generic.hpp th_add), one float a robot
       s.thlo = cfg->model == FMSKF_MODEL_EKF9 ? h->alloc<float>(n) : nullptr;
+      // KF6 with FMSKF_CFG_COMP_POS: the position low parts, tiled like x and P
+      s.xlo = (cfg->flags & FMSKF_CFG_COMP_POS) ? h->alloc<float>((size_t)kKf6LoRows * s.pitch) : nullptr;
+      h->kf6.lo = s.xlo;
       // the WT901 / motor ingest state (~470 B per robot) is allocated on first use
       // (ensure_imu / ensure_motors): a handle fed tick inputs by the caller holds only x, P
       s.counters = h->alloc<unsigned long long>(8);
@@ -835,14 +844,11 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
         h->ens_shift = h->alloc<double>(12);
       }
       h->readout = h->alloc<float>(6 * n);
-      // TABLE512: CMSIS-DSP's sinTable_f32, sin(2 pi i / 512) published as 8-decimal literals
-      // (arm_common_tables.c; the firmware's arm_sin_f32 / arm_cos_f32, util_mymath.hpp:44-45)
-      float tab[513];
-      for (int i = 0; i <= 512; i++) {
-        char lit[32];
-        snprintf(lit, sizeof(lit), "%.8f", sin(2.0 * 3.14159265358979323846 * (double)i / 512.0));
-        tab[i] = strtof(lit, nullptr);
-      }
+      // TABLE512: CMSIS-DSP's sinTable_f32 as its published 8-decimal literals (arm_common_tables.c;
+      // the firmware's arm_sin_f32 / arm_cos_f32, util_mymath.hpp:44-45), cmsis_sintab.inc
+      static const float tab[513] = {
+#include "cmsis_sintab.inc"
+      };
       hip_check(hipMemcpy(s.sintab, tab, sizeof(tab), hipMemcpyHostToDevice), "sintab upload");
       hip_check(hipEventCreate(&h->ev0), "hipEventCreate");
       hip_check(hipEventCreate(&h->ev1), "hipEventCreate");
@@ -1099,6 +1105,9 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
     if (x) h->ens_shift_ok = false;
     // a heading set from outside is exact as given: its compensation term restarts at zero
     if (x && h->s.thlo) hip_check(hipMemsetAsync(h->s.thlo, 0, n * 4, h->stream), "heading low part");
+    // KF6 compensated positions: a state set from outside restarts every low part (x and P)
+    if ((x || p_packed) && h->s.xlo)
+      hip_check(hipMemsetAsync(h->s.xlo, 0, (size_t)kKf6LoRows * h->s.pitch * 4, h->stream), "position low parts");
     finish_out(h, mem);
   });
 }
@@ -1115,8 +1124,12 @@ namespace {
 // and pitch) and a checksum of everything after the header; a file whose layout differs from
 // this build's, or from a format-1 file (which recorded none of the control / motor layout), is
 // rejected instead of being loaded into a scrambled state.  Format 3 ('FMSKFCK3'): the motor
-// group without the dlt and speed planes (no longer kept); format-2 files are rejected.
-constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '3'};
+// group without the dlt and speed planes (no longer kept).  Format 4 ('FMSKFCK4', ABI 3): the
+// motor group with the previous angles (Status::flt_dltOutAngle_rad at readout), the estimator
+// group with KF6's position low parts under FMSKF_CFG_COMP_POS, and the config flags in the
+// header; format-2 and format-3 files are rejected by name.
+constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '4'};
+constexpr char kCkMagicV3[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '3'};
 constexpr char kCkMagicV1[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
 constexpr char kCkMagicV2[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '2'};
 struct CkHeader {
@@ -1126,6 +1139,7 @@ struct CkHeader {
   uint32_t tile, elem, groups, ctrl_tile;  // ctrl_tile: control arrays' tile width (0 = planar)
   uint64_t m_pitch, ctrl_pitch;            // motor sum planes' pitch, control state's pitch
   uint64_t body_bytes, checksum;           // what follows the header, and its hash
+  uint32_t flags, reserved;                // fmskf_config.flags (FMSKF_CFG_*)
 };
 struct CkSection {
   void *dev;
@@ -1141,6 +1155,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     if (s.P) v.push_back({s.P, (size_t)d.nx * (d.nx + 1) / 2 * pp * d.elem});
     if (s.prev_sum) v.push_back({s.prev_sum, (size_t)4 * pp * 8});
     if (s.thlo) v.push_back({s.thlo, (size_t)n * 4});
+    if (s.xlo) v.push_back({s.xlo, (size_t)kKf6LoRows * s.pitch * 4});
     v.push_back({s.counters, 8 * 8});
   }
   if (groups & 2) {
@@ -1153,7 +1168,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_data, (size_t)16 * n * 4});
   }
   if (groups & 4) {
-    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_rpm, (void *)s.m_curr})
+    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
     v.push_back({s.m_head, (size_t)4 * n});
     v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
@@ -1175,6 +1190,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
 void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->abi = FMSKF_ABI_VERSION;
   hd->model = h->cfg.model;
+  hd->flags = h->cfg.flags;
   hd->n = h->s.n;
   hd->pitch = h->s.pitch;
   hd->tile = h->s.tile;
@@ -1303,14 +1319,16 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
       fail(FMSKF_EINVAL, "format-1 checkpoint (older build): its control / motor layout is not recorded");
     if (memcmp(hd.magic, kCkMagicV2, 8) == 0)
       fail(FMSKF_EINVAL, "format-2 checkpoint (older build): its motor group holds the dlt / speed planes this build no longer keeps");
+    if (memcmp(hd.magic, kCkMagicV3, 8) == 0)
+      fail(FMSKF_EINVAL, "format-3 checkpoint (older build): its motor group lacks the previous angles");
     if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
     f.seek(0, SEEK_SET);
     f.read(&hd, sizeof(hd));
     CkHeader me{};
     ck_layout(h, &me);
     if (hd.abi != me.abi || hd.model != me.model || hd.n != me.n || hd.pitch != me.pitch ||
-        hd.tile != me.tile || hd.elem != me.elem || (hd.groups & ~15u))
-      fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, N or layout)");
+        hd.tile != me.tile || hd.elem != me.elem || hd.flags != me.flags || (hd.groups & ~15u))
+      fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, flags, N or layout)");
     if ((hd.groups & 4) && hd.m_pitch != me.m_pitch) fail(FMSKF_EINVAL, "checkpoint motor layout differs");
     if ((hd.groups & 8) && (hd.ctrl_tile != me.ctrl_tile || hd.ctrl_pitch != me.ctrl_pitch))
       fail(FMSKF_EINVAL, "checkpoint control layout differs (tiling / pitch)");
@@ -1419,6 +1437,84 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     // Status::flt_SpeedRadPS is the IIR1 output, i.e. its state y (VD_motor_if_m2006.cpp:63)
     copy_out(h, speed_radps, h->s.m_iir_y, 4 * n * 4, mem);
     finish_out(h, mem);
+  });
+}
+
+int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle, int16_t *rpm,
+                           int16_t *curr, float *dlt_out_angle_rad, float *speed_radps, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    ensure_motors(h);
+    copy_out(h, microsec_id, h->s.m_micro, 4 * n * 2, mem);
+    copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
+    copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
+    copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
+    if (dlt_out_angle_rad) {
+      float *dst = mem == FMSKF_MEM_DEVICE ? dlt_out_angle_rad : (float *)h->out_for(4 * n * 4);
+      launch_check(launch_motor_dlt(h->s.m_angle, h->s.m_prev, dst, 4 * n, h->stream), "motor dlt");
+      if (mem == FMSKF_MEM_HOST) copy_out(h, dlt_out_angle_rad, dst, 4 * n * 4, mem);
+    }
+    // Status::flt_SpeedRadPS [N][4] from the IIR1 output planes [4][N]
+    if (speed_radps) {
+      if (mem == FMSKF_MEM_HOST) {
+        std::vector<float> pl(4 * n);
+        copy_out(h, pl.data(), h->s.m_iir_y, 4 * n * 4, mem);
+        hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+        for (uint64_t i = 0; i < n; i++)
+          for (int w = 0; w < 4; w++) speed_radps[4 * i + w] = pl[(size_t)w * n + i];
+      } else {  // one strided copy per wheel: plane w -> column w
+        for (int w = 0; w < 4; w++)
+          hip_check(hipMemcpy2DAsync(speed_radps + w, 16, h->s.m_iir_y + (size_t)w * n, 4, 4, n,
+                                     hipMemcpyDeviceToDevice, h->stream),
+                    "speed transpose");
+      }
+    }
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_get_state_lo(fmskf_handle h, float *lo, uint32_t *rows, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    const uint32_t r = h->s.thlo ? 1u : h->s.xlo ? kKf6LoRows : 0u;
+    if (rows) *rows = r;
+    if (!lo || !r) return;
+    if (h->s.thlo) {
+      copy_out(h, lo, h->s.thlo, n * 4, mem);
+    } else {
+      void *dense = mem == FMSKF_MEM_DEVICE ? (void *)lo : h->out_for((size_t)r * n * 4);
+      launch_check(launch_untile(h->s.xlo, dense, r, n, 4, h->stream), "untile");
+      if (mem == FMSKF_MEM_HOST) copy_out(h, lo, dense, (size_t)r * n * 4, mem);
+    }
+    finish_out(h, mem);
+  });
+}
+
+int fmskf_set_state_lo(fmskf_handle h, const float *lo, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    if (!lo) fail(FMSKF_EINVAL, "null lo");
+    DeviceGuard g(h->cfg.device);
+    const uint64_t n = h->s.n;
+    const uint32_t r = h->s.thlo ? 1u : h->s.xlo ? kKf6LoRows : 0u;
+    if (!r) fail(FMSKF_ENOTSUP, "this model keeps no low-part rows");
+    const void *src = lo;
+    if (mem == FMSKF_MEM_HOST) {
+      void *stg = h->stage_for((size_t)r * n * 4);
+      hip_check(hipMemcpyAsync(stg, lo, (size_t)r * n * 4, hipMemcpyHostToDevice, h->stream), "stage H2D");
+      src = stg;
+    }
+    if (h->s.thlo) hip_check(hipMemcpyAsync(h->s.thlo, src, n * 4, hipMemcpyDeviceToDevice, h->stream), "lo");
+    else launch_check(launch_tile(src, h->s.xlo, r, n, 4, h->stream), "tile");
+    h->ens_shift_ok = false;
+    finish_out(h, FMSKF_MEM_HOST);
   });
 }
 
@@ -1549,22 +1645,32 @@ namespace {
 struct RcclApi {
   bool ok = false;
   std::string why;
+  std::string path;  // the file the entry points came from (dladdr)
   ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
   ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int *) = nullptr;
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int *) = nullptr;
   const char *(*error_string)(ncclResult_t) = nullptr;
 };
 
 const RcclApi &rccl() {
   static RcclApi api = [] {
     RcclApi a;
-    // FMSKF_RCCL_LIBRARY names another RCCL build (or the tests' one-GPU loopback stand-in,
-    // tests/native/loopback_rccl.cpp); it is used alone, without falling back
+    // FMSKF_RCCL_LIBRARY names the tests' one-GPU loopback stand-in (tests/native/
+    // loopback_rccl.cpp), used alone, without falling back.  Only a library that exports the
+    // stand-in's marker symbol is accepted, so the environment cannot swap a deployed
+    // controller's collective for another implementation.
     const char *alt = getenv("FMSKF_RCCL_LIBRARY");
     void *lib = nullptr;
     if (alt && *alt) {
       lib = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+      if (lib && !dlsym(lib, "fmskf_rccl_stand_in")) {
+        dlclose(lib);
+        a.why = std::string("FMSKF_RCCL_LIBRARY=") + alt + " is not the test stand-in (no fmskf_rccl_stand_in)";
+        return a;
+      }
     } else {
       lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
       if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -1577,9 +1683,14 @@ const RcclApi &rccl() {
     a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(lib, "ncclCommInitRank");
     a.comm_destroy = (decltype(a.comm_destroy))dlsym(lib, "ncclCommDestroy");
     a.all_gather = (decltype(a.all_gather))dlsym(lib, "ncclAllGather");
+    a.comm_count = (decltype(a.comm_count))dlsym(lib, "ncclCommCount");
+    a.comm_user_rank = (decltype(a.comm_user_rank))dlsym(lib, "ncclCommUserRank");
     a.error_string = (decltype(a.error_string))dlsym(lib, "ncclGetErrorString");
-    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.error_string;
+    a.ok = a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.comm_count &&
+           a.comm_user_rank && a.error_string;
     if (!a.ok) a.why = "librccl.so.1 lacks an entry point";
+    Dl_info di{};
+    if (a.all_gather && dladdr((void *)a.all_gather, &di) && di.dli_fname) a.path = di.dli_fname;
     return a;
   }();
   return api;
@@ -1661,6 +1772,29 @@ int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int r
     h->rank = rank;
     h->world = world;
   });
+}
+
+int fmskf_comm_info(fmskf_handle h, int *world, int *rank) {
+  return guarded([&] {
+    check_handle(h);
+    if (!h->comm) fail(FMSKF_EINVAL, "the handle has no communicator (fmskf_comm_init)");
+    const RcclApi &a = need_rccl();
+    int w = 0, r = -1;
+    nccl_check(a.comm_count(h->comm, &w), "ncclCommCount");
+    nccl_check(a.comm_user_rank(h->comm, &r), "ncclCommUserRank");
+    if (world) *world = w;
+    if (rank) *rank = r;
+  });
+}
+
+const char *fmskf_rccl_library(void) {
+  static std::string path;
+  try {
+    path = rccl().path;
+  } catch (...) {
+    path.clear();
+  }
+  return path.c_str();
 }
 
 int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed) {
@@ -1787,6 +1921,11 @@ int fmskf_ensemble_begin(fmskf_handle h) {
 }
 
 int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed) {
+  return fmskf_ensemble_end_count(h, mean, cov_packed, nullptr, nullptr);
+}
+
+int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, double *count,
+                             uint32_t *n_records) {
   return guarded([&] {
     check_handle(h);
     if (h->ens_pending == 0) fail(FMSKF_EINVAL, "no ensemble pending (fmskf_*ensemble_begin)");
@@ -1801,6 +1940,12 @@ int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed) {
     h->ens_pending--;
     const int rc = fmskf_ensemble_combine(h->d.nx, S.host, (uint32_t)S.ranks, mean, cov_packed);
     if (rc != FMSKF_OK) fail(rc, "ensemble combine");
+    // what the gathered records themselves count: every rank's robots, once each
+    const uint32_t len = 1 + h->d.nx + h->d.nx * (h->d.nx + 1) / 2;
+    double c = 0.0;
+    for (int r = 0; r < S.ranks; r++) c += S.host[(size_t)r * len];
+    if (count) *count = c;
+    if (n_records) *n_records = (uint32_t)S.ranks;
   });
 }
 

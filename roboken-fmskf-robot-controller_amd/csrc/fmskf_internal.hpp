@@ -29,6 +29,9 @@ struct DevState {
   void *P = nullptr;
   int64_t *prev_sum = nullptr;  // RS: s64_rawAngleSumPrev [4][N]
   float *thlo = nullptr;        // EKF9: the heading's low part [N] (compensated heading)
+  // KF6 with FMSKF_CFG_COMP_POS: the low parts of px, py, P[0][0], P[1][0], P[1][1], tiled like
+  // x and P ([N/2048][5][2048])
+  float *xlo = nullptr;
   // WT901 / IMU_IF_WT901C
   int16_t *imu_reg = nullptr;     // sReg [0x90][N]
   uint32_t *imu_parser = nullptr; // parser window [3][N] (bytes 0..11, little-endian)
@@ -40,6 +43,8 @@ struct DevState {
   // MOTOR_IF_M2006 x 4 wheels
   int16_t *m_micro = nullptr;  // [N][4]
   int16_t *m_angle = nullptr;  // [N][4]
+  int16_t *m_prev = nullptr;   // [N][4] the angle of the frame before (Status ring entry head - 1):
+                               // flt_dltOutAngle_rad is formed from the two at readout
   int16_t *m_rpm = nullptr;    // [N][4]
   int16_t *m_curr = nullptr;   // [N][4]
   uint8_t *m_head = nullptr;   // [N][4]
@@ -98,7 +103,14 @@ struct KfParams {
   T q[NP];
   T r[MP];
 };
-using Kf6Params = KfParams<float, 21, 10>;
+struct Kf6Params {
+  float dt;
+  float q[21];
+  float r[10];
+  // FMSKF_CFG_COMP_POS: the tiled low-part rows (px, py, P00, P10, P11); null = plain fp32
+  float *lo;
+};
+constexpr uint32_t kKf6LoRows = 5;
 struct Ekf9Params {
   float dt;
   float q[45];
@@ -336,5 +348,7 @@ int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint3
                 hipStream_t st);
 // pose / body velocity readout as float planes: out [6][N] = x, y, th, vx_body_mmps, vy_body_mmps, w
 int launch_readout(const DevState &s, float *out, hipStream_t st);
+// Status::flt_dltOutAngle_rad [N][4] from the last two raw angles (count = 4 N)
+int launch_motor_dlt(const int16_t *angle, const int16_t *prev, float *out, uint64_t count, hipStream_t st);
 
 }  // namespace fmskf

@@ -130,7 +130,8 @@ __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, 
   CtrlLane<true, CPC> L;
   L.load(c, ic);
   tv.store(stab);
-  kf6_tick1<O>(m, stab, a.prm, x, P);
+  Kf6Lo<O> lo;  // COMP never runs fused (launch_isr_kf6)
+  kf6_tick1<O>(m, stab, a.prm, x, P, lo);
   if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
   nan_guard(x, P, a.counters, live);
   if (live) {
@@ -266,7 +267,9 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
   const bool small_ctrl = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   // the tick kernel alone streams its state non-temporal past the cache: keep that regime on
   // the three-kernel path (its own occupancy caps)
-  if (!small_state || !small_ctrl || state_nt(s.n * 108)) return (int)hipErrorNotSupported;
+  // FMSKF_CFG_COMP_POS (the position low parts) runs the tick kernel that carries them, then the
+  // control step and the frame
+  if (!small_state || !small_ctrl || state_nt(s.n * 108) || kp.lo) return (int)hipErrorNotSupported;
   const KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, kp};
   const bool nt = state_nt(ctrl_state_bytes(c) + s.n * 108);
   const bool valid = in.valid != nullptr, rec = in.rec != nullptr;

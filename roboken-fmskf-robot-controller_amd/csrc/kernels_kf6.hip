@@ -54,18 +54,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   const uint32_t ic = live ? i : (uint32_t)n - 1u;
   const uint32_t T = a.in.n_ticks;
   float x[6], P[21];
+  Kf6Lo<O> lo;
   Kf6In ma, mb;
   kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
+  kf6_load_lo<O>(a.prm.lo, ic, lo);
   if (O::UPD) ma = kf6_load_in<O>(a.in, n, 0, ic);
   stage_table<O::LIBM>(stab, a.in.sintab);
   for (uint32_t t = 0; t < T; t += 2) {
     if (O::UPD && t + 1 < T) mb = kf6_load_in<O>(a.in, n, t + 1, ic);
-    kf6_tick1<O>(ma, stab, a.prm, x, P);
+    kf6_tick1<O>(ma, stab, a.prm, x, P, lo);
     if (t + 1 >= T) break;
     if (O::UPD && t + 2 < T) ma = kf6_load_in<O>(a.in, n, t + 2, ic);
-    kf6_tick1<O>(mb, stab, a.prm, x, P);
+    kf6_tick1<O>(mb, stab, a.prm, x, P, lo);
   }
-  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  if (live) {
+    kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+    kf6_store_lo<O>(a.prm.lo, i, lo);
+  }
   nan_guard(x, P, a.counters, live);
 }
 
@@ -90,11 +95,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
   float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
   WaveTable<O::LIBM> tv(a.in.sintab);
+  Kf6Lo<O> lo;
   kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
+  kf6_load_lo<O>(a.prm.lo, ic, lo);
   if (O::UPD) m = kf6_load_in<O>(a.in, n, 0, ic);
   tv.store(stab);
-  kf6_tick1<O>(m, stab, a.prm, x, P);
-  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  kf6_tick1<O>(m, stab, a.prm, x, P, lo);
+  if (live) {
+    kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+    kf6_store_lo<O>(a.prm.lo, i, lo);
+  }
   nan_guard(x, P, a.counters, live);
   if constexpr (O::ENS) {
     float xs[1][6];
@@ -134,10 +144,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE, 8))
   for (int r = 0; r < R; r++) {
     const uint32_t i = i0 + r * G;
     const bool live = i < nn;
+    Kf6Lo<O> lo;
     kf6_load_state<O>(a.x, a.P, a.pitch, live ? i : last, x, P);
+    kf6_load_lo<O>(a.prm.lo, live ? i : last, lo);
     if (r == 0) tv.store(stab);
-    kf6_tick1<O>(m[r], stab, a.prm, x, P);
-    if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+    kf6_tick1<O>(m[r], stab, a.prm, x, P, lo);
+    if (live) {
+      kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+      kf6_store_lo<O>(a.prm.lo, i, lo);
+    }
     nan_guard(x, P, a.counters, live);
     if constexpr (O::ENS) {
 #pragma unroll
@@ -166,7 +181,8 @@ static int kf6_variant() {
 
 template <class O>
 static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
-  const int v = a.in.n_ticks == 1 ? kf6_variant() : 0;
+  // COMP (the position low parts) runs one robot per lane (k_kf6t) at every size
+  const int v = a.in.n_ticks == 1 ? (O::COMP ? 15 : kf6_variant()) : 0;
   if (a.in.n_ticks == 1 && v == 12) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     if constexpr (O::UPD && O::PRED) {
@@ -223,7 +239,7 @@ template <class O>
 static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   using E = WithEns<O>;
   const unsigned carry = a.in.fold_blocks ? (unsigned)EnsRec<6>::LEN : 0u;
-  if (a.n * 124 <= (256ull << 20)) {
+  if (a.n * 124 <= (256ull << 20) && !O::COMP) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     a.in.ens_grid = g;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
@@ -254,8 +270,8 @@ static void launch_sel(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st, int *e
 }
 
 template <bool LIBM, bool UPD, bool PRED, bool REC>
-static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,
-                        int *nb) {
+static void launch_lupr_plain(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,
+                              int *nb) {
   if (small) {
     if (valid) launch_sel<Opt<LIBM, UPD, PRED, true, true, REC>>(a, st, nb);
     else launch_sel<Opt<LIBM, UPD, PRED, true, false, REC>>(a, st, nb);
@@ -263,6 +279,21 @@ static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool vali
     if (valid) launch_sel<Opt<LIBM, UPD, PRED, false, true, REC>>(a, st, nb);
     else launch_sel<Opt<LIBM, UPD, PRED, false, false, REC>>(a, st, nb);
   }
+}
+template <bool LIBM, bool UPD, bool PRED, bool REC>
+static void launch_lupr(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,
+                        int *nb) {
+  if (a.prm.lo) {  // FMSKF_CFG_COMP_POS
+    if (small) {
+      if (valid) launch_sel<Opt<LIBM, UPD, PRED, true, true, REC, false, false, true>>(a, st, nb);
+      else launch_sel<Opt<LIBM, UPD, PRED, true, false, REC, false, false, true>>(a, st, nb);
+    } else {
+      if (valid) launch_sel<Opt<LIBM, UPD, PRED, false, true, REC, false, false, true>>(a, st, nb);
+      else launch_sel<Opt<LIBM, UPD, PRED, false, false, REC, false, false, true>>(a, st, nb);
+    }
+    return;
+  }
+  launch_lupr_plain<LIBM, UPD, PRED, REC>(a, small, valid, st, nb);
 }
 template <bool LIBM, bool UPD, bool PRED>
 static void launch_lup(const KfArgs<MdKF6, Kf6Params> &a, bool small, bool valid, hipStream_t st,

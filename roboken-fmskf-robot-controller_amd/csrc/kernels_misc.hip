@@ -248,6 +248,22 @@ int launch_fill64(void *p, uint64_t bits, uint64_t count, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// Status::flt_dltOutAngle_rad of the last frame of every wheel (VD_motor_if_m2006.cpp:64), formed
+// at readout from the last two raw angles: the CAN tick keeps the previous angle instead of the
+// float, so its bytes stay the decoded ones.  [N][4] int16 in, [N][4] float out.
+__global__ __launch_bounds__(kBlock) void k_motor_dlt(const int16_t *angle, const int16_t *prev, float *out,
+                                                      uint64_t count) {
+  for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < count; g += (uint64_t)gridDim.x * kBlock)
+    out[g] = (float)((int32_t)angle[g] - (int32_t)prev[g]) * K::out_rad_per_raw * K::gear_ratio_inv;
+}
+
+int launch_motor_dlt(const int16_t *angle, const int16_t *prev, float *out, uint64_t count, hipStream_t st) {
+  if (count == 0) return 0;
+  const uint64_t b = (count + kBlock - 1) / kBlock;
+  k_motor_dlt<<<dim3((unsigned)(b < (1u << 22) ? b : (1u << 22))), kBlock, 0, st>>>(angle, prev, out, count);
+  return (int)hipGetLastError();
+}
+
 // Readout in the units of VEHICLE_CTRL::get_vehicle_pos_m_latest (m, m, rad) and
 // get_vehicle_vel_mmps_latest (body frame mm/s, mm/s, rad/s).  The KF6 / KF12D state
 // carries world-frame velocity in m/s: rotate by -theta (libm sin/cos, readout only).

@@ -80,7 +80,10 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 #ifndef FMSKF_IN_CPOL
 #define FMSKF_IN_CPOL 2
 #endif
-template <bool LIBM, int CP = 0>
+// SO (round 4): one span descriptor per array and robot slot (rsrc_span) with the planes of
+// x, prev and the encoder sums reached through soffset, instead of one clamped descriptor per
+// plane (16 -> 5 per slot; the launcher checks the 4 GiB span).
+template <bool LIBM, int CP = 0, bool SO = false>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -102,13 +105,22 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     // the wave's first lane fixes its 256-robot chunk; clamped lanes (n - 1) stay inside it
     hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
     li[r] = (uint32_t)(i - hb[r]);
-    yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
-    const uint64_t rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm),
-                                                          hb[r], n, li[r]);
-    rw[r] = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
+    uint64_t rv;
+    if constexpr (SO) {
+      yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
+      rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
+      const auto rs = rsrc_span(a.in.angle_sum + hb[r]);
 #pragma unroll
-    for (int w = 0; w < 4; w++)
-      sum[r][w] = ld_chunk<int64_t, FMSKF_IN_CPOL>(a.in.angle_sum + w * a.in.sum_pitch, hb[r], n, li[r]);
+      for (int w = 0; w < 4; w++)
+        sum[r][w] = ld_span<int64_t, FMSKF_IN_CPOL>(rs, li[r], w * (uint32_t)(a.in.sum_pitch * 8));
+    } else {
+      yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
+      rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm), hb[r], n, li[r]);
+#pragma unroll
+      for (int w = 0; w < 4; w++)
+        sum[r][w] = ld_chunk<int64_t, FMSKF_IN_CPOL>(a.in.angle_sum + w * a.in.sum_pitch, hb[r], n, li[r]);
+    }
+    rw[r] = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
   }
   tv.store(wtab[WT ? threadIdx.x >> 6 : 0]);
 #pragma unroll
@@ -116,18 +128,34 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     const uint64_t i = i0 + r * G;
     if (i >= n) return;
     RsLane s;
-    s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
-    s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
+    constexpr int SP = st_pol(CP);
+    const auto rx = rsrc_span(a.x + hb[r]), rp = rsrc_span(a.prev + hb[r]);
+    const uint32_t px4 = (uint32_t)(pp * 4), pp8 = (uint32_t)(pp * 8);
+    if constexpr (SO) {
+      s.px = ld_span<float, CP>(rx, li[r], 0);
+      s.py = ld_span<float, CP>(rx, li[r], px4);
 #pragma unroll
-    for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
+      for (int w = 0; w < 4; w++) s.prev[w] = ld_span<int64_t, CP>(rp, li[r], w * pp8);
+    } else {
+      s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
+      s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
+#pragma unroll
+      for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
+    }
     s.th = 0.f;
     rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], tab);
-    constexpr int SP = st_pol(CP);
     const float xs[6] = {s.px, s.py, s.th, s.vx, s.vy, s.vth};
+    if constexpr (SO) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
+      for (int k = 0; k < 6; k++) st_span<float, SP>(rx, li[r], k * px4, xs[k]);
 #pragma unroll
-    for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
+      for (int w = 0; w < 4; w++) st_span<int64_t, SP>(rp, li[r], w * pp8, s.prev[w]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
+#pragma unroll
+      for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
+    }
   }
 }
 
@@ -144,12 +172,30 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
     // past the Infinity Cache: 2 blocks per CU (64 KiB of dynamic LDS).  2^24, kbench, two
     // passes: 436.7-448.2 us uncapped, 429-430 at 48 KiB, 418.5-424.5 at 64 KiB
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_RS_LDS", state_nt(s.n * 124), 64u * 1024u);
+    // FMSKF_RS_VARIANT=0: one clamped descriptor per plane (A/B); the soffset form needs every
+    // plane array within 4 GiB of its chunk base
+    static const int var = [] {
+      const char *e = getenv("FMSKF_RS_VARIANT");
+      return e ? atoi(e) : 1;
+    }();
+    const bool so = var != 0 && 6 * s.pitch * 4 <= 0xFFFFFFFFull && 4 * s.pitch * 8 <= 0xFFFFFFFFull &&
+                    4 * in.sum_pitch * 8 <= 0xFFFFFFFFull;
     if (state_nt(s.n * 124)) {
-      if (libm) k_rs2<true, kStateNT><<<g2, kBlock, lds, st>>>(a);
-      else k_rs2<false, kStateNT><<<g2, kBlock, lds, st>>>(a);
+      if (so) {
+        if (libm) k_rs2<true, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
+        else k_rs2<false, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
+      } else {
+        if (libm) k_rs2<true, kStateNT><<<g2, kBlock, lds, st>>>(a);
+        else k_rs2<false, kStateNT><<<g2, kBlock, lds, st>>>(a);
+      }
     } else {
-      if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
-      else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
+      if (so) {
+        if (libm) k_rs2<true, 0, true><<<g2, kBlock, lds, st>>>(a);
+        else k_rs2<false, 0, true><<<g2, kBlock, lds, st>>>(a);
+      } else {
+        if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
+        else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
+      }
     }
     return (int)hipGetLastError();
   }

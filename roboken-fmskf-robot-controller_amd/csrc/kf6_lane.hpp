@@ -14,17 +14,30 @@ namespace fmskf {
 // NT: the state is loaded and stored non-temporal (fmskf_internal.hpp state_nt)
 // ENS: the tick also writes its block's ensemble record of the post-tick state
 // (fmskf_tick_ensemble; ens_device.hpp), so the record costs no second pass over x
+// COMP: FMSKF_CFG_COMP_POS -- px, py, P00, P10, P11 carried as hi + lo (Kf6Params::lo, 5 tiled
+// rows), every addition to them a TwoSum (oracle orc_kf6_tick_comp)
 template <bool LIBM_, bool UPD_, bool PRED_, bool SMALL_, bool VALID_, bool REC_ = false, bool NT_ = false,
-          bool ENS_ = false>
+          bool ENS_ = false, bool COMP_ = false>
 struct Opt {
   static constexpr bool LIBM = LIBM_, UPD = UPD_, PRED = PRED_, SMALL = SMALL_, VALID = VALID_,
-                        REC = REC_, NT = NT_, ENS = ENS_;
+                        REC = REC_, NT = NT_, ENS = ENS_, COMP = COMP_;
   static constexpr int CP = NT_ ? kStateNT : 0;
 };
 template <class O>
-using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true, O::ENS>;
+using WithNT = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, true, O::ENS, O::COMP>;
 template <class O>
-using WithEns = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, true>;
+using WithEns = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, true, O::COMP>;
+template <class O>
+using WithComp = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, O::ENS, true>;
+
+// the compensated entries of COMP: x 0-1 (px, py), packed P 0-2 (P00, P10, P11)
+constexpr unsigned kKf6CXM = 3u;
+constexpr unsigned long long kKf6CPM = 7ull;
+// the lane's low parts (COMP), one register when unused
+template <class O>
+struct Kf6Lo {
+  float v[O::COMP ? kKf6LoRows : 1];
+};
 
 struct Kf6In {
   float yaw, gz;
@@ -140,6 +153,30 @@ __device__ __forceinline__ void kf6_store_state(float *xg, float *Pg, uint64_t p
   }
 }
 
+// the COMP low-part rows, tiled like x ([N/W][5][W], one scalar descriptor per tile)
+template <class O>
+__device__ __forceinline__ void kf6_load_lo(const float *lg, uint32_t i, Kf6Lo<O> &l) {
+  if constexpr (O::COMP) {
+    constexpr uint32_t W = tile_w<float>();
+    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane(i / W);
+    const uint32_t c = (i - tl * W) * 4u;
+    const auto r = rsrc(lg + (uint64_t)tl * (kKf6LoRows * W), kKf6LoRows * W * 4);
+#pragma unroll
+    for (int k = 0; k < (int)kKf6LoRows; k++) l.v[k] = ld_f32<O::CP>(r, c, k * W * 4);
+  }
+}
+template <class O>
+__device__ __forceinline__ void kf6_store_lo(float *lg, uint32_t i, const Kf6Lo<O> &l) {
+  if constexpr (O::COMP) {
+    constexpr uint32_t W = tile_w<float>();
+    const uint32_t tl = (uint32_t)__builtin_amdgcn_readfirstlane(i / W);
+    const uint32_t c = (i - tl * W) * 4u;
+    const auto r = rsrc(lg + (uint64_t)tl * (kKf6LoRows * W), kKf6LoRows * W * 4);
+#pragma unroll
+    for (int k = 0; k < (int)kKf6LoRows; k++) st_f32<st_pol(O::CP)>(r, c, k * W * 4, l.v[k]);
+  }
+}
+
 // z = (deg2rad(yaw), -deg2rad(gz), wheel velocity rotated by the measured heading)
 // (imu_task_main.cpp:102-104, util_mymath.hpp:16, imu_if_wt901c.cpp:113,
 //  VD_vehicle_controller.cpp:21-33,47-51); y = z - H x with the heading innovation wrapped
@@ -165,18 +202,28 @@ __device__ __forceinline__ void kf6_innov(const Kf6In &m, const float *tab, cons
 
 template <class O>
 __device__ __forceinline__ void kf6_tick1(const Kf6In &m, const float *tab, const Kf6Params &prm,
-                                          float (&x)[6], float (&P)[21]) {
+                                          float (&x)[6], float (&P)[21], Kf6Lo<O> &l) {
   if (O::UPD && (!O::VALID || m.valid)) {
     float y[4];
     kf6_innov<O::LIBM>(m, tab, x, y);
-    kf_update<MdKF6>(x, P, y, prm.r);
+    if constexpr (O::COMP) kf_update<MdKF6, -1, float, 6, 4, 21, kKf6CXM, kKf6CPM>(x, P, y, prm.r, l.v);
+    else kf_update<MdKF6>(x, P, y, prm.r);
   }
   if (O::PRED) {
     const float dt = prm.dt;
-    x[0] = dfma(dt, x[3], x[0]);
-    x[1] = dfma(dt, x[4], x[1]);
-    x[2] = wrap_pi(dfma(dt, x[5], x[2]));
-    kf_predict_cov<MdKF6>(P, [&](int, int) { return dt; }, prm.q);
+    if constexpr (O::COMP) {
+      th_add(x[0], l.v[0], dt * x[3]);
+      th_add(x[1], l.v[1], dt * x[4]);
+      th_norm(x[0], l.v[0]);
+      th_norm(x[1], l.v[1]);
+      x[2] = wrap_pi(dfma(dt, x[5], x[2]));
+      kf_predict_cov_c<MdKF6, kKf6CXM, kKf6CPM>(P, [&](int, int) { return dt; }, prm.q, l.v);
+    } else {
+      x[0] = dfma(dt, x[3], x[0]);
+      x[1] = dfma(dt, x[4], x[1]);
+      x[2] = wrap_pi(dfma(dt, x[5], x[2]));
+      kf_predict_cov<MdKF6>(P, [&](int, int) { return dt; }, prm.q);
+    }
   }
 }
 

@@ -102,6 +102,37 @@ __device__ __forceinline__ void st_chunk(T *plane, uint64_t hb, uint64_t n, uint
   }
 }
 
+// One descriptor for a whole plane array at a wave-uniform chunk base: the record count is the
+// 4 GiB maximum (lanes are clamped, so no access needs the range check), so building it costs
+// no clamp of a 64-bit byte count, and every plane of the array is reached through the scalar
+// soffset (plane k at k * pitch * sizeof(T) bytes: the caller checks that this stays below
+// 4 GiB).  One such descriptor per array replaces one per plane (ld_chunk / st_chunk).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_span(const void *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, -1, 0x00020000);
+}
+template <typename T, int POL>
+__device__ __forceinline__ T ld_span(__amdgpu_buffer_rsrc_t r, uint32_t li, uint32_t soff) {
+  if constexpr (sizeof(T) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, li * 8u, soff, POL);
+    const uint32_t lo = v[0], hi = v[1];  // element copies (see kf6_load_in)
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, li * 4u, soff, POL));
+  }
+}
+template <typename T, int POL>
+__device__ __forceinline__ void st_span(__amdgpu_buffer_rsrc_t r, uint32_t li, uint32_t soff, T v) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    v2u32_t w;
+    w[0] = (uint32_t)u;
+    w[1] = (uint32_t)(u >> 32);
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, li * 8u, soff, POL);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, li * 4u, soff, POL);
+  }
+}
+
 // One tiled state array (ROWS rows, W = tile_w<T>() wide; fmskf_internal.hpp st_at) as one
 // chunk of kBlock instances sees it (by default the calling block's own chunk): the chunk's
 // base is wave-uniform (a scalar descriptor), rows sit W elements apart (a scalar offset per
@@ -177,12 +208,23 @@ __device__ __forceinline__ void th_norm(T &hi, T &lo) {
   hi = s;
 }
 
+// Compensated entries by mask (KF6 with FMSKF_CFG_COMP_POS: CXM = x 0-1, CPM = packed P 0-2):
+// lo[] holds the low parts of the states in CXM (ascending), then of the packed P entries in CPM
+// (ascending); oracle orc_slot_x / orc_slot_p
+__host__ __device__ constexpr int popc_c(unsigned long long v) { return v ? (int)(v & 1ull) + popc_c(v >> 1) : 0; }
+template <unsigned CXM>
+__host__ __device__ constexpr int slot_x(int j) { return popc_c(CXM & ((1ull << j) - 1ull)); }
+template <unsigned CXM, unsigned long long CPM>
+__host__ __device__ constexpr int slot_p(int k) { return popc_c(CXM) + popc_c(CPM & ((1ull << k) - 1ull)); }
+
 // ---------------------------------------------------------------------------
 // generic update / covariance predict (fully unrolled -> registers only)
 // CI >= 0: state CI is compensated (x[CI] + *lo, th_add instead of the plain addition)
+// CXM / CPM: the compensated states / packed P entries (slot_x, slot_p in lo), each added to by
+// TwoSum and renormalised after the update (x slots first); oracle orc_kf_update_m
 // ---------------------------------------------------------------------------
 template <class Md, int CI = -1, typename T = typename Md::T, int N = Md::N, int M = Md::M,
-          int NP = Md::N *(Md::N + 1) / 2>
+          int NP = Md::N *(Md::N + 1) / 2, unsigned CXM = 0, unsigned long long CPM = 0>
 __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M], const T *R,
                                           T *lo = nullptr) {
   T HP[M][N];
@@ -245,6 +287,7 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
 #pragma unroll
     for (int a = 1; a < M; a++) t = dfma<T>(HP[a][j], vw[a], t);
     if (j == CI) th_add(x[j], *lo, t);
+    else if ((CXM >> j) & 1u) th_add(x[j], lo[slot_x<CXM>(j)], t);
     else x[j] = x[j] + t;
   }
 #pragma unroll
@@ -254,9 +297,16 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
       T t = HP[0][i] * V[0][j];
 #pragma unroll
       for (int a = 1; a < M; a++) t = dfma<T>(HP[a][i], V[a][j], t);
-      P[pk(i, j)] = P[pk(i, j)] - t;
+      if ((CPM >> pk(i, j)) & 1ull) th_add(P[pk(i, j)], lo[slot_p<CXM, CPM>(pk(i, j))], -t);
+      else P[pk(i, j)] = P[pk(i, j)] - t;
     }
   }
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if ((CXM >> j) & 1u) th_norm(x[j], lo[slot_x<CXM>(j)]);
+#pragma unroll
+  for (int k = 0; k < NP; k++)
+    if ((CPM >> k) & 1ull) th_norm(P[k], lo[slot_p<CXM, CPM>(k)]);
 }
 
 // Diagonal R: the measurements are independent, so the joint update equals M scalar updates
@@ -331,6 +381,61 @@ __device__ __forceinline__ void kf_predict_cov(T (&P)[NP], const FV &fv, const T
         if (Md::pat(j, k)) t = dfma<T>(fv(j, k), Tm[i][k], t);
       if (!SKIPQ || Q[pk(i, j)] != T(0)) t = t + Q[pk(i, j)];
       P[pk(i, j)] = t;
+    }
+  }
+}
+
+// kf_predict_cov with the packed entries in CPM compensated (lo slots after the CXM states):
+// such an entry starts from its old hi / lo pair and takes, by TwoSum, the rounded products
+// fv(i,k) P[k][j] (pat(i,k), ascending k), then fv(j,k) T[i][k] (pat(j,k), ascending k), then
+// Q, then th_norm; every other entry as kf_predict_cov.  Oracle orc_kf_predict_cov_c.
+template <class Md, unsigned CXM, unsigned long long CPM, class FV, typename T = typename Md::T,
+          int N = Md::N, int NP = Md::N *(Md::N + 1) / 2>
+__device__ __forceinline__ void kf_predict_cov_c(T (&P)[NP], const FV &fv, const T *Q, T *lo) {
+  T Tm[N][N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      T t = P[pk(i, j)];
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(i, k)) t = dfma<T>(fv(i, k), P[pk(k, j)], t);
+      Tm[i][j] = t;
+    }
+  }
+  T hi[NP];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      if (!((CPM >> pk(i, j)) & 1ull)) continue;
+      T h = P[pk(i, j)];
+      T &l = lo[slot_p<CXM, CPM>(pk(i, j))];
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(i, k)) th_add(h, l, fv(i, k) * P[pk(k, j)]);
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(j, k)) th_add(h, l, fv(j, k) * Tm[i][k]);
+      th_add(h, l, Q[pk(i, j)]);
+      th_norm(h, l);
+      hi[pk(i, j)] = h;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      if ((CPM >> pk(i, j)) & 1ull) {
+        P[pk(i, j)] = hi[pk(i, j)];
+        continue;
+      }
+      T t = Tm[i][j];
+#pragma unroll
+      for (int k = 0; k < N; k++)
+        if (Md::pat(j, k)) t = dfma<T>(fv(j, k), Tm[i][k], t);
+      P[pk(i, j)] = t + Q[pk(i, j)];
     }
   }
 }

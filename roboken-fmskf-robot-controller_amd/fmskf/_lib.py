@@ -26,7 +26,8 @@ OK, EINVAL, ENOMEM, EDEVICE, ERCCL, ENOTSUP = range(6)
 MODEL_RS, MODEL_KF6, MODEL_EKF9, MODEL_KF12D = range(4)
 TRIG_TABLE512, TRIG_LIBM = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
+CFG_COMP_POS = 1
 
 MODEL_NAMES = {"rs": MODEL_RS, "kf6": MODEL_KF6, "ekf9": MODEL_EKF9, "kf12d": MODEL_KF12D}
 
@@ -50,6 +51,8 @@ class Config(C.Structure):
         ("p0", C.c_double * 78),
         ("motor_dir", C.c_int8 * 4),
         ("imu_read_reg", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -112,6 +115,9 @@ SIGNATURES = {
     "fmskf_get_imu": (C.c_int, [_H, _P, _P, C.c_uint32]),
     "fmskf_get_imu_regs": (C.c_int, [_H, _P, _P, C.c_uint32]),
     "fmskf_get_motors": (C.c_int, [_H, _P, _P, _P, _P, _P, C.c_uint32]),
+    "fmskf_get_motor_status": (C.c_int, [_H, _P, _P, _P, _P, _P, _P, C.c_uint32]),
+    "fmskf_get_state_lo": (C.c_int, [_H, _P, C.POINTER(C.c_uint32), C.c_uint32]),
+    "fmskf_set_state_lo": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_get_counters": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_ensemble_record_len": (C.c_int, [_H, C.POINTER(C.c_uint32)]),
     "fmskf_ensemble_partial": (C.c_int, [_H, _P, C.c_uint32]),
@@ -122,10 +128,13 @@ SIGNATURES = {
     "fmskf_graph_launch": (C.c_int, [_H, C.c_uint32]),
     "fmskf_comm_unique_id": (C.c_int, [_P]),
     "fmskf_comm_init": (C.c_int, [_H, _P, C.c_int, C.c_int]),
+    "fmskf_comm_info": (C.c_int, [_H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "fmskf_rccl_library": (C.c_char_p, []),
     "fmskf_ensemble_stats": (C.c_int, [_H, _P, _P]),
     "fmskf_tick_ensemble_begin": (C.c_int, [_H, C.POINTER(TickInputs)]),
     "fmskf_ensemble_begin": (C.c_int, [_H]),
     "fmskf_ensemble_end": (C.c_int, [_H, _P, _P]),
+    "fmskf_ensemble_end_count": (C.c_int, [_H, _P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
     "fmskf_ctrl_params_init": (C.c_int, [C.POINTER(CtrlParams)]),
     "fmskf_set_ctrl_params": (C.c_int, [_H, C.POINTER(CtrlParams)]),
     "fmskf_set_power": (C.c_int, [_H, _P, C.c_uint32]),

@@ -93,7 +93,7 @@ class Engine:
     """Batched IMU + mecanum-odometry estimator over N robots on one GPU."""
 
     def __init__(self, model="kf6", n=1, device=0, trig=TRIG_TABLE512, dt=None, q=None, r=None,
-                 p0=None, motor_dir=None, imu_read_reg=None):
+                 p0=None, motor_dir=None, imu_read_reg=None, flags=0):
         L = load()
         self.model = MODEL_NAMES[model] if isinstance(model, str) else int(model)
         self.n = int(n)
@@ -114,6 +114,7 @@ class Engine:
                 cfg.motor_dir[k] = int(motor_dir[k])
         if imu_read_reg is not None:
             cfg.imu_read_reg = int(imu_read_reg)
+        cfg.flags = int(flags)  # FMSKF_CFG_* (CFG_COMP_POS: KF6 compensated positions)
         self.cfg = cfg
         h = C.c_void_p()
         check(L.fmskf_create(C.byref(cfg), C.byref(h)), "create")
@@ -260,6 +261,22 @@ class Engine:
         pP = a.ptr(P, self.dtype) if P is not None else None
         check(load().fmskf_set_state(self.h, px, pP, a.mem), "set_state")
 
+    def get_state_lo(self):
+        """the hidden low-part rows [rows][N] float32 (EKF9: the heading; KF6 with CFG_COMP_POS:
+        px, py, P00, P10, P11), or None when the model keeps none"""
+        rows = C.c_uint32()
+        check(load().fmskf_get_state_lo(self.h, None, C.byref(rows), MEM_HOST), "get_state_lo")
+        if rows.value == 0:
+            return None
+        lo = np.empty((rows.value, self.n), np.float32)
+        check(load().fmskf_get_state_lo(self.h, lo.ctypes.data_as(C.c_void_p), C.byref(rows), MEM_HOST),
+              "get_state_lo")
+        return lo
+
+    def set_state_lo(self, lo):
+        a = _Args()
+        check(load().fmskf_set_state_lo(self.h, a.ptr(lo, np.float32), a.mem), "set_state_lo")
+
     def save_state(self, path):
         """fmskf_save_state: checkpoint every per-robot array of the handle to `path`"""
         check(load().fmskf_save_state(self.h, str(path).encode()), "save_state")
@@ -311,6 +328,17 @@ class Engine:
               "get_motors")
         return dict(angle=ang, rpm=rpm, curr=cur, angle_sum=s, speed_radps=spd)
 
+    def get_motor_status(self):
+        """MOTOR_IF_M2006::get_status_latest of every wheel: [N][4] each of s16_microsec_id,
+        s16_rawAngle, s16_rawSpeedRpm, s16_rawCurr, flt_dltOutAngle_rad, flt_SpeedRadPS"""
+        out = dict(microsec_id=np.empty((self.n, 4), np.int16), angle=np.empty((self.n, 4), np.int16),
+                   rpm=np.empty((self.n, 4), np.int16), curr=np.empty((self.n, 4), np.int16),
+                   dlt_out_angle_rad=np.empty((self.n, 4), np.float32),
+                   speed_radps=np.empty((self.n, 4), np.float32))
+        check(load().fmskf_get_motor_status(self.h, *(a.ctypes.data_as(C.c_void_p) for a in out.values()),
+                                            MEM_HOST), "get_motor_status")
+        return out
+
     # ------------------------------------------------------------------ HIP graph
     def graph_begin(self):
         check(load().fmskf_graph_begin(self.h), "graph_begin")
@@ -326,6 +354,13 @@ class Engine:
         """fmskf_comm_init: an RCCL communicator owned by this handle (one process per GPU)"""
         b = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
         check(load().fmskf_comm_init(self.h, b, int(rank), int(world)), "comm_init")
+
+    def comm_info(self):
+        """(world, rank) of the handle's communicator as RCCL reports them (ncclCommCount,
+        ncclCommUserRank)"""
+        w, r = C.c_int(), C.c_int()
+        check(load().fmskf_comm_info(self.h, C.byref(w), C.byref(r)), "comm_info")
+        return w.value, r.value
 
     def ensemble_stats(self):
         """(mean [n], cov packed [n(n+1)/2]) over all ranks of the communicator (or this
@@ -360,6 +395,18 @@ class Engine:
         check(load().fmskf_ensemble_end(self.h, mean.ctypes.data_as(C.c_void_p),
                                         cov.ctypes.data_as(C.c_void_p)), "ensemble_end")
         return mean, cov
+
+    def ensemble_end_count(self):
+        """fmskf_ensemble_end_count: (mean, cov packed, robots the gathered records count,
+        records folded) of the oldest pending begin"""
+        nx = self.nx
+        mean = np.empty(nx, np.float64)
+        cov = np.empty(nx * (nx + 1) // 2, np.float64)
+        cnt, nrec = C.c_double(), C.c_uint32()
+        check(load().fmskf_ensemble_end_count(self.h, mean.ctypes.data_as(C.c_void_p),
+                                              cov.ctypes.data_as(C.c_void_p), C.byref(cnt), C.byref(nrec)),
+              "ensemble_end_count")
+        return mean, cov, cnt.value, nrec.value
 
     # ------------------------------------------------------------------ control step
     def set_ctrl_params(self, **kw):
@@ -520,6 +567,12 @@ def shard_span(n_total: int, world: int, rank: int) -> tuple[int, int]:
     base, rem = divmod(n_total, world)
     lo = rank * base + min(rank, rem)
     return lo, lo + base + (1 if rank < rem else 0)
+
+
+def rccl_library() -> str:
+    """the file libfmskf resolved RCCL from ("" before its first communicator call)"""
+    v = load().fmskf_rccl_library()
+    return v.decode() if v else ""
 
 
 def comm_unique_id() -> bytes:

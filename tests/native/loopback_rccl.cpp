@@ -1,6 +1,8 @@
-// loopback_rccl.cpp -- test infrastructure: the five RCCL entry points libfmskf resolves
-// (ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclAllGather, ncclGetErrorString),
-// implemented by staging every rank's buffer through a shared directory.
+// loopback_rccl.cpp -- test infrastructure: the seven RCCL entry points libfmskf resolves
+// (ncclGetUniqueId, ncclCommInitRank, ncclCommDestroy, ncclAllGather, ncclCommCount,
+// ncclCommUserRank, ncclGetErrorString), implemented by staging every rank's buffer through a
+// shared directory.  It exports `fmskf_rccl_stand_in`, the marker libfmskf requires of any
+// library FMSKF_RCCL_LIBRARY names.
 //
 // RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so a one-GPU box cannot run
 // libfmskf's communicator at world > 1.  Loaded through FMSKF_RCCL_LIBRARY, this library
@@ -9,6 +11,11 @@
 // `world` records.  It is no collective: ncclAllGather synchronises the stream it is given,
 // copies the send buffer to the host, publishes it as <dir>/<seq>.<rank>, waits for every
 // rank's file of the same call and copies the concatenation into the receive buffer.
+// LOOPBACK_RCCL_MODE=callback instead enqueues the exchange on the stream: a copy of the send
+// buffer into pinned memory, a host function (hipLaunchHostFunc) that publishes it and waits for
+// the other ranks' files, and a copy of the concatenation into the receive buffer -- so the call
+// returns at once and libfmskf's side-stream ordering (gather behind the fold, copy-out behind
+// the gather, the slot's event behind the copy-out) is exercised without the host blocking.
 // Never part of the product; built by the package Makefile into build/.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -29,10 +36,23 @@ typedef struct {
 } ncclUniqueId;
 typedef int ncclDataType_t;
 
+int fmskf_rccl_stand_in(void) { return 1; }
+
 struct LoopComm {
   std::string dir;
   int rank, world;
   unsigned long seq;
+  std::vector<struct Exchange *> pending;  // callback mode: freed at ncclCommDestroy
+};
+
+// one enqueued exchange (callback mode): the pinned [world][bytes] buffer and what the host
+// function needs to fill it
+struct Exchange {
+  LoopComm *comm;
+  unsigned long seq;
+  size_t bytes;
+  char *host;  // pinned
+  int status;
 };
 typedef LoopComm *ncclComm_t;
 
@@ -65,13 +85,66 @@ ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int
   memcpy(dir, id.internal, 128);
   dir[128] = '\0';
   if (access(dir, W_OK) != 0) return 2;
-  *comm = new LoopComm{dir, rank, nranks, 0};
+  *comm = new LoopComm{dir, rank, nranks, 0, {}};
   return 0;
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (!comm) return 4;
+  for (Exchange *x : comm->pending) {
+    (void)hipHostFree(x->host);
+    delete x;
+  }
   delete comm;
   return 0;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int *count) {
+  if (!comm || !count) return 4;
+  *count = comm->world;
+  return 0;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int *rank) {
+  if (!comm || !rank) return 4;
+  *rank = comm->rank;
+  return 0;
+}
+
+static std::string slot_name(const LoopComm *c, unsigned long seq, int r) {
+  return c->dir + "/" + std::to_string(seq) + "." + std::to_string(r);
+}
+
+// publish this rank's part of host[] as <dir>/<seq>.<rank>, then read every other rank's part
+static int exchange(const LoopComm *c, unsigned long seq, char *host, size_t bytes) {
+  const std::string mine = slot_name(c, seq, c->rank), tmp = mine + ".tmp";
+  FILE *f = fopen(tmp.c_str(), "wb");
+  if (!f) return 2;
+  const bool wrote = fwrite(host + bytes * c->rank, 1, bytes, f) == bytes;
+  if (fclose(f) != 0 || !wrote || rename(tmp.c_str(), mine.c_str()) != 0) return 2;
+  const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+  for (int r = 0; r < c->world; r++) {
+    if (r == c->rank) continue;
+    FILE *g = nullptr;
+    while (!(g = fopen(slot_name(c, seq, r).c_str(), "rb"))) {
+      if (std::chrono::steady_clock::now() > until) {
+        fprintf(stderr, "loopback_rccl: rank %d timed out waiting for %s\n", c->rank, slot_name(c, seq, r).c_str());
+        return 2;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    const bool ok = fread(host + bytes * r, 1, bytes, g) == bytes;
+    fclose(g);
+    if (!ok) return 2;
+  }
+  return 0;
+}
+
+// the host function of callback mode: runs in stream order, calls no HIP API
+static void exchange_cb(void *arg) {
+  Exchange *x = (Exchange *)arg;
+  x->status = exchange(x->comm, x->seq, x->host, x->bytes);
+  if (x->status) fprintf(stderr, "loopback_rccl: callback exchange %lu failed\n", x->seq);
 }
 
 ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataType_t type, ncclComm_t comm,
@@ -80,30 +153,24 @@ ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataT
   if (!comm || !tb) return 4;
   const size_t bytes = count * tb;
   const unsigned long seq = comm->seq++;
+  const char *mode = getenv("LOOPBACK_RCCL_MODE");
+  if (mode && strcmp(mode, "callback") == 0) {
+    Exchange *x = new Exchange{comm, seq, bytes, nullptr, 0};
+    if (hipHostMalloc((void **)&x->host, bytes * comm->world, hipHostMallocDefault) != hipSuccess) {
+      delete x;
+      return 2;
+    }
+    comm->pending.push_back(x);
+    if (hipMemcpyAsync(x->host + bytes * comm->rank, send, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipLaunchHostFunc(stream, exchange_cb, x) != hipSuccess ||
+        hipMemcpyAsync(recv, x->host, bytes * comm->world, hipMemcpyHostToDevice, stream) != hipSuccess)
+      return 2;
+    return 0;
+  }
   std::vector<char> host(bytes * comm->world);
   if (hipStreamSynchronize(stream) != hipSuccess) return 2;
   if (hipMemcpy(host.data() + bytes * comm->rank, send, bytes, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-  auto name = [&](int r) { return comm->dir + "/" + std::to_string(seq) + "." + std::to_string(r); };
-  const std::string mine = name(comm->rank), tmp = mine + ".tmp";
-  FILE *f = fopen(tmp.c_str(), "wb");
-  if (!f) return 2;
-  const bool wrote = fwrite(host.data() + bytes * comm->rank, 1, bytes, f) == bytes;
-  if (fclose(f) != 0 || !wrote || rename(tmp.c_str(), mine.c_str()) != 0) return 2;
-  const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(60);
-  for (int r = 0; r < comm->world; r++) {
-    if (r == comm->rank) continue;
-    FILE *g = nullptr;
-    while (!(g = fopen(name(r).c_str(), "rb"))) {
-      if (std::chrono::steady_clock::now() > until) {
-        fprintf(stderr, "loopback_rccl: rank %d timed out waiting for %s\n", comm->rank, name(r).c_str());
-        return 2;
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
-    const bool ok = fread(host.data() + bytes * r, 1, bytes, g) == bytes;
-    fclose(g);
-    if (!ok) return 2;
-  }
+  if (exchange(comm, seq, host.data(), bytes) != 0) return 2;
   if (hipMemcpyAsync(recv, host.data(), host.size(), hipMemcpyHostToDevice, stream) != hipSuccess) return 2;
   if (hipStreamSynchronize(stream) != hipSuccess) return 2;
   return 0;

@@ -43,6 +43,8 @@ def main():
     local, got = [], []
     with Engine(model, n) as a, Engine(model, n) as b:
         b.comm_init(uid, rank, world)
+        info = b.comm_info()  # (world, rank) as the communicator itself reports them
+        counts = []
         pending = 0
         for t in range(T):
             if (t + 1) % every == 0:
@@ -50,13 +52,17 @@ def main():
                 b.tick_ensemble_begin(**kw(t))
                 pending += 1
                 if pending == 3:
-                    got.append(b.ensemble_end())
+                    m_, c_, cnt, nrec = b.ensemble_end_count()
+                    got.append((m_, c_))
+                    counts.append((cnt, nrec))
                     pending -= 1
             else:
                 a.tick(**kw(t))
                 b.tick(**kw(t))
         while pending:
-            got.append(b.ensemble_end())
+            m_, c_, cnt, nrec = b.ensemble_end_count()
+            got.append((m_, c_))
+            counts.append((cnt, nrec))
             pending -= 1
         ms, cs = b.ensemble_stats()              # synchronous: partial, ncclAllGather, fold
         b.ensemble_begin()                       # asynchronous stand-alone record
@@ -66,7 +72,8 @@ def main():
         xb, _ = b.get_state()
     np.savez(out, local=np.stack(local), got_mean=np.stack([g[0] for g in got]),
              got_cov=np.stack([g[1] for g in got]), sync_mean=ms, sync_cov=cs, alone_mean=ma,
-             alone_cov=ca, final=final, same_state=np.array(np.array_equal(xa.view(np.uint8), xb.view(np.uint8))))
+             alone_cov=ca, final=final, comm_info=np.array(info), counts=np.array(counts),
+             rccl_library=np.array(fmskf.rccl_library()), same_state=np.array(np.array_equal(xa.view(np.uint8), xb.view(np.uint8))))
 
 
 if __name__ == "__main__":

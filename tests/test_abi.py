@@ -176,3 +176,33 @@ def test_loopback_exports_the_rccl_entry_points():
     names = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert {"ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclAllGather",
             "ncclGetErrorString"} <= names
+
+
+def test_rccl_override_needs_the_stand_in_marker():
+    """FMSKF_RCCL_LIBRARY is honoured only for a library exporting `fmskf_rccl_stand_in` (the
+    tests' loopback): any other file is refused with FMSKF_ERCCL, so the environment cannot swap
+    a deployed controller's collective; the loopback is accepted and reported by
+    fmskf_rccl_library.  No GPU: fmskf_comm_unique_id resolves the entry points first."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    loop = os.path.join(root, "build", "libloopback_rccl.so")
+    script = (
+        "import sys\n"
+        "sys.path.insert(0, sys.argv[1])\n"
+        "import fmskf\n"
+        "try:\n"
+        "    fmskf.comm_unique_id()\n"
+        "    print('ok', fmskf.rccl_library())\n"
+        "except fmskf.FmskfError as e:\n"
+        "    print('refused', e.code, e)\n")
+    pkg = os.path.join(root, "roboken-fmskf-robot-controller_amd")
+    libm = next(p for p in ("/lib/x86_64-linux-gnu/libm.so.6", "/usr/lib64/libm.so.6") if os.path.exists(p))
+    out = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, FMSKF_RCCL_LIBRARY=libm, LOOPBACK_RCCL_DIR="/tmp"))
+    assert out.stdout.startswith("refused 4"), out.stdout + out.stderr
+    assert "fmskf_rccl_stand_in" in out.stdout
+    if os.path.exists(loop):
+        out = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=120,
+                             env=dict(os.environ, FMSKF_RCCL_LIBRARY=loop, LOOPBACK_RCCL_DIR="/tmp"))
+        assert out.stdout.strip() == "ok " + loop, out.stdout + out.stderr

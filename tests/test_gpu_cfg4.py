@@ -127,8 +127,8 @@ def test_bench_world2_rehearsal_same_gpu(strong, gather, tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
            "--steps", "32", "--warmup", "4", "--ensemble-every", "8", *size,
            "--no-cpu-baseline", "--no-fused", "--no-secondary", "--backend", "gloo", "--same-device",
-           "--check-ensemble", "--gather", gather]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+           "--check-ensemble", "--gather", gather, "--cfg4-steps", "32"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["n_gpus"] == 2 and out["config"]["global_instances"] == total
@@ -137,6 +137,18 @@ def test_bench_world2_rehearsal_same_gpu(strong, gather, tmp_path):
     assert chk["count"] == total
     assert chk["mean_max_rel"] < 1e-12, chk
     assert chk["cov_max_rel"] < 1e-9, chk
-    assert out["ensemble"]["count"] == total
+    assert out["ensemble"]["count"] == total  # the gathered records' own count rows
     assert out["nonfinite_instances"] == 0
     assert out["config"]["gather"] == gather
+    if gather == "native":
+        # what the communicator itself reports, from every rank (ncclCommCount / UserRank)
+        assert out["rccl_ranks"] == 2 and out["rccl"]["user_ranks"] == [0, 1], out["rccl"]
+        assert out["rccl"]["library"].endswith("libloopback_rccl.so")
+        assert out["ensemble"]["records_folded"] == 2
+    # BASELINE configs[3] in the same invocation: 2^24 robots over the two ranks
+    c4 = out["cfg4_16M"]
+    assert c4["instances_total"] == 1 << 24 and c4["n_gpus"] == 2
+    assert c4["gathered_count"] == 1 << 24 and c4["records_folded"] == 2, c4
+    assert c4["ensemble_every_16"]["steps_per_s"] > 0 and c4["ensemble_every_1"]["steps_per_s"] > 0
+    if gather == "native":
+        assert c4["rccl_ranks"] == 2

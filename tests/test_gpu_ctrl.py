@@ -187,8 +187,13 @@ def test_fleet_loop_cpp_host_program():
     # 12 records, the fleet mean of x between the slowest and fastest robots' x
     assert lines[3].startswith("fleet (1 rank): 12 ensemble records"), lines[3]
     mx = float(lines[3].split("mean x=")[1].split()[0])
-    vx = float(lines[3].split("var x=")[1].split()[0])
+    vx = float(lines[3].split("var x=")[1].split()[0].rstrip(","))
     assert 0.0 < mx < 1.0 and vx > 0.0
+    assert lines[3].endswith("4096 robots in 1 records"), lines[3]  # fmskf_ensemble_end_count
+    # MOTOR_IF_M2006::get_status_latest: robot 0's FL wheel advances 1 count (1 raw angle) a tick
+    assert lines[4].startswith("robot 0 FL: microsec_id="), lines[4]
+    dlt = float(lines[4].split("dlt=")[1].split()[0])
+    assert abs(dlt - 2 * 3.1415926 / 8191 / 36) < 1e-6 * dlt, lines[4]
 
 
 def test_reset_zeroes_control_state():
@@ -351,7 +356,8 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
 
     def readout(e):
         x, P = e.get_state()
-        out = dict(x=x, ctrl=e.get_ctrl(), motors=e.get_motors(), imu=e.get_imu())
+        motors = dict(e.get_motors(), **{"status_" + k: v for k, v in e.get_motor_status().items()})
+        out = dict(x=x, ctrl=e.get_ctrl(), motors=motors, imu=e.get_imu())
         if P is not None:
             out["P"] = P
         return out
@@ -393,10 +399,12 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
     flipped = blob[:mid] + bytes([blob[mid] ^ 0x40]) + blob[mid + 1:]
     v1 = b"FMSKFCK1" + blob[8:]
     v2 = b"FMSKFCK2" + blob[8:]  # format 2 kept the dlt / speed motor planes
+    v3 = b"FMSKFCK3" + blob[8:]  # format 3 had no previous motor angles (ABI 2)
     with Engine(model, n) as e:
         e.load_state(ck)
         before = readout(e)
-        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2)):
+        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2),
+                           ("v3", v3)):
             bad = tmp_path / name
             bad.write_bytes(data)
             with pytest.raises(fmskf.FmskfError):

@@ -571,12 +571,19 @@ def test_can_ingest_bitexact(orc, masked, n=1001):
                     if (present[i] >> w) & 1:
                         motors[i][w].rx(frames[i, w], int(stamps[i, w]))
         m = e.get_motors()
+        st = e.get_motor_status()
     for i in range(n):
         for w in range(4):
             s = motors[i][w].s
             assert m["angle"][i, w] == s.angle and m["rpm"][i, w] == s.rpm
             assert m["curr"][i, w] == s.curr and m["angle_sum"][w, i] == s.angle_sum
             bits_equal(m["speed_radps"][w, i:i + 1], np.float32([s.speed_radps]), "speed")
+            # MOTOR_IF_M2006::get_status_latest: the full Status (VD_motor_if_m2006.hpp:23-30),
+            # flt_dltOutAngle_rad formed at readout from the last two angles
+            assert st["microsec_id"][i, w] == s.micro and st["angle"][i, w] == s.angle
+            assert st["rpm"][i, w] == s.rpm and st["curr"][i, w] == s.curr
+            bits_equal(st["dlt_out_angle_rad"][i, w:w + 1], np.float32([s.dlt_out_angle_rad]), "dlt")
+            bits_equal(st["speed_radps"][i, w:w + 1], np.float32([s.speed_radps]), "status speed")
 
 
 def test_full_pipeline_rs_device_resident(orc):
@@ -1005,3 +1012,102 @@ def test_rs_one_robot_per_lane_bitexact():
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "rs ok" in out.stdout
+
+
+_WT901_TR_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = sys.argv[1:3]
+from fmskf import Engine
+from fmskf.synth import wt901_frame
+from oracle import oracle as orc
+rng = np.random.default_rng(4242)
+stride = 48
+
+
+def clean(m):
+    fr = np.zeros((m, 4, 11), np.uint8)
+    fr[:, :, 0] = 0x55
+    fr[:, :, 1] = np.array([0x51, 0x52, 0x53, 0x59], np.uint8)
+    fr[:, :, 2:10] = rng.integers(0, 256, (m, 4, 8), dtype=np.uint8)
+    fr[:, :, 10] = (fr[:, :, :10].sum(axis=2, dtype=np.uint32) & 0xFF).astype(np.uint8)
+    return fr.reshape(m, 44)
+
+
+# n % 8 == 0 with a partial last wave, n % 8 != 0 (per-lane stores only), one full wave
+for n in (2584, 2585, 64):
+    nw = -(-n // 64)
+    ob = orc.Wt901Batch(n)
+    with Engine("kf6", n) as e:
+        for k in range(6):
+            buf = np.zeros((n, stride), np.uint8)
+            buf[:, :44] = clean(n)
+            lens = np.full(n, 44, np.uint32)
+            for w in range(nw):
+                lo, hi = 64 * w, min(64 * w + 64, n)
+                kind = (w + k) % 5
+                if kind == 1:  # one damaged byte in one lane
+                    buf[lo + (w % (hi - lo)), 7] ^= 0x5A
+                elif kind == 2:  # a torn poll: its tail is pending in the next poll's window
+                    lens[lo + (3 * w) % (hi - lo)] = 30
+                elif kind == 3:  # a different frame order in one lane
+                    r = lo + (5 * w) % (hi - lo)
+                    buf[r, :44] = np.frombuffer(b"".join(wt901_frame(t, rng.integers(0, 65536, 4))
+                                                         for t in (0x59, 0x51, 0x52, 0x53)), np.uint8)
+                # kind 0 and 4: every lane a clean standard poll (the transposed store)
+            ob.update(buf, lens, latch_qinit=(k == 0))
+            e.ingest_wt901(buf, lens, latch_qinit=(k == 0))
+            regs, pending = e.get_imu_regs()
+            data, err = e.get_imu()
+            st = orc._struct_view(ob.s, orc.Wt901State)
+            assert np.array_equal(regs, st["reg"].T), (n, k)
+            assert np.array_equal(pending, st["cnt"].astype(np.uint8)), (n, k)
+            assert np.array_equal(err, st["is_error"]), (n, k)
+            assert np.array_equal(data.view(np.uint32), ob.data.view(np.uint32)), (n, k)
+print("wt901 ok")
+"""
+
+
+@pytest.mark.parametrize("variant", ["0", "1", "2"])
+def test_wt901_transposed_waves_bitexact(variant):
+    """k_wt901's three store forms (FMSKF_WT901_VARIANT, in a child process): per-lane stores
+    (0), the LDS-transposed stores of a wave whose every lane took the standard poll (1), and
+    those plus the LDS-staged poll rows (2, the default).  Waves of clean standard polls next to
+    waves with one damaged, torn or reordered lane, a partial last wave, N % 8 != 0 (per-lane
+    stores only) and a single wave; every robot's register file, parser backlog, error flag and
+    Data page against the oracle after every poll, bit for bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FMSKF_WT901_VARIANT=variant)
+    out = subprocess.run([sys.executable, "-c", _WT901_TR_SCRIPT, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "wt901 ok" in out.stdout
+
+
+def test_can_rs_per_plane_descriptor_forms_bitexact():
+    """The per-plane descriptor forms of k_can4 and k_rs2 (FMSKF_CAN_VARIANT=0,
+    FMSKF_RS_VARIANT=0; the default reaches every plane of an array through one descriptor and
+    soffset) in a child process: the CAN ingest and RS tick parity tests against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys\n"
+        "sys.path[:0] = sys.argv[1:4]\n"
+        "from oracle import oracle as orc\n"
+        "import test_gpu_parity as T\n"
+        "T.test_can_ingest_bitexact(orc, False)\n"
+        "T.test_rs_tick_bitexact(orc, T.TABLE)\n"
+        "T.test_rs_tick_bitexact(orc, T.LIBM)\n"
+        "print('planes ok')\n")
+    env = dict(os.environ, FMSKF_CAN_VARIANT="0", FMSKF_RS_VARIANT="0")
+    out = subprocess.run([sys.executable, "-c", script, root,
+                          os.path.join(root, "roboken-fmskf-robot-controller_amd"),
+                          os.path.join(root, "tests")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "planes ok" in out.stdout

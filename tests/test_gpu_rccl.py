@@ -24,7 +24,11 @@ def test_ensemble_stats_over_rccl_world1(orc):
         m0, c0 = e.ensemble_stats()                    # no communicator: this handle
         uid = fmskf.comm_unique_id()
         assert len(uid) == 128
+        with pytest.raises(fmskf.FmskfError):
+            e.comm_info()                              # no communicator yet
         e.comm_init(uid, 0, 1)
+        assert e.comm_info() == (1, 0)                 # ncclCommCount / ncclCommUserRank
+        assert "librccl" in fmskf.rccl_library()       # the real RCCL, not a stand-in
         m1, c1 = e.ensemble_stats()                    # through ncclAllGather
         rec = e.ensemble_partial()
         x, _ = e.get_state()

@@ -26,10 +26,10 @@ LOOPBACK = os.path.join(ROOT, "build", "libloopback_rccl.so")
 WORKER = os.path.join(ROOT, "tests", "native", "rccl_rank_worker.py")
 
 
-def run_ranks(tmp_path, model, sizes, T, every):
+def run_ranks(tmp_path, model, sizes, T, every, mode="sync"):
     assert os.path.exists(LOOPBACK), "build() makes build/libloopback_rccl.so"
     world = len(sizes)
-    env = dict(os.environ, FMSKF_RCCL_LIBRARY=LOOPBACK, LOOPBACK_RCCL_DIR=str(tmp_path))
+    env = dict(os.environ, FMSKF_RCCL_LIBRARY=LOOPBACK, LOOPBACK_RCCL_DIR=str(tmp_path), LOOPBACK_RCCL_MODE=mode)
     id_file = str(tmp_path / "uid")
     procs = [subprocess.Popen([sys.executable, WORKER, model, str(r), str(world), str(n), str(T), str(every),
                                id_file, str(tmp_path / f"rank{r}.npz")], env=env)
@@ -45,18 +45,32 @@ def run_ranks(tmp_path, model, sizes, T, every):
     return [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
 
 
-@pytest.mark.parametrize("model,sizes,every", [("kf6", [70001, 65536], 1), ("kf6", [1 << 20, 1000, 4097], 2),
-                                               ("ekf9", [5001, 30000], 1), ("kf12d", [3001, 2000], 2),
-                                               ("rs", [4097, 1023, 512], 1)])
-def test_native_communicator_world_gt_1(tmp_path, model, sizes, every):
+@pytest.mark.parametrize("model,sizes,every,mode", [("kf6", [70001, 65536], 1, "sync"),
+                                                    ("kf6", [1 << 20, 1000, 4097], 2, "sync"),
+                                                    ("kf6", [70001, 65536, 3], 1, "callback"),
+                                                    ("ekf9", [5001, 30000], 1, "sync"),
+                                                    ("ekf9", [5001, 30000], 1, "callback"),
+                                                    ("kf12d", [3001, 2000], 2, "sync"),
+                                                    ("rs", [4097, 1023, 512], 1, "sync")])
+def test_native_communicator_world_gt_1(tmp_path, model, sizes, every, mode):
+    """mode "callback": the stand-in enqueues its exchange on the side stream as a host function
+    between two asynchronous copies, so the library's ordering (gather behind the fold, the copy
+    of the gathered records and the slot's event behind the gather) is exercised with no host
+    wait inside ncclAllGather."""
     T = 7
-    outs = run_ranks(tmp_path, model, sizes, T, every)
+    outs = run_ranks(tmp_path, model, sizes, T, every, mode)
     L = outs[0]["local"].shape[1]
     nx = next(k for k in range(1, 16) if 1 + k + k * (k + 1) // 2 == L)  # record {count, mean, M2}
     events = T // every
     for r, o in enumerate(outs):
         assert bool(o["same_state"]), f"rank {r}: the communicator changed the tick"
         assert o["got_mean"].shape[0] == events
+        # the communicator's own size and rank (fmskf_comm_info: ncclCommCount / ncclCommUserRank)
+        assert tuple(o["comm_info"]) == (len(sizes), r)
+        # every gathered result counts the whole fleet, folded from `world` records
+        assert o["counts"].shape == (events, 2)
+        assert np.all(o["counts"][:, 0] == float(sum(sizes))) and np.all(o["counts"][:, 1] == len(sizes))
+        assert str(o["rccl_library"]) == LOOPBACK
     for k in range(events):
         want_m, want_c = fmskf.ensemble_combine(nx, np.stack([o["local"][k] for o in outs]))
         for r, o in enumerate(outs):
@@ -100,3 +114,4 @@ def test_fleet_loop_cpp_two_ranks(tmp_path):
     solo = one.stdout.strip().splitlines()[3]
     mean = lambda line: line.split("last mean ")[1].split(", var")[0]  # noqa: E731
     assert mean(fleet[0]) == mean(solo), (fleet[0], solo)
+    assert fleet[0].endswith("8192 robots in 2 records"), fleet[0]  # both ranks' robots, two records

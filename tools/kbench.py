@@ -13,7 +13,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")]
 
-BYTES = {"kf6": 232, "rs": 144, "ekf9": 456, "kf12d": 1504}  # EKF9: + the heading low-part row
+# SURVEY.md 8(d) algorithmic bytes (RS: theta is overwritten, never read); --comp: KF6 272
+BYTES = {"kf6": 232, "rs": 140, "ekf9": 448, "kf12d": 1504}
 
 
 def main():
@@ -30,6 +31,7 @@ def main():
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
     ap.add_argument("--valid", action="store_true", help="a validity mask per tick (9 in 10 robots valid)")
+    ap.add_argument("--comp", action="store_true", help="KF6 with FMSKF_CFG_COMP_POS (compensated positions)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -38,7 +40,10 @@ def main():
 
     dev = torch.device("cuda", 0)
     n, R = args.n, max(args.ring, args.many)  # tick_many reads `many` ticks of the ring
-    e = fmskf.Engine(args.model, n, trig=fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512)
+    e = fmskf.Engine(args.model, n, trig=fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512,
+                     flags=fmskf.CFG_COMP_POS if args.comp else 0)
+    if args.comp:
+        BYTES["kf6"] = 272
     st = torch.cuda.current_stream()
     e.set_stream(st)
     yaw, gz, rpm = kf6_ring_torch(n, R, device=dev)
@@ -325,7 +330,9 @@ def bench_io(args, e, n, R, dev, rpm, st):
             polls.append(torch.from_numpy(np.tile(row, (n, 1))).to(dev))
         lens = torch.full((n,), 44, dtype=torch.int32, device=dev)
         run = lambda k: e.ingest_wt901(polls[k % len(polls)], lens)  # noqa: E731
-        bpr = 44 + 4
+        # the standard poll (bench.py PATH_BYTES): row 48 + len 4, parser window / count / flags r+w,
+        # error, 15 registers, magnetometer + q_init read, Data page written
+        bpr = 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64
     else:  # can
         rng = np.random.default_rng(2)
         fr = [torch.from_numpy(rng.integers(0, 256, (n, 4, 8)).astype(np.uint8)).to(dev) for _ in range(4)]
@@ -333,8 +340,8 @@ def bench_io(args, e, n, R, dev, rpm, st):
                for k in range(4)]
         run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
         # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), head 1, IIR y / x (4 + 4) and
-        # the int64 sum read and written; rpm, curr (2 + 2) written
-        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2)
+        # the int64 sum read and written; rpm, curr, the previous angle (2 + 2 + 2) written
+        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2 + 2)
     for k in range(10):
         run(k)
     torch.cuda.synchronize()
