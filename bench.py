@@ -163,21 +163,24 @@ def secondary_configs(dev, stream, ticks: int, trig):
     out = {}
     # HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE, calibrated on same-width
     # patterns (tools/pmc_traffic.py secondary; profiles/pmc_traffic_secondary.json)
+    # (the 2^20 COMP line is calibrated like the path rows: profiles/pmc_traffic_paths.json)
     sec_traffic = {}
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_secondary.json")
-    if os.path.exists(tpath):
-        try:
-            sec_traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
-                           if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
-        except Exception:
-            sec_traffic = {}
+    for tname in ("pmc_traffic_secondary.json", "pmc_traffic_paths.json"):
+        tpath = os.path.join(ROOT, "profiles", tname)
+        if os.path.exists(tpath):
+            try:
+                sec_traffic.update({k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
+                                    if isinstance(v, dict) and "hbm_bytes_per_launch" in v})
+            except Exception:
+                pass
     # algorithmic bytes per robot-tick as SURVEY.md 8(d) prices them (x and P read and written +
     # the inputs): EKF9 448 (its compensated heading's hidden low-part row, 8 B more read and
-    # written, is reported beside it as `bytes_with_hidden_rows`), KF12D 1504, KF6 232; the KF6
-    # with FMSKF_CFG_COMP_POS (the position low parts: 5 rows read and written) 272
+    # written, is reported beside it as `bytes_with_hidden_rows`), KF12D 1504, KF6 232; with
+    # FMSKF_CFG_COMP_POS (the position low parts: 5 rows read and written, 40 B) KF6 272, EKF9 488
     specs = [("cfg3_ekf9_2p22", "ekf9", 1 << 22, 448, 456, 0), ("cfg5_kf12d_2p20", "kf12d", 1 << 20, 1504, None, 0),
              ("cfg2_kf6_2p24", "kf6", 1 << 24, 232, None, 0),
-             ("cfg2_kf6_comp_pos_2p20", "kf6", 1 << 20, 272, None, fmskf.CFG_COMP_POS)]
+             ("cfg2_kf6_comp_pos_2p20", "kf6", 1 << 20, 272, None, fmskf.CFG_COMP_POS),
+             ("cfg3_ekf9_comp_pos_2p22", "ekf9", 1 << 22, 488, 496, fmskf.CFG_COMP_POS)]
     R = 4
     for key, model, n, bps, bps_hidden, flags in specs:
         e = fmskf.Engine(model, n, device=dev.index, trig=trig, flags=flags)

@@ -101,12 +101,12 @@ typedef struct fmskf_config {
   uint32_t reserved;     /* must be 0 */
 } fmskf_config;
 
-/* KF6: carry the open-loop integrals -- px, py and the position block of P (P[0][0], P[1][0],
- * P[1][1]) -- as compensated fp32 pairs (hi + lo; every addition to them a TwoSum), so that
- * they track the float64 filter over long horizons (60 s at 1 kHz within 1e-5, where plain
- * fp32 drifts to 2e-5 / 6e-5).  fmskf_get_state returns hi (hi + lo rounded is hi); the lo
- * parts are readable through fmskf_get_state_lo.  +40 B per robot-tick (232 -> 272).  Off by
- * default: the plain fp32 filter is the headline. */
+/* KF6, EKF9: carry the open-loop integrals -- px, py and the position block of P (P[0][0],
+ * P[1][0], P[1][1]) -- as compensated fp32 pairs (hi + lo; every addition to them a TwoSum), so
+ * that they track the float64 filter over long horizons (60 s at 1 kHz within 1e-5, where plain
+ * fp32 drifts to 2e-5 - 6e-5).  fmskf_get_state returns hi (hi + lo rounded is hi); the lo parts
+ * are readable through fmskf_get_state_lo.  +40 B per robot-tick (KF6 232 -> 272, EKF9 456 ->
+ * 496).  Off by default: the plain fp32 filters are the headline and cfg 3. */
 #define FMSKF_CFG_COMP_POS 1u
 
 /* Fill defaults for `model` with `n` instances (dt = 1 ms, TABLE512, reference motor
@@ -206,9 +206,10 @@ int fmskf_get_vel(fmskf_handle h, float *vx, float *vy, float *vth, uint32_t mem
  * fmskf_load_state keep everything). */
 int fmskf_get_state(fmskf_handle h, void *x, void *p_packed, uint32_t mem);
 int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_t mem);
-/* The hidden low-part rows [rows][N] float: EKF9 1 row (heading); KF6 with FMSKF_CFG_COMP_POS
- * 5 rows (px, py, P[0][0], P[1][0], P[1][1]); *rows receives the count (0: the model keeps none,
- * and lo may be NULL).  set_state_lo after set_state restores a handle bit for bit. */
+/* The hidden low-part rows [rows][N] float: EKF9's heading (1 row), then with
+ * FMSKF_CFG_COMP_POS the 5 rows px, py, P[0][0], P[1][0], P[1][1] (KF6: those 5 only); *rows
+ * receives the count (0: the model keeps none, and lo may be NULL).  set_state_lo after
+ * set_state restores a handle bit for bit. */
 int fmskf_get_state_lo(fmskf_handle h, float *lo, uint32_t *rows, uint32_t mem);
 int fmskf_set_state_lo(fmskf_handle h, const float *lo, uint32_t mem);
 /* RS: the int64 s64_rawAngleSumPrev [4][N] (VD_vehicle_controller.hpp:75) */

@@ -556,7 +556,7 @@ void orc_kf6_tick_comp(size_t n, float *x, float *P, float *lo, const float *yaw
       y[1] = z[1] - xs[5];
       y[2] = z[2] - xs[3];
       y[3] = z[3] - xs[4];
-      orc_kf_update_m_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r, ls, -1, cxm, cpm);
+      orc_kf_update_m_f32(6, 4, xs, Ps, k_kf6_h1, k_kf6_h2, y, prm->r, NULL, -1, ls, cxm, cpm);
     }
     if (do_predict) {
       orc_th_add_f32(&xs[0], &ls[0], prm->dt * xs[3]);
@@ -606,6 +606,15 @@ static const int k_ekf9_h2[6] = {-1, 6, -1, -1, -1, -1};
 
 void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8_t *valid,
                    const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads) {
+  orc_ekf9_tick_comp(n, x, P, NULL, raw, valid, prm, do_update, do_predict, nthreads);
+}
+
+/* EKF9; clo [5][n] non-NULL: FMSKF_CFG_COMP_POS -- px, py and P00, P10, P11 compensated as in
+ * orc_kf6_tick_comp (the heading's own low part stays row 9 of x) */
+void orc_ekf9_tick_comp(size_t n, float *x, float *P, float *clo, const int16_t *raw, const uint8_t *valid,
+                        const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads) {
+  const unsigned cxm = clo ? 3u : 0u;
+  const unsigned long long cpm = clo ? 7ull : 0ull;
   unsigned char pat[ORC_NMAX][ORC_NMAX];
   memset(pat, 0, sizeof(pat));
   pat[0][2] = pat[0][3] = pat[0][4] = 1;
@@ -625,6 +634,9 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
     for (int k = 0; k < 9; k++) xs[k] = x[k * n + i];
     float lo = x[9 * n + i];  /* row 9: the compensated heading's low part */
     for (int k = 0; k < 45; k++) Ps[k] = P[k * n + i];
+    float ls[5] = {0, 0, 0, 0, 0};
+    if (clo)
+      for (int k = 0; k < 5; k++) ls[k] = clo[k * n + i];
     if (do_update && (!valid || valid[i])) {
       float z[6], y[6];
       orc_ekf9_meas1(raw + i * 8, z);
@@ -635,8 +647,8 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
       y[4] = z[4] - xs[3];
       y[5] = z[5] - xs[4];
       /* canonical order: sequential scalar updates for a diagonal R, else the joint LDL^T */
-      if (rdiag) orc_kf_update_seq_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2);
-      else orc_kf_update_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2);
+      if (rdiag) orc_kf_update_seq_m_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2, ls, cxm, cpm);
+      else orc_kf_update_m_f32(9, 6, xs, Ps, k_ekf9_h1, k_ekf9_h2, y, prm->r, &lo, 2, ls, cxm, cpm);
       orc_th_norm_f32(&xs[2], &lo);
     }
     if (do_predict) {
@@ -656,8 +668,15 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
       F[2][5] = dt;
       F[3][7] = dt;
       F[4][8] = dt;
-      xs[0] = xs[0] + vwx * dt;
-      xs[1] = xs[1] + vwy * dt;
+      if (clo) {
+        orc_th_add_f32(&xs[0], &ls[0], vwx * dt);
+        orc_th_add_f32(&xs[1], &ls[1], vwy * dt);
+        orc_th_norm_f32(&xs[0], &ls[0]);
+        orc_th_norm_f32(&xs[1], &ls[1]);
+      } else {
+        xs[0] = xs[0] + vwx * dt;
+        xs[1] = xs[1] + vwy * dt;
+      }
       orc_th_add_f32(&xs[2], &lo, xs[5] * dt);
       /* wrap of the compensated heading: hi -/+ fp32(2 pi) is exact, the rest of 2 pi to lo */
       if (xs[2] >= ORC_PI_F) {
@@ -670,11 +689,14 @@ void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8
       orc_th_norm_f32(&xs[2], &lo);
       xs[3] = xs[3] + xs[7] * dt;
       xs[4] = xs[4] + xs[8] * dt;
-      orc_kf_predict_cov_f32(9, Ps, F, pat, prm->q);
+      if (clo) orc_kf_predict_cov_c_f32(9, Ps, F, pat, prm->q, ls, cxm, cpm);
+      else orc_kf_predict_cov_f32(9, Ps, F, pat, prm->q);
     }
     for (int k = 0; k < 9; k++) x[k * n + i] = xs[k];
     x[9 * n + i] = lo;
     for (int k = 0; k < 45; k++) P[k * n + i] = Ps[k];
+    if (clo)
+      for (int k = 0; k < 5; k++) clo[k * n + i] = ls[k];
   }
 }
 

@@ -132,6 +132,9 @@ typedef struct {
  * int16 words (yaw, gz, ax, ay, rpm FL BL BR FR) */
 void orc_ekf9_tick(size_t n, float *x, float *P, const int16_t *raw, const uint8_t *valid,
                    const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads);
+/* EKF9 with FMSKF_CFG_COMP_POS: clo [5][n] = low parts of px, py, P00, P10, P11 (NULL: plain) */
+void orc_ekf9_tick_comp(size_t n, float *x, float *P, float *clo, const int16_t *raw, const uint8_t *valid,
+                        const orc_ekf9_params *prm, int do_update, int do_predict, int nthreads);
 void orc_ekf9_measure(size_t n, const int16_t *raw, float *z /*[6][n]*/);
 
 /* ---------------- 12-state linear KF, fp64 -------------------------------- */

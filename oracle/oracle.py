@@ -157,6 +157,8 @@ def lib():
         L.orc_kf6_measure.argtypes = [C.c_size_t, _f32p, _f32p, _i16p, _f32p, C.c_int]
         L.orc_ekf9_tick.argtypes = [C.c_size_t, _f32p, _f32p, _vp, _vp,
                                     C.POINTER(Ekf9Params), C.c_int, C.c_int, C.c_int]
+        L.orc_ekf9_tick_comp.argtypes = [C.c_size_t, _f32p, _f32p, _f32p, _vp, _vp,
+                                         C.POINTER(Ekf9Params), C.c_int, C.c_int, C.c_int]
         L.orc_ekf9_measure.argtypes = [C.c_size_t, _i16p, _f32p]
         L.orc_kf12d_tick.argtypes = [C.c_size_t, _f64p, _f64p, _vp, _vp,
                                      C.POINTER(Kf12dParams), C.c_int, C.c_int, C.c_int]
@@ -417,6 +419,15 @@ def ekf9_tick(x, P, raw, valid, prm, do_update=True, do_predict=True, nthreads=1
     n = x.shape[1]
     lib().orc_ekf9_tick(n, x, P, _ptr(raw), _ptr(valid), C.byref(prm), int(do_update),
                         int(do_predict), nthreads)
+
+
+def ekf9_tick_comp(x, P, clo, raw, valid, prm, do_update=True, do_predict=True, nthreads=1):
+    """EKF9 with compensated positions (FMSKF_CFG_COMP_POS): clo [5][n] float32 (px, py, P00,
+    P10, P11 low parts); x [10][n] keeps the heading's low part in row 9 as ekf9_tick"""
+    n = x.shape[1]
+    assert clo.shape == (5, n) and clo.dtype == np.float32 and clo.flags.c_contiguous
+    lib().orc_ekf9_tick_comp(n, x, P, clo, _ptr(raw), _ptr(valid), C.byref(prm), int(do_update),
+                             int(do_predict), nthreads)
 
 
 def ekf9_measure(raw):

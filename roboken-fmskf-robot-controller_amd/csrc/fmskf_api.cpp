@@ -799,8 +799,8 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
     if (!(cfg->dt > 0.0) || !isfinite(cfg->dt)) fail(FMSKF_EINVAL, "dt must be > 0");
     if (cfg->imu_read_reg + 4 > 0x90) fail(FMSKF_EINVAL, "imu_read_reg out of range");
     if ((cfg->flags & ~FMSKF_CFG_COMP_POS) || cfg->reserved) fail(FMSKF_EINVAL, "unknown config flags");
-    if ((cfg->flags & FMSKF_CFG_COMP_POS) && cfg->model != FMSKF_MODEL_KF6)
-      fail(FMSKF_ENOTSUP, "FMSKF_CFG_COMP_POS is a KF6 mode");
+    if ((cfg->flags & FMSKF_CFG_COMP_POS) && cfg->model != FMSKF_MODEL_KF6 && cfg->model != FMSKF_MODEL_EKF9)
+      fail(FMSKF_ENOTSUP, "FMSKF_CFG_COMP_POS is a KF6 / EKF9 mode");
     for (int w = 0; w < 4; w++)
       if (cfg->motor_dir[w] != 1 && cfg->motor_dir[w] != -1) fail(FMSKF_EINVAL, "motor_dir must be +-1");
     int ndev = 0;
@@ -826,7 +826,7 @@ int fmskf_create(const fmskf_config *cfg, fmskf_handle *out) {
       s.prev_sum = cfg->model == FMSKF_MODEL_RS ? h->alloc<int64_t>(4 * s.pitch) : nullptr;
       // EKF9: the compensated heading's hidden low part (kf_generic.hpp th_add), one float a robot
       s.thlo = cfg->model == FMSKF_MODEL_EKF9 ? h->alloc<float>(n) : nullptr;
-      // KF6 with FMSKF_CFG_COMP_POS: the position low parts, tiled like x and P
+      // KF6 / EKF9 with FMSKF_CFG_COMP_POS: the position low parts, tiled like x and P
       s.xlo = (cfg->flags & FMSKF_CFG_COMP_POS) ? h->alloc<float>((size_t)kKf6LoRows * s.pitch) : nullptr;
       h->kf6.lo = s.xlo;
       // the WT901 / motor ingest state (~470 B per robot) is allocated on first use
@@ -1105,7 +1105,7 @@ int fmskf_set_state(fmskf_handle h, const void *x, const void *p_packed, uint32_
     if (x) h->ens_shift_ok = false;
     // a heading set from outside is exact as given: its compensation term restarts at zero
     if (x && h->s.thlo) hip_check(hipMemsetAsync(h->s.thlo, 0, n * 4, h->stream), "heading low part");
-    // KF6 compensated positions: a state set from outside restarts every low part (x and P)
+    // compensated positions: a state set from outside restarts every low part (x and P)
     if ((x || p_packed) && h->s.xlo)
       hip_check(hipMemsetAsync(h->s.xlo, 0, (size_t)kKf6LoRows * h->s.pitch * 4, h->stream), "position low parts");
     finish_out(h, mem);
@@ -1482,15 +1482,15 @@ int fmskf_get_state_lo(fmskf_handle h, float *lo, uint32_t *rows, uint32_t mem) 
     if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
-    const uint32_t r = h->s.thlo ? 1u : h->s.xlo ? kKf6LoRows : 0u;
-    if (rows) *rows = r;
-    if (!lo || !r) return;
-    if (h->s.thlo) {
-      copy_out(h, lo, h->s.thlo, n * 4, mem);
-    } else {
-      void *dense = mem == FMSKF_MEM_DEVICE ? (void *)lo : h->out_for((size_t)r * n * 4);
-      launch_check(launch_untile(h->s.xlo, dense, r, n, 4, h->stream), "untile");
-      if (mem == FMSKF_MEM_HOST) copy_out(h, lo, dense, (size_t)r * n * 4, mem);
+    const uint32_t rh = h->s.thlo ? 1u : 0u, rx = h->s.xlo ? kKf6LoRows : 0u;
+    if (rows) *rows = rh + rx;
+    if (!lo || !(rh + rx)) return;
+    if (rh) copy_out(h, lo, h->s.thlo, n * 4, mem);
+    if (rx) {
+      float *dst = lo + (size_t)rh * n;
+      void *dense = mem == FMSKF_MEM_DEVICE ? (void *)dst : h->out_for((size_t)rx * n * 4);
+      launch_check(launch_untile(h->s.xlo, dense, rx, n, 4, h->stream), "untile");
+      if (mem == FMSKF_MEM_HOST) copy_out(h, dst, dense, (size_t)rx * n * 4, mem);
     }
     finish_out(h, mem);
   });
@@ -1503,16 +1503,16 @@ int fmskf_set_state_lo(fmskf_handle h, const float *lo, uint32_t mem) {
     if (!lo) fail(FMSKF_EINVAL, "null lo");
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
-    const uint32_t r = h->s.thlo ? 1u : h->s.xlo ? kKf6LoRows : 0u;
+    const uint32_t rh = h->s.thlo ? 1u : 0u, rx = h->s.xlo ? kKf6LoRows : 0u, r = rh + rx;
     if (!r) fail(FMSKF_ENOTSUP, "this model keeps no low-part rows");
-    const void *src = lo;
+    const float *src = lo;
     if (mem == FMSKF_MEM_HOST) {
       void *stg = h->stage_for((size_t)r * n * 4);
       hip_check(hipMemcpyAsync(stg, lo, (size_t)r * n * 4, hipMemcpyHostToDevice, h->stream), "stage H2D");
-      src = stg;
+      src = (const float *)stg;
     }
-    if (h->s.thlo) hip_check(hipMemcpyAsync(h->s.thlo, src, n * 4, hipMemcpyDeviceToDevice, h->stream), "lo");
-    else launch_check(launch_tile(src, h->s.xlo, r, n, 4, h->stream), "tile");
+    if (rh) hip_check(hipMemcpyAsync(h->s.thlo, src, n * 4, hipMemcpyDeviceToDevice, h->stream), "lo");
+    if (rx) launch_check(launch_tile(src + (size_t)rh * n, h->s.xlo, rx, n, 4, h->stream), "tile");
     h->ens_shift_ok = false;
     finish_out(h, FMSKF_MEM_HOST);
   });

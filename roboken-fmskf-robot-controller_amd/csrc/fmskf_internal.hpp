@@ -116,6 +116,8 @@ struct Ekf9Params {
   float q[45];
   float r[21];
   float *thlo;  // [N] the compensated heading's low part (a hidden state row; th_add)
+  // FMSKF_CFG_COMP_POS: the tiled low-part rows (px, py, P00, P10, P11); null = plain
+  float *clo;
 };
 struct Kf12dParams {
   double dt;

@@ -128,27 +128,6 @@ struct Wt901Parser {
   }
 };
 
-// The 15 registers the standard 10 ms poll writes (0x51: AX..AZ, TEMP; 0x52: GX..GZ; 0x53:
-// ROLL..YAW, VERSION; 0x59: Q0..Q3), in the order the LDS-transposed store takes them
-__device__ __forceinline__ uint32_t std4_reg(uint32_t p) {
-  return p < 3 ? R_AX + p : p < 6 ? R_GX + (p - 3) : p < 9 ? R_ROLL + (p - 6) : p == 9 ? R_TEMP
-       : p == 10 ? R_VERSION : R_Q0 + (p - 11);
-}
-
-// register std4_reg(k)'s value: word w of frame f (sw[f][w]; frames 0x51, 0x52, 0x53, 0x59)
-__device__ __forceinline__ uint32_t std4_word(const uint32_t (&sw)[4][4], int k) {
-  return sw[k < 3 ? 0 : k < 6 ? 1 : k < 9 ? 2 : k == 9 ? 0 : k == 10 ? 2 : 3][k < 9 ? k % 3 : k < 11 ? 3 : k - 11];
-}
-
-// Per-wave LDS staging of the transposed variants (TRV > 0): the wave's poll rows (TRV 2: <= 64 B
-// per IMU, fetched as whole contiguous 1 KiB runs), then in the same bytes the Data page
-// [16][64] floats; the 15 standard-poll registers [15][64] int16 after it.
-struct Wt901Lds {
-  uint32_t u[1024];
-  uint16_t reg[15 * 64];
-};
-constexpr unsigned kWt901Lds = (kBlock / 64) * (unsigned)sizeof(Wt901Lds);
-
 // VEC: the poll buffer rows are 16-byte aligned and at most 64 bytes (the 44-byte standard
 // poll in a 48-byte row): the lane's whole row is fetched with up to four 16-byte loads
 // issued before any byte is parsed, instead of one dependent byte load per parser step.
@@ -158,37 +137,19 @@ constexpr unsigned kWt901Lds = (kBlock / 64) * (unsigned)sizeof(Wt901Lds);
 // (registers 2k, 2k + 1 in one dword, so 5 of the poll's 15 register stores become dword
 // pairs), 38.7-38.9 against 35-36: the remaining single-register stores then half-fill the
 // lines they touch; the magnetometer / q_init loads issued with the poll instead of after the
-// parse, neutral.
-//
-// TRV (round 4): per-lane stores leave a standard poll's 109 B of results as 37 store
-// instructions (15 int16 register planes, 16 float Data-page planes, 3 parser words, 3 byte
-// planes: 3 B per lane-store on average; wave-state counters: 46 % of the wave cycles waiting
-// on memory, 43 % waiting to issue).  When every lane of a full wave took the standard poll,
-// TRV >= 1 stages the registers and the Data page in LDS and stores them transposed: each lane
-// writes 16 contiguous bytes of one plane (8 IMUs of a register, 4 of a Data-page row), and
-// the wave's zeroed parser words and byte flags go out as one instruction -- 7 stores per wave
-// instead of 37.  TRV 2 also fetches the wave's poll rows as contiguous 1 KiB runs into LDS
-// instead of 48-byte-strided 16-byte lane loads.  Any other wave keeps the per-lane stores.
-// The register planes must be 16-byte aligned (N % 8 == 0; the launcher checks).
-// TRV 3: the transposed stores of TRV 1 ordered within the wave only (LDS ops of one wave retire
-// in order: a wave barrier and an LDS fence instead of the block barrier).  WPE: minimum waves
-// per SIMD the register allocation must allow (0: the compiler's choice).
-template <bool VEC, int TRV, int WPE = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE ? WPE : 1, 8))) void k_wt901(
-    Wt901Args a) {
+// parse, neutral.  Round 4 (kbench at 2^20 standard polls, two passes each on one box, against
+// 34.9-35.3 us for this kernel): when every lane of a full wave took the standard poll, staging
+// its 15 registers and 16 Data-page floats in LDS and storing them transposed (each lane 16
+// contiguous bytes of one plane, 7 store instructions per wave instead of 37) measured
+// 35.8-35.9 us with a block barrier and 35.4-35.7 with wave-local ordering; fetching the
+// wave's poll rows as contiguous 1 KiB runs through LDS as well, 36.9-37.0; forcing 8 waves
+// per SIMD (64 VGPRs, 20 B of scratch), 37.2; 24 / 32 KiB occupancy caps, 34.6-36.6.  The
+// narrow stores are not what bounds the kernel, and none of these was kept.
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   const uint64_t n = a.n;
-  const uint64_t gi = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if constexpr (TRV == 0) {
-    if (gi >= n) return;
-  }
-  // TRV: every lane stays to the block barriers; lanes past N parse instance N - 1 and store
-  // nothing
-  const bool live = gi < n;
-  const uint64_t i = live ? gi : n - 1;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wb = gi - lane;  // the wave's first instance
-  extern __shared__ Wt901Lds wt_lds[];
-  Wt901Lds &L = wt_lds[TRV ? threadIdx.x >> 6 : 0];
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
   Wt901Parser ps;
   ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
   ps.hi = (uint64_t)a.parser[2 * n + i];
@@ -205,26 +166,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE ? WP
   if constexpr (VEC) {
     const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
     uint4 ch[4];
-    if constexpr (TRV == 2) {
-      // the wave's rows are 64 * stride contiguous bytes: chunk e (16 B) at byte e * 16, one
-      // coalesced 1 KiB run per load instruction, then each lane takes its own row from LDS
-      const uint64_t rows = wb < n ? (n - wb) * (uint64_t)a.stride : 0;
-      const auto rb = rsrc(a.bytes + wb * (uint64_t)a.stride, rows);
 #pragma unroll
-      for (uint32_t c = 0; c < 4; c++)
-        if (c < nch) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, (c * 64u + lane) * 16u, 0, 0);
-          *reinterpret_cast<uint4 *>(&L.u[(c * 64u + lane) * 4u]) = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++)
-        ch[c] = c < nch ? *reinterpret_cast<const uint4 *>(&L.u[(lane * nch + c) * 4u]) : make_uint4(0, 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-        ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
-    }
+    for (int c = 0; c < 4; c++)
+      ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
     // Whole-frame fast path.  With an empty parser window and a poll made of complete frames
     // (0x55 header and a valid checksum every 11 bytes), the byte-serial parser accepts frame
     // k at bytes 11k..11k+10 and never resyncs: dispatch the frames directly (static byte
@@ -260,8 +204,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE ? WP
     std4 = fast && nfr == 4 && ftype(w0[0]) == 0x51u && ftype(w0[1]) == 0x52u &&
            ftype(w0[2]) == 0x53u && ftype(w0[3]) == 0x59u;
     if (std4) {
-      // CopeWitData of the four frames with their register runs known statically (stored
-      // below: per lane, or transposed through LDS)
+      // CopeWitData of the four frames with their register runs known statically
 #pragma unroll
       for (int f = 0; f < 4; f++) {
         sw[f][0] = (uint32_t)(w0[f] >> 16) & 0xFFFFu;
@@ -269,15 +212,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE ? WP
         sw[f][2] = (uint32_t)(w0[f] >> 48) & 0xFFFFu;
         sw[f][3] = (uint32_t)w1[f] & 0xFFFFu;
       }
+      int16_t *reg = a.reg;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        reg[(R_AX + k) * n + i] = (int16_t)sw[0][k];
+        reg[(R_GX + k) * n + i] = (int16_t)sw[1][k];
+        reg[(R_ROLL + k) * n + i] = (int16_t)sw[2][k];
+      }
+      reg[R_TEMP * n + i] = (int16_t)sw[0][3];
+      reg[R_VERSION * n + i] = (int16_t)sw[2][3];
+#pragma unroll
+      for (int k = 0; k < 4; k++) reg[(R_Q0 + k) * n + i] = (int16_t)sw[3][k];
       ps.flags |= flags_of(R_AX, 3) | flags_of(R_TEMP, 1) | flags_of(R_GX, 3) | flags_of(R_ROLL, 3) |
                   flags_of(R_VERSION, 1) | flags_of(R_Q0, 4);
     } else if (fast) {
-      if (live) {
 #pragma unroll
-        for (int f = 0; f < 5; f++)
-          if ((uint32_t)f < nfr) ps.dispatch(w0[f], w1[f], a, i);
-      }
-    } else if (live) {
+      for (int f = 0; f < 5; f++)
+        if ((uint32_t)f < nfr) ps.dispatch(w0[f], w1[f], a, i);
+    } else {
     // one parser body: the next chunk's bytes are consumed from the bottom of a 128-bit
     // shift register
 #pragma unroll 1
@@ -298,140 +250,76 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE ? WP
     }
     }
   } else {
-    if (live)
-      for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);
+    for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);
   }
   uint64_t lo = ps.lo, hi = ps.hi;
   uint32_t cnt = ps.cnt, flags = ps.flags;
   int16_t *reg = a.reg;
-  // the transposed store: a full wave whose every lane took the standard poll from an empty
-  // window (the parser words, count, flags and error then all go to 0)
-  bool wave_tr = false;
-  if constexpr (TRV > 0) wave_tr = wb + 64 <= n && __all(std4 && (lo | hi) == 0);
-  if (std4 && !wave_tr && live) {
-#pragma unroll
-    for (int k = 0; k < 15; k++) reg[std4_reg(k) * n + i] = (int16_t)std4_word(sw, k);
-  }
   // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
   const bool ok = (flags & F_QUAT) != 0;
   if (ok) flags = 0;
-  if (wave_tr) {
-    // the parser words [3][N] (48 lanes x 16 B) and the error / count / flag bytes (4 lanes x
-    // 16 B each) of the wave's 64 IMUs, all zero, in one store instruction
-    if (lane < 48) {
-      *reinterpret_cast<uint4 *>(a.parser + (uint64_t)(lane >> 4) * n + wb + (lane & 15u) * 4u) = make_uint4(0, 0, 0, 0);
-    } else if (lane < 60) {
-      const uint32_t q = (lane - 48u) >> 2;
-      uint8_t *b = q == 0 ? a.err : q == 1 ? a.cnt : a.flags;
-      *reinterpret_cast<uint4 *>(b + wb + (lane & 3u) * 16u) = make_uint4(0, 0, 0, 0);
-    }
-  } else if (live) {
-    a.err[i] = ok ? 0 : 1;
-    a.parser[i] = (uint32_t)lo;
-    a.parser[n + i] = (uint32_t)(lo >> 32);
-    a.parser[2 * n + i] = (uint32_t)hi;
-    a.cnt[i] = (uint8_t)cnt;
-    a.flags[i] = (uint8_t)flags;
-  }
-  if constexpr (TRV == 0) {
-    if (!ok) return;
-  }
+  a.err[i] = ok ? 0 : 1;
+  a.parser[i] = (uint32_t)lo;
+  a.parser[n + i] = (uint32_t)(lo >> 32);
+  a.parser[2 * n + i] = (uint32_t)hi;
+  a.cnt[i] = (uint8_t)cnt;
+  a.flags[i] = (uint8_t)flags;
+  if (!ok) return;
   // updateData, imu_if_wt901c.cpp:91-129
-  float dp[16];
-  if (ok) {
-    float acc[3], gyr[3], mag[3], ang[3], q[4], qi[4];
-    int16_t ra[3], rg[3], rr[3], rq[4];
-    if (std4) {
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        ra[k] = (int16_t)sw[0][k];
-        rg[k] = (int16_t)sw[1][k];
-        rr[k] = (int16_t)sw[2][k];
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) rq[k] = (int16_t)sw[3][k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        ra[k] = reg[(R_AX + k) * n + i];
-        rg[k] = reg[(R_GX + k) * n + i];
-        rr[k] = reg[(R_ROLL + k) * n + i];
-      }
-#pragma unroll
-      for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
-    }
+  float acc[3], gyr[3], mag[3], ang[3], q[4], qi[4];
+  int16_t ra[3], rg[3], rr[3], rq[4];
+  if (std4) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      acc[k] = (float)ra[k] / 32768.0f * 16.0f;
-      gyr[k] = (float)rg[k] / 32768.0f * 2000.0f;
-      mag[k] = (float)reg[(R_HX + k) * n + i];
-      ang[k] = (float)rr[k] / 32768.0f * 180.0f;
+      ra[k] = (int16_t)sw[0][k];
+      rg[k] = (int16_t)sw[1][k];
+      rr[k] = (int16_t)sw[2][k];
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      q[k] = (float)rq[k] / 32768.0f;
-      qi[k] = a.qinit[k * n + i];
-    }
-    dp[0] = acc[0];
-    dp[1] = -acc[1];
-    dp[2] = -acc[2];
-    dp[3] = gyr[0];
-    dp[4] = -gyr[1];
-    dp[5] = -gyr[2];
-    dp[6] = mag[0];
-    dp[7] = -mag[1];
-    dp[8] = -mag[2];
-    dp[9] = normalize_deg_0to360(ang[0]) - 180.0f;
-    dp[10] = ang[1];
-    dp[11] = ang[2];
-    dp[14] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
-    dp[13] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
-    dp[12] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
-    dp[15] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
-    if (a.latch_qinit && live) {
+    for (int k = 0; k < 4; k++) rq[k] = (int16_t)sw[3][k];
+  } else {
 #pragma unroll
-      for (int k = 0; k < 4; k++) a.qinit[k * n + i] = q[k];
+    for (int k = 0; k < 3; k++) {
+      ra[k] = reg[(R_AX + k) * n + i];
+      rg[k] = reg[(R_GX + k) * n + i];
+      rr[k] = reg[(R_ROLL + k) * n + i];
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
   }
-  if constexpr (TRV > 0) {
-    if (wave_tr) {
 #pragma unroll
-      for (int k = 0; k < 16; k++) L.u[k * 64 + lane] = __builtin_bit_cast(uint32_t, dp[k]);
-#pragma unroll
-      for (int k = 0; k < 15; k++)
-        L.reg[k * 64 + lane] = (uint16_t)std4_word(sw, k);
-    }
-    if constexpr (TRV == 3) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    } else {
-      __syncthreads();
-    }
-    if (wave_tr) {
-      // registers: 15 planes x 8 chunks of 8 IMUs (16 B); Data page: 16 rows x 16 chunks of 4
-#pragma unroll
-      for (uint32_t r = 0; r < 2; r++) {
-        const uint32_t e = r * 64u + lane;
-        if (e < 120u) {
-          const uint32_t pl = e >> 3, c = e & 7u;
-          *reinterpret_cast<uint4 *>(reg + (uint64_t)std4_reg(pl) * n + wb + c * 8u) =
-              *reinterpret_cast<const uint4 *>(&L.reg[pl * 64u + c * 8u]);
-        }
-      }
-#pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        const uint32_t e = r * 64u + lane, pl = e >> 4, c = e & 15u;
-        *reinterpret_cast<uint4 *>(a.data + (uint64_t)pl * n + wb + c * 4u) =
-            *reinterpret_cast<const uint4 *>(&L.u[pl * 64u + c * 4u]);
-      }
-      return;
-    }
+  for (int k = 0; k < 3; k++) {
+    acc[k] = (float)ra[k] / 32768.0f * 16.0f;
+    gyr[k] = (float)rg[k] / 32768.0f * 2000.0f;
+    mag[k] = (float)reg[(R_HX + k) * n + i];
+    ang[k] = (float)rr[k] / 32768.0f * 180.0f;
   }
-  if (!ok || !live) return;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    q[k] = (float)rq[k] / 32768.0f;
+    qi[k] = a.qinit[k * n + i];
+  }
   float *d = a.data;
+  d[0 * n + i] = acc[0];
+  d[1 * n + i] = -acc[1];
+  d[2 * n + i] = -acc[2];
+  d[3 * n + i] = gyr[0];
+  d[4 * n + i] = -gyr[1];
+  d[5 * n + i] = -gyr[2];
+  d[6 * n + i] = mag[0];
+  d[7 * n + i] = -mag[1];
+  d[8 * n + i] = -mag[2];
+  d[9 * n + i] = normalize_deg_0to360(ang[0]) - 180.0f;
+  d[10 * n + i] = ang[1];
+  d[11 * n + i] = ang[2];
+  d[14 * n + i] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
+  d[13 * n + i] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
+  d[12 * n + i] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
+  d[15 * n + i] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
+  if (a.latch_qinit) {
 #pragma unroll
-  for (int k = 0; k < 16; k++) d[k * n + i] = dp[k];
+    for (int k = 0; k < 4; k++) a.qinit[k * n + i] = q[k];
+  }
 }
 
 int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
@@ -441,20 +329,8 @@ int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const
               s.imu_err,    s.imu_qinit,    s.imu_data};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   const bool vec = stride % 16 == 0 && stride <= 64 && ((uintptr_t)bytes & 15) == 0;
-  // FMSKF_WT901_VARIANT: 0 per-lane stores, 1 LDS-transposed stores, 2 (default) transposed
-  // stores and LDS-staged poll rows; the transposed forms need 16-byte aligned register planes
-  static const int var = [] {
-    const char *e = getenv("FMSKF_WT901_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  const int trv = vec && s.n % 8 == 0 ? var : 0;
-  if (vec && trv == 5) k_wt901<true, 3, 8><<<g, kBlock, kWt901Lds, st>>>(a);
-  else if (vec && trv == 4) k_wt901<true, 0, 8><<<g, kBlock, 0, st>>>(a);
-  else if (vec && trv == 3) k_wt901<true, 3><<<g, kBlock, kWt901Lds, st>>>(a);
-  else if (vec && trv == 2) k_wt901<true, 2><<<g, kBlock, kWt901Lds, st>>>(a);
-  else if (vec && trv == 1) k_wt901<true, 1><<<g, kBlock, kWt901Lds, st>>>(a);
-  else if (vec) k_wt901<true, 0><<<g, kBlock, FMSKF_LDS_CAP("FMSKF_WT901_LDS", false, 0u), st>>>(a);
-  else k_wt901<false, 0><<<g, kBlock, 0, st>>>(a);
+  if (vec) k_wt901<true><<<g, kBlock, 0, st>>>(a);
+  else k_wt901<false><<<g, kBlock, 0, st>>>(a);
   return (int)hipGetLastError();
 }
 

@@ -55,16 +55,20 @@ __device__ __forceinline__ uint4 ekf9_raw_at(const int16_t *raw, uint64_t i) {
 // one EKF9 tick (update with the measurement frontend, then the nonlinear predict)
 // SEQ: R is diagonal -> the sequential scalar update (kf_update_seq), else the joint LDL^T one
 // lo: the compensated heading's low part (th_add, kf_generic.hpp)
-template <bool LIBM, bool UPD, bool PRED, bool SEQ>
+// COMP: FMSKF_CFG_COMP_POS -- px, py, P00, P10, P11 compensated too (cl: their five low parts;
+// oracle orc_ekf9_tick_comp)
+template <bool LIBM, bool UPD, bool PRED, bool SEQ, bool COMP = false>
 __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, const uint4 raw,
                                            bool have, const float *stab, float (&x)[9],
-                                           float (&P)[45], float &lo) {
+                                           float (&P)[45], float &lo, float *cl = nullptr) {
+  constexpr unsigned CXM = COMP ? kPosCXM : 0u;
+  constexpr unsigned long long CPM = COMP ? kPosCPM : 0ull;
   const float dt = a.prm.dt;
   if (UPD && have) {
     float y[6];
     ekf9_innov(raw, x, lo, y);
-    if constexpr (SEQ) kf_update_seq<MdEKF9, 2>(x, P, y, a.prm.r, &lo);
-    else kf_update<MdEKF9, 2>(x, P, y, a.prm.r, &lo);
+    if constexpr (SEQ) kf_update_seq<MdEKF9, 2, float, 9, 6, 45, CXM, CPM>(x, P, y, a.prm.r, &lo, cl);
+    else kf_update<MdEKF9, 2, float, 9, 6, 45, CXM, CPM>(x, P, y, a.prm.r, &lo, cl);
     th_norm(x[2], lo);
   }
   if (PRED) {
@@ -76,8 +80,15 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
     const float vwy = x[3] * s + x[4] * c;
     const float f02 = -(vwy * dt), f03 = c * dt, f04 = -(s * dt);
     const float f12 = vwx * dt, f13 = s * dt, f14 = c * dt;
-    x[0] = x[0] + vwx * dt;
-    x[1] = x[1] + vwy * dt;
+    if constexpr (COMP) {
+      th_add(x[0], cl[0], vwx * dt);
+      th_add(x[1], cl[1], vwy * dt);
+      th_norm(x[0], cl[0]);
+      th_norm(x[1], cl[1]);
+    } else {
+      x[0] = x[0] + vwx * dt;
+      x[1] = x[1] + vwy * dt;
+    }
     th_add(x[2], lo, x[5] * dt);
     wrap_pi_c(x[2], lo);
     th_norm(x[2], lo);
@@ -88,13 +99,34 @@ __device__ __forceinline__ void ekf9_tick1(const KfArgs<MdEKF9, Ekf9Params> &a, 
       if (r == 1) return k == 2 ? f12 : k == 3 ? f13 : f14;
       return dt;
     };
-    kf_predict_cov<MdEKF9>(P, fv, a.prm.q);
+    if constexpr (COMP) kf_predict_cov_c<MdEKF9, kPosCXM, kPosCPM>(P, fv, a.prm.q, cl);
+    else kf_predict_cov<MdEKF9>(P, fv, a.prm.q);
   }
 }
 
+// the COMP low-part rows of one 256-robot chunk (tiled like x, kKf6LoRows rows)
+template <bool COMP, int CP>
+struct Ekf9Lo {
+  float v[COMP ? kKf6LoRows : 1];
+  __device__ __forceinline__ void load(const float *clo, uint32_t chunk, uint32_t slot) {
+    if constexpr (COMP) {
+      const TileRows<float, kKf6LoRows, CP> t(const_cast<float *>(clo), chunk, slot, 0);
+#pragma unroll
+      for (int k = 0; k < (int)kKf6LoRows; k++) v[k] = t.ld(k);
+    }
+  }
+  __device__ __forceinline__ void store(float *clo, uint32_t chunk, uint32_t slot) const {
+    if constexpr (COMP) {
+      const TileRows<float, kKf6LoRows, CP> t(clo, chunk, slot, 0);
+#pragma unroll
+      for (int k = 0; k < (int)kKf6LoRows; k++) t.st(k, v[k]);
+    }
+  }
+};
+
 // tick_many: T ticks per launch, state in VGPRs; the next tick's raw record (16 B) and validity
 // byte are loaded while the current tick computes (ping-pong registers, loop unrolled by two)
-template <bool LIBM, bool UPD, bool PRED, bool SEQ>
+template <bool LIBM, bool UPD, bool PRED, bool SEQ, bool COMP = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   __shared__ float stab[LIBM ? 1 : 513];
@@ -129,6 +161,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
     for (int k = 0; k < NP; k++) P[k] = a.P[k * pp + ic];
   }
   float lo = a.prm.thlo[ic];
+  Ekf9Lo<COMP, 0> cl;
+  cl.load(a.prm.clo, blockIdx.x, tile_slot(n));
   uint4 ra = raw_at(0), rb;
   bool ha = have_at(0), hb;
   for (uint32_t t = 0; t < T; t += 2) {
@@ -136,16 +170,17 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
       rb = raw_at(t + 1);
       hb = have_at(t + 1);
     }
-    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, ra, ha, stab, x, P, lo);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ, COMP>(a, ra, ha, stab, x, P, lo, cl.v);
     if (t + 1 >= T) break;
     if (t + 2 < T) {
       ra = raw_at(t + 2);
       ha = have_at(t + 2);
     }
-    ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, rb, hb, stab, x, P, lo);
+    ekf9_tick1<LIBM, UPD, PRED, SEQ, COMP>(a, rb, hb, stab, x, P, lo, cl.v);
   }
   if (live) {
     a.prm.thlo[i] = lo;
+    cl.store(a.prm.clo, blockIdx.x, tile_slot(n));
     if constexpr (FMSKF_TILED) {
 #pragma unroll
       for (int k = 0; k < N; k++) tx.st(k, x[k]);
@@ -164,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9(KfArgs<MdEKF9, Ekf9Params> a) {
 // Single tick, straight line (as k_kf6t): no tick loop, clamped index for lanes past N (only
 // their stores and NaN count are masked), every load issued before the table barrier.
 // ENS: the record epilogue of fmskf_tick_ensemble (ens_device.hpp)
-template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool ENS = false>
+template <bool LIBM, bool UPD, bool PRED, bool SEQ, int CP = 0, bool ENS = false, bool COMP = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   uint32_t bid = blockIdx.x;  // the tick block (the carried fold blocks come first)
@@ -197,10 +232,13 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
   const uint4 raw = UPD ? ekf9_raw_at<false>(a.in.raw, ic) : make_uint4(0, 0, 0, 0);
   const uint64_t hb0 = (uint64_t)bid * kBlock;
   float lo = ld_chunk<float, CP>(a.prm.thlo, hb0, n, sl);
+  Ekf9Lo<COMP, CP> cl;
+  cl.load(a.prm.clo, bid, sl);
   tv.store(stab);
-  ekf9_tick1<LIBM, UPD, PRED, SEQ>(a, raw, have, stab, x, P, lo);
+  ekf9_tick1<LIBM, UPD, PRED, SEQ, COMP>(a, raw, have, stab, x, P, lo, cl.v);
   if (live) {
     st_chunk<float, st_pol(CP)>(a.prm.thlo, hb0, n, sl, lo);
+    cl.store(a.prm.clo, bid, sl);
     if constexpr (FMSKF_TILED) {
 #pragma unroll
       for (int k = 0; k < N; k++) tx.st(k, x[k]);
@@ -226,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 // Two robots per lane (256-robot chunks b and b + G of the tiled state, G the tick blocks):
 // robot B's 54 state loads and its raw record are issued before robot A's update, so they
 // stream in while A computes (see launch_ekf9).
-template <bool LIBM, bool SEQ, int CP, bool ENS = false>
+template <bool LIBM, bool SEQ, int CP, bool ENS = false, bool COMP = false>
 __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) {
   constexpr int N = 9, NP = 45;
   uint32_t bid = blockIdx.x;  // the tick block (the carried fold blocks come first)
@@ -266,10 +304,14 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
   for (int k = 0; k < NP; k++) Pb[k] = tpb.ld(k);
   float loa = ld_chunk<float, CP>(a.prm.thlo, (uint64_t)ta * kBlock, n, slot(ta));
   float lob = ld_chunk<float, CP>(a.prm.thlo, (uint64_t)tb * kBlock, n, slot(tb));
+  Ekf9Lo<COMP, CP> cla, clb;
+  cla.load(a.prm.clo, ta, slot(ta));
+  clb.load(a.prm.clo, tb, slot(tb));
   tv.store(stab);
-  ekf9_tick1<LIBM, true, true, SEQ>(a, ra, ha, stab, xa, Pa, loa);
+  ekf9_tick1<LIBM, true, true, SEQ, COMP>(a, ra, ha, stab, xa, Pa, loa, cla.v);
   if (live_a) {
     st_chunk<float, st_pol(CP)>(a.prm.thlo, (uint64_t)ta * kBlock, n, slot(ta), loa);
+    cla.store(a.prm.clo, ta, slot(ta));
 #pragma unroll
     for (int k = 0; k < N; k++) txa.st(k, xa[k]);
 #pragma unroll
@@ -281,9 +323,10 @@ __global__ __launch_bounds__(kBlock) void k_ekf9p(KfArgs<MdEKF9, Ekf9Params> a) 
 #pragma unroll
     for (int k = 0; k < N; k++) xs[0][k] = xa[k];
   }
-  ekf9_tick1<LIBM, true, true, SEQ>(a, rb, hb, stab, xb, Pb, lob);
+  ekf9_tick1<LIBM, true, true, SEQ, COMP>(a, rb, hb, stab, xb, Pb, lob, clb.v);
   if (live_b) {
     st_chunk<float, st_pol(CP)>(a.prm.thlo, (uint64_t)tb * kBlock, n, slot(tb), lob);
+    clb.store(a.prm.clo, tb, slot(tb));
 #pragma unroll
     for (int k = 0; k < N; k++) txb.st(k, xb[k]);
 #pragma unroll
@@ -560,16 +603,16 @@ __global__ __launch_bounds__(kBlock) void k_kf12s(KfArgs<MdKF12D, Kf12dParams> a
 // fused tick + record (fmskf_tick_ensemble): the default single-tick kernel with the record
 // epilogue (and the carried fold blocks past the tick blocks when in.fold_blocks is set);
 // returns the tick grid (= the number of block records)
-template <bool LIBM, bool SEQ>
+template <bool LIBM, bool SEQ, bool COMP>
 static int launch_ekf9_ens(KfArgs<MdEKF9, Ekf9Params> a, const DevState &s, bool nt, hipStream_t st) {
   const unsigned carry = a.in.fold_blocks ? (unsigned)EnsRec<9>::LEN : 0u;
-  if (!LIBM && s.n * 220 <= (256ull << 20)) {
+  if (!LIBM && s.n * (COMP ? 240 : 220) <= (256ull << 20)) {
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const unsigned g2 = (ntiles + 1) / 2;
     a.in.ens_grid = g2;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) launch_signal(k_ekf9p<false, SEQ, kStateNT, true>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
-    else launch_signal(k_ekf9p<false, SEQ, 0, true>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
+    if (nt) launch_signal(k_ekf9p<false, SEQ, kStateNT, true, COMP>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
+    else launch_signal(k_ekf9p<false, SEQ, 0, true, COMP>, dim3(g2 + carry), lds, st, a.in.ens_done, a);
     return (int)g2;
   }
   // past the Infinity Cache the record epilogue (fp64 sums and their cross-lane reduction)
@@ -578,17 +621,17 @@ static int launch_ekf9_ens(KfArgs<MdEKF9, Ekf9Params> a, const DevState &s, bool
   const unsigned g = grid_for(s.n).x;
   a.in.ens_grid = g;
   const unsigned lds = LIBM ? 0u : FMSKF_LDS_CAP("FMSKF_EKF9E_LDS", nt, 32u * 1024u);
-  if (nt) launch_signal(k_ekf9t<LIBM, true, true, SEQ, kStateNT, true>, dim3(g + carry), lds, st, a.in.ens_done, a);
-  else launch_signal(k_ekf9t<LIBM, true, true, SEQ, 0, true>, dim3(g + carry), lds, st, a.in.ens_done, a);
+  if (nt) launch_signal(k_ekf9t<LIBM, true, true, SEQ, kStateNT, true, COMP>, dim3(g + carry), lds, st, a.in.ens_done, a);
+  else launch_signal(k_ekf9t<LIBM, true, true, SEQ, 0, true, COMP>, dim3(g + carry), lds, st, a.in.ens_done, a);
   return (int)g;
 }
 
-template <bool SEQ>
+template <bool SEQ, bool COMP>
 static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s, const TickIn &in, bool libm,
                          bool upd, bool pred, bool nt, hipStream_t st, int *ens_nb) {
   const dim3 g = grid_for(s.n);
   if (in.ens_blocks) {
-    *ens_nb = libm ? launch_ekf9_ens<true, SEQ>(a, s, nt, st) : launch_ekf9_ens<false, SEQ>(a, s, nt, st);
+    *ens_nb = libm ? launch_ekf9_ens<true, SEQ, COMP>(a, s, nt, st) : launch_ekf9_ens<false, SEQ, COMP>(a, s, nt, st);
     return (int)hipGetLastError();
   }
   // Single-tick kernel: two robots per lane (k_ekf9p) while the 216-byte state fits the 256 MiB
@@ -601,23 +644,23 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
     const char *e = getenv("FMSKF_EKF9_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  const int v = var == 2 || var == 4 ? var : (s.n * 220 <= (256ull << 20) ? 2 : 4);
+  const int v = var == 2 || var == 4 ? var : (s.n * (COMP ? 240 : 220) <= (256ull << 20) ? 2 : 4);
   if (FMSKF_TILED && in.n_ticks == 1 && upd && pred && !libm && v == 2) {
     const uint32_t ntiles = (uint32_t)((s.n + kBlock - 1) / kBlock);
     const dim3 g2((ntiles + 1) / 2);
     // 64 KiB of dynamic LDS (2 blocks per CU): 2^20 71.2 -> 70.5-70.7 us (two passes)
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9P_LDS", true, 64u * 1024u);
-    if (nt) k_ekf9p<false, SEQ, kStateNT><<<g2, kBlock, lds, st>>>(a);
-    else k_ekf9p<false, SEQ, 0><<<g2, kBlock, lds, st>>>(a);
+    if (nt) k_ekf9p<false, SEQ, kStateNT, false, COMP><<<g2, kBlock, lds, st>>>(a);
+    else k_ekf9p<false, SEQ, 0, false, COMP><<<g2, kBlock, lds, st>>>(a);
     return (int)hipGetLastError();
   }
   // predict-only launches run no update: one (SEQ = false) instantiation serves both
   if (in.n_ticks == 1) {
     if (libm) {
-      if (upd && pred && nt) k_ekf9t<true, true, true, SEQ, kStateNT><<<g, kBlock, 0, st>>>(a);
-      else if (upd && pred) k_ekf9t<true, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
-      else if (upd) k_ekf9t<true, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<true, false, true, false><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<true, true, true, SEQ, kStateNT, false, COMP><<<g, kBlock, 0, st>>>(a);
+      else if (upd && pred) k_ekf9t<true, true, true, SEQ, 0, false, COMP><<<g, kBlock, 0, st>>>(a);
+      else if (upd) k_ekf9t<true, true, false, SEQ, 0, false, COMP><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<true, false, true, false, 0, false, COMP><<<g, kBlock, 0, st>>>(a);
     } else {
       // Past the Infinity Cache (non-temporal state) the occupancy is capped at 2 blocks per CU
       // with 64 KiB of dynamic LDS: fewer concurrent tile streams per HBM channel.  2^22:
@@ -625,19 +668,19 @@ static int launch_ekf9_s(const KfArgs<MdEKF9, Ekf9Params> &a, const DevState &s,
       // 382-383 at 80 KiB (kbench, two boxes, two passes each); the same-bytes tiled pattern
       // (membench) 299 us.  FMSKF_EKF9_LDS overrides the byte count.
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_EKF9_LDS", nt, 64u * 1024u);
-      if (upd && pred && nt) k_ekf9t<false, true, true, SEQ, kStateNT><<<g, kBlock, lds, st>>>(a);
-      else if (upd && pred) k_ekf9t<false, true, true, SEQ><<<g, kBlock, lds, st>>>(a);
-      else if (upd) k_ekf9t<false, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
-      else k_ekf9t<false, false, true, false><<<g, kBlock, 0, st>>>(a);
+      if (upd && pred && nt) k_ekf9t<false, true, true, SEQ, kStateNT, false, COMP><<<g, kBlock, lds, st>>>(a);
+      else if (upd && pred) k_ekf9t<false, true, true, SEQ, 0, false, COMP><<<g, kBlock, lds, st>>>(a);
+      else if (upd) k_ekf9t<false, true, false, SEQ, 0, false, COMP><<<g, kBlock, 0, st>>>(a);
+      else k_ekf9t<false, false, true, false, 0, false, COMP><<<g, kBlock, 0, st>>>(a);
     }
   } else if (libm) {
-    if (upd && pred) k_ekf9<true, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
-    else if (upd) k_ekf9<true, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
-    else k_ekf9<true, false, true, false><<<g, kBlock, 0, st>>>(a);
+    if (upd && pred) k_ekf9<true, true, true, SEQ, COMP><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_ekf9<true, true, false, SEQ, COMP><<<g, kBlock, 0, st>>>(a);
+    else k_ekf9<true, false, true, false, COMP><<<g, kBlock, 0, st>>>(a);
   } else {
-    if (upd && pred) k_ekf9<false, true, true, SEQ><<<g, kBlock, 0, st>>>(a);
-    else if (upd) k_ekf9<false, true, false, SEQ><<<g, kBlock, 0, st>>>(a);
-    else k_ekf9<false, false, true, false><<<g, kBlock, 0, st>>>(a);
+    if (upd && pred) k_ekf9<false, true, true, SEQ, COMP><<<g, kBlock, 0, st>>>(a);
+    else if (upd) k_ekf9<false, true, false, SEQ, COMP><<<g, kBlock, 0, st>>>(a);
+    else k_ekf9<false, false, true, false, COMP><<<g, kBlock, 0, st>>>(a);
   }
   return (int)hipGetLastError();
 }
@@ -646,15 +689,19 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
                 bool pred, hipStream_t st, int *ens_nb) {
   KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, p};
   a.prm.thlo = s.thlo;
-  if (!s.thlo) return (int)hipErrorInvalidValue;
-  const bool nt = FMSKF_TILED && state_nt(s.n * 55 * 4);
+  a.prm.clo = s.xlo;  // FMSKF_CFG_COMP_POS
+  if (!s.thlo || (s.xlo && !FMSKF_TILED)) return (int)hipErrorInvalidValue;
+  const bool nt = FMSKF_TILED && state_nt(s.n * (s.xlo ? 60 : 55) * 4);
   if ((in.ens_blocks && (!FMSKF_TILED || !ens_nb || !upd || !pred || in.n_ticks != 1)) ||
       (in.fold_blocks && !in.ens_blocks))
     return (int)hipErrorInvalidValue;
   // canonical update order (oracle orc_ekf9_tick): sequential scalar updates when R is
   // diagonal, the joint LDL^T update otherwise
-  if (ekf9_r_diagonal(p.r)) return launch_ekf9_s<true>(a, s, in, libm, upd, pred, nt, st, ens_nb);
-  return launch_ekf9_s<false>(a, s, in, libm, upd, pred, nt, st, ens_nb);
+  const bool diag = ekf9_r_diagonal(p.r);
+  if (s.xlo) return diag ? launch_ekf9_s<true, true>(a, s, in, libm, upd, pred, nt, st, ens_nb)
+                         : launch_ekf9_s<false, true>(a, s, in, libm, upd, pred, nt, st, ens_nb);
+  return diag ? launch_ekf9_s<true, false>(a, s, in, libm, upd, pred, nt, st, ens_nb)
+              : launch_ekf9_s<false, false>(a, s, in, libm, upd, pred, nt, st, ens_nb);
 }
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,

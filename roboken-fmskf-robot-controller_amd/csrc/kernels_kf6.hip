@@ -181,18 +181,19 @@ static int kf6_variant() {
 
 template <class O>
 static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
-  // COMP (the position low parts) runs one robot per lane (k_kf6t) at every size
-  const int v = a.in.n_ticks == 1 ? (O::COMP ? 15 : kf6_variant()) : 0;
+  const int v = a.in.n_ticks == 1 ? kf6_variant() : 0;
+  // state bytes per robot (COMP: + the five low-part rows) and with one tick's 16-byte inputs
+  constexpr uint64_t SB = O::COMP ? 128 : 108, RB = SB + 16;
   if (a.in.n_ticks == 1 && v == 12) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     if constexpr (O::UPD && O::PRED) {
-      if (state_nt(a.n * 108)) {
+      if (state_nt(a.n * SB)) {
         k_kf6p<4, 2, WithNT<O>><<<g, kBlock, 0, st>>>(a);
         return;
       }
     }
     k_kf6p<4, 2, O><<<g, kBlock, 0, st>>>(a);
-  } else if (a.in.n_ticks == 1 && v == 0 && a.n * 124 <= (256ull << 20)) {
+  } else if (a.in.n_ticks == 1 && v == 0 && a.n * RB <= (256ull << 20)) {
     // state + one tick's inputs resident in the 256 MiB Infinity Cache: two robots per lane,
     // both robots' inputs loaded up front, one wave round (2^20: 39.7 -> 37.4-38.1 us,
     // 2^21: 75.9 -> 71.5; at 2^24, HBM-bound, it is 3% slower than one robot per lane)
@@ -204,10 +205,10 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     // 48 KiB 36.67-36.93, 64 KiB 36.61-36.97, 80 KiB 44.0, uncapped 38.0).  Plane inputs and
     // 2^21 records stay at 32 KiB (48 KiB: 2^20 planes 37.49 -> 37.72-38.07, 2^21 records
     // 68.3-68.4 -> 69.0, 2^21 planes 69.5-69.7 -> 71.2-71.4)
-    const bool rec_half = a.in.rec != nullptr && a.n * 124 <= (128ull << 20);
+    const bool rec_half = a.in.rec != nullptr && a.n * RB <= (128ull << 20);
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, rec_half ? 48u * 1024u : 32u * 1024u);
     if constexpr (O::UPD && O::PRED) {
-      if (state_nt(a.n * 108)) {  // only when forced: this branch's state fits the cache
+      if (state_nt(a.n * SB)) {  // only when forced: this branch's state fits the cache
         k_kf6p<4, 2, WithNT<O>><<<g, kBlock, lds, st>>>(a);
         return;
       }
@@ -217,9 +218,9 @@ static void launch_o(const KfArgs<MdKF6, Kf6Params> &a, hipStream_t st) {
     // past the Infinity Cache: at most 3 blocks per CU (48 KiB of dynamic LDS).  2^24, records,
     // kbench, one box, two passes: 691-704 us uncapped, 671-684 at 32 KiB, 627-641 at 48 KiB,
     // 626-639 at 64 KiB, 809-826 at 80 KiB (two blocks of 4 waves per CU are too few)
-    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6_LDS", state_nt(a.n * 108), 48u * 1024u);
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6_LDS", state_nt(a.n * SB), 48u * 1024u);
     if constexpr (O::UPD && O::PRED) {
-      if (state_nt(a.n * 108)) {
+      if (state_nt(a.n * SB)) {
         k_kf6t<4, WithNT<O>><<<grid_for(a.n), kBlock, lds, st>>>(a);
         return;
       }
@@ -239,11 +240,12 @@ template <class O>
 static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   using E = WithEns<O>;
   const unsigned carry = a.in.fold_blocks ? (unsigned)EnsRec<6>::LEN : 0u;
-  if (a.n * 124 <= (256ull << 20) && !O::COMP) {
+  constexpr uint64_t SB = O::COMP ? 128 : 108, RB = SB + 16;
+  if (a.n * RB <= (256ull << 20)) {
     const unsigned g = (unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock));
     a.in.ens_grid = g;
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6P_LDS", true, 32u * 1024u);
-    if (state_nt(a.n * 108)) launch_signal(k_kf6p<4, 2, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
+    if (state_nt(a.n * SB)) launch_signal(k_kf6p<4, 2, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
     else launch_signal(k_kf6p<4, 2, E>, dim3(g + carry), lds, st, a.in.ens_done, a);
     return (int)g;
   }
@@ -252,8 +254,8 @@ static int launch_ens_o(KfArgs<MdKF6, Kf6Params> a, hipStream_t st) {
   // 665-670 at 32 KiB, 680-689 at 24 KiB, 722-724 uncapped (the plain tick: 619-628)
   const unsigned g = grid_for(a.n).x;
   a.in.ens_grid = g;
-  const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6E_LDS", state_nt(a.n * 108), 32u * 1024u);
-  if (state_nt(a.n * 108)) launch_signal(k_kf6t<4, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
+  const unsigned lds = FMSKF_LDS_CAP("FMSKF_KF6E_LDS", state_nt(a.n * SB), 32u * 1024u);
+  if (state_nt(a.n * SB)) launch_signal(k_kf6t<4, WithNT<E>>, dim3(g + carry), lds, st, a.in.ens_done, a);
   else launch_signal(k_kf6t<4, E>, dim3(g + carry), lds, st, a.in.ens_done, a);
   return (int)g;
 }

@@ -31,8 +31,8 @@ template <class O>
 using WithComp = Opt<O::LIBM, O::UPD, O::PRED, O::SMALL, O::VALID, O::REC, O::NT, O::ENS, true>;
 
 // the compensated entries of COMP: x 0-1 (px, py), packed P 0-2 (P00, P10, P11)
-constexpr unsigned kKf6CXM = 3u;
-constexpr unsigned long long kKf6CPM = 7ull;
+constexpr unsigned kKf6CXM = kPosCXM;
+constexpr unsigned long long kKf6CPM = kPosCPM;
 // the lane's low parts (COMP), one register when unused
 template <class O>
 struct Kf6Lo {
@@ -206,7 +206,7 @@ __device__ __forceinline__ void kf6_tick1(const Kf6In &m, const float *tab, cons
   if (O::UPD && (!O::VALID || m.valid)) {
     float y[4];
     kf6_innov<O::LIBM>(m, tab, x, y);
-    if constexpr (O::COMP) kf_update<MdKF6, -1, float, 6, 4, 21, kKf6CXM, kKf6CPM>(x, P, y, prm.r, l.v);
+    if constexpr (O::COMP) kf_update<MdKF6, -1, float, 6, 4, 21, kKf6CXM, kKf6CPM>(x, P, y, prm.r, nullptr, l.v);
     else kf_update<MdKF6>(x, P, y, prm.r);
   }
   if (O::PRED) {

@@ -217,16 +217,32 @@ __host__ __device__ constexpr int slot_x(int j) { return popc_c(CXM & ((1ull << 
 template <unsigned CXM, unsigned long long CPM>
 __host__ __device__ constexpr int slot_p(int k) { return popc_c(CXM) + popc_c(CPM & ((1ull << k) - 1ull)); }
 
+// FMSKF_CFG_COMP_POS (KF6, EKF9): the compensated entries -- x 0-1 (px, py), packed P 0-2 (P00,
+// P10, P11) -- in the kKf6LoRows low-part rows
+constexpr unsigned kPosCXM = 3u;
+constexpr unsigned long long kPosCPM = 7ull;
+
 // ---------------------------------------------------------------------------
 // generic update / covariance predict (fully unrolled -> registers only)
 // CI >= 0: state CI is compensated (x[CI] + *lo, th_add instead of the plain addition)
-// CXM / CPM: the compensated states / packed P entries (slot_x, slot_p in lo), each added to by
+// CXM / CPM: the compensated states / packed P entries (slot_x, slot_p in clo), each added to by
 // TwoSum and renormalised after the update (x slots first); oracle orc_kf_update_m
 // ---------------------------------------------------------------------------
+// every compensated pair renormalised, x slots first (oracle orc_comp_norm)
+template <unsigned CXM, unsigned long long CPM, typename T, int N, int NP>
+__device__ __forceinline__ void comp_norm(T (&x)[N], T (&P)[NP], T *clo) {
+#pragma unroll
+  for (int j = 0; j < N; j++)
+    if ((CXM >> j) & 1u) th_norm(x[j], clo[slot_x<CXM>(j)]);
+#pragma unroll
+  for (int k = 0; k < NP; k++)
+    if ((CPM >> k) & 1ull) th_norm(P[k], clo[slot_p<CXM, CPM>(k)]);
+}
+
 template <class Md, int CI = -1, typename T = typename Md::T, int N = Md::N, int M = Md::M,
           int NP = Md::N *(Md::N + 1) / 2, unsigned CXM = 0, unsigned long long CPM = 0>
 __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M], const T *R,
-                                          T *lo = nullptr) {
+                                          T *lo = nullptr, T *clo = nullptr) {
   T HP[M][N];
 #pragma unroll
   for (int a = 0; a < M; a++) {
@@ -287,7 +303,7 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
 #pragma unroll
     for (int a = 1; a < M; a++) t = dfma<T>(HP[a][j], vw[a], t);
     if (j == CI) th_add(x[j], *lo, t);
-    else if ((CXM >> j) & 1u) th_add(x[j], lo[slot_x<CXM>(j)], t);
+    else if ((CXM >> j) & 1u) th_add(x[j], clo[slot_x<CXM>(j)], t);
     else x[j] = x[j] + t;
   }
 #pragma unroll
@@ -297,16 +313,11 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
       T t = HP[0][i] * V[0][j];
 #pragma unroll
       for (int a = 1; a < M; a++) t = dfma<T>(HP[a][i], V[a][j], t);
-      if ((CPM >> pk(i, j)) & 1ull) th_add(P[pk(i, j)], lo[slot_p<CXM, CPM>(pk(i, j))], -t);
+      if ((CPM >> pk(i, j)) & 1ull) th_add(P[pk(i, j)], clo[slot_p<CXM, CPM>(pk(i, j))], -t);
       else P[pk(i, j)] = P[pk(i, j)] - t;
     }
   }
-#pragma unroll
-  for (int j = 0; j < N; j++)
-    if ((CXM >> j) & 1u) th_norm(x[j], lo[slot_x<CXM>(j)]);
-#pragma unroll
-  for (int k = 0; k < NP; k++)
-    if ((CPM >> k) & 1ull) th_norm(P[k], lo[slot_p<CXM, CPM>(k)]);
+  comp_norm<CXM, CPM>(x, P, clo);
 }
 
 // Diagonal R: the measurements are independent, so the joint update equals M scalar updates
@@ -315,10 +326,11 @@ __device__ __forceinline__ void kf_update(T (&x)[N], T (&P)[NP], const T (&y)[M]
 // of P, or the sum of two), s = H_a hp + r_aa, g = y_a / s, x += hp g, P -= (hp / s) hp^T.
 // About 2/3 of the LDL^T form's VALU (EKF9: no 6x9 U / V matrices, no forward substitution).
 // Canonical order of oracle orc_kf_update_seq.
+// CXM / CPM (clo): compensated entries as in kf_update, renormalised after the last measurement
 template <class Md, int CI = -1, typename T = typename Md::T, int N = Md::N, int M = Md::M,
-          int NP = Md::N *(Md::N + 1) / 2>
+          int NP = Md::N *(Md::N + 1) / 2, unsigned CXM = 0, unsigned long long CPM = 0>
 __device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], const T *R,
-                                              T *lo = nullptr) {
+                                              T *lo = nullptr, T *clo = nullptr) {
 #pragma unroll
   for (int a = 0; a < M; a++) {
     T hp[N];
@@ -336,6 +348,7 @@ __device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], 
 #pragma unroll
     for (int j = 0; j < N; j++) {
       if (j == CI) th_add(x[j], *lo, hp[j] * g);
+      else if ((CXM >> j) & 1u) th_add(x[j], clo[slot_x<CXM>(j)], hp[j] * g);
       else x[j] = dfma<T>(hp[j], g, x[j]);
     }
 #pragma unroll
@@ -348,9 +361,13 @@ __device__ __forceinline__ void kf_update_seq(T (&x)[N], T (&P)[NP], T (&y)[M], 
     for (int i = 0; i < N; i++) {
       const T t = hp[i] * si;
 #pragma unroll
-      for (int j = 0; j <= i; j++) P[pk(i, j)] = dfma<T>(-t, hp[j], P[pk(i, j)]);
+      for (int j = 0; j <= i; j++) {
+        if ((CPM >> pk(i, j)) & 1ull) th_add(P[pk(i, j)], clo[slot_p<CXM, CPM>(pk(i, j))], -(t * hp[j]));
+        else P[pk(i, j)] = dfma<T>(-t, hp[j], P[pk(i, j)]);
+      }
     }
   }
+  comp_norm<CXM, CPM>(x, P, clo);
 }
 
 // P <- F P F^T + Q, F = I + Fv(i,k) on the compile-time pattern Md::pat

@@ -1,6 +1,6 @@
-"""FMSKF_CFG_COMP_POS: the KF6 with px, py and the position block of P (P00, P10, P11) carried as
-compensated fp32 pairs (hi + lo, every addition a TwoSum), against the oracle's restatement
-(oracle/fmskf_oracle.c orc_kf6_tick_comp) bit for bit -- state, covariance and the five low-part
+"""FMSKF_CFG_COMP_POS: the KF6 (and the EKF9) with px, py and the position block of P (P00, P10,
+P11) carried as compensated fp32 pairs (hi + lo, every addition a TwoSum), against the oracle's
+restatement (oracle/fmskf_oracle.c orc_kf6_tick_comp, orc_ekf9_tick_comp) bit for bit -- state, covariance and the five low-part
 rows -- on every entry point that ticks the filter: tick with planes and records, a validity mask,
 correct / predict alone, tick_many, the fused record (tick_ensemble), the firmware ISR (which runs
 the tick kernel, then the control step and the frame), the non-temporal instantiation, and the
@@ -34,16 +34,24 @@ def _fresh(n):
             np.zeros((5, n), np.float32))
 
 
-def _same(e, xo, Po, lo, what):
+def _same(e, xo, Po, lo, what, exact=True):
+    """bit for bit (TABLE512); LIBM (device sinf / cosf against the host's) within 1e-5"""
     x, P = e.get_state()
     lg = e.get_state_lo()
     assert lg.shape == (5, e.n)
+    if not exact:
+        np.testing.assert_allclose(x, xo, rtol=1e-5, atol=1e-6, err_msg=what)
+        np.testing.assert_allclose(P, Po, rtol=1e-5, atol=1e-9, err_msg=what)
+        return
     for name, a, b in (("x", x, xo), ("P", P, Po), ("lo", lg, lo)):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f"{what}: {name}"
 
 
 @pytest.mark.parametrize("trig", [fmskf.TRIG_TABLE512, fmskf.TRIG_LIBM])
 def test_comp_tick_bitexact(orc, trig):
+    """TABLE512 bit-exact against the oracle; LIBM (the device's sinf / cosf are not the host's)
+    within 1e-5"""
+    exact = trig == fmskf.TRIG_TABLE512
     for n in (1, 777, 5000):
         T = 12
         tr = Trajectory(n, T, seed=900 + n)
@@ -68,12 +76,12 @@ def test_comp_tick_bitexact(orc, trig):
                 else:
                     e.tick(kf6_rec=rec[t])
                     orc.kf6_tick_comp(xo, Po, lo, yaw[t], gz[t], rpm[t], None, prm)
-                _same(e, xo, Po, lo, f"n={n} t={t}")
+                _same(e, xo, Po, lo, f"n={n} t={t}", exact)
             # T ticks in one launch (k_kf6, state and low parts held in registers)
             e.tick_many(T, kf6_rec=rec, valid=valid)
             for t in range(T):
                 orc.kf6_tick_comp(xo, Po, lo, yaw[t], gz[t], rpm[t], valid[t], prm)
-            _same(e, xo, Po, lo, f"n={n} tick_many")
+            _same(e, xo, Po, lo, f"n={n} tick_many", exact)
         assert np.any(lo != 0)  # the low parts carry something
 
 
@@ -128,9 +136,12 @@ def test_comp_state_round_trip_and_checkpoint(orc, tmp_path):
 
 
 def test_comp_config_rules():
-    with pytest.raises(fmskf.FmskfError) as ei:
-        Engine("ekf9", 16, flags=COMP)
-    assert ei.value.code == 5  # FMSKF_ENOTSUP: a KF6 mode
+    for model in ("rs", "kf12d"):
+        with pytest.raises(fmskf.FmskfError) as ei:
+            Engine(model, 16, flags=COMP)
+        assert ei.value.code == 5  # FMSKF_ENOTSUP: a KF6 / EKF9 mode
+    with Engine("ekf9", 16, flags=COMP) as e:
+        assert e.get_state_lo().shape == (6, 16)  # the heading's low part, then the five
     with pytest.raises(fmskf.FmskfError) as ei:
         Engine("kf6", 16, flags=0x80)
     assert ei.value.code == 1
@@ -189,6 +200,22 @@ from oracle import oracle as orc
 for n in (1, 700, 3000):
     T = 5
     tr = Trajectory(n, T, seed=60 + n)
+    raw = tr.ekf9_raw()
+    vm = (np.random.default_rng(n + 1).random((T, n)) > 0.2).astype(np.uint8)
+    cfg = fmskf.default_config("ekf9", n)
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+    xo = np.zeros((10, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    clo = np.zeros((5, n), np.float32)
+    with Engine("ekf9", n, flags=fmskf.CFG_COMP_POS) as e:
+        for t in range(T):
+            e.tick(raw=raw[t], valid=vm[t])
+            orc.ekf9_tick_comp(xo, Po, clo, raw[t], vm[t], prm)
+        x, P = e.get_state()
+        lg = e.get_state_lo()
+    assert np.array_equal(x.view(np.uint32), xo[:9].view(np.uint32)), ("ekf9", n)
+    assert np.array_equal(P.view(np.uint32), Po.view(np.uint32)), ("ekf9", n)
+    assert np.array_equal(lg[1:].view(np.uint32), clo.view(np.uint32)), ("ekf9", n)
     yaw, gz, rpm = tr.kf6_inputs()
     valid = (np.random.default_rng(n).random((T, n)) > 0.2).astype(np.uint8)
     cfg = fmskf.default_config("kf6", n)
@@ -209,11 +236,15 @@ print("comp nt ok")
 """
 
 
-def test_comp_nontemporal_bitexact():
-    """the non-temporal instantiation (chosen once the state outgrows the Infinity Cache) forced
-    at small N in a child process (FMSKF_STATE_NT=1), bit-exact against the oracle"""
+@pytest.mark.parametrize("force", [{"FMSKF_STATE_NT": "1"}, {"FMSKF_KF6_VARIANT": "15", "FMSKF_EKF9_VARIANT": "4"},
+                                   {"FMSKF_STATE_NT": "1", "FMSKF_KF6_VARIANT": "15", "FMSKF_EKF9_VARIANT": "4"}])
+def test_comp_kernel_variants_bitexact(force):
+    """the COMP instantiations the launcher picks past the Infinity Cache, forced at small N in a
+    child process: the non-temporal state (FMSKF_STATE_NT=1) and one robot per lane (k_kf6t /
+    k_ekf9t, FMSKF_KF6_VARIANT=15 / FMSKF_EKF9_VARIANT=4; the default at these sizes is two per
+    lane), KF6 and EKF9, bit-exact against the oracle"""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FMSKF_STATE_NT="1")
+    env = dict(os.environ, **force)
     out = subprocess.run([sys.executable, "-c", _NT_SCRIPT, root,
                           os.path.join(root, "roboken-fmskf-robot-controller_amd")],
                          capture_output=True, text=True, timeout=240, env=env)
@@ -243,3 +274,47 @@ def test_comp_60000_ticks_bitexact(orc):
             _same(e, xo, Po, lo, f"tick {t0 + chunk - 1}")
         assert e.get_counters()[0] == 0
     assert np.abs(xo[:2]).max() > 1.0
+
+
+def _ekf9_run(orc, n, T, seed, r=None, valid=True, many=False):
+    from fmskf.synth import Trajectory as Tr
+    tr = Tr(n, T, seed=seed)
+    raw = tr.ekf9_raw()
+    vm = (np.random.default_rng(seed).random((T, n)) > 0.2).astype(np.uint8) if valid else None
+    cfg = fmskf.default_config("ekf9", n)
+    rr = np.array(cfg.r[:21]) if r is None else r
+    prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), rr, orc.TRIG_TABLE512)
+    xo = np.zeros((10, n), np.float32)
+    Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    clo = np.zeros((5, n), np.float32)
+    with Engine("ekf9", n, r=rr, flags=COMP) as e:
+        if many:
+            e.tick_many(T, raw=raw, valid=vm) if valid else e.tick_many(T, raw=raw)
+        for t in range(T):
+            if not many:
+                if valid:
+                    e.tick(raw=raw[t], valid=vm[t])
+                else:
+                    e.tick(raw=raw[t])
+            orc.ekf9_tick_comp(xo, Po, clo, raw[t], vm[t] if valid else None, prm)
+        x, P = e.get_state()
+        lo = e.get_state_lo()
+    assert np.array_equal(x.view(np.uint32), xo[:9].view(np.uint32)), ("x", n)
+    assert np.array_equal(P.view(np.uint32), Po.view(np.uint32)), ("P", n)
+    assert np.array_equal(lo[0].view(np.uint32), xo[9].view(np.uint32)), ("heading lo", n)
+    assert np.array_equal(lo[1:].view(np.uint32), clo.view(np.uint32)), ("position lo", n)
+    return clo
+
+
+@pytest.mark.parametrize("n", [1, 700, 3000])
+def test_comp_ekf9_bitexact(orc, n):
+    """the EKF9 with compensated positions (orc_ekf9_tick_comp): the sequential scalar update of
+    a diagonal R and the joint LDL^T update of a correlated one, single ticks with a validity
+    mask and tick_many, bit for bit with the heading's and the positions' low parts"""
+    clo = _ekf9_run(orc, n, 8, 70 + n)
+    assert n == 1 or np.any(clo != 0)
+    cfg = fmskf.default_config("ekf9", n)
+    r = np.array(cfg.r[:21])
+    r[4 * 5 // 2 + 3] = 1e-3  # a correlated R (rows 4, 3): the joint update
+    _ekf9_run(orc, n, 6, 80 + n, r=r)
+    _ekf9_run(orc, n, 6, 90 + n, valid=False, many=True)

@@ -1067,22 +1067,19 @@ print("wt901 ok")
 """
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2"])
-def test_wt901_transposed_waves_bitexact(variant):
-    """k_wt901's three store forms (FMSKF_WT901_VARIANT, in a child process): per-lane stores
-    (0), the LDS-transposed stores of a wave whose every lane took the standard poll (1), and
-    those plus the LDS-staged poll rows (2, the default).  Waves of clean standard polls next to
-    waves with one damaged, torn or reordered lane, a partial last wave, N % 8 != 0 (per-lane
-    stores only) and a single wave; every robot's register file, parser backlog, error flag and
-    Data page against the oracle after every poll, bit for bit."""
+def test_wt901_wave_patterns_bitexact():
+    """k_wt901 on wave-structured polls (round 4 measured LDS-transposed stores for waves of
+    standard polls and kept the per-lane form; this pattern set checked all three bit-exact):
+    waves of clean standard polls next to waves with one damaged, torn or reordered lane, a
+    partial last wave, N % 8 != 0 and a single wave; every robot's register file, parser backlog,
+    error flag and Data page against the oracle after every poll, bit for bit (child process)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FMSKF_WT901_VARIANT=variant)
     out = subprocess.run([sys.executable, "-c", _WT901_TR_SCRIPT, root,
                           os.path.join(root, "roboken-fmskf-robot-controller_amd")],
-                         capture_output=True, text=True, timeout=240, env=env)
+                         capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "wt901 ok" in out.stdout
 

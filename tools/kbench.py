@@ -43,7 +43,7 @@ def main():
     e = fmskf.Engine(args.model, n, trig=fmskf.TRIG_LIBM if args.trig == "libm" else fmskf.TRIG_TABLE512,
                      flags=fmskf.CFG_COMP_POS if args.comp else 0)
     if args.comp:
-        BYTES["kf6"] = 272
+        BYTES["kf6"], BYTES["ekf9"] = 272, 488
     st = torch.cuda.current_stream()
     e.set_stream(st)
     yaw, gz, rpm = kf6_ring_torch(n, R, device=dev)

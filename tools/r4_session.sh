@@ -35,6 +35,16 @@ for s in $STEPS; do
                python tools/kbench.py --op wt901 --ticks 30
              run pmc_path_can_ingest_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_can_ingest_2p20_$c" -o run -- \
                python tools/kbench.py --op can --ticks 30
+             run pmc_path_cfg2_kf6_comp_pos_2p20_$c 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_path_cfg2_kf6_comp_pos_2p20_$c" -o run -- \
+               python tools/kbench.py --packed --comp --ticks 30
+           done ;;
+    sqab)  # wave-state counters per SQ_LIST entry "name|VAR=v ...|kbench args" (';'-separated)
+           SQC="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"
+           IFS=';' read -ra SQL <<< "${SQ_LIST:-}"; for ent in "${SQL[@]}"; do
+             IFS='|' read -r nm ev ka <<< "$ent"
+             for kv in $ev; do export "$kv"; done
+             run sq_$nm 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_$nm" -o run -- python tools/kbench.py $ka
+             for kv in $ev; do unset "${kv%%=*}"; done
            done ;;
     sq)    # one pass of wave-state counters per path-row kernel (7 SQ + 1 GRBM: within one pass)
            SQC="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE"
