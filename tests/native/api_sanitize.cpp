@@ -29,6 +29,30 @@ int main() {
   std::printf("create rc=%d (%s) err=%s\n", rc, fmskf_strerror(rc), fmskf_last_error());
   if (rc == FMSKF_OK) fmskf_destroy(h);
   if (fmskf_tick(nullptr, nullptr) != FMSKF_EINVAL) return 7;
+  // ABI 3: an ABI-2 caller, unknown flags, the reserved word and a COMP model mismatch are refused
+  // before any device is touched
+  fmskf_config c2;
+  if (fmskf_config_init(&c2, FMSKF_MODEL_KF6, 100) != FMSKF_OK || c2.abi_version != 3u || c2.flags) return 8;
+  c2.abi_version = 2u;
+  if (fmskf_create(&c2, &h) != FMSKF_EINVAL) return 9;
+  c2.abi_version = FMSKF_ABI_VERSION;
+  c2.flags = 0x80u;
+  if (fmskf_create(&c2, &h) != FMSKF_EINVAL) return 10;
+  c2.flags = 0u;
+  c2.reserved = 1u;
+  if (fmskf_create(&c2, &h) != FMSKF_EINVAL) return 11;
+  if (fmskf_config_init(&c2, FMSKF_MODEL_KF12D, 100) != FMSKF_OK) return 12;
+  c2.flags = FMSKF_CFG_COMP_POS;
+  if (fmskf_create(&c2, &h) != FMSKF_ENOTSUP) return 13;
+  int w = 0, r = 0;
+  if (fmskf_comm_info(nullptr, &w, &r) != FMSKF_EINVAL) return 14;
+  if (fmskf_ensemble_end_count(nullptr, nullptr, nullptr, nullptr, nullptr) != FMSKF_EINVAL) return 15;
+  if (fmskf_get_motor_status(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, FMSKF_MEM_HOST) !=
+      FMSKF_EINVAL)
+    return 16;
+  uint32_t rows = 0;
+  if (fmskf_get_state_lo(nullptr, nullptr, &rows, FMSKF_MEM_HOST) != FMSKF_EINVAL) return 17;
+  (void)strlen(fmskf_rccl_library());
   std::printf("api sanitize ok\n");
   return 0;
 }
