@@ -130,9 +130,13 @@ __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, 
   CtrlLane<true, CPC> L;
   L.load(c, ic);
   tv.store(stab);
-  Kf6Lo<O> lo;  // COMP never runs fused (launch_isr_kf6)
+  Kf6Lo<O> lo;  // O::COMP: the position low parts (FMSKF_CFG_COMP_POS)
+  kf6_load_lo<O>(a.prm.lo, ic, lo);
   kf6_tick1<O>(m, stab, a.prm, x, P, lo);
-  if (live) kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+  if (live) {
+    kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
+    kf6_store_lo<O>(a.prm.lo, i, lo);
+  }
   nan_guard(x, P, a.counters, live);
   if (live) {
     const uint2 cw = L.step(c, p, i, m.rpm);
@@ -247,10 +251,10 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
 // per lane), the control planes in one window.  Returns hipErrorNotSupported otherwise (the
 // caller then runs the three kernels).  Past the Infinity Cache (KF6 state + control state
 // > 256 MiB) the control planes are non-temporal, as in k_isr_rs.
-template <bool LIBM, bool VALID, bool REC>
+template <bool LIBM, bool VALID, bool REC, bool COMP>
 static int isr_kf6_v(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
                      bool nt, hipStream_t st) {
-  using O = Opt<LIBM, true, true, true, VALID, REC>;
+  using O = Opt<LIBM, true, true, true, VALID, REC, false, false, COMP>;
   if (nt) {
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
     k_isr_kf6<O, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames);
@@ -260,6 +264,21 @@ static int isr_kf6_v(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const 
   return (int)hipGetLastError();
 }
 
+template <bool COMP>
+static int isr_kf6_c(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames, bool nt,
+                     hipStream_t st, bool libm, bool valid, bool rec) {
+  if (libm) {
+    if (valid) return rec ? isr_kf6_v<true, true, true, COMP>(a, c, p, frames, nt, st)
+                          : isr_kf6_v<true, true, false, COMP>(a, c, p, frames, nt, st);
+    return rec ? isr_kf6_v<true, false, true, COMP>(a, c, p, frames, nt, st)
+               : isr_kf6_v<true, false, false, COMP>(a, c, p, frames, nt, st);
+  }
+  if (valid) return rec ? isr_kf6_v<false, true, true, COMP>(a, c, p, frames, nt, st)
+                        : isr_kf6_v<false, true, false, COMP>(a, c, p, frames, nt, st);
+  return rec ? isr_kf6_v<false, false, true, COMP>(a, c, p, frames, nt, st)
+             : isr_kf6_v<false, false, false, COMP>(a, c, p, frames, nt, st);
+}
+
 int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
                    const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
   if (c.n == 0) return 0;
@@ -267,18 +286,14 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
   const bool small_ctrl = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   // the tick kernel alone streams its state non-temporal past the cache: keep that regime on
   // the three-kernel path (its own occupancy caps)
-  // FMSKF_CFG_COMP_POS (the position low parts) runs the tick kernel that carries them, then the
-  // control step and the frame
-  if (!small_state || !small_ctrl || state_nt(s.n * 108) || kp.lo) return (int)hipErrorNotSupported;
+  // KF6 state bytes per robot (FMSKF_CFG_COMP_POS: + the position low parts)
+  const uint64_t sb = kp.lo ? 128 : 108;
+  if (!small_state || !small_ctrl || state_nt(s.n * sb)) return (int)hipErrorNotSupported;
   const KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, kp};
-  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * 108);
+  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * sb);
   const bool valid = in.valid != nullptr, rec = in.rec != nullptr;
-  if (libm) {
-    if (valid) return rec ? isr_kf6_v<true, true, true>(a, c, p, frames, nt, st) : isr_kf6_v<true, true, false>(a, c, p, frames, nt, st);
-    return rec ? isr_kf6_v<true, false, true>(a, c, p, frames, nt, st) : isr_kf6_v<true, false, false>(a, c, p, frames, nt, st);
-  }
-  if (valid) return rec ? isr_kf6_v<false, true, true>(a, c, p, frames, nt, st) : isr_kf6_v<false, true, false>(a, c, p, frames, nt, st);
-  return rec ? isr_kf6_v<false, false, true>(a, c, p, frames, nt, st) : isr_kf6_v<false, false, false>(a, c, p, frames, nt, st);
+  return kp.lo ? isr_kf6_c<true>(a, c, p, frames, nt, st, libm, valid, rec)
+               : isr_kf6_c<false>(a, c, p, frames, nt, st, libm, valid, rec);
 }
 
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {

@@ -2,8 +2,8 @@
 P11) carried as compensated fp32 pairs (hi + lo, every addition a TwoSum), against the oracle's
 restatement (oracle/fmskf_oracle.c orc_kf6_tick_comp, orc_ekf9_tick_comp) bit for bit -- state, covariance and the five low-part
 rows -- on every entry point that ticks the filter: tick with planes and records, a validity mask,
-correct / predict alone, tick_many, the fused record (tick_ensemble), the firmware ISR (which runs
-the tick kernel, then the control step and the frame), the non-temporal instantiation, and the
+correct / predict alone, tick_many, the fused record (tick_ensemble), the fused firmware ISR
+(k_isr_kf6: tick, control step and frame in one kernel), the non-temporal instantiation, and the
 state / checkpoint round trips.  Its accuracy against float64 over 60 s is
 tests/test_oracle_kf_long.py's (every state within 1e-5, positions and P at 6e-8)."""
 import os
@@ -153,7 +153,7 @@ def test_comp_config_rules():
 
 def test_comp_fused_record_and_isr(orc):
     """the fused tick + record of a COMP handle equals its stand-alone record of the same state;
-    its firmware ISR (tick kernel, control step, 0x200 frame) equals the three calls"""
+    its fused firmware ISR (one kernel: tick, control step, 0x200 frame) equals the three calls"""
     n, T = 4097, 6
     tr = Trajectory(n, T, seed=5)
     yaw, gz, rpm = tr.kf6_inputs()

@@ -6,7 +6,8 @@ matches it bit for bit (tests/test_gpu_parity.py), so what is measured here is t
 the library itself.  The reference is oracle/kf_dense_ref.c (full matrices, LU solve, Joseph
 update in float64; checked against the numpy restatement oracle/kf_ref.py below), fed the same
 fp32 measurement vectors.  Horizon: BASELINE.json configs[0]'s 60 000 ticks (60 s at 1 kHz),
-1024 robots (trajectory_chunks), every 100th tick compared.
+512 robots here (trajectory_chunks; the DESIGN.md figures are 1024-robot runs of the same
+functions), every 100th tick compared.
 
 Errors are relative per physical quantity over the fleet (the normwise relative error of that
 quantity's vector across robots): for state k in group g,
@@ -29,6 +30,8 @@ North-star bar 1e-5.  Measured over 60 000 ticks:
   P 6.1e-5; EKF9 positions 3.1e-5, P 1.1e-5).  With FMSKF_CFG_COMP_POS (KF6; compensated px, py
   and position block of P) every state is within 1e-5 over the whole horizon (5.8e-8 / 6.0e-8).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -38,7 +41,10 @@ from oracle import kf_ref
 
 TOL = 1e-5
 T_LONG = 60000
-N_LONG = 1024
+N_LONG = 512
+# the oracle's worker threads (0: one per core) only when pytest runs serially: under xdist every
+# worker would start one per core on each of the 60 000 ticks
+NTHREADS = 1 if os.environ.get("PYTEST_XDIST_WORKER") else 0
 EVERY = 100
 GROUPS = {6: {"pos": (0, 1), "th": (2,), "vel": (3, 4), "rate": (5,)},
           9: {"pos": (0, 1), "th": (2,), "vel": (3, 4), "rate": (5, 6), "acc": (7, 8)}}
@@ -79,16 +85,16 @@ def run_long(orc, model, n=N_LONG, ticks=T_LONG, every=EVERY, seed=0x464D534B ^ 
             if model == "kf6":
                 z = orc.kf6_measure(yaw[k], gz[k], rpm[k], orc.TRIG_TABLE512)
                 if comp:
-                    orc.kf6_tick_comp(x, P, lo, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=0)
+                    orc.kf6_tick_comp(x, P, lo, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=NTHREADS)
                 else:
-                    orc.kf6_tick(x, P, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=0)
+                    orc.kf6_tick(x, P, yaw[k], gz[k], rpm[k], valid[k], prm, nthreads=NTHREADS)
                 ref.step(z.astype(np.float64), valid[k])
             else:
                 z = orc.ekf9_measure(raw[k])
                 if comp:
-                    orc.ekf9_tick_comp(x, P, lo, raw[k], None, prm, nthreads=0)
+                    orc.ekf9_tick_comp(x, P, lo, raw[k], None, prm, nthreads=NTHREADS)
                 else:
-                    orc.ekf9_tick(x, P, raw[k], None, prm, nthreads=0)
+                    orc.ekf9_tick(x, P, raw[k], None, prm, nthreads=NTHREADS)
                 ref.step(z.astype(np.float64))
             t = t0 + k
             if t % every == every - 1:
@@ -122,19 +128,19 @@ def _assert_long(model, samples, gerr, perr, observable, caps=None):
 
 
 @pytest.mark.slow
-def test_kf6_60000_ticks_1024_robots_vs_fp64(orc):
+def test_kf6_60000_ticks_vs_fp64(orc):
     samples, gerr, perr = run_long(orc, "kf6")
     _assert_long("kf6", samples, gerr, perr, ("th", "vel", "rate"), CAPS["kf6"])
 
 
 @pytest.mark.slow
-def test_ekf9_60000_ticks_1024_robots_vs_fp64(orc):
+def test_ekf9_60000_ticks_vs_fp64(orc):
     samples, gerr, perr = run_long(orc, "ekf9")
     _assert_long("ekf9", samples, gerr, perr, ("th", "vel", "rate", "acc"), CAPS["ekf9"])
 
 
 @pytest.mark.slow
-def test_kf6_comp_pos_60000_ticks_1024_robots_vs_fp64(orc):
+def test_kf6_comp_pos_60000_ticks_vs_fp64(orc):
     """FMSKF_CFG_COMP_POS (orc_kf6_tick_comp, which the GPU matches bit for bit): with px, py and
     the position block of P carried as compensated pairs, EVERY state -- the positions and the
     covariance included -- stays within the north star's 1e-5 of the float64 filter over the whole
@@ -149,8 +155,8 @@ def test_kf6_comp_pos_60000_ticks_1024_robots_vs_fp64(orc):
 def test_ekf9_comp_pos_60000_ticks_vs_fp64(orc):
     """the EKF9 with FMSKF_CFG_COMP_POS (orc_ekf9_tick_comp; its heading is compensated in any
     case): every state within 1e-5 of the float64 filter over 60 s (measured at 1024 robots:
-    positions 2.1e-7, P 2.2e-8, against 3.1e-5 / 1.1e-5 without); 512 robots here"""
-    samples, gerr, perr = run_long(orc, "ekf9", n=512, comp=True)
+    positions 2.1e-7, P 2.2e-8, against 3.1e-5 / 1.1e-5 without)"""
+    samples, gerr, perr = run_long(orc, "ekf9", comp=True)
     _assert_long("ekf9 comp", samples, gerr, perr, ("th", "vel", "rate", "acc"))
     assert gerr["pos"].max() <= 1e-6 and perr.max() <= 1e-6
 
