@@ -551,8 +551,12 @@ def test_wt901_ingest_random_streams(orc, stride):
 
 
 # ----------------------------------------------------------------------------- CAN ingest
-@pytest.mark.parametrize("masked", [True, False])  # wheel per lane (k_can) / robot per lane (k_can4)
+@pytest.mark.parametrize("masked", [True, False, "mixed"])
 def test_can_ingest_bitexact(orc, masked, n=1001):
+    """masked: every tick with a `present` mask (k_can, wheel per lane); False: every wheel
+    present (k_can4, robot per lane); "mixed": one masked tick in three, so the robots' Status
+    ring heads fall out of step and k_can4 blocks meet robots whose wheels sit in other slots
+    of the angle ring than the block's first robot."""
     T = 25
     rng = np.random.default_rng(7)
     dirs = [1, 1, -1, -1]
@@ -564,8 +568,9 @@ def test_can_ingest_bitexact(orc, masked, n=1001):
             frames[rng.random((n, 4)) < 0.05, 0] |= 0x80  # some out-of-range / negative
             stamps = rng.integers(0, 0x8000, (n, 4)).astype(np.int16)
             stamps[rng.random((n, 4)) < 0.05] = 1234  # equal stamps -> usec_dlt == 0
-            present = rng.integers(0, 16, n).astype(np.uint8) if masked else np.full(n, 15, np.uint8)
-            e.ingest_can(frames, stamps, present if masked else None)
+            mask_now = masked is True or (masked == "mixed" and t % 3 == 1)
+            present = rng.integers(0, 16, n).astype(np.uint8) if mask_now else np.full(n, 15, np.uint8)
+            e.ingest_can(frames, stamps, present if mask_now else None)
             for i in range(n):
                 for w in range(4):
                     if (present[i] >> w) & 1:
@@ -1098,6 +1103,7 @@ def test_can_rs_per_plane_descriptor_forms_bitexact():
         "from oracle import oracle as orc\n"
         "import test_gpu_parity as T\n"
         "T.test_can_ingest_bitexact(orc, False)\n"
+        "T.test_can_ingest_bitexact(orc, 'mixed')\n"
         "T.test_rs_tick_bitexact(orc, T.TABLE)\n"
         "T.test_rs_tick_bitexact(orc, T.LIBM)\n"
         "print('planes ok')\n")

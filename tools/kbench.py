@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--many", type=int, default=0, help="ticks per launch (tick_many)")
     ap.add_argument("--packed", action="store_true", help="KF6: fmskf_kf6_record inputs")
     ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
+    ap.add_argument("--can-desync", action="store_true",
+                    help="--op can: one masked tick before timing (robots' ring heads out of step)")
     ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
@@ -339,6 +341,8 @@ def bench_io(args, e, n, R, dev, rpm, st):
         stp = [torch.from_numpy((np.arange(4)[None, :] * 250 + k * 1000 + np.zeros((n, 1))).astype(np.int16)).to(dev)
                for k in range(4)]
         run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
+        if args.can_desync:  # one masked tick first: random robots' Status ring heads fall out of step
+            e.ingest_can(fr[0], stp[0], torch.from_numpy(rng.integers(0, 16, n).astype(np.uint8)).to(dev))
         # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), head 1, IIR y / x (4 + 4) and
         # the int64 sum read and written; rpm, curr, the previous angle (2 + 2 + 2) written
         bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2 + 2)

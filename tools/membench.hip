@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #define CK(x)                                                                 \
   do {                                                                        \
@@ -523,6 +524,44 @@ __global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, 
   for (int k = 0; k < NS; k++) dst[o + k * T] = s[k] + m;
 }
 
+// a path row's byte mix with no arithmetic (membench LG 1 mix): RO read-only, RW read and
+// written, WO write-only dword planes per robot, planar at a padded pitch (plane_pitch: n
+// rounded to 512 + 256; an exact power-of-two stride aliases), V robots per lane (dword /
+// dwordx2 accesses) -- the streaming ceiling of a kernel moving those bytes in the same regime
+template <int RO, int RW, int WO, int V>
+__global__ __launch_bounds__(256) void k_mix(uint32_t *st, uint64_t n, uint64_t pitch, uint32_t sink) {
+  using T = typename std::conditional<V == 1, uint32_t, uint2>::type;
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n / V) return;
+  T s[RW + 1];
+  uint32_t m = sink;
+#pragma unroll
+  for (int k = 0; k < RW; k++) s[k] = reinterpret_cast<const T *>(st + k * pitch)[v];
+#pragma unroll
+  for (int k = 0; k < RO; k++) {
+    const T r = reinterpret_cast<const T *>(st + (RW + k) * pitch)[v];
+    if constexpr (V == 1) m ^= r;
+    else m ^= r.x ^ r.y;
+  }
+#pragma unroll
+  for (int k = 0; k < RW; k++) {
+    T t = s[k];
+    if constexpr (V == 1) t ^= (m & 1);
+    else {
+      t.x ^= (m & 1);
+      t.y ^= (m & 1);
+    }
+    reinterpret_cast<T *>(st + k * pitch)[v] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < WO; k++) {
+    T t;
+    if constexpr (V == 1) t = m + k;
+    else t = make_uint2(m + k, m - k);
+    reinterpret_cast<T *>(st + (RW + RO + k) * pitch)[v] = t;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -595,6 +634,41 @@ int main(int argc, char **argv) {
         tm("kf12d_nt_fma1536", kb, [&] { k_tiled_delay64<90, 1536><<<g, 256, L>>>(sb, ib, n, 0.0); });
         tm("kf12d_nt_fma2048", kb, [&] { k_tiled_delay64<90, 2048><<<g, 256, L>>>(sb, ib, n, 0.0); });
       }
+    return 0;
+  }
+  if (argc > 3 && argv[3][0] == 'm') {
+    // membench LG 1 mix: the path rows' byte mixes (bench.py PATH_BYTES, pmc_traffic.py PATHS;
+    // the CAN RX's 124 / 108 is the KF6 tick's)
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    uint32_t *mb;
+    CK(hipMalloc(&mb, (size_t)64 * (n + 1024) * 4));
+    k_fill_rand<<<4096, 256>>>(mb, (uint64_t)64 * (n + 1024), 5);
+    CK(hipDeviceSynchronize());
+    auto tm = [&](const char *name, int bpr, auto launch) {
+      for (int w = 0; w < 5; w++) launch();
+      for (int rep = 0; rep < 2; rep++) {
+        CK(hipEventRecord(f0));
+        for (int it = 0; it < 50; it++) launch();
+        CK(hipEventRecord(f1));
+        CK(hipEventSynchronize(f1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, f0, f1));
+        const double us = ms * 1e3 / 50;
+        printf("{\"n\": %llu, \"mix\": \"%s\", \"bytes_per_robot\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+               (unsigned long long)n, name, bpr, us, (double)bpr * n / (us * 1e-6) / 1e9);
+      }
+    };
+    const uint64_t pp = ((n + 511) / 512) * 512 + 256;
+    const unsigned g1 = (unsigned)((n + 255) / 256), g2 = (unsigned)((n / 2 + 255) / 256);
+    tm("kf6_r124_w108", 232, [&] { k_mix<4, 27, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
+    tm("kf6_r124_w108_x2", 232, [&] { k_mix<4, 27, 0, 2><<<g2, 256>>>(mb, n, pp, 0); });
+    tm("rs_r84_w56", 140, [&] { k_mix<7, 14, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
+    tm("rs_r84_w56_x2", 140, [&] { k_mix<7, 14, 0, 2><<<g2, 256>>>(mb, n, pp, 0); });
+    tm("wt901_r88_w108", 196, [&] { k_mix<0, 22, 5, 1><<<g1, 256>>>(mb, n, pp, 0); });
+    tm("wt901_r88_w108_x2", 196, [&] { k_mix<0, 22, 5, 2><<<g2, 256>>>(mb, n, pp, 0); });
+    tm("ekf9_r224_w224", 448, [&] { k_mix<0, 56, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
     return 0;
   }
   if (argc > 3 && argv[3][0] == 'o') {

@@ -53,6 +53,10 @@ for s in $STEPS; do
            run sq_wt901 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_wt901" -o run -- python tools/kbench.py --op wt901 --ticks 30
            run sq_can 120 rocprofv3 --pmc $SQC --output-format csv -d "$OUT/sq_can" -o run -- python tools/kbench.py --op can --ticks 30
            ;;
+    mix)   # streaming ceilings of the path rows' byte mixes (tools/membench.hip k_mix) at 2^20 and 2^22
+           [ -x build/membench ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/membench.hip -o build/membench
+           run mix20 120 build/membench 20 1 mix
+           run mix22 120 build/membench 22 1 mix ;;
     kb)    # KB_LIST: entries separated by ';', each "[VAR=value ...] kbench args"; KB_PASSES passes
            for p in $(seq 1 "${KB_PASSES:-1}"); do
              i=0; IFS=';' read -ra KBL <<< "${KB_LIST:-}"; for ent in "${KBL[@]}"; do
