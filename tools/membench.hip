@@ -524,25 +524,34 @@ __global__ __launch_bounds__(256) void k_model_tiled_pp(const TT *src, TT *dst, 
   for (int k = 0; k < NS; k++) dst[o + k * T] = s[k] + m;
 }
 
-// a path row's byte mix with no arithmetic (membench LG 1 mix): RO read-only, RW read and
-// written, WO write-only dword planes per robot, planar at a padded pitch (plane_pitch: n
-// rounded to 512 + 256; an exact power-of-two stride aliases), V robots per lane (dword /
-// dwordx2 accesses) -- the streaming ceiling of a kernel moving those bytes in the same regime
-template <int RO, int RW, int WO, int V>
-__global__ __launch_bounds__(256) void k_mix(uint32_t *st, uint64_t n, uint64_t pitch, uint32_t sink) {
+// a path row's byte mix with no arithmetic (membench LG 1 mix): RI dword planes of tick inputs
+// read from a ring of 16 tick slots (as tools/kbench.py feeds the kernels: fresh inputs every
+// tick), RW state planes read and written, WO state planes only written, V robots per lane
+// (dword / dwordx2 accesses), planar at a padded pitch (plane_pitch: n rounded to 512 + 256;
+// an exact power-of-two stride aliases) -- the streaming ceiling of a kernel moving those bytes
+// in the same cache regime.  W > 0: the state tiled instead ([n/W][planes][W], V == 1).
+template <int RI, int RW, int WO, int V, int W = 0>
+__global__ __launch_bounds__(256) void k_mix(uint32_t *st, const uint32_t *in, uint64_t n, uint64_t pitch,
+                                             uint32_t sink) {
   using T = typename std::conditional<V == 1, uint32_t, uint2>::type;
-  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (v >= n / V) return;
-  T s[RW + 1];
   uint32_t m = sink;
 #pragma unroll
-  for (int k = 0; k < RW; k++) s[k] = reinterpret_cast<const T *>(st + k * pitch)[v];
-#pragma unroll
-  for (int k = 0; k < RO; k++) {
-    const T r = reinterpret_cast<const T *>(st + (RW + k) * pitch)[v];
+  for (int k = 0; k < RI; k++) {
+    const T r = reinterpret_cast<const T *>(in + k * pitch)[v];
     if constexpr (V == 1) m ^= r;
     else m ^= r.x ^ r.y;
   }
+  uint64_t sp = pitch;
+  if constexpr (W > 0) {  // plane k of robot v at tile base + k * W
+    st += (v / W) * (uint64_t)(RW + WO) * W;
+    v %= W;
+    sp = W;
+  }
+  T s[RW + 1];
+#pragma unroll
+  for (int k = 0; k < RW; k++) s[k] = reinterpret_cast<const T *>(st + k * sp)[v];
 #pragma unroll
   for (int k = 0; k < RW; k++) {
     T t = s[k];
@@ -551,15 +560,49 @@ __global__ __launch_bounds__(256) void k_mix(uint32_t *st, uint64_t n, uint64_t 
       t.x ^= (m & 1);
       t.y ^= (m & 1);
     }
-    reinterpret_cast<T *>(st + k * pitch)[v] = t;
+    reinterpret_cast<T *>(st + k * sp)[v] = t;
   }
 #pragma unroll
   for (int k = 0; k < WO; k++) {
     T t;
     if constexpr (V == 1) t = m + k;
     else t = make_uint2(m + k, m - k);
-    reinterpret_cast<T *>(st + (RW + RO + k) * pitch)[v] = t;
+    reinterpret_cast<T *>(st + (RW + k) * sp)[v] = t;
   }
+}
+
+// the same with the planes' access widths of the real kernels: dword (A4) and qword (A8) planes
+// of ring-fed inputs (RI), state read and written (RW) and state written (WO), one robot per lane
+template <int RI4, int RI8, int RW4, int RW8, int WO4, int WO8>
+__global__ __launch_bounds__(256) void k_mixw(uint32_t *st, const uint32_t *in, uint64_t n, uint64_t pitch,
+                                              uint32_t sink) {
+  const uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  uint32_t m = sink;
+#pragma unroll
+  for (int k = 0; k < RI4; k++) m ^= in[k * pitch + v];
+#pragma unroll
+  for (int k = 0; k < RI8; k++) {
+    const uint2 r = reinterpret_cast<const uint2 *>(in + (RI4 + 2 * k) * pitch)[v];
+    m ^= r.x ^ r.y;
+  }
+  uint32_t a[RW4 + 1];
+  uint2 b[RW8 + 1];
+#pragma unroll
+  for (int k = 0; k < RW4; k++) a[k] = st[k * pitch + v];
+#pragma unroll
+  for (int k = 0; k < RW8; k++) b[k] = reinterpret_cast<const uint2 *>(st + (RW4 + 2 * k) * pitch)[v];
+#pragma unroll
+  for (int k = 0; k < RW4; k++) st[k * pitch + v] = a[k] ^ (m & 1);
+#pragma unroll
+  for (int k = 0; k < RW8; k++)
+    reinterpret_cast<uint2 *>(st + (RW4 + 2 * k) * pitch)[v] = make_uint2(b[k].x ^ (m & 1), b[k].y);
+  constexpr int B = RW4 + 2 * RW8;
+#pragma unroll
+  for (int k = 0; k < WO4; k++) st[(B + k) * pitch + v] = m + k;
+#pragma unroll
+  for (int k = 0; k < WO8; k++)
+    reinterpret_cast<uint2 *>(st + (B + WO4 + 2 * k) * pitch)[v] = make_uint2(m + k, m - k);
 }
 
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
@@ -637,38 +680,53 @@ int main(int argc, char **argv) {
     return 0;
   }
   if (argc > 3 && argv[3][0] == 'm') {
-    // membench LG 1 mix: the path rows' byte mixes (bench.py PATH_BYTES, pmc_traffic.py PATHS;
-    // the CAN RX's 124 / 108 is the KF6 tick's)
+    // membench LG 1 mix: the path rows' byte mixes (bench.py PATH_BYTES, pmc_traffic.py PATHS),
+    // tick inputs from a 16-slot ring / state read+written / state written, in dwords per robot:
+    //   KF6 record tick 4 / 27 / 0 (124 r, 108 w); RS tick 11 / 10 / 4 (84, 56);
+    //   CAN RX 10 / 21 / 6 (124, 108); WT901 standard poll 13 / 9 / 18 (88, 108)
     hipEvent_t f0, f1;
     CK(hipEventCreate(&f0));
     CK(hipEventCreate(&f1));
-    uint32_t *mb;
-    CK(hipMalloc(&mb, (size_t)64 * (n + 1024) * 4));
-    k_fill_rand<<<4096, 256>>>(mb, (uint64_t)64 * (n + 1024), 5);
+    const uint64_t pp = ((n + 511) / 512) * 512 + 256;
+    constexpr int kRing = 16;
+    uint32_t *mb, *ib;
+    CK(hipMalloc(&mb, (size_t)64 * pp * 4));
+    CK(hipMalloc(&ib, (size_t)kRing * 16 * pp * 4));
+    k_fill_rand<<<4096, 256>>>(mb, (uint64_t)64 * pp, 5);
+    k_fill_rand<<<4096, 256>>>(ib, (uint64_t)kRing * 16 * pp, 6);
     CK(hipDeviceSynchronize());
+    int tick = 0;
     auto tm = [&](const char *name, int bpr, auto launch) {
-      for (int w = 0; w < 5; w++) launch();
+      for (int w = 0; w < 2 * kRing; w++) launch(ib + (size_t)(tick++ % kRing) * 16 * pp);
       for (int rep = 0; rep < 2; rep++) {
         CK(hipEventRecord(f0));
-        for (int it = 0; it < 50; it++) launch();
+        for (int it = 0; it < 64; it++) launch(ib + (size_t)(tick++ % kRing) * 16 * pp);
         CK(hipEventRecord(f1));
         CK(hipEventSynchronize(f1));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, f0, f1));
-        const double us = ms * 1e3 / 50;
+        const double us = ms * 1e3 / 64;
         printf("{\"n\": %llu, \"mix\": \"%s\", \"bytes_per_robot\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
                (unsigned long long)n, name, bpr, us, (double)bpr * n / (us * 1e-6) / 1e9);
       }
     };
-    const uint64_t pp = ((n + 511) / 512) * 512 + 256;
     const unsigned g1 = (unsigned)((n + 255) / 256), g2 = (unsigned)((n / 2 + 255) / 256);
-    tm("kf6_r124_w108", 232, [&] { k_mix<4, 27, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
-    tm("kf6_r124_w108_x2", 232, [&] { k_mix<4, 27, 0, 2><<<g2, 256>>>(mb, n, pp, 0); });
-    tm("rs_r84_w56", 140, [&] { k_mix<7, 14, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
-    tm("rs_r84_w56_x2", 140, [&] { k_mix<7, 14, 0, 2><<<g2, 256>>>(mb, n, pp, 0); });
-    tm("wt901_r88_w108", 196, [&] { k_mix<0, 22, 5, 1><<<g1, 256>>>(mb, n, pp, 0); });
-    tm("wt901_r88_w108_x2", 196, [&] { k_mix<0, 22, 5, 2><<<g2, 256>>>(mb, n, pp, 0); });
-    tm("ekf9_r224_w224", 448, [&] { k_mix<0, 56, 0, 1><<<g1, 256>>>(mb, n, pp, 0); });
+    tm("kf6_in16_rw108", 232, [&](const uint32_t *in) { k_mix<4, 27, 0, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("kf6_in16_rw108_tiled2048", 232, [&](const uint32_t *in) { k_mix<4, 27, 0, 1, 2048><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("rs_in44_rw40_w16", 140, [&](const uint32_t *in) { k_mix<11, 10, 4, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("rs_in44_rw40_w16_x2", 140, [&](const uint32_t *in) { k_mix<11, 10, 4, 2><<<g2, 256>>>(mb, in, n, pp, 0); });
+    tm("rs_in44_rw40_w16_tiled2048", 140, [&](const uint32_t *in) { k_mix<11, 10, 4, 1, 2048><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("can_in40_rw84_w24", 232, [&](const uint32_t *in) { k_mix<10, 21, 6, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("can_in40_rw84_w24_x2", 232, [&](const uint32_t *in) { k_mix<10, 21, 6, 2><<<g2, 256>>>(mb, in, n, pp, 0); });
+    tm("can_in40_rw84_w24_tiled2048", 232, [&](const uint32_t *in) { k_mix<10, 21, 6, 1, 2048><<<g1, 256>>>(mb, in, n, pp, 0); });
+    // the real kernels' access widths: RS yaw / rpm + 4 sums, px py / 4 prev, th vx vy vth;
+    // CAN 40 B of frame + stamps as 5 qwords, head + 8 IIR / micro angle + 4 sums, prev rpm curr
+    tm("rs_widths_q", 140, [&](const uint32_t *in) { k_mixw<1, 5, 2, 4, 4, 0><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("rs_widths_d", 140, [&](const uint32_t *in) { k_mixw<11, 0, 10, 0, 4, 0><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("can_widths_q", 232, [&](const uint32_t *in) { k_mixw<0, 5, 9, 6, 0, 3><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("can_widths_d", 232, [&](const uint32_t *in) { k_mixw<10, 0, 21, 0, 6, 0><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("wt901_in52_rw36_w72", 196, [&](const uint32_t *in) { k_mix<13, 9, 18, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
+    tm("wt901_in52_rw36_w72_tiled2048", 196, [&](const uint32_t *in) { k_mix<13, 9, 18, 1, 2048><<<g1, 256>>>(mb, in, n, pp, 0); });
     return 0;
   }
   if (argc > 3 && argv[3][0] == 'o') {
