@@ -144,7 +144,10 @@ struct Wt901Parser {
 // 35.8-35.9 us with a block barrier and 35.4-35.7 with wave-local ordering; fetching the
 // wave's poll rows as contiguous 1 KiB runs through LDS as well, 36.9-37.0; forcing 8 waves
 // per SIMD (64 VGPRs, 20 B of scratch), 37.2; 24 / 32 KiB occupancy caps, 34.6-36.6.  The
-// narrow stores are not what bounds the kernel, and none of these was kept.
+// narrow stores are not what bounds the kernel, and none of these was kept.  Nor the KF6 tick's
+// cache policies through buffer descriptors (same box, against 35.4-36.9 plain): `sc1` state
+// stores 36.0-36.3; `nt` poll-row loads 41.2-42.0, since a 16-byte load of 48-byte rows uses a
+// third of every line it touches and `nt` evicts the line before the next load reads the rest.
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   const uint64_t n = a.n;
