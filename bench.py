@@ -577,21 +577,49 @@ def main():
 
     if args.gather == "auto":
         args.gather = "async" if (gloo or args.same_device) else "native"
+    def native_comm(e):
+        """the handle's own RCCL communicator: rank 0's unique id reaches the others over the
+        torch.distributed group, then fmskf_comm_init on every rank.  Returns every rank's error
+        (empty when every communicator came up): all ranks learn the same list over torch's own
+        group, so on any failure they all measure with torch's all-gather instead, and the line
+        says why -- a failure is reported, never silent."""
+        err, uid = None, [None]
+        if rank == 0:
+            try:
+                uid = [fmskf.comm_unique_id()]
+            except Exception as ex:  # noqa: BLE001
+                err = f"rank 0: fmskf_comm_unique_id: {ex}"
+        dist.broadcast_object_list(uid, src=0)
+        if err is None and uid[0] is None:
+            err = f"rank {rank}: no communicator id from rank 0"
+        elif err is None:
+            try:
+                e.comm_init(uid[0], rank, world)
+            except Exception as ex:  # noqa: BLE001
+                err = f"rank {rank}: fmskf_comm_init: {ex}"
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        return [x for x in errs if x]
+
     rccl = None
+    gather_fallback = None
     if args.gather == "native" and distributed:
         # the handle's own RCCL communicator: rank 0's unique id reaches the others over the
         # torch.distributed group (without a launcher there is no communicator: the fold writes
         # this GPU's record straight into the handle's pinned result slot)
-        uid = [fmskf.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0], rank, world)
-        # what RCCL itself reports (ncclCommCount / ncclCommUserRank), from every rank: a
-        # one-rank communicator inside an N-process job would show here
-        cw, cr = eng.comm_info()
-        seen = [None] * world
-        dist.all_gather_object(seen, (cw, cr))
-        rccl = {"ranks": cw, "user_ranks": sorted(r for _, r in seen), "sizes": sorted({w for w, _ in seen}),
-                "library": fmskf.rccl_library()}
+        errs = native_comm(eng)
+        if errs:
+            gather_fallback = {"from": "native", "to": "async", "errors": errs}
+            print(f"bench: fmskf_comm_init failed ({errs[0]}); measuring with --gather async", file=sys.stderr)
+            args.gather = "async"
+        else:
+            # what RCCL itself reports (ncclCommCount / ncclCommUserRank), from every rank: a
+            # one-rank communicator inside an N-process job would show here
+            cw, cr = eng.comm_info()
+            seen = [None] * world
+            dist.all_gather_object(seen, (cw, cr))
+            rccl = {"ranks": cw, "user_ranks": sorted(r for _, r in seen), "sizes": sorted({w for w, _ in seen}),
+                    "library": fmskf.rccl_library()}
     native_stats = [None]
     native_pending = [0]
     # ring index of every tick applied to `eng`, in order: the post-timing parity replay
@@ -656,10 +684,11 @@ def main():
         native4 = args.gather == "native"
         info = None
         if native4 and distributed:
-            uid4 = [fmskf.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid4, src=0)
-            e4.comm_init(uid4[0], rank, world)
-            info = e4.comm_info()
+            errs4 = native_comm(e4)
+            if errs4:  # every rank falls back together (torch's all-gather)
+                native4 = False
+            else:
+                info = e4.comm_info()
         rb = torch.empty(e4.ensemble_record_len(), dtype=torch.float64, device=dev)
         gb = torch.empty(world, e4.ensemble_record_len(), dtype=torch.float64, device=dev)
         pend, last = [0], [None]
@@ -686,7 +715,9 @@ def main():
             collect(0)
 
         res = {"instances_total": n_total, "instances_this_rank": n4, "n_gpus": world, "scaling": "strong",
-               "inputs": "records", "gather": args.gather}
+               "inputs": "records", "gather": args.gather if native4 or args.gather != "native" else "async"}
+        if not native4 and args.gather == "native":
+            res["gather_fallback"] = errs4
         for label, every in (("ensemble_every_16", 16), ("ensemble_every_1", 1)):
             run(every, 2 * every + 6)  # warm-up: every kernel and result slot of this sequence
             torch.cuda.synchronize()
@@ -964,6 +995,8 @@ def main():
     }
     if ens_check is not None:
         out["ensemble_check"] = ens_check
+    if gather_fallback is not None:
+        out["gather_fallback"] = gather_fallback
     if rccl is not None:
         # the communicator libfmskf's asynchronous exchange ran over, as RCCL reports it
         out["rccl_ranks"] = rccl["ranks"]

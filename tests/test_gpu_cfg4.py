@@ -152,3 +152,31 @@ def test_bench_world2_rehearsal_same_gpu(strong, gather, tmp_path):
     assert c4["ensemble_every_16"]["steps_per_s"] > 0 and c4["ensemble_every_1"]["steps_per_s"] > 0
     if gather == "native":
         assert c4["rccl_ranks"] == 2
+
+
+def test_bench_native_gather_falls_back_together(tmp_path):
+    """When libfmskf's communicator cannot come up (here FMSKF_RCCL_LIBRARY names a missing
+    library, so fmskf_comm_unique_id fails on rank 0), every rank learns it over torch's group and
+    all of them measure with torch's all-gather instead; the line says so (`gather_fallback`, the
+    config's gather "async"), the ensemble check stays green and cfg4_16M measures the same way,
+    instead of the 8-GPU run dying or its ranks disagreeing."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1",
+               FMSKF_RCCL_LIBRARY=str(tmp_path / "missing_librccl.so"))
+    n = 1 << 18
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "16", "--warmup", "4", "--ensemble-every", "8", "--n-per-gpu", str(n),
+           "--no-cpu-baseline", "--no-fused", "--no-secondary", "--backend", "gloo", "--same-device",
+           "--check-ensemble", "--gather", "native", "--cfg4-steps", "16"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    fb = out["gather_fallback"]
+    assert fb["from"] == "native" and fb["to"] == "async" and fb["errors"], fb
+    assert out["config"]["gather"] == "async" and "rccl_ranks" not in out
+    chk = out["ensemble_check"]
+    assert chk["count"] == 2 * n and chk["mean_max_rel"] < 1e-12 and chk["cov_max_rel"] < 1e-9, chk
+    c4 = out["cfg4_16M"]
+    assert c4["gather"] == "async", c4  # the run had already fallen back
+    assert c4["gathered_count"] == 1 << 24
+
