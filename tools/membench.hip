@@ -605,6 +605,45 @@ __global__ __launch_bounds__(256) void k_mixw(uint32_t *st, const uint32_t *in, 
     reinterpret_cast<uint2 *>(st + (B + WO4 + 2 * k) * pitch)[v] = make_uint2(m + k, m - k);
 }
 
+// the WT901 poll's exact accesses with no parsing (membench LG 1 mix): the lane's 48-byte poll
+// row as three 16-byte loads and its length (ring-fed), the parser window (3 dword planes), the
+// count / flags / error byte planes, 3 magnetometer and 15 written int16 register planes of a
+// [0x90][n] register file, 4 q_init and 16 Data-page dword planes.  PACK: count, flags and
+// error in one dword plane instead of three byte planes
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_mix_wt901(const uint4 *rows, const uint32_t *len, uint32_t *parser,
+                                                   uint8_t *cnt, uint8_t *flg, uint8_t *err, uint32_t *packed,
+                                                   int16_t *reg, const float *qinit, float *data, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint4 a = rows[3 * i], b = rows[3 * i + 1], c = rows[3 * i + 2];
+  uint32_t m = a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ len[i];
+  const uint32_t p0 = parser[i], p1 = parser[n + i], p2 = parser[2 * n + i];
+  uint32_t st;
+  if constexpr (PACK) st = packed[i];
+  else st = cnt[i] | ((uint32_t)flg[i] << 8);
+  m ^= p0 ^ p1 ^ p2 ^ st;
+  const int16_t h0 = reg[0x3a * n + i], h1 = reg[0x3b * n + i], h2 = reg[0x3c * n + i];
+  float q[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) q[k] = qinit[k * n + i];
+  m ^= (uint32_t)(h0 ^ h1 ^ h2);
+  parser[i] = p0 ^ m;
+  parser[n + i] = p1;
+  parser[2 * n + i] = p2;
+  if constexpr (PACK) packed[i] = st ^ (m & 0xFF0000u);
+  else {
+    cnt[i] = (uint8_t)st;
+    flg[i] = (uint8_t)(st >> 8);
+    err[i] = (uint8_t)m;
+  }
+  const uint32_t rk[15] = {0x34, 0x35, 0x36, 0x40, 0x37, 0x38, 0x39, 0x3d, 0x3e, 0x3f, 0x2e, 0x51, 0x52, 0x53, 0x54};
+#pragma unroll
+  for (int k = 0; k < 15; k++) reg[rk[k] * n + i] = (int16_t)(m >> k);
+#pragma unroll
+  for (int k = 0; k < 16; k++) data[k * n + i] = q[k & 3] + (float)(m & 7) * (float)k;
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -725,6 +764,37 @@ int main(int argc, char **argv) {
     tm("rs_widths_d", 140, [&](const uint32_t *in) { k_mixw<11, 0, 10, 0, 4, 0><<<g1, 256>>>(mb, in, n, pp, 0); });
     tm("can_widths_q", 232, [&](const uint32_t *in) { k_mixw<0, 5, 9, 6, 0, 3><<<g1, 256>>>(mb, in, n, pp, 0); });
     tm("can_widths_d", 232, [&](const uint32_t *in) { k_mixw<10, 0, 21, 0, 6, 0><<<g1, 256>>>(mb, in, n, pp, 0); });
+    {
+      // the WT901 poll's exact planes (k_mix_wt901); rows from a 16-slot ring of [n][48 B]
+      uint8_t *wb;
+      const size_t rowb = (size_t)n * 48, regb = (size_t)0x90 * n * 2;
+      const size_t tot = kRing * rowb + kRing * n * 4 + 3 * n * 4 + 3 * n + n * 4 + regb + 4 * n * 4 + 16 * n * 4;
+      CK(hipMalloc(&wb, tot));
+      k_fill_rand<<<4096, 256>>>((uint32_t *)wb, tot / 4, 11);
+      CK(hipDeviceSynchronize());
+      uint8_t *q = wb + kRing * rowb;
+      uint32_t *lens = (uint32_t *)q;
+      q += kRing * n * 4;
+      uint32_t *par = (uint32_t *)q;
+      q += 3 * n * 4;
+      uint8_t *cn = q, *fl = q + n, *er = q + 2 * n;
+      q += 3 * n;
+      uint32_t *pk = (uint32_t *)((uintptr_t)(q + 3) & ~(uintptr_t)3);
+      q += n * 4;
+      int16_t *rg = (int16_t *)q;
+      q += regb;
+      float *qi = (float *)q, *dt = (float *)(q + 4 * n * 4);
+      int slot = 0;
+      auto w = [&](bool pack) {
+        const int s = slot++ % kRing;
+        const uint4 *rows = (const uint4 *)(wb + s * rowb);
+        if (pack) k_mix_wt901<true><<<g1, 256>>>(rows, lens + s * n, par, cn, fl, er, pk, rg, qi, dt, n);
+        else k_mix_wt901<false><<<g1, 256>>>(rows, lens + s * n, par, cn, fl, er, pk, rg, qi, dt, n);
+      };
+      tm("wt901_exact_planes", 197, [&](const uint32_t *) { w(false); });
+      tm("wt901_exact_planes_packed_bytes", 197, [&](const uint32_t *) { w(true); });
+      CK(hipFree(wb));
+    }
     tm("wt901_in52_rw36_w72", 196, [&](const uint32_t *in) { k_mix<13, 9, 18, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
     tm("wt901_in52_rw36_w72_tiled2048", 196, [&](const uint32_t *in) { k_mix<13, 9, 18, 1, 2048><<<g1, 256>>>(mb, in, n, pp, 0); });
     return 0;
