@@ -644,6 +644,44 @@ __global__ __launch_bounds__(256) void k_mix_wt901(const uint4 *rows, const uint
   for (int k = 0; k < 16; k++) data[k * n + i] = q[k & 3] + (float)(m & 7) * (float)k;
 }
 
+// the same planes with two adjacent IMUs per lane: every int16 register access a dword, every
+// dword plane a dwordx2, the byte planes 2 bytes, the two 48-byte rows six 16-byte loads
+__global__ __launch_bounds__(256) void k_mix_wt901_pair(const uint4 *rows, const uint32_t *len, uint32_t *parser,
+                                                        uint8_t *cnt, uint8_t *flg, uint8_t *err, int16_t *reg,
+                                                        const float *qinit, float *data, uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;  // IMUs 2j, 2j + 1
+  if (2 * j >= n) return;
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const uint4 a = rows[6 * j + k];
+    m ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  const uint2 l = reinterpret_cast<const uint2 *>(len)[j];
+  m ^= l.x ^ l.y;
+  uint2 pw[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pw[k] = reinterpret_cast<const uint2 *>(parser + k * n)[j];
+  const uint16_t c2 = reinterpret_cast<const uint16_t *>(cnt)[j], f2 = reinterpret_cast<const uint16_t *>(flg)[j];
+  m ^= pw[0].x ^ pw[1].y ^ pw[2].x ^ c2 ^ f2;
+#pragma unroll
+  for (int k = 0; k < 3; k++) m ^= reinterpret_cast<const uint32_t *>(reg + (0x3a + k) * n)[j];
+  float2 q[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) q[k] = reinterpret_cast<const float2 *>(qinit + k * n)[j];
+#pragma unroll
+  for (int k = 0; k < 3; k++) reinterpret_cast<uint2 *>(parser + k * n)[j] = make_uint2(pw[k].x ^ m, pw[k].y);
+  reinterpret_cast<uint16_t *>(cnt)[j] = (uint16_t)(c2 ^ m);
+  reinterpret_cast<uint16_t *>(flg)[j] = (uint16_t)(f2 ^ (m >> 3));
+  reinterpret_cast<uint16_t *>(err)[j] = (uint16_t)(m >> 5);
+  const uint32_t rk[15] = {0x34, 0x35, 0x36, 0x40, 0x37, 0x38, 0x39, 0x3d, 0x3e, 0x3f, 0x2e, 0x51, 0x52, 0x53, 0x54};
+#pragma unroll
+  for (int k = 0; k < 15; k++) reinterpret_cast<uint32_t *>(reg + rk[k] * n)[j] = m >> k;
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    reinterpret_cast<float2 *>(data + k * n)[j] = make_float2(q[k & 3].x + (float)(m & 7) * (float)k, q[k & 3].y);
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -793,6 +831,11 @@ int main(int argc, char **argv) {
       };
       tm("wt901_exact_planes", 197, [&](const uint32_t *) { w(false); });
       tm("wt901_exact_planes_packed_bytes", 197, [&](const uint32_t *) { w(true); });
+      const unsigned gp = (unsigned)((n / 2 + 255) / 256);
+      tm("wt901_exact_planes_two_per_lane", 197, [&](const uint32_t *) {
+        const int s = slot++ % kRing;
+        k_mix_wt901_pair<<<gp, 256>>>((const uint4 *)(wb + s * rowb), lens + s * n, par, cn, fl, er, rg, qi, dt, n);
+      });
       CK(hipFree(wb));
     }
     tm("wt901_in52_rw36_w72", 196, [&](const uint32_t *in) { k_mix<13, 9, 18, 1><<<g1, 256>>>(mb, in, n, pp, 0); });
