@@ -440,7 +440,6 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_prev, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_head, 0, 4 * n, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_sum, 0, 4 * s.m_pitch * 8, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
@@ -515,7 +514,6 @@ void ensure_motors(fmskf_ctx *h) {
   s.m_prev = h->alloc<int16_t>(4 * n);
   s.m_rpm = h->alloc<int16_t>(4 * n);
   s.m_curr = h->alloc<int16_t>(4 * n);
-  s.m_head = h->alloc<uint8_t>(4 * n);
   s.m_pitch = plane_pitch(n);
   s.m_sum = h->alloc<int64_t>(4 * s.m_pitch);
   s.m_iir_y = h->alloc<float>(4 * n);
@@ -1170,7 +1168,6 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
   if (groups & 4) {
     for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
-    v.push_back({s.m_head, (size_t)4 * n});
     v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
     for (void *p : {(void *)s.m_iir_y, (void *)s.m_iir_x})
       v.push_back({p, (size_t)4 * n * 4});

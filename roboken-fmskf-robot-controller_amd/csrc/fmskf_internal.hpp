@@ -47,7 +47,6 @@ struct DevState {
                                // flt_dltOutAngle_rad is formed from the two at readout
   int16_t *m_rpm = nullptr;    // [N][4]
   int16_t *m_curr = nullptr;   // [N][4]
-  uint8_t *m_head = nullptr;   // [N][4]
   int64_t *m_sum = nullptr;    // [4][m_pitch]: the encoder sums the RS tick reads, at a padded
                                // plane pitch (a power-of-two stride N aliases: RS tick 2^20
                                // 27.5-27.8 us from [4][2^20] sums, 24.7 from [4][2^20 + 512])

@@ -348,7 +348,6 @@ struct CanArgs {
   int8_t dir[4];
   int16_t *micro, *angle, *rpm, *curr;
   int16_t *prev;  // [N][4] the angle before this frame (Status::flt_dltOutAngle_rad at readout)
-  uint8_t *head;
   int64_t *sum;  // [4][sum_pitch]
   uint64_t sum_pitch;
   float *iir_y, *iir_x;  // UTIL::IIR1 state; y is also Status::flt_SpeedRadPS
@@ -368,21 +367,21 @@ __device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
 }
 
 // one wheel's rx_callback on its 8-byte frame and microsecond stamp (VD_motor_if_m2006.cpp:
-// 32-72): the decoded fields, the ring-buffer head, the IIR1 speed state and the int64 sum
+// 32-72): the decoded fields, the IIR1 speed state and the int64 sum.  The Status ring's head
+// (:33-34, 71) is not kept: both readers, get_status_latest and get_status_estimate
+// (VD_motor_if_m2006.hpp:44-47, .cpp:11-24), read only the newest entry, which is what the
+// engine stores, so the head selects nothing that can be observed (round 4: 232 -> 224 B)
 struct CanWheel {
   int16_t angle, rpm, curr;
-  uint32_t head;
   float iir_y, iir_x;
   int64_t sum;
 };
 __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t micro, int dir,
-                                              int16_t old_micro, int16_t old_angle, uint32_t old_head,
+                                              int16_t old_micro, int16_t old_angle,
                                               float py, float pxv, int64_t sum) {
   const uint32_t b0 = fx & 0xFF, b1 = (fx >> 8) & 0xFF, b2 = (fx >> 16) & 0xFF, b3 = fx >> 24;
   const uint32_t b4 = fy & 0xFF, b5 = (fy >> 8) & 0xFF;
   CanWheel o;
-  o.head = old_head + 1u;
-  if (o.head >= 3u) o.head = 0;
   const int16_t new_angle =
       dir == 1 ? s16_of(b0, b1) : (int16_t)(K::raw_per_rot - s16_of(b0, b1));
   o.angle = new_angle;
@@ -414,7 +413,7 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
   const uint64_t pw = (uint64_t)w * n + i;
   const uint64_t ps = (uint64_t)w * a.sum_pitch + i;
-  const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g], a.head[g],
+  const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g],
                                a.iir_y[pw], a.iir_x[pw], a.sum[ps]);
   a.iir_y[pw] = o.iir_y;
   a.iir_x[pw] = o.iir_x;
@@ -424,7 +423,6 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   a.angle[g] = o.angle;
   a.rpm[g] = o.rpm;
   a.curr[g] = o.curr;
-  a.head[g] = (uint8_t)o.head;
 }
 
 // one wheel per lane: any `present` mask (absent wheels keep their state).  Grid-stride: 4 N
@@ -466,7 +464,6 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   const uint4 f01 = make_uint4(v0[0], v0[1], v0[2], v0[3]);
   const uint4 f23 = make_uint4(v1[0], v1[1], v1[2], v1[3]);
   uint64_t sv, mv, av;
-  uint32_t oh;
   // SO: the [N][4] arrays and the [4][N] arrays' chunk bases, wheel planes at soffset w * pitch
   const auto r_iy = rsrc_span(a.iir_y + hb), r_ix = rsrc_span(a.iir_x + hb), r_sm = rsrc_span(a.sum + hb);
   const uint32_t pf = (uint32_t)(n * 4), ps = (uint32_t)(a.sum_pitch * 8);
@@ -474,7 +471,6 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
     mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);
     av = ld_span<uint64_t, LP>(rsrc_span(a.angle + hb * 4), li, 0);
-    oh = ld_span<uint32_t, LP>(rsrc_span(a.head + hb * 4), li, 0);
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       py[w] = ld_span<float, LP>(r_iy, li, w * pf);
@@ -485,7 +481,6 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     sv = ld_chunk<uint64_t, IP>(reinterpret_cast<const uint64_t *>(a.stamps), hb, n, li);
     mv = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.micro), hb, n, li);
     av = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.angle), hb, n, li);
-    oh = ld_chunk<uint32_t, LP>(reinterpret_cast<const uint32_t *>(a.head), hb, n, li);
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       py[w] = ld_chunk<float, LP>(a.iir_y + (uint64_t)w * n, hb, n, li);
@@ -497,13 +492,12 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   const uint2 om = make_uint2((uint32_t)mv, (uint32_t)(mv >> 32)), oa = make_uint2((uint32_t)av, (uint32_t)(av >> 32));
   const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
   const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
-  uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0}, nh = 0;
+  uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0};
 #pragma unroll
   for (int w = 0; w < 4; w++) {
     const int sh = 16 * (w & 1);
     const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
-                                 (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
-                                 (oh >> (8 * w)) & 0xFF, py[w], px[w], sm[w]);
+                                 (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh), py[w], px[w], sm[w]);
     if constexpr (SO) {
       st_span<float, SP>(r_iy, li, w * pf, o.iir_y);
       st_span<float, SP>(r_ix, li, w * pf, o.iir_x);
@@ -516,7 +510,6 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
     nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
     nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
-    nh |= o.head << (8 * w);
   }
   const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
   if constexpr (SO) {
@@ -525,14 +518,12 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
     st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, av);
     st_span<uint64_t, SP>(rsrc_span(a.rpm + hb * 4), li, 0, pk(nr[0], nr[1]));
     st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
-    st_span<uint32_t, SP>(rsrc_span(a.head + hb * 4), li, 0, nh);
   } else {
     st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.micro), hb, n, li, pk(st.x, st.y));
     st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.angle), hb, n, li, pk(na[0], na[1]));
     st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.prev), hb, n, li, av);
     st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.rpm), hb, n, li, pk(nr[0], nr[1]));
     st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.curr), hb, n, li, pk(nc[0], nc[1]));
-    st_chunk<uint32_t, SP>(reinterpret_cast<uint32_t *>(a.head), hb, n, li, nh);
   }
 }
 
@@ -549,7 +540,6 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.prev = s.m_prev;
   a.rpm = s.m_rpm;
   a.curr = s.m_curr;
-  a.head = s.m_head;
   a.sum = s.m_sum;
   a.sum_pitch = s.m_pitch;
   a.iir_y = s.m_iir_y;

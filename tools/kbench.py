@@ -343,9 +343,9 @@ def bench_io(args, e, n, R, dev, rpm, st):
         run = lambda k: e.ingest_can(fr[k % 4], stp[k % 4])  # noqa: E731
         if args.can_desync:  # one masked tick first: random robots' Status ring heads fall out of step
             e.ingest_can(fr[0], stp[0], torch.from_numpy(rng.integers(0, 16, n).astype(np.uint8)).to(dev))
-        # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), head 1, IIR y / x (4 + 4) and
-        # the int64 sum read and written; rpm, curr, the previous angle (2 + 2 + 2) written
-        bpr = 4 * (10 + 2 * (2 + 2 + 1 + 4 + 4 + 8) + 2 + 2 + 2)
+        # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), IIR y / x (4 + 4) and the int64
+        # sum read and written; rpm, curr, the previous angle (2 + 2 + 2) written
+        bpr = 4 * (10 + 2 * (2 + 2 + 4 + 4 + 8) + 2 + 2 + 2)
     for k in range(10):
         run(k)
     torch.cuda.synchronize()
