@@ -234,9 +234,10 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
                      int64_t *angle_sum, float *speed_radps, uint32_t mem);
 /* MOTOR_IF_M2006::get_status_latest (VD_motor_if_m2006.hpp:23-30,47-50) for every wheel of every
  * robot, [N][4] each (FL, BL, BR, FR): s16_microsec_id, s16_rawAngle, s16_rawSpeedRpm,
- * s16_rawCurr, flt_dltOutAngle_rad (VD_motor_if_m2006.cpp:64: the unwrapped raw angle step of
- * the last frame x OUT_RAD_PER_RAW_ANGLE x GEAR_RATIO_INV, formed at readout from the last two
- * angles), flt_SpeedRadPS.  Any pointer may be NULL. */
+ * s16_rawCurr, flt_dltOutAngle_rad (VD_motor_if_m2006.cpp:64: the raw angle difference of the
+ * last two frames, not wrap-corrected, as the firmware computes it -- a wheel crossing 8191 -> 0
+ * reports about -2*pi/36 rad -- x OUT_RAD_PER_RAW_ANGLE x GEAR_RATIO_INV, formed at readout from
+ * the last two angles), flt_SpeedRadPS.  Any pointer may be NULL. */
 int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle, int16_t *rpm,
                            int16_t *curr, float *dlt_out_angle_rad, float *speed_radps, uint32_t mem);
 /* counters: [0] = instances whose state went non-finite (NaN/Inf guard) */
@@ -278,10 +279,15 @@ int fmskf_comm_init(fmskf_handle h, const uint8_t id[FMSKF_COMM_ID_BYTES], int r
 /* The handle's communicator as RCCL itself reports it (ncclCommCount, ncclCommUserRank);
  * EINVAL when the handle has none. */
 int fmskf_comm_info(fmskf_handle h, int *world, int *rank);
-/* The file the RCCL entry points were resolved from (dladdr of ncclAllGather; "" before the
- * first communicator call or when RCCL cannot be loaded).  FMSKF_RCCL_LIBRARY may name another
- * file only if it exports `fmskf_rccl_stand_in` (the tests' one-GPU loopback): a deployed
- * controller cannot have its collective swapped by the environment. */
+/* The file the RCCL entry points were resolved from (dladdr of ncclAllGather), or "" while no
+ * communicator call has loaded RCCL yet or when it cannot be loaded.  It never loads RCCL itself,
+ * and the string stays valid and unchanged for the life of the process.  FMSKF_RCCL_LIBRARY may
+ * name another file for the tests' one-GPU loopback stand-in: the library is accepted only if
+ * its dynamic symbol table (read from the file before it is loaded, so a rejected file's
+ * constructors never run) exports `fmskf_rccl_stand_in`.  That refuses an RCCL build or another
+ * collective library picked up by mistake; it is not a defence against a hostile library, which
+ * can export the same marker -- an environment that can set FMSKF_RCCL_LIBRARY can already load
+ * code into the process. */
 const char *fmskf_rccl_library(void);
 /* mean [n], cov packed [n(n+1)/2] (unbiased) over every robot of every rank (the ranks of
  * fmskf_comm_init; without a communicator, this handle's robots): device partial record,

@@ -230,7 +230,7 @@ __device__ __forceinline__ void ens_fold_block(const double *__restrict__ blocks
     else if (k <= (uint32_t)NX) r = shift[k - 1] + (c > 0.0 ? tot[3] / c : 0.0);
     else r = c > 0.0 ? tot[3] - tot[1] * tot[2] / c : 0.0;
     // a system-scope store (written through the caches): `out` may be a pinned host slot the
-    // host reads behind an event without the system-scope release (fmskf_api.cpp kSyncEvent)
+    // host reads behind an event without the system-scope release (api_ctx.hpp kSyncEvent)
     __hip_atomic_store(out + k, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }

@@ -1,4 +1,4 @@
-// fmskf_internal.hpp -- structures shared by the C-ABI layer (fmskf_api.cpp) and the
+// fmskf_internal.hpp -- structures shared by the C-ABI layer (api_*.cpp) and the
 // kernel launchers (kernels_*.hip).  Not part of the public ABI.
 #pragma once
 #include <cstdlib>

@@ -13,8 +13,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (MEM_DEVICE, MEM_HOST, MODEL_EKF9, MODEL_KF6, MODEL_KF12D, MODEL_NAMES,
-                   MODEL_RS, TRIG_LIBM, TRIG_TABLE512, Config, CtrlParams, TickInputs, check,
-                   load)
+                   MODEL_RS, TRIG_LIBM, TRIG_TABLE512, Config, CtrlParams, ENOTSUP, FmskfError,
+                   TickInputs, check, load)
 
 # fmskf_vehicle_info (include/fmskf.h): the VehicleInfo message layout, 84 bytes
 VEHICLE_INFO_DTYPE = np.dtype([("pos_x", "<i4"), ("pos_y", "<i4"), ("pos_theta", "<f4"),
@@ -274,6 +274,23 @@ class Engine:
         return lo
 
     def set_state_lo(self, lo):
+        """restore the hidden low-part rows: `lo` must be [rows][N] float32 (host or device),
+        rows as get_state_lo returns them"""
+        if lo is None:
+            raise ValueError("set_state_lo: lo is None")
+        rows = C.c_uint32()
+        check(load().fmskf_get_state_lo(self.h, None, C.byref(rows), MEM_HOST), "get_state_lo")
+        if rows.value == 0:
+            raise FmskfError(ENOTSUP, "set_state_lo", "this model keeps no low-part rows")
+        want = (rows.value, self.n)
+        if tuple(lo.shape) != want:
+            raise ValueError(f"set_state_lo: shape {tuple(lo.shape)}, want {want}")
+        if _is_torch(lo):
+            import torch
+            if lo.dtype != torch.float32:
+                raise ValueError(f"set_state_lo: dtype {lo.dtype}, want float32")
+        elif np.asarray(lo).dtype != np.float32:
+            raise ValueError(f"set_state_lo: dtype {np.asarray(lo).dtype}, want float32")
         a = _Args()
         check(load().fmskf_set_state_lo(self.h, a.ptr(lo, np.float32), a.mem), "set_state_lo")
 

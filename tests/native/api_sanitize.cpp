@@ -1,4 +1,4 @@
-// api_sanitize.cpp -- TEST INFRASTRUCTURE: the library's host code (csrc/fmskf_api.cpp, built
+// api_sanitize.cpp -- TEST INFRASTRUCTURE: the library's host code (csrc/api_*.cpp, built
 // with -Xarch_host -fsanitize=address,undefined; device code unchanged) driven through the
 // entry points that need no GPU: config / model / control-parameter defaults, the host
 // ensemble fold, status strings, argument rejection, and fmskf_create failing cleanly without

@@ -52,7 +52,7 @@ struct Exchange {
   unsigned long seq;
   size_t bytes;
   char *host;  // pinned
-  int status;
+  hipEvent_t done;  // behind the exchange's last copy: the buffer may be freed once it completed
 };
 typedef LoopComm *ncclComm_t;
 
@@ -92,6 +92,8 @@ ncclResult_t ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return 4;
   for (Exchange *x : comm->pending) {
+    (void)hipEventSynchronize(x->done);
+    (void)hipEventDestroy(x->done);
     (void)hipHostFree(x->host);
     delete x;
   }
@@ -140,11 +142,30 @@ static int exchange(const LoopComm *c, unsigned long seq, char *host, size_t byt
   return 0;
 }
 
-// the host function of callback mode: runs in stream order, calls no HIP API
+// the host function of callback mode: runs in stream order, calls no HIP API.  ncclAllGather
+// returned success long ago, so a failed exchange cannot be reported through it: the process
+// aborts instead of leaving the receive buffer with stale bytes (test infrastructure only)
 static void exchange_cb(void *arg) {
   Exchange *x = (Exchange *)arg;
-  x->status = exchange(x->comm, x->seq, x->host, x->bytes);
-  if (x->status) fprintf(stderr, "loopback_rccl: callback exchange %lu failed\n", x->seq);
+  if (exchange(x->comm, x->seq, x->host, x->bytes) != 0) {
+    fprintf(stderr, "loopback_rccl: callback exchange %lu failed: aborting\n", x->seq);
+    abort();
+  }
+}
+
+// free the pinned buffers of exchanges whose stream work has completed
+static void reap(LoopComm *c) {
+  size_t k = 0;
+  for (Exchange *x : c->pending) {
+    if (hipEventQuery(x->done) == hipSuccess) {
+      (void)hipEventDestroy(x->done);
+      (void)hipHostFree(x->host);
+      delete x;
+    } else {
+      c->pending[k++] = x;
+    }
+  }
+  c->pending.resize(k);
 }
 
 ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataType_t type, ncclComm_t comm,
@@ -155,15 +176,22 @@ ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataT
   const unsigned long seq = comm->seq++;
   const char *mode = getenv("LOOPBACK_RCCL_MODE");
   if (mode && strcmp(mode, "callback") == 0) {
-    Exchange *x = new Exchange{comm, seq, bytes, nullptr, 0};
+    reap(comm);
+    Exchange *x = new Exchange{comm, seq, bytes, nullptr, nullptr};
     if (hipHostMalloc((void **)&x->host, bytes * comm->world, hipHostMallocDefault) != hipSuccess) {
+      delete x;
+      return 2;
+    }
+    if (hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+      (void)hipHostFree(x->host);
       delete x;
       return 2;
     }
     comm->pending.push_back(x);
     if (hipMemcpyAsync(x->host + bytes * comm->rank, send, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipLaunchHostFunc(stream, exchange_cb, x) != hipSuccess ||
-        hipMemcpyAsync(recv, x->host, bytes * comm->world, hipMemcpyHostToDevice, stream) != hipSuccess)
+        hipMemcpyAsync(recv, x->host, bytes * comm->world, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipEventRecord(x->done, stream) != hipSuccess)
       return 2;
     return 0;
   }

@@ -206,3 +206,27 @@ def test_rccl_override_needs_the_stand_in_marker():
         out = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=120,
                              env=dict(os.environ, FMSKF_RCCL_LIBRARY=loop, LOOPBACK_RCCL_DIR="/tmp"))
         assert out.stdout.strip() == "ok " + loop, out.stdout + out.stderr
+
+
+def test_rccl_override_refused_before_load(tmp_path):
+    """a library named by FMSKF_RCCL_LIBRARY without the stand-in marker is refused from its ELF
+    dynamic symbol table, before dlopen: its constructor never runs.  fmskf_rccl_library never
+    loads RCCL itself: "" before any communicator call"""
+    import subprocess
+    import sys
+    src = tmp_path / "ctor.c"
+    marker = tmp_path / "ran"
+    src.write_text('#include <stdio.h>\n__attribute__((constructor)) static void c(void) {'
+                   ' FILE *f = fopen("%s", "w"); if (f) fclose(f); }\n'
+                   'int ncclGetUniqueId(void *id) { (void)id; return 0; }\n' % marker)
+    so = tmp_path / "libctor.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    pkg = os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")
+    script = ("import sys\nsys.path.insert(0, sys.argv[1])\nimport fmskf\n"
+              "print('before', repr(fmskf.rccl_library()))\n"
+              "try:\n    fmskf.comm_unique_id()\n    print('ok')\n"
+              "except fmskf.FmskfError as e:\n    print('refused', e.code)\n")
+    out = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, FMSKF_RCCL_LIBRARY=str(so)))
+    assert "before ''" in out.stdout and "refused 4" in out.stdout, out.stdout + out.stderr
+    assert not marker.exists(), "the refused library's constructor ran"

@@ -118,6 +118,15 @@ def test_comp_state_round_trip_and_checkpoint(orc, tmp_path):
         a.save_state(ck)
         b.set_state(x, P)
         assert not np.any(b.get_state_lo())  # set_state restarts the low parts
+        # the host mirror checks shape and dtype before the library reads rows x N floats
+        for bad in (None, lo[:, :-1], lo[:-1], lo.astype(np.float64),
+                    __import__("torch").from_numpy(lo.astype(np.float64)).cuda()):
+            with pytest.raises(ValueError):
+                b.set_state_lo(bad)
+        with Engine("kf6", 64) as plain:
+            with pytest.raises(fmskf.FmskfError):
+                plain.set_state_lo(np.zeros((5, 64), np.float32))
+        b.set_state_lo(__import__("torch").from_numpy(lo).cuda())
         b.set_state_lo(lo)
         c.load_state(ck)
         for t in range(T, 2 * T):

@@ -1,5 +1,5 @@
 """Host-resident inputs and outputs of up to 1 MiB per call go through the handle's pinned slots
-(fmskf_api.cpp `Stager`, `copy_out_sync`): by default the kernels read the
+(api_ctx.hpp `Stager`, api_handle.cpp `copy_out_sync`): by default the kernels read the
 packed inputs and write their host-bound frames in place over PCIe.  The boundary's contract
 (caller-owned pointers, no retention after return) must hold whatever the
 staging: a caller may overwrite its host buffer as soon as a call returns, and asynchronous

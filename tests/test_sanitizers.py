@@ -3,7 +3,7 @@
 * The oracle (the parity checker): oracle/sanitize_main.c drives every entry point of
   oracle/fmskf_oracle.c on random and adversarial inputs (garbage WT901 streams, CAN extremes,
   NaN / huge KF inputs, validity masks, control events, empty ensemble ranges).
-* The library's host code (csrc/fmskf_api.cpp built with -Xarch_host sanitizers):
+* The library's host code (csrc/api_*.cpp built with -Xarch_host sanitizers):
   tests/native/api_sanitize.cpp exercises the entry points that need no GPU and fmskf_create's
   clean failure without a device.
 Any sanitizer report aborts the program (halt / abort on error)."""
