@@ -34,6 +34,65 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_STEP = {"kf6": 2 * 6 * 4 + 2 * 21 * 4 + 16}
 
 
+def event_ms(stream, run, ticks: int, prequeue: int = 8) -> float:
+    """Average GPU time per call of `run(k)` over `ticks` back-to-back calls between two HIP events
+    on `stream` (the stream the kernels run on).  `prequeue` calls are queued before the first
+    event, so the GPU is already busy when it is recorded and the host's launch lag at the start
+    stays outside the timed span (round 4 recorded the first event on an idle stream: the
+    average then exceeded the step itself)."""
+    import torch
+    for k in range(prequeue):
+        run(k)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for k in range(ticks):
+        run(prequeue + k)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / ticks
+
+
+def mall_regime(state_and_input_bytes: float) -> str:
+    """'hbm+mall' while one launch's state and inputs fit the 256 MiB Infinity Cache (MALL), so
+    part of the traffic is served there; 'hbm' once they stream from HBM.  The headline passes
+    124 B x N (the KF6 state read plus the 16-byte record); the other lines half their
+    algorithmic bytes (every state byte is read once and written once)"""
+    return "hbm+mall" if state_and_input_bytes <= (256 << 20) else "hbm"
+
+
+def traffic_of(entry):
+    """(PMC bytes per launch, where they came from) of a profiles/pmc_traffic*.json entry"""
+    if not isinstance(entry, dict) or "hbm_bytes_per_launch" not in entry:
+        return None, None
+    src = entry.get("source") or {}
+    what = f"{src.get('round', '?')} rocprofv3 FETCH_SIZE + WRITE_SIZE passes of {src.get('kernel', entry.get('kernel'))}"
+    if src.get("committed_as"):
+        what += " (" + ", ".join(src["committed_as"]) + ")"
+    return entry["hbm_bytes_per_launch"], what
+
+
+def scaling_diag(per_rank, exch_per_rank, value: float, ms_per_step: float, tick_ms_max: float) -> dict:
+    """Why an N > 1 line's value is what it is.  per_rank: (rank, robots, plain-tick kernel ms) of
+    every rank, measured with no collective in flight; exch_per_rank: every rank's side-stream
+    exchange times (ms) of the timed region's ensemble events (fmskf_ensemble_exchange_ms).
+    scaling_self = value / the sum of the ranks' plain-tick rates: 1.0 is perfect weak scaling of
+    the kernels themselves; what is missing went to launch gaps, the ensemble ticks' record
+    epilogue, the barrier and the exchange."""
+    rates = [nr / (ms * 1e-3) for _, nr, ms in per_rank]
+    kms = [ms for _, _, ms in per_rank]
+    diag = {"tick_kernel_ms_min": min(kms), "tick_kernel_ms_max": max(kms), "tick_kernel_ms_per_rank": kms,
+            "rank_local_rate_sum": sum(rates), "scaling_self": value / sum(rates),
+            "ms_per_step_over_tick_kernel": ms_per_step / tick_ms_max}
+    allx = [v for r in exch_per_rank for v in (r or [])]
+    diag["exchange_ms"] = None if not allx else {
+        "what": "side stream: ncclAllGather of the 28-double record + copy of the gathered records to "
+                "pinned host memory (fmskf_ensemble_exchange_ms)",
+        "events_per_rank": max(len(r or []) for r in exch_per_rank), "mean": sum(allx) / len(allx),
+        "max_over_ranks": max(allx), "per_rank_max": [max(r) if r else None for r in exch_per_rank]}
+    return diag
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -169,8 +228,8 @@ def secondary_configs(dev, stream, ticks: int, trig):
         tpath = os.path.join(ROOT, "profiles", tname)
         if os.path.exists(tpath):
             try:
-                sec_traffic.update({k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
-                                    if isinstance(v, dict) and "hbm_bytes_per_launch" in v})
+                sec_traffic.update({k: (*traffic_of(v), f"profiles/{tname}") for k, v in json.load(open(tpath)).items()
+                                    if traffic_of(v)[0] is not None})
             except Exception:
                 pass
     # algorithmic bytes per robot-tick as SURVEY.md 8(d) prices them (x and P read and written +
@@ -208,14 +267,7 @@ def secondary_configs(dev, stream, ticks: int, trig):
         for k in range(3):
             e.tick_prepared(preps[k % R])
         torch.cuda.synchronize()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        for k in range(ticks):
-            e.tick_prepared(preps[k % R])
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        ms = ev0.elapsed_time(ev1) / ticks
+        ms = event_ms(stream, lambda k: e.tick_prepared(preps[k % R]), ticks)
         cnt = e.get_counters()
         e.close()
         del preps, keep
@@ -224,7 +276,10 @@ def secondary_configs(dev, stream, ticks: int, trig):
         out[key] = {"model": model, "instances": n, "steps_per_s": n / (ms * 1e-3), "kernel_ms": ms,
                     "ticks": ticks, "nonfinite_instances": int(cnt[0]),
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                 "frac": gbps / HBM_PEAK_GBPS, "traffic": sec_traffic.get(key),
+                                 "frac": gbps / HBM_PEAK_GBPS, "regime": mall_regime(bps * n / 2),
+                                 "traffic": sec_traffic.get(key, (None,))[0],
+                                 "traffic_source": (f"{sec_traffic[key][2]}: {sec_traffic[key][1]}"
+                                                    if key in sec_traffic else None),
                                  "bytes_per_step": bps}}
         if flags:
             out[key]["config_flags"] = "FMSKF_CFG_COMP_POS"
@@ -282,8 +337,8 @@ def path_rows(dev, stream, ticks: int, trig):
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic_paths.json")
     if os.path.exists(tpath):
         try:
-            path_traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(open(tpath)).items()
-                            if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
+            path_traffic = {k: traffic_of(v) for k, v in json.load(open(tpath)).items()
+                            if traffic_of(v)[0] is not None}
         except Exception:
             path_traffic = {}
 
@@ -291,19 +346,17 @@ def path_rows(dev, stream, ticks: int, trig):
         for k in range(3):
             run(k)
         torch.cuda.synchronize()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        for k in range(ticks):
-            run(k)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        ms = ev0.elapsed_time(ev1) / ticks
+        # the prequeued calls keep the loop's own k sequence (the firmware loop's WT901 poll
+        # every 10th tick), so a multiple of 10 is queued ahead
+        ms = event_ms(stream, run, ticks, prequeue=10)
         gbps = PATH_BYTES[key] * n / (ms * 1e-3) / 1e9
+        tr = path_traffic.get(key, (None, None))
         out[key] = {"instances": n, "kernel_ms": ms, "robots_per_s": n / (ms * 1e-3), "ticks": ticks,
                     "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                  "frac": gbps / HBM_PEAK_GBPS, "bytes_per_step": PATH_BYTES[key],
-                                 "traffic": path_traffic.get(key)}}
+                                 "regime": mall_regime(PATH_BYTES[key] * n / 2),
+                                 "traffic": tr[0],
+                                 "traffic_source": f"profiles/pmc_traffic_paths.json: {tr[1]}" if tr[1] else None}}
         e.close()
 
     e = fmskf.Engine("rs", n, device=dev.index, trig=trig)
@@ -622,6 +675,7 @@ def main():
                     "library": fmskf.rccl_library()}
     native_stats = [None]
     native_pending = [0]
+    exch_ms = []  # side-stream all-gather + copy-out time of every collected native result
     # ring index of every tick applied to `eng`, in order: the post-timing parity replay
     applied = []
 
@@ -635,6 +689,9 @@ def main():
         while native_pending[0] > keep:
             native_stats[0] = eng.ensemble_end_count()
             native_pending[0] -= 1
+            xms = eng.ensemble_exchange_ms()  # -1 without a communicator (no side-stream gather)
+            if xms >= 0:
+                exch_ms.append(xms)
 
     def ens_event(k):
         """one ensemble event after tick k: record (fused into the tick, or a separate pass),
@@ -768,12 +825,14 @@ def main():
     torch.cuda.synchronize()
     # exactly the K timed ticks, wall clock between the two synchronisations (no event
     # record inside: its host call would delay the first launch)
+    exch_ms.clear()
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
     t_sub = time.perf_counter()
     join()
     t_join = time.perf_counter()
+    timed_exch = list(exch_ms)  # the exchanges of the timed region's ensemble events
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -794,29 +853,27 @@ def main():
     torch.cuda.synchronize()
     region_ms = ev0.elapsed_time(ev1)
 
-    # the tick kernel's own average launch duration (the roofline's denominator): K more
-    # back-to-back ticks on the same stream, without the ensemble kernels, HIP events around
-    # them (rocprofv3's per-kernel average for the same command: profiles/)
-    ek0 = torch.cuda.Event(enable_timing=True)
-    ek1 = torch.cuda.Event(enable_timing=True)
-    ek0.record(stream)
-    for k in range(args.steps):
-        tick(k % R)
-    ek1.record(stream)
-    torch.cuda.synchronize()
-    tick_ms = ek0.elapsed_time(ek1)
+    # the tick kernel's own average launch duration (the roofline's denominator): KT >= 200 more
+    # back-to-back plain ticks on the kernel's stream, no ensemble kernel and no collective in
+    # flight, 8 ticks queued before the first HIP event (rocprofv3's per-kernel average for the
+    # same command: profiles/)
+    KT = max(200, args.steps)
+    tick_ms = event_ms(stream, lambda k: tick(k % R), KT)
     # secondary: the same tick fed the three input planes (when the headline uses records)
     planes_ms = tick_ms
     if args.inputs == "records":
-        ek0.record(stream)
-        for k in range(args.steps):
-            tick(k % R, planes)
-        ek1.record(stream)
-        torch.cuda.synchronize()
-        planes_ms = ek0.elapsed_time(ek1)
+        planes_ms = event_ms(stream, lambda k: tick(k % R, planes), KT)
+    local_tick_ms = tick_ms
+    per_rank = None
     if distributed:
+        # each rank's own plain-tick time (min / max over ranks) and the rate it implies: a
+        # scaling curve below world x that rate comes from outside the tick (launch, barrier,
+        # the exchange), and the line says so (`scaling_diag`)
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, n, local_tick_ms))
+        per_rank = sorted(seen)
         elapsed, region_ms, tick_ms, planes_ms = max_over_ranks([elapsed, region_ms, tick_ms, planes_ms])
-    kern_avg_ms = tick_ms / args.steps
+    kern_avg_ms = tick_ms
 
     total_steps = n_global * args.steps
     value = total_steps / elapsed
@@ -920,16 +977,17 @@ def main():
                  "input_bytes_per_step": 16}
         e2.close()
 
-    traffic = None
+    traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get("n_instances") == n and tj.get("kernel", "").startswith("k_kf6") and \
                     tj.get("inputs", "planes") == args.inputs:
-                traffic = tj.get("hbm_bytes_per_launch")
+                traffic, traffic_src = traffic_of(tj)
+                traffic_src = f"profiles/pmc_traffic.json: {traffic_src}"
         except Exception:
-            traffic = None
+            traffic, traffic_src = None, None
 
     bpl = BYTES_PER_STEP["kf6"] * n  # algorithmic bytes per launch (one tick of one GPU)
     achieved = bpl / (kern_avg_ms * 1e-3) / 1e9
@@ -977,6 +1035,9 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            # the PMC bytes are not collected inside this run (rocprofv3 counter passes need runs
+            # of their own): the committed profile they come from
+            "traffic_source": traffic_src,
             "bytes_per_step": BYTES_PER_STEP["kf6"],
             "kernel_ms": kern_avg_ms,
             # the launcher's choice (kernels_kf6.hip launch_o): 2 robots per lane while the
@@ -984,7 +1045,12 @@ def main():
             "kernel": ("k_kf6p<4, 2, " if n * 124 <= (256 << 20) else "k_kf6t<4, ") +
                       "Opt<TABLE512, UPD, PRED, SMALL, !VALID" + (", REC>>" if krec is not None else ">>"),
             "timed_region_ms_per_step": region_ms / args.steps,
-            "kernel_ms_plane_inputs": planes_ms / args.steps,
+            "kernel_ms_plane_inputs": planes_ms,
+            "kernel_ticks_timed": KT,
+            # 124 B per robot (the state read + the 16-byte record) against the 256 MiB
+            # Infinity Cache: at 2^20 the state stays MALL-resident between ticks, so `achieved`
+            # is HBM + MALL; secondary.cfg2_kf6_2p24 is the HBM-only figure
+            "regime": mall_regime(124 * n),
         },
         "timed_region_host": host_split,
         "cpu_baseline": None,
@@ -997,6 +1063,13 @@ def main():
         out["ensemble_check"] = ens_check
     if gather_fallback is not None:
         out["gather_fallback"] = gather_fallback
+    if per_rank is not None:
+        # why the N > 1 value is what it is: each rank's plain tick alone (no collective in flight)
+        # against the whole job's rate, and what the ensemble exchange cost on the side stream
+        xs = [None] * world
+        dist.all_gather_object(xs, timed_exch)
+        diag = scaling_diag(per_rank, xs, value, ms_per_step, tick_ms)
+        out["scaling_diag"] = diag
     if rccl is not None:
         # the communicator libfmskf's asynchronous exchange ran over, as RCCL reports it
         out["rccl_ranks"] = rccl["ranks"]

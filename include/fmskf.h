@@ -319,6 +319,12 @@ int fmskf_ensemble_end(fmskf_handle h, double *mean, double *cov_packed);
  * pointer may be NULL. */
 int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, double *count,
                              uint32_t *n_records);
+/* How long the exchange of the result the last fmskf_ensemble_end / _end_count collected took on
+ * the handle's side stream: ncclAllGather of the record plus the copy of the gathered records to
+ * pinned host memory, between two timing events recorded around them (ms).  -1 when that result
+ * needed no exchange (no communicator: the fold wrote the pinned slot itself) or none was
+ * collected yet.  Lets an N > 1 run say what its collective costs beside the tick. */
+int fmskf_ensemble_exchange_ms(fmskf_handle h, float *ms);
 
 /* ---- vehicle control step -------------------------- */
 /* Per-robot control state is allocated on the first call of any entry point below

@@ -185,13 +185,20 @@ void fmskf::capi::ens_gather_async(fmskf_ctx *h, fmskf_ctx::EnsSlot &S) {
     hip_check(hipEventCreateWithFlags(&h->ens_ticked, kSyncEvent), "hipEventCreate");
   }
   const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
+  if (!S.x0) {  // timing events on the side stream only (the tick stream records none)
+    hip_check(hipEventCreate(&S.x0), "hipEventCreate");
+    hip_check(hipEventCreate(&S.x1), "hipEventCreate");
+  }
   hip_check(hipEventRecord(h->ens_ticked, h->stream), "hipEventRecord");
   hip_check(hipStreamWaitEvent(h->ens_stream, h->ens_ticked, 0), "hipStreamWaitEvent");
+  hip_check(hipEventRecord(S.x0, h->ens_stream), "hipEventRecord");
   nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
              "ncclAllGather");
   hip_check(hipMemcpyAsync(S.host, S.gather, (size_t)S.ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream),
             "D2H");
+  hip_check(hipEventRecord(S.x1, h->ens_stream), "hipEventRecord");
   hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
+  S.exchanged = true;
 }
 
 
@@ -365,6 +372,7 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
   }
   S.nb = nb;
   S.ranks = ranks;
+  S.exchanged = false;  // set when its fold is queued to the side stream (ens_gather_async)
   h->ens_carry = si;
   h->ens_pending++;
 }
@@ -400,6 +408,11 @@ int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, d
       ens_flush(h);
     }
     hip_check(hipEventSynchronize(S.done), "hipEventSynchronize");
+    h->ens_xms = -1.f;
+    if (S.exchanged) {
+      hip_check(hipEventElapsedTime(&h->ens_xms, S.x0, S.x1), "hipEventElapsedTime");
+      S.exchanged = false;
+    }
     h->ens_head = (h->ens_head + 1) % fmskf_ctx::kEnsSlots;
     h->ens_pending--;
     const int rc = fmskf_ensemble_combine(h->d.nx, S.host, (uint32_t)S.ranks, mean, cov_packed);
@@ -410,6 +423,14 @@ int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, d
     for (int r = 0; r < S.ranks; r++) c += S.host[(size_t)r * len];
     if (count) *count = c;
     if (n_records) *n_records = (uint32_t)S.ranks;
+  });
+}
+
+int fmskf_ensemble_exchange_ms(fmskf_handle h, float *ms) {
+  return guarded([&] {
+    check_handle(h);
+    if (!ms) fail(FMSKF_EINVAL, "null ms");
+    *ms = h->ens_xms;
   });
 }
 

@@ -147,6 +147,9 @@ struct fmskf_ctx {
     double *host_dev = nullptr;  // the device's address of `host` (the fold writes it over PCIe)
     size_t cap = 0;          // ranks the gather / host buffers hold
     hipEvent_t done = nullptr;
+    // timing events around the side stream's all-gather + copy-out (fmskf_ensemble_exchange_ms)
+    hipEvent_t x0 = nullptr, x1 = nullptr;
+    bool exchanged = false;  // the pending result went through the side stream
     int nb = 0;              // the event's block records
     int ranks = 1;
   } eslot[kEnsSlots];
@@ -154,6 +157,7 @@ struct fmskf_ctx {
   hipStream_t ens_stream = nullptr;
   int ens_head = 0, ens_pending = 0;
   int ens_carry = -1;  // the newest event's slot while its fold is not queued yet
+  float ens_xms = -1.f;  // the last collected result's exchange time (fmskf_ensemble_exchange_ms)
   // vehicle control state (allocated on first use) and its parameters
   CtrlDev ctrl{};
   fmskf_ctrl_params cprm{};
@@ -283,6 +287,8 @@ struct fmskf_ctx {
     for (EnsSlot &e : eslot) {
       if (e.host) (void)hipHostFree(e.host);
       if (e.done) (void)hipEventDestroy(e.done);
+      if (e.x0) (void)hipEventDestroy(e.x0);
+      if (e.x1) (void)hipEventDestroy(e.x1);
     }
     if (ens_ticked) (void)hipEventDestroy(ens_ticked);
     if (ens_stream) (void)hipStreamDestroy(ens_stream);

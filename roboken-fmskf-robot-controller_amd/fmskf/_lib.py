@@ -135,6 +135,7 @@ SIGNATURES = {
     "fmskf_ensemble_begin": (C.c_int, [_H]),
     "fmskf_ensemble_end": (C.c_int, [_H, _P, _P]),
     "fmskf_ensemble_end_count": (C.c_int, [_H, _P, _P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
+    "fmskf_ensemble_exchange_ms": (C.c_int, [_H, C.POINTER(C.c_float)]),
     "fmskf_ctrl_params_init": (C.c_int, [C.POINTER(CtrlParams)]),
     "fmskf_set_ctrl_params": (C.c_int, [_H, C.POINTER(CtrlParams)]),
     "fmskf_set_power": (C.c_int, [_H, _P, C.c_uint32]),

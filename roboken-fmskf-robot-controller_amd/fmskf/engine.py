@@ -425,6 +425,13 @@ class Engine:
               "ensemble_end_count")
         return mean, cov, cnt.value, nrec.value
 
+    def ensemble_exchange_ms(self) -> float:
+        """fmskf_ensemble_exchange_ms: the side stream's all-gather + copy-out time of the result
+        the last ensemble_end collected (ms), -1 when it needed no exchange"""
+        ms = C.c_float()
+        check(load().fmskf_ensemble_exchange_ms(self.h, C.byref(ms)), "ensemble_exchange_ms")
+        return ms.value
+
     # ------------------------------------------------------------------ control step
     def set_ctrl_params(self, **kw):
         """FF_PI_D / interpolator / current-limit parameters (fmskf_ctrl_params); unspecified

@@ -29,3 +29,32 @@ def test_no_spawn_under_launcher_or_single_gpu():
 def test_cpu_share_reports_affinity():
     s = bench.cpu_share()
     assert s["affinity_cpus"] >= 1 and s["host_cpus"] >= s["affinity_cpus"]
+
+
+def test_scaling_diag_fields():
+    """the N > 1 line's self-explanation (bench.scaling_diag): per-rank plain-tick times, the sum
+    of the ranks' plain-tick rates, scaling_self = value / that sum, and the side-stream exchange
+    times max over ranks"""
+    per_rank = [(0, 1 << 20, 0.0370), (1, 1 << 20, 0.0380)]
+    rates = (1 << 20) / 0.0370e-3 + (1 << 20) / 0.0380e-3
+    value = 0.9 * rates
+    d = bench.scaling_diag(per_rank, [[0.020, 0.031], [0.025]], value, 0.0400, 0.0380)
+    assert d["tick_kernel_ms_min"] == 0.0370 and d["tick_kernel_ms_max"] == 0.0380
+    assert abs(d["rank_local_rate_sum"] - rates) < 1e-6 * rates
+    assert abs(d["scaling_self"] - 0.9) < 1e-12
+    assert abs(d["ms_per_step_over_tick_kernel"] - 0.0400 / 0.0380) < 1e-12
+    x = d["exchange_ms"]
+    assert x["max_over_ranks"] == 0.031 and x["per_rank_max"] == [0.031, 0.025] and x["events_per_rank"] == 2
+    assert bench.scaling_diag(per_rank, [[], []], value, 0.04, 0.038)["exchange_ms"] is None
+
+
+def test_mall_regime_and_traffic_provenance():
+    assert bench.mall_regime(124 * (1 << 20)) == "hbm+mall"
+    assert bench.mall_regime(124 * (1 << 24)) == "hbm"
+    import json
+    tj = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    b, src = bench.traffic_of(tj)
+    assert b == tj["hbm_bytes_per_launch"] and "FETCH_SIZE" in src and tj["source"]["round"] in src
+    for f in tj["source"]["committed_as"]:
+        assert os.path.exists(os.path.join(ROOT, f)), f
+    assert bench.traffic_of({"kernel": "x"}) == (None, None)

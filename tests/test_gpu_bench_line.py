@@ -44,6 +44,16 @@ def test_driver_bench_line_contract():
     assert rf["achieved"] == pytest.approx(232 * (1 << 20) / (rf["kernel_ms"] * 1e-3) / 1e9, rel=1e-6)
     assert 0.5 < rf["frac"] < 1.0
     assert rf["traffic"] == pytest.approx(232 * (1 << 20), rel=0.05)  # PMC bytes per launch
+    assert "FETCH_SIZE" in rf["traffic_source"] and rf["traffic_source"].startswith("profiles/pmc_traffic.json")
+    # the roofline's denominator is consistent with the run's own clock: the kernel's average
+    # (>= 200 prequeued plain ticks) cannot exceed the timed region's GPU time per step (which
+    # also holds the ensemble ticks' record epilogue), and frac follows from that region
+    assert rf["kernel_ticks_timed"] >= 200
+    assert rf["kernel_ms"] <= 1.01 * rf["timed_region_ms_per_step"], rf
+    assert rf["kernel_ms"] <= 1.01 * out["ms_per_step"], (rf, out["ms_per_step"])
+    region_frac = 232 * (1 << 20) / (rf["timed_region_ms_per_step"] * 1e-3) / 8e12
+    assert rf["frac"] == pytest.approx(region_frac, rel=0.03), (rf["frac"], region_frac)
+    assert rf["regime"] == "hbm+mall"  # 124 B x 2^20 fits the 256 MiB Infinity Cache
     cb = out["cpu_baseline"]
     assert cb["value"] > 0 and cb["unit"] == "steps/s" and cb["cores"] >= 1
     assert cb["kind"] == "port" and cb["sample"]
@@ -54,6 +64,9 @@ def test_driver_bench_line_contract():
         sec = out["secondary"][key]["roofline"]
         assert sec["bytes_per_step"] == b, key
         assert 0.3 < sec["frac"] < 1.0, (key, sec)
+    assert out["secondary"]["cfg2_kf6_2p24"]["roofline"]["regime"] == "hbm"
+    for key in ("cfg3_ekf9_2p22", "cfg5_kf12d_2p20", "cfg2_kf6_2p24"):
+        assert out["secondary"][key]["roofline"]["traffic_source"], key
     for key, b in PATH_BYTES.items():
         row = out["path_rows"][key]["roofline"]
         assert row["bytes_per_step"] == b, key

@@ -1,9 +1,9 @@
 """Copy the profiling session's outputs from gpurun_out/ into profiles/ under a round prefix:
     python tools/collect_profiles.py r3 [--pmc-kf6] [--secondary]
 always: bench.log / prof.log lines, the rocprofv3 kernel / domain stats and the fmskf kernel trace
-of the driver's command, and the path-row PMC passes (pmc_path_*, tools/r3_session.sh) when
+of the driver's command, and the path-row PMC passes (pmc_path_*, tools/session.sh) when
 present; --pmc-kf6: the headline kernel's FETCH / WRITE passes and their calibration pattern
-(tools/profile_session.sh); --secondary: the HBM-regime PMC passes and the prof_* kernel stats"""
+(tools/session.sh); --secondary: the HBM-regime PMC passes and the prof_* kernel stats"""
 import csv
 import glob
 import json
@@ -52,7 +52,7 @@ def main():
                 shutil.copy(src, os.path.join(P, f"{tag}_pmc_{'kf6' if kind == 'kf6' else 'pattern'}_{c}.csv"))
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), G,
                         os.path.join(P, "pmc_traffic.json"), "records"], check=True, stdout=subprocess.DEVNULL)
-    # the rows either side of the tick (r3_session.sh pmc): calibrated traffic + the counter rows
+    # the rows either side of the tick (tools/session.sh paths): calibrated traffic + the counter rows
     if glob.glob(os.path.join(G, "pmc_path_*")):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "paths", G,
                         os.path.join(P, "pmc_traffic_paths.json")], check=True, stdout=subprocess.DEVNULL)
@@ -67,7 +67,7 @@ def main():
                 w = csv.writer(fo)
                 w.writerow(rows_in[0])
                 w.writerows(keep)
-    # wave-state counters of the path-row kernels (r3_session.sh sq) and their per-kernel summary
+    # wave-state counters of the path-row kernels (tools/session.sh sq) and their per-kernel summary
     sq = []
     for d in sorted(glob.glob(os.path.join(G, "sq_*"))):
         f = os.path.join(d, "run_counter_collection.csv")
@@ -98,7 +98,7 @@ def main():
                        "active_frac": a["SQ_ACTIVE_INST_ANY"] / wc})
     if sq:
         json.dump(sq, open(os.path.join(P, f"{tag}_sq_summary.json"), "w"), indent=1)
-    # HBM-regime bench lines (profile_session.sh PMC_SEC=1): calibrated traffic + the counter rows
+    # HBM-regime bench lines (tools/session.sh sec): calibrated traffic + the counter rows
     if secondary and glob.glob(os.path.join(G, "pmc_sec_*")):
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), "secondary", G,
                         os.path.join(P, "pmc_traffic_secondary.json")], check=True, stdout=subprocess.DEVNULL)

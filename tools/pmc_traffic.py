@@ -17,6 +17,15 @@ import json
 import os
 import sys
 
+# the round the counters were collected in (PMC_TAG=r5 ...): recorded as each file's `source`,
+# which bench.py reports beside the traffic figure (`traffic_source`)
+TAG = os.environ.get("PMC_TAG", "")
+
+
+def source(root, dirs, kernel):
+    return {"round": TAG, "kernel": kernel, "passes": [f"{root}/{d}" for d in dirs],
+            "committed_as": [f"profiles/{TAG}_{d}.csv" for d in dirs] if TAG else []}
+
 
 def read(dirname, kernel_substr):
     vals = []
@@ -53,7 +62,8 @@ def secondary(root, out):
     2^24 tick kernels (gpurun_out/pmc_sec_{kernel,pattern}_{FETCH,WRITE}_SIZE)."""
     res = {"unit": "bytes per launch", "calibration": "tools/membench.hip caps patterns, same widths, same N"}
     for key, ksub, psub, pn, prd, pwr, ard, awr, n in SECONDARY:
-        ent = {"n_instances": n, "kernel": ksub, "pattern": psub}
+        ent = {"n_instances": n, "kernel": ksub, "pattern": psub,
+               "source": source(root, [f"pmc_sec_{key}_FETCH_SIZE", f"pmc_sec_{key}_WRITE_SIZE"], ksub)}
         for c, pbytes, abytes in (("FETCH_SIZE", prd * pn, ard * n), ("WRITE_SIZE", pwr * pn, awr * n)):
             pat = read_grid(os.path.join(root, f"pmc_sec_pattern_{c}"), psub, pn)
             kf = read(os.path.join(root, f"pmc_sec_{key}_{c}"), ksub)
@@ -103,7 +113,8 @@ def paths(root, out, calib="profiles/pmc_traffic.json"):
     res = {"unit": "bytes per launch", "n_instances": n,
            "calibration": f"{calib} (KF6 pattern): FETCH x {fac['FETCH_SIZE']:.4f}, WRITE x {fac['WRITE_SIZE']:.4f}"}
     for key, ksub, rd, wr in PATHS:
-        ent = {"kernel": ksub}
+        ent = {"kernel": ksub,
+               "source": source(root, [f"pmc_path_{key}_FETCH_SIZE", f"pmc_path_{key}_WRITE_SIZE"], ksub)}
         for c, algo in (("FETCH_SIZE", rd * n), ("WRITE_SIZE", wr * n)):
             kv = read(os.path.join(root, f"pmc_path_{key}_{c}"), ksub)
             if not kv:
@@ -134,7 +145,8 @@ def main():
     n = 1 << 20
     inputs = sys.argv[3] if len(sys.argv) > 3 else "records"
     res = {"n_instances": n, "kernel": "k_kf6 (tick, TABLE512, N=2^20)", "inputs": inputs,
-           "unit": "bytes per launch"}
+           "unit": "bytes per launch",
+           "source": source(root, ["pmc_kf6_FETCH_SIZE", "pmc_kf6_WRITE_SIZE"], "k_kf6p (tools/kbench.py --packed)")}
     for c, algo in (("FETCH_SIZE", 124 * n), ("WRITE_SIZE", 108 * n)):
         pat = read(os.path.join(root, f"pmc_pat_{c}"), "k_pattern<1>")
         kf = read(os.path.join(root, f"pmc_kf6_{c}"), "k_kf6")
