@@ -140,9 +140,13 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(yaw, gz, rpm, sample_s: float):
-    """The oracle's C restatement of the same KF6 tick (OpenMP over instances, -O3,
-    contraction off) timed on this host on a bounded sample: all threads, then one thread on
-    the same instance count (so the two rates are per the same working set)."""
+    """The same KF6 tick on this host's CPU cores, on a bounded sample (the first 2^18 robots of
+    the bench's inputs).  `value` is the tuned port (oracle/cpu_port.c: the tick specialised for
+    KF6, the robots of a block in AVX-512 / AVX2 lanes, OpenMP threads over blocks, the oracle's
+    operation order -- bitwise the checker's, verified on the sample here); `value_checker` is
+    the generic one-robot-at-a-time oracle the tests check against.  Also the reference-semantics
+    RS tick (the firmware ISR's arithmetic, VD_vehicle_controller.cpp:11-51) through the same
+    port.  All on the process's OpenMP threads and on one thread."""
     import numpy as np
     import fmskf
     from oracle import oracle as orc
@@ -151,33 +155,67 @@ def cpu_baseline(yaw, gz, rpm, sample_s: float):
     cfg = fmskf.default_config("kf6", n)
     prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]))
     threads = orc.max_threads()
-    res = {}
-    for label, nt, budget in (("all", threads, sample_s), ("one", 1, max(2.0, sample_s / 3))):
+    p0 = np.float32(np.array(cfg.p0[:21]))
+
+    def rate(fn, budget):
         x = np.zeros((6, n), np.float32)
-        P = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+        P = np.repeat(p0[:, None], n, 1).copy()
         ticks = 0
         t0 = time.perf_counter()
         while True:
-            t = ticks % T
-            orc.kf6_tick(x, P, yaw[t], gz[t], rpm[t], None, prm, nthreads=nt)
+            fn(x, P, ticks % T)
             ticks += 1
             el = time.perf_counter() - t0
             if el >= budget and ticks >= 3:
+                return n * ticks / el, ticks, el
+
+    port = lambda nt: (lambda x, P, t: orc.port_kf6_tick(x, P, yaw[t], gz[t], rpm[t], prm, nthreads=nt))  # noqa: E731
+    chk = lambda nt: (lambda x, P, t: orc.kf6_tick(x, P, yaw[t], gz[t], rpm[t], None, prm, nthreads=nt))  # noqa: E731
+    # the port against the checker on the sample: three ticks from the same start, bit for bit
+    xs = [np.zeros((6, n), np.float32) for _ in range(2)]
+    Ps = [np.repeat(p0[:, None], n, 1).copy() for _ in range(2)]
+    for t in range(3):
+        port(threads)(xs[0], Ps[0], t)
+        chk(threads)(xs[1], Ps[1], t)
+    same = bool(np.array_equal(xs[0].view(np.uint32), xs[1].view(np.uint32)) and
+                np.array_equal(Ps[0].view(np.uint32), Ps[1].view(np.uint32)))
+    v, ticks, el = rate(port(threads), sample_s * 0.45)
+    v1, t1, e1 = rate(port(1), max(1.5, sample_s * 0.15))
+    vc, tc, ec = rate(chk(threads), max(1.5, sample_s * 0.15))
+    # the reference-semantics tick (RS): encoder sums drifting by a few counts per tick
+    sums = np.cumsum(np.random.default_rng(5).integers(-40, 40, (T, 4, n)), 0).astype(np.int64)
+    pos, vel, prev = np.zeros((3, n), np.float32), np.zeros((3, n), np.float32), np.zeros((4, n), np.int64)
+    rs = {}
+    for label, nt, budget in (("all", threads, sample_s * 0.15), ("one", 1, max(1.0, sample_s * 0.1))):
+        k, t0 = 0, time.perf_counter()
+        while True:
+            orc.port_rs_tick(pos, vel, prev, yaw[k % T], sums[k % T], rpm[k % T], nthreads=nt)
+            k += 1
+            el_rs = time.perf_counter() - t0
+            if el_rs >= budget and k >= 3:
                 break
-        res[label] = (n * ticks / el, ticks, el)
-    v, ticks, el = res["all"]
+        rs[label] = n * k / el_rs
     share = cpu_share()
+    isa = orc.port().isa
     return {
         "value": v, "unit": "steps/s", "cores": threads, "kind": "port",
+        "variant": f"tuned port: oracle/cpu_port.c, -march=x86-64-{isa} "
+                   f"({'AVX-512' if isa == 'v4' else 'AVX2'}), robots in SIMD lanes, OpenMP over blocks",
+        "bitexact_vs_checker": same,
         "cores_why": f"OpenMP threads = omp_get_max_threads() = {threads} (OMP_NUM_THREADS="
                      f"{share['omp_num_threads_env']}: the pool's per-GPU CPU share); process affinity "
                      f"{share['affinity_cpus']} of {share['host_cpus']} host CPUs",
         **share,
-        "sample": f"{n} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick, "
-                  f"oracle/fmskf_oracle.c -O3 -ffp-contract=off, OpenMP {threads} threads; "
-                  f"1 thread: {n} instances x {res['one'][1]} ticks ({res['one'][2]:.1f} s)",
+        "sample": f"{n} instances x {ticks} ticks ({el:.1f} s) of the same fused KF6 tick through the tuned "
+                  f"port on {threads} threads; 1 thread {t1} ticks ({e1:.1f} s); the checker "
+                  f"(oracle/fmskf_oracle.c orc_kf6_tick, generic n-state, one robot at a time, -O3 "
+                  f"-march=x86-64-v3) {tc} ticks ({ec:.1f} s) on {threads} threads",
         "cpu_model": cpu_model(),
-        "value_1core": res["one"][0],
+        "value_1core": v1,
+        "value_checker": vc,
+        "rs_tick": {"steps_per_s": rs["all"], "steps_per_s_1core": rs["one"],
+                    "what": "reference-semantics tick (correct + odometry predict, VD_vehicle_controller.cpp:"
+                            "11-51) through oracle/cpu_port.c port_rs_tick, bitwise orc_rs_tick"},
     }
 
 
@@ -1093,9 +1131,10 @@ def main():
     # the CPU baseline on rank 0 after every timed region (at N > 1 the other ranks wait at
     # the final barrier): the same KF6 tick on a bounded 2^18-robot sample
     if rank == 0 and not args.no_cpu_baseline:
-        y = yaw[:8, : 1 << 18].cpu().numpy()
-        g = gz[:8, : 1 << 18].cpu().numpy()
-        r = rpm[:8, : 1 << 18].cpu().numpy()
+        import numpy as np
+        y = np.ascontiguousarray(yaw[:8, : 1 << 18].cpu().numpy())
+        g = np.ascontiguousarray(gz[:8, : 1 << 18].cpu().numpy())
+        r = np.ascontiguousarray(rpm[:8, : 1 << 18].cpu().numpy())
         cb = cpu_baseline(y, g, r, args.cpu_sample_s)
         cb["gpu_over_cpu"] = value / cb["value"]  # the driver-timed value, not the kernel time
         out["cpu_baseline"] = cb

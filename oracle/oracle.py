@@ -35,7 +35,7 @@ def build(quiet: bool = True) -> None:
     kw = dict(cwd=HERE, check=True)
     if quiet:
         kw.update(stdout=subprocess.DEVNULL)
-    subprocess.run(["make", "-s", "liboracle.so", "libkfref.so"], **kw)
+    subprocess.run(["make", "-s", "liboracle.so", "libkfref.so", "libcpuport_v3.so", "libcpuport_v4.so"], **kw)
     if os.path.isdir("/root/reference/lib/wt901c"):
         subprocess.run(["make", "-s", "ref"], **kw)
 
@@ -196,6 +196,53 @@ def lib():
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ----------------------------------------------------------------------------- CPU baseline port
+_port = None
+
+
+def port_isa() -> str:
+    """the widest cpu_port build this host runs: 'v4' (AVX-512 F/BW/CD/DQ/VL) or 'v3' (AVX2)"""
+    flags = set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        pass
+    return "v4" if {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"} <= flags else "v3"
+
+
+def port():
+    """oracle/cpu_port.c (bench.py's CPU baseline; bit-exact to orc_kf6_tick / orc_rs_tick)"""
+    global _port
+    if _port is None:
+        path = os.path.join(HERE, f"libcpuport_{port_isa()}.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.port_kf6_tick.argtypes = [C.c_size_t, _f32p, _f32p, _vp, _vp, _vp, C.POINTER(Kf6Params), C.c_int]
+        L.port_kf6_tick.restype = C.c_int
+        L.port_rs_tick.argtypes = [C.c_size_t, _f32p, _f32p, _i64p, _vp, _i64p, _i16p, C.c_int, C.c_int]
+        L.port_rs_tick.restype = C.c_int
+        L.port_max_threads.restype = C.c_int
+        L.isa = port_isa()
+        _port = L
+    return _port
+
+
+def port_kf6_tick(x, P, yaw, gz, rpm, prm, nthreads=0):
+    """the tuned KF6 tick (no validity mask, TABLE512): same bits as kf6_tick"""
+    n = x.shape[1]
+    assert port().port_kf6_tick(n, x, P, _ptr(yaw), _ptr(gz), _ptr(rpm), C.byref(prm), nthreads) == 0
+
+
+def port_rs_tick(pos, vel, prev, yaw_deg, angle_sum, rpm, nthreads=0):
+    """the tuned reference-semantics tick (TABLE512): same bits as rs_tick"""
+    n = pos.shape[1]
+    assert port().port_rs_tick(n, pos, vel, prev, _ptr(yaw_deg), angle_sum, rpm, TRIG_TABLE512, nthreads) == 0
 
 
 # ----------------------------------------------------------------------------- scalar

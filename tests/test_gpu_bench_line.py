@@ -57,6 +57,9 @@ def test_driver_bench_line_contract():
     cb = out["cpu_baseline"]
     assert cb["value"] > 0 and cb["unit"] == "steps/s" and cb["cores"] >= 1
     assert cb["kind"] == "port" and cb["sample"]
+    # the tuned port is bitwise the checker on the sample, and both rates are reported
+    assert cb["bitexact_vs_checker"] is True and cb["value_checker"] > 0 and cb["value_1core"] > 0
+    assert cb["rs_tick"]["steps_per_s"] > 0 and cb["rs_tick"]["steps_per_s_1core"] > 0
     assert out["parity_sampled"]["bitexact"] and out["parity_sampled"]["mismatched_robots"] == 0
     assert out["nonfinite_instances"] == 0
     assert out["ensemble"]["count"] == 1 << 20
