@@ -18,8 +18,11 @@ namespace {
 // group without the dlt and speed planes (no longer kept).  Format 4 ('FMSKFCK4', ABI 3): the
 // motor group with the previous angles (Status::flt_dltOutAngle_rad at readout), the estimator
 // group with KF6's position low parts under FMSKF_CFG_COMP_POS, and the config flags in the
-// header; format-2 and format-3 files are rejected by name.
-constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '4'};
+// header; format-2 and format-3 files are rejected by name.  Format 5 ('FMSKFCK5', round 5):
+// the motor group's IIR1 state as [N][4] rows (k_can4 moves each in one 16-byte access);
+// format-4 files, whose IIR state is [4][N] planes, are rejected by name.
+constexpr char kCkMagic[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '5'};
+constexpr char kCkMagicV4[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '4'};
 constexpr char kCkMagicV3[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '3'};
 constexpr char kCkMagicV1[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '1'};
 constexpr char kCkMagicV2[8] = {'F', 'M', 'S', 'K', 'F', 'C', 'K', '2'};
@@ -211,6 +214,8 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
       fail(FMSKF_EINVAL, "format-2 checkpoint (older build): its motor group holds the dlt / speed planes this build no longer keeps");
     if (memcmp(hd.magic, kCkMagicV3, 8) == 0)
       fail(FMSKF_EINVAL, "format-3 checkpoint (older build): its motor group lacks the previous angles");
+    if (memcmp(hd.magic, kCkMagicV4, 8) == 0)
+      fail(FMSKF_EINVAL, "format-4 checkpoint (older build): its motor IIR state is [4][N] planes, this build keeps [N][4] rows");
     if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
     f.seek(0, SEEK_SET);
     f.read(&hd, sizeof(hd));

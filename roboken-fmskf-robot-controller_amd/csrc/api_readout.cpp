@@ -50,8 +50,24 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
     copy_planes_out(h, angle_sum, h->s.m_sum, n * 8, h->s.m_pitch * 8, 4, mem);
-    // Status::flt_SpeedRadPS is the IIR1 output, i.e. its state y (VD_motor_if_m2006.cpp:63)
-    copy_out(h, speed_radps, h->s.m_iir_y, 4 * n * 4, mem);
+    // Status::flt_SpeedRadPS is the IIR1 output, i.e. its state y (VD_motor_if_m2006.cpp:63):
+    // [4][N] planes out of the device's [N][4] rows
+    if (speed_radps) {
+      if (mem == FMSKF_MEM_HOST) {
+        std::vector<float> rows(4 * n);
+        copy_out(h, rows.data(), h->s.m_iir_y, 4 * n * 4, mem);
+        hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+        for (uint64_t i = 0; i < n; i++)
+          for (int w = 0; w < 4; w++) speed_radps[(size_t)w * n + i] = rows[4 * i + w];
+      } else if (mem == FMSKF_MEM_DEVICE) {  // one strided copy per wheel: column w -> plane w
+        for (int w = 0; w < 4; w++)
+          hip_check(hipMemcpy2DAsync(speed_radps + (size_t)w * n, 4, h->s.m_iir_y + w, 16, 4, n,
+                                     hipMemcpyDeviceToDevice, h->stream),
+                    "speed transpose");
+      } else {
+        fail(FMSKF_EINVAL, "bad mem flag");
+      }
+    }
     finish_out(h, mem);
   });
 }
@@ -73,21 +89,8 @@ int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle,
       launch_check(launch_motor_dlt(h->s.m_angle, h->s.m_prev, dst, 4 * n, h->stream), "motor dlt");
       if (mem == FMSKF_MEM_HOST) copy_out(h, dlt_out_angle_rad, dst, 4 * n * 4, mem);
     }
-    // Status::flt_SpeedRadPS [N][4] from the IIR1 output planes [4][N]
-    if (speed_radps) {
-      if (mem == FMSKF_MEM_HOST) {
-        std::vector<float> pl(4 * n);
-        copy_out(h, pl.data(), h->s.m_iir_y, 4 * n * 4, mem);
-        hip_check(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
-        for (uint64_t i = 0; i < n; i++)
-          for (int w = 0; w < 4; w++) speed_radps[4 * i + w] = pl[(size_t)w * n + i];
-      } else {  // one strided copy per wheel: plane w -> column w
-        for (int w = 0; w < 4; w++)
-          hip_check(hipMemcpy2DAsync(speed_radps + w, 16, h->s.m_iir_y + (size_t)w * n, 4, 4, n,
-                                     hipMemcpyDeviceToDevice, h->stream),
-                    "speed transpose");
-      }
-    }
+    // Status::flt_SpeedRadPS [N][4]: the IIR1 output rows as the device keeps them
+    copy_out(h, speed_radps, h->s.m_iir_y, 4 * n * 4, mem);
     finish_out(h, mem);
   });
 }

@@ -51,8 +51,8 @@ struct DevState {
                                // plane pitch (a power-of-two stride N aliases: RS tick 2^20
                                // 27.5-27.8 us from [4][2^20] sums, 24.7 from [4][2^20 + 512])
   uint64_t m_pitch = 0;
-  float *m_iir_y = nullptr;    // [4][N]
-  float *m_iir_x = nullptr;    // [4][N]
+  float *m_iir_y = nullptr;    // [N][4] (one 16-byte access per robot in k_can4)
+  float *m_iir_x = nullptr;    // [N][4]
   unsigned long long *counters = nullptr;  // [8]
   float *sintab = nullptr;                 // [513]
 };

@@ -350,7 +350,7 @@ struct CanArgs {
   int16_t *prev;  // [N][4] the angle before this frame (Status::flt_dltOutAngle_rad at readout)
   int64_t *sum;  // [4][sum_pitch]
   uint64_t sum_pitch;
-  float *iir_y, *iir_x;  // UTIL::IIR1 state; y is also Status::flt_SpeedRadPS
+  float *iir_y, *iir_x;  // [N][4] UTIL::IIR1 state; y is also Status::flt_SpeedRadPS
 };
 
 __device__ __forceinline__ int16_t s16_of(uint32_t h, uint32_t l) { return (int16_t)((h << 8) | l); }
@@ -411,12 +411,11 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   const int w = (int)(g & 3);
   if (a.present && !((a.present[i] >> w) & 1)) return;
   const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
-  const uint64_t pw = (uint64_t)w * n + i;
   const uint64_t ps = (uint64_t)w * a.sum_pitch + i;
   const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g],
-                               a.iir_y[pw], a.iir_x[pw], a.sum[ps]);
-  a.iir_y[pw] = o.iir_y;
-  a.iir_x[pw] = o.iir_x;
+                               a.iir_y[g], a.iir_x[g], a.sum[ps]);
+  a.iir_y[g] = o.iir_y;
+  a.iir_x[g] = o.iir_x;
   a.sum[ps] = o.sum;
   a.micro[g] = a.stamps[g];
   a.prev[g] = a.angle[g];
@@ -435,18 +434,19 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
 }
 
 // one robot per lane, every wheel present (no mask): the robot's 32 frame bytes, its four
-// stamps and its [N][4] int16 / u8 state in single 16-, 8- and 4-byte accesses, and each
-// [4][N] plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines:
-// 2^20 57.4-57.7 -> 42.1-44.1 us, 2^22 232-239 -> 211).  Every access goes through a scalar
-// descriptor at the block's 256-robot chunk (ld_chunk / st_chunk) with the KF6 tick's cache
-// policies: the frames and stamps (read once) `nt`, the state stored `sc1` while
-// cache-resident; NT: the motor state streams from HBM (past the Infinity Cache), `nt` loads
-// and stores.  Plain global accesses measured 43.4-44.6 (2^20) and 191-195 us (2^22) against
-// 43.0-43.1 and 185-189.
-// SO (round 4): one span descriptor per array (rsrc_span) with the wheel planes of the [4][N]
-// arrays reached through soffset, instead of one clamped descriptor per plane (19 -> 10
-// descriptors; the launcher checks the 4 GiB span).
-template <bool NT, bool SO = false>
+// stamps and its [N][4] int16 / float state in single 16- and 8-byte accesses, and each [4][N]
+// sum plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines: 2^20
+// 57.4-57.7 -> 42.1-44.1 us, 2^22 232-239 -> 211).  Every access goes through a scalar
+// descriptor at the block's 256-robot chunk with the KF6 tick's cache policies: the frames and
+// stamps (read once) `nt`, the state stored `sc1` while cache-resident; NT: the motor state
+// streams from HBM (past the Infinity Cache), `nt` loads and stores.  Plain global accesses
+// measured 43.4-44.6 (2^20) and 191-195 us (2^22) against 43.0-43.1 and 185-189.
+// Round 5: the IIR1 state x / y of the four wheels as [N][4] floats, one 16-byte access each
+// (8 dword loads and 8 dword stores per lane before: the wave waited to issue memory
+// instructions 79% of its cycles, profiles/r4_sq_summary.json).
+// SO: the sum array's wheel planes reached through soffset from one descriptor (the launcher
+// checks the 4 GiB span); else one clamped descriptor per plane.
+template <bool NT, bool SO>
 __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -456,75 +456,54 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   constexpr int LP = NT ? kStateNT : 0, SP = st_pol(LP), IP = 2;  // IP: inputs nt
   const uint64_t hb = (uint64_t)(__builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1));
   const uint32_t li = (uint32_t)(i - hb);
-  float py[4], px[4];
   int64_t sm[4];
-  const auto rf = SO ? rsrc_span(a.frames + hb * 32) : rsrc(a.frames + hb * 32, (n - hb) * 32);
+  const auto rf = rsrc_span(a.frames + hb * 32);
   const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u, 0, IP);
   const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u + 16u, 0, IP);
   const uint4 f01 = make_uint4(v0[0], v0[1], v0[2], v0[3]);
   const uint4 f23 = make_uint4(v1[0], v1[1], v1[2], v1[3]);
-  uint64_t sv, mv, av;
-  // SO: the [N][4] arrays and the [4][N] arrays' chunk bases, wheel planes at soffset w * pitch
-  const auto r_iy = rsrc_span(a.iir_y + hb), r_ix = rsrc_span(a.iir_x + hb), r_sm = rsrc_span(a.sum + hb);
-  const uint32_t pf = (uint32_t)(n * 4), ps = (uint32_t)(a.sum_pitch * 8);
-  if constexpr (SO) {
-    sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
-    mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);
-    av = ld_span<uint64_t, LP>(rsrc_span(a.angle + hb * 4), li, 0);
+  const auto r_iy = rsrc_span(a.iir_y + hb * 4), r_ix = rsrc_span(a.iir_x + hb * 4);
+  const auto iy = __builtin_amdgcn_raw_buffer_load_b128(r_iy, li * 16u, 0, LP);
+  const auto ix = __builtin_amdgcn_raw_buffer_load_b128(r_ix, li * 16u, 0, LP);
+  const uint64_t sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
+  const uint64_t mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);
+  const uint64_t av = ld_span<uint64_t, LP>(rsrc_span(a.angle + hb * 4), li, 0);
+  const auto r_sm = rsrc_span(a.sum + hb);
+  const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-      py[w] = ld_span<float, LP>(r_iy, li, w * pf);
-      px[w] = ld_span<float, LP>(r_ix, li, w * pf);
-      sm[w] = ld_span<int64_t, LP>(r_sm, li, w * ps);
-    }
-  } else {
-    sv = ld_chunk<uint64_t, IP>(reinterpret_cast<const uint64_t *>(a.stamps), hb, n, li);
-    mv = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.micro), hb, n, li);
-    av = ld_chunk<uint64_t, LP>(reinterpret_cast<const uint64_t *>(a.angle), hb, n, li);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      py[w] = ld_chunk<float, LP>(a.iir_y + (uint64_t)w * n, hb, n, li);
-      px[w] = ld_chunk<float, LP>(a.iir_x + (uint64_t)w * n, hb, n, li);
-      sm[w] = ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li);
-    }
-  }
+  for (int w = 0; w < 4; w++)
+    sm[w] = SO ? ld_span<int64_t, LP>(r_sm, li, w * ps) : ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li);
+  // element copies before use (see kf6_load_in: an ext_vector element read through a bit cast
+  // miscompiled once)
+  const uint32_t iyw[4] = {iy[0], iy[1], iy[2], iy[3]}, ixw[4] = {ix[0], ix[1], ix[2], ix[3]};
   const uint2 st = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
   const uint2 om = make_uint2((uint32_t)mv, (uint32_t)(mv >> 32)), oa = make_uint2((uint32_t)av, (uint32_t)(av >> 32));
   const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
   const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
   uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0};
+  v4u32_t oy, ox;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
     const int sh = 16 * (w & 1);
     const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
-                                 (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh), py[w], px[w], sm[w]);
-    if constexpr (SO) {
-      st_span<float, SP>(r_iy, li, w * pf, o.iir_y);
-      st_span<float, SP>(r_ix, li, w * pf, o.iir_x);
-      st_span<int64_t, SP>(r_sm, li, w * ps, o.sum);
-    } else {
-      st_chunk<float, SP>(a.iir_y + (uint64_t)w * n, hb, n, li, o.iir_y);
-      st_chunk<float, SP>(a.iir_x + (uint64_t)w * n, hb, n, li, o.iir_x);
-      st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li, o.sum);
-    }
+                                 (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
+                                 __builtin_bit_cast(float, iyw[w]), __builtin_bit_cast(float, ixw[w]), sm[w]);
+    oy[w] = __builtin_bit_cast(uint32_t, o.iir_y);
+    ox[w] = __builtin_bit_cast(uint32_t, o.iir_x);
+    if constexpr (SO) st_span<int64_t, SP>(r_sm, li, w * ps, o.sum);
+    else st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, n, li, o.sum);
     na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
     nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
     nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
   }
+  __builtin_amdgcn_raw_buffer_store_b128(oy, r_iy, li * 16u, 0, SP);
+  __builtin_amdgcn_raw_buffer_store_b128(ox, r_ix, li * 16u, 0, SP);
   const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
-  if constexpr (SO) {
-    st_span<uint64_t, SP>(rsrc_span(a.micro + hb * 4), li, 0, pk(st.x, st.y));
-    st_span<uint64_t, SP>(rsrc_span(a.angle + hb * 4), li, 0, pk(na[0], na[1]));
-    st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, av);
-    st_span<uint64_t, SP>(rsrc_span(a.rpm + hb * 4), li, 0, pk(nr[0], nr[1]));
-    st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
-  } else {
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.micro), hb, n, li, pk(st.x, st.y));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.angle), hb, n, li, pk(na[0], na[1]));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.prev), hb, n, li, av);
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.rpm), hb, n, li, pk(nr[0], nr[1]));
-    st_chunk<uint64_t, SP>(reinterpret_cast<uint64_t *>(a.curr), hb, n, li, pk(nc[0], nc[1]));
-  }
+  st_span<uint64_t, SP>(rsrc_span(a.micro + hb * 4), li, 0, pk(st.x, st.y));
+  st_span<uint64_t, SP>(rsrc_span(a.angle + hb * 4), li, 0, pk(na[0], na[1]));
+  st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, av);
+  st_span<uint64_t, SP>(rsrc_span(a.rpm + hb * 4), li, 0, pk(nr[0], nr[1]));
+  st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
 }
 
 int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
@@ -551,21 +530,16 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
     // 132 B of motor state per robot.  Non-temporal with 2 blocks per CU once it is well past
     // the Infinity Cache; measured (kbench, two passes): 2^22 plain 191.6-192.8 us, nt
     // 183.9-187.2, nt + 64 KiB cap 176.7-179.8; at 2^21 (277 MB) plain 83.3-85.1, nt 87.5-87.9
-    // FMSKF_CAN_VARIANT=0: one clamped descriptor per plane (A/B); the soffset form needs the
-    // [4][N] arrays' wheel planes within 4 GiB of their chunk base
-    static const int var = [] {
-      const char *e = getenv("FMSKF_CAN_VARIANT");
-      return e ? atoi(e) : 1;
-    }();
-    const bool so = var != 0 && 4 * s.n * 4 <= 0xFFFFFFFFull && 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
+    // the sum array's wheel planes through soffset while they lie within 4 GiB of a chunk base
+    const bool so = 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
     if (state_nt(s.n * 66)) {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
       if (so) k_can4<true, true><<<g, kBlock, lds, st>>>(a);
-      else k_can4<true><<<g, kBlock, lds, st>>>(a);
+      else k_can4<true, false><<<g, kBlock, lds, st>>>(a);
     } else {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", false, 0u);
       if (so) k_can4<false, true><<<g, kBlock, lds, st>>>(a);
-      else k_can4<false><<<g, kBlock, lds, st>>>(a);
+      else k_can4<false, false><<<g, kBlock, lds, st>>>(a);
     }
   } else {
     const uint64_t blocks = (4 * s.n + kBlock - 1) / kBlock;

@@ -72,6 +72,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
       0x00020000);
 }
 typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 
 // One element of a plane at a lane of a 256-robot chunk starting at hb (wave-uniform: the
 // wave's first lane rounded down; clamped lanes stay inside the chunk), through a scalar

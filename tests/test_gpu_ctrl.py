@@ -400,11 +400,12 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
     v1 = b"FMSKFCK1" + blob[8:]
     v2 = b"FMSKFCK2" + blob[8:]  # format 2 kept the dlt / speed motor planes
     v3 = b"FMSKFCK3" + blob[8:]  # format 3 had no previous motor angles (ABI 2)
+    v4 = b"FMSKFCK4" + blob[8:]  # format 4 kept the motor IIR state as [4][N] planes
     with Engine(model, n) as e:
         e.load_state(ck)
         before = readout(e)
         for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2),
-                           ("v3", v3)):
+                           ("v3", v3), ("v4", v4)):
             bad = tmp_path / name
             bad.write_bytes(data)
             with pytest.raises(fmskf.FmskfError):
