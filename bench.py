@@ -338,8 +338,10 @@ PATH_BYTES = {
     "rs_tick_2p20_padded_sums": 140,
     "rs_tick_2p20_device_state": 140,
     # WT901 standard poll: row 48 + len 4, parser window / count / flags 14 r+w, error 1,
-    # 15 registers 30 w, magnetometer 6 + q_init 16 r, Data page 64 w
-    "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64,
+    # 15 registers 30 w, magnetometer 6 r, the snapshot row 32 w (the words updateData reads:
+    # the Data page is formed at readout), yaw and gyro z 8 w (round 4: q_init 16 r and the
+    # 64-byte page w instead of the last two: 197 B)
+    "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, IIR y / x, int64 sum r+w; rpm, curr
     # and the previous angle w (the speed is the IIR state y; Status's dlt is formed at readout
     # from the angle and the previous one; the Status ring head is not kept)
@@ -352,7 +354,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 224 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 16 + 64) / 10,
+    "firmware_loop_kf6_2p20": 224 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8) / 10,
 }
 
 

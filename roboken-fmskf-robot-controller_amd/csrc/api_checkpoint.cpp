@@ -59,7 +59,10 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_flags, (size_t)n});
     v.push_back({s.imu_err, (size_t)n});
     v.push_back({s.imu_qinit, (size_t)4 * n * 4});
-    v.push_back({s.imu_data, (size_t)16 * n * 4});
+    v.push_back({s.imu_snap, (size_t)kSnapWords * n * 2});
+    v.push_back({s.imu_yaw, (size_t)n * 4});
+    v.push_back({s.imu_gz, (size_t)n * 4});
+    v.push_back({s.imu_qprev, (size_t)4 * n * 4});
   }
   if (groups & 4) {
     for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_rpm, (void *)s.m_curr})
@@ -215,7 +218,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (memcmp(hd.magic, kCkMagicV3, 8) == 0)
       fail(FMSKF_EINVAL, "format-3 checkpoint (older build): its motor group lacks the previous angles");
     if (memcmp(hd.magic, kCkMagicV4, 8) == 0)
-      fail(FMSKF_EINVAL, "format-4 checkpoint (older build): its motor IIR state is [4][N] planes, this build keeps [N][4] rows");
+      fail(FMSKF_EINVAL, "format-4 checkpoint (older build): it keeps the IMU Data page and [4][N] motor IIR planes, this build the snapshot rows and [N][4] IIR rows");
     if (memcmp(hd.magic, kCkMagic, 8) != 0) fail(FMSKF_EINVAL, "not an fmskf checkpoint");
     f.seek(0, SEEK_SET);
     f.read(&hd, sizeof(hd));

@@ -110,7 +110,10 @@ void zero_imu(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.imu_flags, 0, n, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_data, 0, 16 * n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_snap, 0, kSnapWords * n * 2, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_yaw, 0, n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_gz, 0, n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_qprev, 0, 4 * n * 4, st), "reset imu");
 }
 void zero_motors(fmskf_ctx *h) {
   DevState &s = h->s;
@@ -137,7 +140,10 @@ void ensure_imu(fmskf_ctx *h) {
   s.imu_flags = h->alloc<uint8_t>(n);
   s.imu_err = h->alloc<uint8_t>(n);
   s.imu_qinit = h->alloc<float>(4 * n);
-  s.imu_data = h->alloc<float>(16 * n);
+  s.imu_snap = h->alloc<int16_t>(kSnapWords * n);
+  s.imu_yaw = h->alloc<float>(n);
+  s.imu_gz = h->alloc<float>(n);
+  s.imu_qprev = h->alloc<float>(4 * n);
   zero_imu(h);
 }
 void ensure_motors(fmskf_ctx *h) {
@@ -277,7 +283,7 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.yaw_deg, "yaw_deg");
         if (!t.yaw_deg) {
           ensure_imu(h);
-          t.yaw_deg = s.imu_data + 11 * n;  // IMT::get_status_now_yaw
+          t.yaw_deg = s.imu_yaw;  // IMT::get_status_now_yaw: Data.angle[2]
         }
       }
       if (need_pred) {
@@ -298,8 +304,8 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.rpm, "rpm");
         if (!t.yaw_deg || !t.gyro_z) ensure_imu(h);
         if (!t.rpm) ensure_motors(h);
-        if (!t.yaw_deg) t.yaw_deg = s.imu_data + 11 * n;
-        if (!t.gyro_z) t.gyro_z = s.imu_data + 5 * n;
+        if (!t.yaw_deg) t.yaw_deg = s.imu_yaw;  // Data.angle[2]
+        if (!t.gyro_z) t.gyro_z = s.imu_gz;     // Data.gyro[2]
         if (!t.rpm) t.rpm = s.m_rpm;
       }
       break;

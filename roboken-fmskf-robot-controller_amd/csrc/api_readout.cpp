@@ -22,7 +22,12 @@ int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem) 
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     ensure_imu(h);
-    copy_out(h, data, h->s.imu_data, 16 * h->s.n * 4, mem);
+    if (data) {  // the page formed from the last successful poll's snapshot (imu_data_page)
+      if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+      float *dst = mem == FMSKF_MEM_DEVICE ? data : (float *)h->out_for(16 * h->s.n * 4);
+      launch_check(launch_imu_data(h->s, dst, h->stream), "imu data");
+      if (mem == FMSKF_MEM_HOST) copy_out(h, data, dst, 16 * h->s.n * 4, mem);
+    }
     copy_out(h, is_error, h->s.imu_err, h->s.n, mem);
     finish_out(h, mem);
   });

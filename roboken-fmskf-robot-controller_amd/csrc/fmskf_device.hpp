@@ -145,6 +145,50 @@ __device__ __forceinline__ double wrap_innov(double a) {
   return a;
 }
 
+// ---------------------------------------------------------------------------
+// IMU_IF_WT901C::Data, formed where it is read.  updateData (imu_if_wt901c.cpp:91-129) is a
+// pure function of 16 register words and q_init, so the WT901 kernel keeps the words of the
+// last successful poll (the snapshot row) and the two values the tick consumes (yaw, gyro z),
+// and the readers (fmskf_get_imu, VehicleInfo) form the page from them.  Snapshot row [N][16]
+// int16: accel x y z (0-2), gyro x y (3-4), mag x y z (5-7), roll, pitch (8-9), q0-q3 (10-13),
+// word 14 the flags below, word 15 zero.
+// (the row's flags and width: fmskf_internal.hpp kSnapValid / kSnapLatched / kSnapWords)
+
+// the Data page of a snapshot row (same operations and order as updateData): yaw = angle[2]
+// and gz = gyro[2] as the kernel stored them; qi: q_init as it was when the poll ran
+__device__ __forceinline__ void imu_data_page(const int16_t *w, float yaw, float gz, const float qi[4],
+                                              float d[16]) {
+  float acc[3], gyr[2], mag[3], ang[2], q[4];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    acc[k] = (float)w[k] / 32768.0f * 16.0f;
+    mag[k] = (float)w[5 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    gyr[k] = (float)w[3 + k] / 32768.0f * 2000.0f;
+    ang[k] = (float)w[8 + k] / 32768.0f * 180.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) q[k] = (float)w[10 + k] / 32768.0f;
+  d[0] = acc[0];
+  d[1] = -acc[1];
+  d[2] = -acc[2];
+  d[3] = gyr[0];
+  d[4] = -gyr[1];
+  d[5] = gz;
+  d[6] = mag[0];
+  d[7] = -mag[1];
+  d[8] = -mag[2];
+  d[9] = normalize_deg_0to360(ang[0]) - 180.0f;
+  d[10] = ang[1];
+  d[11] = yaw;
+  d[14] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
+  d[13] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
+  d[12] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
+  d[15] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
+}
+
 __host__ __device__ constexpr int pk(int i, int j) {
   return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
 }

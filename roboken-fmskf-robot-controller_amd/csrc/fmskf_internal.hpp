@@ -11,6 +11,11 @@ namespace fmskf {
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
+// WT901 snapshot rows (DevState::imu_snap, fmskf_device.hpp imu_data_page): int16 words per
+// robot, and word 14's flags: a successful poll happened / that poll latched q_init
+constexpr int kSnapWords = 16;
+enum : int { kSnapValid = 1, kSnapLatched = 2 };
+
 // Device-resident state of one handle.  Every array is plane-major (SoA): element k of
 // instance i lives at [k * N + i] unless the comment says [N][k].
 struct DevState {
@@ -39,7 +44,12 @@ struct DevState {
   uint8_t *imu_flags = nullptr;   // s_cDataUpdate [N]
   uint8_t *imu_err = nullptr;     // is_error [N]
   float *imu_qinit = nullptr;     // q_init [4][N]
-  float *imu_data = nullptr;      // Data page [16][N]
+  // IMU_IF::Data is not stored: the WT901 kernel keeps the register words updateData reads
+  // (fmskf_device.hpp imu_data_page), and the readers form the page
+  int16_t *imu_snap = nullptr;    // snapshot rows [N][16] of the last successful poll
+  float *imu_yaw = nullptr;       // Data.angle[2] [N] (deg): what the tick reads as its yaw
+  float *imu_gz = nullptr;        // Data.gyro[2] [N] (deg/s, negated as Data publishes it)
+  float *imu_qprev = nullptr;     // [4][N] q_init before a poll that latched it (kSnapLatched)
   // MOTOR_IF_M2006 x 4 wheels
   int16_t *m_micro = nullptr;  // [N][4]
   int16_t *m_angle = nullptr;  // [N][4]
@@ -335,6 +345,8 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
 // the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
                   const CtrlPrm &p, uint8_t *frames, hipStream_t st);
+// IMU_IF::Data [16][N] formed from the snapshot (fmskf_get_imu)
+int launch_imu_data(const DevState &s, float *out, hipStream_t st);
 int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
                         const float *cam_pitch, const uint32_t *fault, hipStream_t st);
 // readout helpers

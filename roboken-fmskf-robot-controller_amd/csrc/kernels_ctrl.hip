@@ -155,9 +155,13 @@ __global__ __launch_bounds__(kBlock) void k_can_tx(const int16_t *curr, uint64_t
 // lane builds its record in LDS, then the block writes its 256 records as one contiguous
 // run of dwords (coalesced), instead of 21 strided stores per lane.
 constexpr int kViWords = 21;
-__global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, const float *imu_data,
-                                                         const uint8_t *imu_err, uint64_t n,
-                                                         uint64_t ipitch, uint32_t *out,
+struct ImuView {  // the IMU state VehicleInfo reads (the snapshot: fmskf_device.hpp imu_data_page)
+  const int16_t *snap;
+  const float *yaw, *gz, *qinit, *qprev;
+  const uint8_t *err;
+};
+__global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, ImuView im, uint64_t n,
+                                                         uint32_t *out,
                                                          const uint8_t *floor,
                                                          const float *cam_pitch,
                                                          const uint32_t *fault) {
@@ -174,15 +178,33 @@ __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, const 
     r[3] = (uint32_t)f2i32_arm(vx);
     r[4] = (uint32_t)f2i32_arm(vy);
     r[5] = __builtin_bit_cast(uint32_t, vth);
-    const bool err = imu_err[i] != 0;
+    const bool err = im.err[i] != 0;
     r[6] = err ? 0xFFu : 0u;
-    // Data page [16][N]: accel 0-2, gyro 3-5, mag 6-8, angle 9-11, qut 12-15
+    // the Data page (accel 0-2, gyro 3-5, mag 6-8, angle 9-11, qut 12-15) of the last
+    // successful poll, formed from its snapshot row; zeros before the first one
+    float d[16];
 #pragma unroll
-    for (int k = 0; k < 4; k++) r[7 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[(12 + k) * ipitch + i]);
+    for (int k = 0; k < 16; k++) d[k] = 0.0f;
+    const uint4 r0 = reinterpret_cast<const uint4 *>(im.snap + (uint64_t)kSnapWords * i)[0];
+    const uint4 r1 = reinterpret_cast<const uint4 *>(im.snap + (uint64_t)kSnapWords * i)[1];
+    const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    int16_t w[kSnapWords];
 #pragma unroll
-    for (int k = 0; k < 3; k++) r[11 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[(3 + k) * ipitch + i]);
+    for (int k = 0; k < 8; k++) {
+      w[2 * k] = (int16_t)(rw[k] & 0xFFFFu);
+      w[2 * k + 1] = (int16_t)(rw[k] >> 16);
+    }
+    if (!err && (w[14] & kSnapValid)) {
+      const float *q = (w[14] & kSnapLatched) ? im.qprev : im.qinit;
+      const float qi[4] = {q[i], q[n + i], q[2 * n + i], q[3 * n + i]};
+      imu_data_page(w, im.yaw[i], im.gz[i], qi, d);
+    }
 #pragma unroll
-    for (int k = 0; k < 3; k++) r[14 + k] = err ? 0u : __builtin_bit_cast(uint32_t, imu_data[k * ipitch + i]);
+    for (int k = 0; k < 4; k++) r[7 + k] = err ? 0u : __builtin_bit_cast(uint32_t, d[12 + k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) r[11 + k] = err ? 0u : __builtin_bit_cast(uint32_t, d[3 + k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) r[14 + k] = err ? 0u : __builtin_bit_cast(uint32_t, d[k]);
     if (floor) {
       const uint2 f = reinterpret_cast<const uint2 *>(floor)[i];
       r[17] = f.x;
@@ -305,8 +327,8 @@ int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {
 int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
                         const float *cam_pitch, const uint32_t *fault, hipStream_t st) {
   if (s.n == 0) return 0;
-  k_vehicle_info<<<grid1(s.n), kBlock, 0, st>>>(readout, s.imu_data, s.imu_err, s.n, s.n,
-                                                (uint32_t *)out, floor, cam_pitch, fault);
+  const ImuView im{s.imu_snap, s.imu_yaw, s.imu_gz, s.imu_qinit, s.imu_qprev, s.imu_err};
+  k_vehicle_info<<<grid1(s.n), kBlock, 0, st>>>(readout, im, s.n, (uint32_t *)out, floor, cam_pitch, fault);
   return (int)hipGetLastError();
 }
 

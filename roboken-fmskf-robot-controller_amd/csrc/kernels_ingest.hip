@@ -53,7 +53,9 @@ struct Wt901Args {
   uint8_t *flags;
   uint8_t *err;
   float *qinit;
-  float *data;
+  int16_t *snap;  // [N][16] snapshot rows (fmskf_device.hpp imu_data_page)
+  float *yaw, *gz;
+  float *qprev;
 };
 
 // One byte through WitSerialDataIn (wit_c_sdk.c:132-198): append to the window, resync by
@@ -268,9 +270,12 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   a.cnt[i] = (uint8_t)cnt;
   a.flags[i] = (uint8_t)flags;
   if (!ok) return;
-  // updateData, imu_if_wt901c.cpp:91-129
-  float acc[3], gyr[3], mag[3], ang[3], q[4], qi[4];
-  int16_t ra[3], rg[3], rr[3], rq[4];
+  // updateData, imu_if_wt901c.cpp:91-129: the page is not formed here.  Its 16 words are kept
+  // (the snapshot row: one 32-byte row, two 16-byte stores) and the yaw and gyro z the tick reads;
+  // fmskf_get_imu and VehicleInfo form the page from them (imu_data_page), so a poll moves 157 B
+  // instead of 197 (the 64-byte page written, q_init read).  Only a latching poll reads q_init,
+  // to keep it (qprev) for the page of that very poll, which used the old one.
+  int16_t ra[3], rg[3], rr[3], rq[4], rm[3];
   if (std4) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -291,45 +296,65 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
     for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
   }
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    acc[k] = (float)ra[k] / 32768.0f * 16.0f;
-    gyr[k] = (float)rg[k] / 32768.0f * 2000.0f;
-    mag[k] = (float)reg[(R_HX + k) * n + i];
-    ang[k] = (float)rr[k] / 32768.0f * 180.0f;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    q[k] = (float)rq[k] / 32768.0f;
-    qi[k] = a.qinit[k * n + i];
-  }
-  float *d = a.data;
-  d[0 * n + i] = acc[0];
-  d[1 * n + i] = -acc[1];
-  d[2 * n + i] = -acc[2];
-  d[3 * n + i] = gyr[0];
-  d[4 * n + i] = -gyr[1];
-  d[5 * n + i] = -gyr[2];
-  d[6 * n + i] = mag[0];
-  d[7 * n + i] = -mag[1];
-  d[8 * n + i] = -mag[2];
-  d[9 * n + i] = normalize_deg_0to360(ang[0]) - 180.0f;
-  d[10 * n + i] = ang[1];
-  d[11 * n + i] = ang[2];
-  d[14 * n + i] = -(qi[3] * q[0] + qi[2] * q[1] - qi[1] * q[2] - qi[0] * q[3]);
-  d[13 * n + i] = (-qi[2] * q[0] + qi[3] * q[1] + qi[0] * q[2] - qi[1] * q[3]);
-  d[12 * n + i] = -(qi[1] * q[0] - qi[0] * q[1] + qi[3] * q[2] - qi[2] * q[3]);
-  d[15 * n + i] = (qi[0] * q[0] + qi[1] * q[1] + qi[2] * q[2] + qi[3] * q[3]);
+  for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+  a.yaw[i] = (float)rr[2] / 32768.0f * 180.0f;
+  a.gz[i] = -((float)rg[2] / 32768.0f * 2000.0f);
+  uint32_t snapf = kSnapValid;
   if (a.latch_qinit) {
+    snapf |= kSnapLatched;
 #pragma unroll
-    for (int k = 0; k < 4; k++) a.qinit[k * n + i] = q[k];
+    for (int k = 0; k < 4; k++) {
+      a.qprev[k * n + i] = a.qinit[k * n + i];
+      a.qinit[k * n + i] = (float)rq[k] / 32768.0f;
+    }
   }
+  const auto u = [](int16_t lo, int16_t hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
+  uint4 *row = reinterpret_cast<uint4 *>(a.snap + (uint64_t)kSnapWords * i);
+  row[0] = make_uint4(u(ra[0], ra[1]), u(ra[2], rg[0]), u(rg[1], rm[0]), u(rm[1], rm[2]));
+  row[1] = make_uint4(u(rr[0], rr[1]), u(rq[0], rq[1]), u(rq[2], rq[3]), snapf);
+}
+
+// IMU_IF::Data [16][N] of every robot from its snapshot (fmskf_get_imu): zeros until the first
+// successful poll, like the firmware's zero-initialised page
+__global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const float *yaw, const float *gz,
+                                                     const float *qinit, const float *qprev, uint64_t n,
+                                                     float *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  int16_t w[kSnapWords];
+  const uint4 r0 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[0];
+  const uint4 r1 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[1];
+  const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    w[2 * k] = (int16_t)(rw[k] & 0xFFFFu);
+    w[2 * k + 1] = (int16_t)(rw[k] >> 16);
+  }
+  float d[16];
+  if (w[14] & kSnapValid) {
+    const float *q = (w[14] & kSnapLatched) ? qprev : qinit;
+    const float qi[4] = {q[i], q[n + i], q[2 * n + i], q[3 * n + i]};
+    imu_data_page(w, yaw[i], gz[i], qi, d);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) out[k * n + i] = d[k];
+}
+
+int launch_imu_data(const DevState &s, float *out, hipStream_t st) {
+  if (s.n == 0) return 0;
+  k_imu_data<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_yaw, s.imu_gz,
+                                                                                s.imu_qinit, s.imu_qprev, s.n, out);
+  return (int)hipGetLastError();
 }
 
 int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
                  int latch_qinit, uint32_t read_reg_index, hipStream_t st) {
-  Wt901Args a{s.n,          bytes,          stride,       len,         latch_qinit,
-              read_reg_index, s.imu_reg,    s.imu_parser, s.imu_cnt,   s.imu_flags,
-              s.imu_err,    s.imu_qinit,    s.imu_data};
+  Wt901Args a{s.n,       bytes,      stride,   len,        latch_qinit,  read_reg_index, s.imu_reg,
+              s.imu_parser, s.imu_cnt, s.imu_flags, s.imu_err, s.imu_qinit, s.imu_snap, s.imu_yaw,
+              s.imu_gz,  s.imu_qprev};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   const bool vec = stride % 16 == 0 && stride <= 64 && ((uintptr_t)bytes & 15) == 0;
   if (vec) k_wt901<true><<<g, kBlock, 0, st>>>(a);

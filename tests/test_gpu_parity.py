@@ -550,6 +550,51 @@ def test_wt901_ingest_random_streams(orc, stride):
         bits_equal(data[:, i], orcs[i].data, f"data {i}")
 
 
+@pytest.mark.parametrize("stride", [48, 96])
+def test_wt901_data_page_across_latches(orc, stride):
+    """The Data page is formed at readout from the last successful poll's snapshot row (round
+    5): after EVERY poll it equals the oracle's eagerly written page bit for bit -- before the
+    first successful poll (all zeros), on the poll that latches q_init (its page uses the OLD
+    q_init, kept as qprev), on the polls after it, across a second latch, and for robots whose
+    poll failed (the page of their last success stays).  VehicleInfo reads the same page."""
+    n, polls = 1537, 9
+    rng = np.random.default_rng(41 + stride)
+    orcs = [orc.Wt901(0x51) for _ in range(n)]
+    latch = {1, 5}
+    with Engine("kf6", n) as e:
+        for k in range(polls):
+            buf = np.zeros((n, stride), np.uint8)
+            lens = np.zeros(n, np.uint32)
+            for i in range(n):
+                r = rng.random()
+                if k == 0 and i % 3:  # most robots have no successful poll before the first latch
+                    ts = (0x51, 0x52, 0x53)
+                elif r < 0.7:  # the standard poll (fast path)
+                    ts = (0x51, 0x52, 0x53, 0x59)
+                elif r < 0.85:  # no quaternion frame: the poll fails, the page stays
+                    ts = (0x51, 0x53)
+                else:  # a quaternion frame among others, through the parser
+                    ts = (0x54, 0x59, 0x52)
+                b = np.frombuffer(b"".join(wt901_frame(t, rng.integers(0, 65536, 4)) for t in ts), np.uint8)
+                buf[i, :b.size] = b
+                lens[i] = b.size
+                orcs[i].update(b, latch_qinit=(k in latch))
+            e.ingest_wt901(buf, lens, latch_qinit=(k in latch))
+            data, err = e.get_imu()
+            for i in range(n):
+                assert err[i] == orcs[i].is_error
+                bits_equal(data[:, i], orcs[i].data, f"data {i} poll {k}")
+        vi = e.export_vehicle_info()
+    for i in range(0, n, 5):
+        d = orcs[i].data
+        if orcs[i].is_error:
+            assert vi["imu_fault"][i] == 0xFF and not np.any(vi["imu_q"][i])
+        else:
+            bits_equal(vi["imu_q"][i], d[12:16], f"vi q {i}")
+            bits_equal(vi["imu_g"][i], d[3:6], f"vi g {i}")
+            bits_equal(vi["imu_a"][i], d[0:3], f"vi a {i}")
+
+
 # ----------------------------------------------------------------------------- CAN ingest
 @pytest.mark.parametrize("masked", [True, False, "mixed"])
 def test_can_ingest_bitexact(orc, masked, n=1001):
