@@ -342,10 +342,11 @@ PATH_BYTES = {
     # the Data page is formed at readout), yaw and gyro z 8 w (round 4: q_init 16 r and the
     # 64-byte page w instead of the last two: 197 B)
     "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8,
-    # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, IIR y / x, int64 sum r+w; rpm, curr
-    # and the previous angle w (the speed is the IIR state y; Status's dlt is formed at readout
-    # from the angle and the previous one; the Status ring head is not kept)
-    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 4 + 4 + 8) + 2 + 2 + 2),
+    # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
+    # output y, int64 sum read and written; rpm and curr written (the speed is the IIR state y;
+    # Status's dlt is formed at readout from the angle and the previous one; the IIR input state
+    # x is formed from the previous frame's angle and stamp (round 5: 224 -> 216 B))
+    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 8) + 2 + 2),
     # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
     "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
     # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
@@ -354,7 +355,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 224 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8) / 10,
+    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8) / 10,
 }
 
 

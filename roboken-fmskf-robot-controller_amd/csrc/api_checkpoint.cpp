@@ -65,11 +65,11 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_qprev, (size_t)4 * n * 4});
   }
   if (groups & 4) {
-    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_rpm, (void *)s.m_curr})
+    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_prev_micro,
+                    (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
     v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
-    for (void *p : {(void *)s.m_iir_y, (void *)s.m_iir_x})
-      v.push_back({p, (size_t)4 * n * 4});
+    v.push_back({s.m_iir_y, (size_t)4 * n * 4});
   }
   if (groups & 8) {
     const CtrlDev &c = h->ctrl;

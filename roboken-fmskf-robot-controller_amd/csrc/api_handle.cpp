@@ -126,7 +126,7 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_sum, 0, 4 * s.m_pitch * 8, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_iir_x, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_prev_micro, 0, 4 * n * 2, st), "reset motors");
 }
 
 void ensure_imu(fmskf_ctx *h) {
@@ -159,7 +159,7 @@ void ensure_motors(fmskf_ctx *h) {
   s.m_pitch = plane_pitch(n);
   s.m_sum = h->alloc<int64_t>(4 * s.m_pitch);
   s.m_iir_y = h->alloc<float>(4 * n);
-  s.m_iir_x = h->alloc<float>(4 * n);
+  s.m_prev_micro = h->alloc<int16_t>(4 * n);
   zero_motors(h);
 }
 

@@ -62,7 +62,8 @@ struct DevState {
                                // 27.5-27.8 us from [4][2^20] sums, 24.7 from [4][2^20 + 512])
   uint64_t m_pitch = 0;
   float *m_iir_y = nullptr;    // [N][4] (one 16-byte access per robot in k_can4)
-  float *m_iir_x = nullptr;    // [N][4]
+  int16_t *m_prev_micro = nullptr;  // [N][4] the stamp of the frame before (the IIR1's previous
+                                    // sample x is formed from it: kernels_ingest.hip can_wheel)
   unsigned long long *counters = nullptr;  // [8]
   float *sintab = nullptr;                 // [513]
 };

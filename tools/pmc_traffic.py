@@ -90,8 +90,8 @@ def secondary(root, out):
 # kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
 # written (56); WT901 standard poll: row, len, parser window / count / flags, magnetometer
 # read (72), parser state, error, 15 registers, snapshot row, yaw / gyro z written (85); CAN RX, four
-# wheels: frame, stamp, micro, angle, IIR y / x, sum read (120), those state fields plus rpm,
-# curr and the previous angle written (104); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
+# wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, sum read (120), those
+# state fields plus rpm and curr written (96); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128).  The
 # counters are corrected with the KF6 calibration of profiles/pmc_traffic.json (the same
 # streaming dword / 8- / 16-byte lane accesses: FETCH_SIZE counts half, WRITE_SIZE exact).
@@ -99,7 +99,7 @@ PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 72, 85),
-    ("can_ingest_2p20", "k_can4", 120, 104),
+    ("can_ingest_2p20", "k_can4", 120, 96),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
 ]
 
