@@ -569,8 +569,14 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
     // 132 B of motor state per robot.  Non-temporal with 2 blocks per CU once it is well past
     // the Infinity Cache; measured (kbench, two passes): 2^22 plain 191.6-192.8 us, nt
     // 183.9-187.2, nt + 64 KiB cap 176.7-179.8; at 2^21 (277 MB) plain 83.3-85.1, nt 87.5-87.9
-    // the sum array's wheel planes through soffset while they lie within 4 GiB of a chunk base
-    const bool so = 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
+    // the sum array's wheel planes through soffset while they lie within 4 GiB of a chunk base;
+    // FMSKF_CAN_VARIANT=0 forces one clamped descriptor per sum plane (the form past that, so
+    // the tests check it at small N)
+    static const int var = [] {
+      const char *e = getenv("FMSKF_CAN_VARIANT");
+      return e ? atoi(e) : 1;
+    }();
+    const bool so = var != 0 && 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
     if (state_nt(s.n * 66)) {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
       if (so) k_can4<true, true><<<g, kBlock, lds, st>>>(a);
