@@ -44,7 +44,7 @@ def main():
     with Engine(model, n) as a, Engine(model, n) as b:
         b.comm_init(uid, rank, world)
         info = b.comm_info()  # (world, rank) as the communicator itself reports them
-        counts = []
+        counts, xms = [], []
         pending = 0
         for t in range(T):
             if (t + 1) % every == 0:
@@ -55,6 +55,7 @@ def main():
                     m_, c_, cnt, nrec = b.ensemble_end_count()
                     got.append((m_, c_))
                     counts.append((cnt, nrec))
+                    xms.append(b.ensemble_exchange_ms())
                     pending -= 1
             else:
                 a.tick(**kw(t))
@@ -63,6 +64,7 @@ def main():
             m_, c_, cnt, nrec = b.ensemble_end_count()
             got.append((m_, c_))
             counts.append((cnt, nrec))
+            xms.append(b.ensemble_exchange_ms())
             pending -= 1
         ms, cs = b.ensemble_stats()              # synchronous: partial, ncclAllGather, fold
         b.ensemble_begin()                       # asynchronous stand-alone record
@@ -72,7 +74,7 @@ def main():
         xb, _ = b.get_state()
     np.savez(out, local=np.stack(local), got_mean=np.stack([g[0] for g in got]),
              got_cov=np.stack([g[1] for g in got]), sync_mean=ms, sync_cov=cs, alone_mean=ma,
-             alone_cov=ca, final=final, comm_info=np.array(info), counts=np.array(counts),
+             alone_cov=ca, final=final, comm_info=np.array(info), counts=np.array(counts), exchange_ms=np.array(xms),
              rccl_library=np.array(fmskf.rccl_library()), same_state=np.array(np.array_equal(xa.view(np.uint8), xb.view(np.uint8))))
 
 

@@ -128,6 +128,10 @@ def test_async_ensemble_matches_sync(model, n, every, comm):
         while pending:
             got.append(b.ensemble_end())
             pending -= 1
+        # the side stream's all-gather + copy-out time of the last collected result: measured with
+        # a communicator, -1 without one (the fold wrote the pinned slot itself)
+        xms = b.ensemble_exchange_ms()
+        assert (xms >= 0.0) if comm else (xms == -1.0), xms
         with pytest.raises(fmskf.FmskfError):
             b.ensemble_end()                               # nothing pending
         xa, Pa = a.get_state()

@@ -71,6 +71,9 @@ def test_native_communicator_world_gt_1(tmp_path, model, sizes, every, mode):
         assert o["counts"].shape == (events, 2)
         assert np.all(o["counts"][:, 0] == float(sum(sizes))) and np.all(o["counts"][:, 1] == len(sizes))
         assert str(o["rccl_library"]) == LOOPBACK
+        # every collected result went through the side stream's exchange, and its time is known
+        # (fmskf_ensemble_exchange_ms, the N > 1 bench line's scaling_diag.exchange_ms)
+        assert o["exchange_ms"].shape == (events,) and np.all(o["exchange_ms"] >= 0.0), o["exchange_ms"]
     for k in range(events):
         want_m, want_c = fmskf.ensemble_combine(nx, np.stack([o["local"][k] for o in outs]))
         for r, o in enumerate(outs):
