@@ -23,7 +23,7 @@ TAG = os.environ.get("PMC_TAG", "")
 
 
 def source(root, dirs, kernel):
-    return {"round": TAG, "kernel": kernel, "passes": [f"{root}/{d}" for d in dirs],
+    return {"round": TAG, "kernel": kernel, "passes": [f"{os.path.relpath(root)}/{d}" for d in dirs],
             "committed_as": [f"profiles/{TAG}_{d}.csv" for d in dirs] if TAG else []}
 
 
