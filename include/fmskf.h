@@ -224,7 +224,9 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem);
  * case load leaves the handle's state untouched (lengths are validated before any copy). */
 int fmskf_save_state(fmskf_handle h, const char *path);
 int fmskf_load_state(fmskf_handle h, const char *path);
-/* IMU_IF::Data page [16][N] (accel3, gyro3, mag3, angle3, qut4), is_error [N] */
+/* IMU_IF::Data page [16][N] (accel3, gyro3, mag3, angle3, qut4) of each robot's last successful
+ * poll (zeros before one), formed here from the register words that poll left (updateData,
+ * imu_if_wt901c.cpp:91-129; the ingest keeps the words, not the page), is_error [N] */
 int fmskf_get_imu(fmskf_handle h, float *data, uint8_t *is_error, uint32_t mem);
 /* WT901 register file sReg [0x90][N] (int16) and parser bytes pending [N] */
 int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t mem);

@@ -14,6 +14,7 @@
 #   mix     tools/membench.hip byte-mix streaming ceilings at 2^20 and 2^22
 #   kb      tools/kbench.py per KB_LIST entry "[VAR=v ...] kbench args" (';'-separated),
 #           KB_PASSES passes, one JSON line per run appended to gpurun_out/kb.jsonl
+#   dist1   the distributed code at world 1 under torch.distributed.run (real RCCL, native gather)
 #   world4  four ranks on the one GPU through the loopback RCCL stand-in (rehearsal of the
 #           driver's --gpus N line; rates meaningless)
 # Each GPU step runs under its own time limit; a crash / abort / timeout (rc not in {0, 1})
@@ -105,6 +106,8 @@ for s in $STEPS; do
                echo "{\"pass\": $p, \"env\": \"${envs[*]}\", \"args\": \"${args[*]}\", \"out\": $(tail -n 1 $OUT/kb${p}_$i.log)}" >> "$OUT/kb.jsonl"
              done
            done ;;
+    dist1) run dist1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+             --master-port 29531 bench.py --gpus 1 --steps 200 --warmup 20 --no-cpu-baseline --no-fused --no-secondary ;;
     world4) run world4 600 env FMSKF_RCCL_LIBRARY="$PWD/build/libloopback_rccl.so" LOOPBACK_RCCL_DIR=/tmp \
               LOOPBACK_RCCL_MODE=callback python bench.py --gpus 4 --backend gloo --same-device --gather native \
               --steps 64 --warmup 8 --no-cpu-baseline --no-fused --no-secondary --cfg4-steps 16 ;;
