@@ -337,11 +337,12 @@ PATH_BYTES = {
     "rs_tick_2p20": 140,
     "rs_tick_2p20_padded_sums": 140,
     "rs_tick_2p20_device_state": 140,
-    # WT901 standard poll: row 48 + len 4, parser window / count / flags 14 r+w, error 1,
-    # 15 registers 30 w, magnetometer 6 r, the snapshot row 32 w (the words updateData reads:
-    # the Data page is formed at readout), yaw and gyro z 8 w (round 4: q_init 16 r and the
-    # 64-byte page w instead of the last two: 197 B)
-    "wt901_ingest_2p20": 48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8,
+    # WT901 standard poll: row 48 + len 4, the parser count and update flags 2 r, flags and error
+    # 2 w, 15 registers 30 w, magnetometer 6 r, the snapshot row 32 w (the words updateData
+    # reads: the Data page is formed at readout), yaw and gyro z 8 w; the parser window is empty
+    # before and after such a poll, so its words are neither read nor written (round 4: 197 B,
+    # with the window words, q_init read and the 64-byte page written)
+    "wt901_ingest_2p20": 48 + 4 + 2 + 2 + 30 + 6 + 32 + 8,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
     # output y, int64 sum read and written; rpm and curr written (the speed is the IIR state y;
     # Status's dlt is formed at readout from the angle and the previous one; the IIR input state
@@ -355,7 +356,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 * 14 + 1 + 30 + 6 + 32 + 8) / 10,
+    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
 }
 
 

@@ -156,9 +156,18 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   Wt901Parser ps;
-  ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
-  ps.hi = (uint64_t)a.parser[2 * n + i];
+  // The parser window holds exactly cnt bytes and is zero past them, so an empty window (the
+  // state every poll of whole frames leaves) is all zero: its three words are read only when
+  // bytes are pending, and written only when a window was or is now pending (round 5: the
+  // standard poll moves 132 B instead of 157).
   ps.cnt = a.cnt[i];
+  const uint32_t cnt_in = ps.cnt;
+  ps.lo = 0;
+  ps.hi = 0;
+  if (cnt_in != 0) {
+    ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
+    ps.hi = (uint64_t)a.parser[2 * n + i];
+  }
   ps.flags = a.flags[i];
   const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
   const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
@@ -264,16 +273,18 @@ __global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
   const bool ok = (flags & F_QUAT) != 0;
   if (ok) flags = 0;
   a.err[i] = ok ? 0 : 1;
-  a.parser[i] = (uint32_t)lo;
-  a.parser[n + i] = (uint32_t)(lo >> 32);
-  a.parser[2 * n + i] = (uint32_t)hi;
-  a.cnt[i] = (uint8_t)cnt;
+  if (cnt_in != 0 || cnt != 0) {
+    a.parser[i] = (uint32_t)lo;
+    a.parser[n + i] = (uint32_t)(lo >> 32);
+    a.parser[2 * n + i] = (uint32_t)hi;
+    a.cnt[i] = (uint8_t)cnt;
+  }
   a.flags[i] = (uint8_t)flags;
   if (!ok) return;
   // updateData, imu_if_wt901c.cpp:91-129: the page is not formed here.  Its 16 words are kept
   // (the snapshot row: one 32-byte row, two 16-byte stores) and the yaw and gyro z the tick reads;
   // fmskf_get_imu and VehicleInfo form the page from them (imu_data_page), so a poll moves 157 B
-  // instead of 197 (the 64-byte page written, q_init read).  Only a latching poll reads q_init,
+  // instead of 197 (the 64-byte page written, q_init read; 132 B with the empty-window rule above).  Only a latching poll reads q_init,
   // to keep it (qprev) for the page of that very poll, which used the old one.
   int16_t ra[3], rg[3], rr[3], rq[4], rm[3];
   if (std4) {

@@ -88,8 +88,9 @@ def secondary(root, out):
 
 # The rows either side of the tick at 2^20 (bench path_rows): (bench key, kernel substring,
 # kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
-# written (56); WT901 standard poll: row, len, parser window / count / flags, magnetometer
-# read (72), parser state, error, 15 registers, snapshot row, yaw / gyro z written (85); CAN RX, four
+# written (56); WT901 standard poll: row, len, parser count / flags, magnetometer read (60),
+# flags, error, 15 registers, snapshot row, yaw / gyro z written (72; the empty parser window is
+# neither read nor written); CAN RX, four
 # wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, sum read (120), those
 # state fields plus rpm and curr written (96); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128).  The
@@ -98,7 +99,7 @@ def secondary(root, out):
 PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
-    ("wt901_ingest_2p20", "k_wt901", 72, 85),
+    ("wt901_ingest_2p20", "k_wt901", 60, 72),
     ("can_ingest_2p20", "k_can4", 120, 96),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
 ]
