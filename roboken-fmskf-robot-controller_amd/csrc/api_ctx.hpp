@@ -91,13 +91,11 @@ inline Dims dims_of(uint32_t model) {
 }  // namespace capi
 }  // namespace fmskf
 
-using namespace fmskf;
-using namespace fmskf::capi;
 
 struct fmskf_ctx {
   fmskf_config cfg{};
-  Dims d{};
-  DevState s{};
+  fmskf::capi::Dims d{};
+  fmskf::DevState s{};
   hipStream_t stream = nullptr;
   std::vector<void *> allocs;
   // staging for host-resident inputs
@@ -159,13 +157,13 @@ struct fmskf_ctx {
   int ens_carry = -1;  // the newest event's slot while its fold is not queued yet
   float ens_xms = -1.f;  // the last collected result's exchange time (fmskf_ensemble_exchange_ms)
   // vehicle control state (allocated on first use) and its parameters
-  CtrlDev ctrl{};
+  fmskf::CtrlDev ctrl{};
   fmskf_ctrl_params cprm{};
   bool ctrl_ready = false;
   // model parameters (fp32 / fp64 copies of cfg)
-  Kf6Params kf6{};
-  Ekf9Params ekf9{};
-  Kf12dParams kf12{};
+  fmskf::Kf6Params kf6{};
+  fmskf::Ekf9Params ekf9{};
+  fmskf::Kf12dParams kf12{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // pooled per-launch events (fmskf_kernel_time_total)
@@ -178,18 +176,18 @@ struct fmskf_ctx {
     if (tcount < kMaxTimed) {
       while (tpool.size() < 2 * (tcount + 1)) {
         hipEvent_t e;
-        hip_check(hipEventCreate(&e), "hipEventCreate");
+        fmskf::capi::hip_check(hipEventCreate(&e), "hipEventCreate");
         tpool.push_back(e);
       }
-      hip_check(hipEventRecord(tpool[2 * tcount], stream), "hipEventRecord");
+      fmskf::capi::hip_check(hipEventRecord(tpool[2 * tcount], stream), "hipEventRecord");
     }
-    hip_check(hipEventRecord(ev0, stream), "hipEventRecord");
+    fmskf::capi::hip_check(hipEventRecord(ev0, stream), "hipEventRecord");
   }
   void time_end() {
     if (!timing) return;
-    hip_check(hipEventRecord(ev1, stream), "hipEventRecord");
+    fmskf::capi::hip_check(hipEventRecord(ev1, stream), "hipEventRecord");
     if (tcount < kMaxTimed) {
-      hip_check(hipEventRecord(tpool[2 * tcount + 1], stream), "hipEventRecord");
+      fmskf::capi::hip_check(hipEventRecord(tpool[2 * tcount + 1], stream), "hipEventRecord");
       tcount++;
     }
   }
@@ -199,7 +197,7 @@ struct fmskf_ctx {
     void *p = nullptr;
     if (count == 0) count = 1;
     hipError_t e = hipMalloc(&p, count * sizeof(T));
-    if (e != hipSuccess) fail(FMSKF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (e != hipSuccess) fmskf::capi::fail(FMSKF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     allocs.push_back(p);
     return (T *)p;
   }
@@ -208,7 +206,7 @@ struct fmskf_ctx {
     if (!p) return;
     for (size_t i = 0; i < allocs.size(); i++)
       if (allocs[i] == p) {
-        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        fmskf::capi::hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
         (void)hipFree(p);
         allocs.erase(allocs.begin() + (long)i);
         return;
@@ -217,13 +215,13 @@ struct fmskf_ctx {
   void *stage_for(size_t bytes) {
     if (bytes > stage_bytes) {
       if (stage) {
-        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-        hip_check(hipFree(stage), "hipFree");
+        fmskf::capi::hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        fmskf::capi::hip_check(hipFree(stage), "hipFree");
         stage = nullptr;
         stage_bytes = 0;  // a failed hipMalloc below must not leave a stale capacity
       }
       hipError_t e = hipMalloc(&stage, bytes);
-      if (e != hipSuccess) fail(FMSKF_ENOMEM, "staging hipMalloc failed");
+      if (e != hipSuccess) fmskf::capi::fail(FMSKF_ENOMEM, "staging hipMalloc failed");
       stage_bytes = bytes;
     }
     return stage;
@@ -234,40 +232,40 @@ struct fmskf_ctx {
   char *pinned_in() {
     const int prev = pin_slot ^ 1, slot = pin_slot;
     if (pin_open[prev]) {
-      hip_check(hipEventRecord(pin_ev[prev], stream), "hipEventRecord");
+      fmskf::capi::hip_check(hipEventRecord(pin_ev[prev], stream), "hipEventRecord");
       pin_open[prev] = false;
     }
     pin_slot ^= 1;
     if (!pin_in[slot]) {
-      hip_check(hipHostMalloc(&pin_in[slot], kPinned, hipHostMallocDefault), "hipHostMalloc");
-      hip_check(hipEventCreateWithFlags(&pin_ev[slot], kSyncEvent), "hipEventCreate");
+      fmskf::capi::hip_check(hipHostMalloc(&pin_in[slot], kPinned, hipHostMallocDefault), "hipHostMalloc");
+      fmskf::capi::hip_check(hipEventCreateWithFlags(&pin_ev[slot], fmskf::capi::kSyncEvent), "hipEventCreate");
     } else {
-      hip_check(hipEventSynchronize(pin_ev[slot]), "hipEventSynchronize");
+      fmskf::capi::hip_check(hipEventSynchronize(pin_ev[slot]), "hipEventSynchronize");
     }
     pin_open[slot] = true;
     return (char *)pin_in[slot];
   }
   char *pinned_out() {
-    if (!pin_out) hip_check(hipHostMalloc(&pin_out, kPinned, hipHostMallocDefault), "hipHostMalloc");
+    if (!pin_out) fmskf::capi::hip_check(hipHostMalloc(&pin_out, kPinned, hipHostMallocDefault), "hipHostMalloc");
     return (char *)pin_out;
   }
   // the device's address of a pinned host slot (kernels read / write it over PCIe)
   static void *dev_ptr(void *host) {
     void *d = nullptr;
-    hip_check(hipHostGetDevicePointer(&d, host, 0), "hipHostGetDevicePointer");
+    fmskf::capi::hip_check(hipHostGetDevicePointer(&d, host, 0), "hipHostGetDevicePointer");
     return d;
   }
   void destroy_comm();
   void *out_for(size_t bytes) {
     if (bytes > oscratch_bytes) {
       if (oscratch) {
-        hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
-        hip_check(hipFree(oscratch), "hipFree");
+        fmskf::capi::hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+        fmskf::capi::hip_check(hipFree(oscratch), "hipFree");
         oscratch = nullptr;
         oscratch_bytes = 0;
       }
       hipError_t e = hipMalloc(&oscratch, bytes);
-      if (e != hipSuccess) fail(FMSKF_ENOMEM, "output scratch hipMalloc failed");
+      if (e != hipSuccess) fmskf::capi::fail(FMSKF_ENOMEM, "output scratch hipMalloc failed");
       oscratch_bytes = bytes;
     }
     return oscratch;
