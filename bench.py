@@ -357,6 +357,9 @@ PATH_BYTES = {
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
     "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
+    # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
+    # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
+    "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
 }
 
 
@@ -476,6 +479,13 @@ def path_rows(dev, stream, ticks: int, trig):
             e.ingest_wt901(poll, lens, latch_qinit=(k == 0))
         e.isr_tick(out=fr)
     timed("firmware_loop_kf6_2p20", loop, e)
+    e = driven("kf6")
+
+    def loop_fused(k):
+        if k % 10 == 0:
+            e.ingest_wt901(poll, lens, latch_qinit=(k == 0))
+        e.isr_tick_can(frames[k % R], stamps[k % R], out=fr)
+    timed("firmware_loop_kf6_fused_2p20", loop_fused, e)
     del yaw, gz, rpm, fr, frames, stamps, poll
     torch.cuda.empty_cache()
     return out

@@ -185,6 +185,33 @@ static bool isr_kf6_fused() {
   return v;
 }
 
+// the ISR's launches for resolved inputs `t` (frames into `dst`, or none)
+static void isr_launches(fmskf_ctx *h, const TickIn &t, uint8_t *dst) {
+  const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+  const CtrlPrm p = make_ctrl_prm(h);
+  int fused = (int)hipErrorNotSupported;
+  if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused()) {
+    if (!t.rec && !t.rpm) ensure_motors(h);
+    fused = launch_isr_kf6(h->s, t, h->kf6, libm, h->ctrl, p, dst, h->stream);
+    if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
+  }
+  if (h->cfg.model == FMSKF_MODEL_RS) {
+    launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
+  } else if (fused == (int)hipErrorNotSupported) {  // estimator tick, then the control step and the frame (three launches)
+    int e = 0;
+    switch (h->cfg.model) {
+      case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream); break;
+      case FMSKF_MODEL_EKF9: e = launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream); break;
+      case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream); break;
+    }
+    launch_check(e, "tick kernel launch");
+    if (!t.rec && !t.rpm) ensure_motors(h);
+    const int16_t *rpm = t.rec ? (const int16_t *)(t.rec + 2) : t.rpm ? t.rpm : h->s.m_rpm;
+    launch_check(launch_ctrl_step(h->ctrl, p, rpm, t.rec ? 2 : 1, h->stream), "control launch");
+    if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
+  }
+}
+
 int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem) {
   return guarded([&] {
     check_handle(h);
@@ -192,32 +219,52 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
     DeviceGuard g(h->cfg.device);
     ensure_ctrl(h);
     const uint64_t n = h->s.n;
-    TickIn t = resolve_inputs(h, in, true, true, 1, n);
+    const TickIn t = resolve_inputs(h, in, true, true, 1, n);
+    const size_t bytes = n * 8;
+    uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)host_result(h, bytes);
+    h->time_begin();
+    isr_launches(h, t, dst);
+    h->time_end();
+    if (frames) copy_out_sync(h, frames, dst, bytes, mem);
+  });
+}
+
+int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t *can_stamps,
+                       const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem) {
+  return guarded([&] {
+    check_handle(h);
+    if (!can_frames || !can_stamps) fail(FMSKF_EINVAL, "null can_frames/can_stamps");
+    if (!in) fail(FMSKF_EINVAL, "null inputs");
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    DeviceGuard g(h->cfg.device);
+    ensure_ctrl(h);
+    ensure_motors(h);
+    const uint64_t n = h->s.n;
+    const void *f = can_frames, *s = can_stamps;
+    std::vector<std::pair<const void **, size_t>> cf{{&f, n * 32}, {&s, n * 8}};
+    // one staging round for the CAN frames and the tick inputs when they share a mem flag
+    const bool together = in->mem == mem;
+    const TickIn t = resolve_inputs(h, in, true, true, 1, n, together ? &cf : nullptr);
+    if (!together) {
+      Stager sg(h, mem);
+      for (const auto &it : cf) sg.add(it.first, it.second);
+      sg.run();
+    }
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     const size_t bytes = n * 8;
     uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)host_result(h, bytes);
-    const CtrlPrm p = make_ctrl_prm(h);
-    h->time_begin();
     int fused = (int)hipErrorNotSupported;
-    if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused()) {
-      if (!t.rec && !t.rpm) ensure_motors(h);
-      fused = launch_isr_kf6(h->s, t, h->kf6, libm, h->ctrl, p, dst, h->stream);
-      if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
+    h->time_begin();
+    // one launch where the tick reads the rpm the frames carry (no caller rpm / records)
+    if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused() && !in->kf6_rec && !in->rpm) {
+      fused = launch_isr_kf6_can(h->s, t, h->kf6, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+                                 (const int16_t *)s, h->cfg.motor_dir, h->stream);
+      if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr+can launch");
     }
-    if (h->cfg.model == FMSKF_MODEL_RS) {
-      launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
-    } else if (fused == (int)hipErrorNotSupported) {  // estimator tick, then the control step and the frame (three launches)
-      int e = 0;
-      switch (h->cfg.model) {
-        case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream); break;
-        case FMSKF_MODEL_EKF9: e = launch_ekf9(h->s, t, h->ekf9, libm, true, true, h->stream); break;
-        case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, true, true, h->stream); break;
-      }
-      launch_check(e, "tick kernel launch");
-      if (!t.rec && !t.rpm) ensure_motors(h);
-      const int16_t *rpm = t.rec ? (const int16_t *)(t.rec + 2) : t.rpm ? t.rpm : h->s.m_rpm;
-      launch_check(launch_ctrl_step(h->ctrl, p, rpm, t.rec ? 2 : 1, h->stream), "control launch");
-      if (dst) launch_check(launch_can_tx(h->ctrl, dst, h->stream), "can_tx launch");
+    if (fused == (int)hipErrorNotSupported) {  // CAN RX, then the ISR of fmskf_isr_tick
+      launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, nullptr, h->cfg.motor_dir, h->stream),
+                   "can launch");
+      isr_launches(h, t, dst);
     }
     h->time_end();
     if (frames) copy_out_sync(h, frames, dst, bytes, mem);

@@ -353,8 +353,12 @@ void zero_imu(fmskf_ctx *h);
 void zero_motors(fmskf_ctx *h);
 void ensure_imu(fmskf_ctx *h);
 void ensure_motors(fmskf_ctx *h);
+// extra: more host planes of the same call staged together with the tick inputs (one pinned
+// slot per call: two staging rounds in one call would release the first slot before the
+// kernel that reads it is queued); they must share in->mem
 TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, bool need_pred,
-                      uint32_t n_ticks, uint64_t stride);
+                      uint32_t n_ticks, uint64_t stride,
+                      const std::vector<std::pair<const void **, size_t>> *extra = nullptr);
 void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, uint32_t n_ticks,
               uint64_t stride);
 void copy_out(fmskf_ctx *h, void *dst, const void *src, size_t bytes, uint32_t mem);

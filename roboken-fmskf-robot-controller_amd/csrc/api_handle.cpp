@@ -235,7 +235,8 @@ namespace capi {
 // Resolve the tick inputs of a call (NULL -> device-resident ingest state), stage host
 // planes and validate what the model needs.
 TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, bool need_pred,
-                      uint32_t n_ticks, uint64_t stride) {
+                      uint32_t n_ticks, uint64_t stride,
+                      const std::vector<std::pair<const void **, size_t>> *extra) {
   if (!in) fail(FMSKF_EINVAL, "null inputs");
   DevState &s = h->s;
   const uint64_t n = s.n;
@@ -272,6 +273,8 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
   sg.add((const void **)&t.z, ((uint64_t)(n_ticks - 1) * stride * 8 + 7 * stride + n) * 8);
   sg.add((const void **)&t.valid, span);
   sg.add((const void **)&t.rec, span * 16);
+  if (extra)
+    for (const auto &it : *extra) sg.add(it.first, it.second);
   sg.run();
   const bool many = n_ticks > 1 || stride != n;
   auto dev_default = [&](const void *p, const char *name) {

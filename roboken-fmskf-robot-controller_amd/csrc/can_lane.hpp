@@ -1,0 +1,181 @@
+// can_lane.hpp -- MOTOR_IF_M2006::rx_callback (VD_motor_if_m2006.cpp:32-72) as lane functions,
+// shared by the CAN RX kernels (kernels_ingest.hip k_can4 / k_can) and the fused firmware tick
+// (kernels_ctrl.hip k_isr_kf6 with CAN: the tick's four frames per robot, then the ISR, in one
+// kernel).  Cortex-M7 integer semantics: wrapping MUL, SDIV x/0 = 0.
+#pragma once
+#include "fmskf_device.hpp"
+#include "fmskf_internal.hpp"
+#include "kf_generic.hpp"
+
+#pragma clang fp contract(off)
+
+namespace fmskf {
+
+struct CanArgs {
+  uint64_t n;
+  const uint8_t *frames;
+  const int16_t *stamps;
+  const uint8_t *present;
+  int8_t dir[4];
+  int16_t *micro, *angle, *rpm, *curr;
+  int16_t *prev;  // [N][4] the angle before this frame (Status::flt_dltOutAngle_rad at readout)
+  int16_t *prev_micro;  // [N][4] the stamp before this frame (the IIR1's previous sample, speed_x)
+  int64_t *sum;  // [4][sum_pitch]
+  uint64_t sum_pitch;
+  float *iir_y;  // [N][4] UTIL::IIR1 output state, also Status::flt_SpeedRadPS
+};
+
+__device__ __forceinline__ int16_t s16_of(uint32_t h, uint32_t l) { return (int16_t)((h << 8) | l); }
+__device__ __forceinline__ int32_t mul_wrap(int32_t a, int32_t b) {
+  return (int32_t)((uint32_t)a * (uint32_t)b);
+}
+// Cortex-M7 SDIV: x/0 = 0 (CCR.DIV_0_TRP = 0 at reset), INT_MIN/-1 = INT_MIN
+// Branch-free: the two special cases divide by 1 and select, so the wave runs one division
+// instead of two exec-masked regions per wheel
+__device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
+  const bool ovf = a == INT32_MIN && b == -1;
+  const int32_t q = a / (b == 0 || ovf ? 1 : b);
+  return b == 0 ? 0 : q;
+}
+
+// one wheel's rx_callback on its 8-byte frame and microsecond stamp (VD_motor_if_m2006.cpp:
+// 32-72): the decoded fields, the IIR1 speed state and the int64 sum.  The Status ring's head
+// (:33-34, 71) is not kept: both readers, get_status_latest and get_status_estimate
+// (VD_motor_if_m2006.hpp:44-47, .cpp:11-24), read only the newest entry, which is what the
+// engine stores, so the head selects nothing that can be observed (round 4: 232 -> 224 B)
+struct CanWheel {
+  int16_t angle, rpm, curr;
+  float iir_y;
+  int64_t sum;
+};
+// the speed sample rx_callback feeds the IIR1 (VD_motor_if_m2006.cpp:49-63): the wrapped angle
+// step over the wrapped microsecond step, with the M7's wrapping MUL and SDIV x/0 = 0
+__device__ __forceinline__ float speed_x(int16_t new_angle, int16_t old_angle, int16_t micro, int16_t old_micro) {
+  int32_t raw_ang_dlt = new_angle - old_angle;
+  int32_t usec_dlt = micro - old_micro;
+  if (raw_ang_dlt > (K::raw_per_rot / 2)) raw_ang_dlt = raw_ang_dlt - K::raw_per_rot;
+  else if (raw_ang_dlt < -(K::raw_per_rot / 2)) raw_ang_dlt = raw_ang_dlt + K::raw_per_rot;
+  if (usec_dlt > 0x7FFF) usec_dlt = usec_dlt - 0x7FFF;
+  else if (usec_dlt < -0x7FFF) usec_dlt = usec_dlt + 0x7FFF;
+  const int32_t num = mul_wrap(mul_wrap(raw_ang_dlt, 2), 3141593);
+  return (float)sdiv_arm(num, usec_dlt) / (float)K::raw_per_rot;
+}
+// IIR1's state x (prev_X_, util_iir.hpp:39-45) is not stored (round 5): it is the previous
+// frame's speed sample, a pure function of that frame's angle / stamp and the ones before it
+// (prev_angle / prev_micro, which the engine keeps for Status::flt_dltOutAngle_rad and here), so
+// it is formed again from them: 4 B read + 2 B written per wheel instead of a float read and
+// written (224 -> 216 B per robot).  All zero after reset gives x = 0 (SDIV 0/0 = 0), the
+// zero-initialised filter's prev_X_.
+__device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t micro, int dir,
+                                              int16_t old_micro, int16_t old_angle, int16_t prev_micro,
+                                              int16_t prev_angle, float py, int64_t sum) {
+  const uint32_t b0 = fx & 0xFF, b1 = (fx >> 8) & 0xFF, b2 = (fx >> 16) & 0xFF, b3 = fx >> 24;
+  const uint32_t b4 = fy & 0xFF, b5 = (fy >> 8) & 0xFF;
+  CanWheel o;
+  const int16_t new_angle =
+      dir == 1 ? s16_of(b0, b1) : (int16_t)(K::raw_per_rot - s16_of(b0, b1));
+  o.angle = new_angle;
+  o.rpm = (int16_t)(s16_of(b2, b3) * dir);
+  o.curr = (int16_t)(s16_of(b4, b5) * dir);
+  const float x = speed_x(new_angle, old_angle, micro, old_micro);
+  const float pxv = speed_x(old_angle, prev_angle, old_micro, prev_micro);
+  o.iir_y = 0.8f * py + 0.1f * x + 0.1f * pxv;  // UTIL::IIR1::update, util_iir.hpp:39-45
+  // Status::flt_dltOutAngle_rad (VD_motor_if_m2006.cpp:64) is formed at readout from this angle and
+  // the previous one, which the caller stores (k_motor_dlt)
+  int16_t d = (int16_t)(new_angle - old_angle);
+  d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
+  o.sum = sum + d;
+  return o;
+}
+
+// One robot per lane, every wheel present: the robot's 32 frame bytes, its four stamps and its
+// [N][4] int16 / float state in single 16- and 8-byte accesses, and each [4][N] sum plane row
+// coalesced across the wave, every access through a scalar descriptor at the block's 256-robot
+// chunk hb (wave-uniform) with the KF6 tick's cache policies: the frames and stamps (read once)
+// `nt`, the state stored `sc1` while cache-resident; NT: the motor state streams from HBM,
+// `nt` loads and stores.  SO: the sum array's wheel planes at soffset from one descriptor (the
+// launcher checks the 4 GiB span); else one clamped descriptor per plane.  load() issues every
+// load; step() computes the four wheels and stores (`live` lanes only: the fused ISR runs
+// clamped lanes past N) and returns the new rpm of the four wheels (s16_rawSpeedRpm) packed.
+template <bool NT, bool SO>
+struct Can4Lane {
+  static constexpr int LP = NT ? kStateNT : 0, SP = st_pol(LP), IP = 2;  // IP: inputs nt
+  uint64_t hb;
+  uint32_t li;
+  uint4 f01, f23;
+  uint32_t iyw[4];
+  uint64_t sv, mv, av, pmv, pav;
+  int64_t sm[4];
+
+  __device__ __forceinline__ void load(const CanArgs &a, uint64_t hb_, uint32_t li_) {
+    hb = hb_;
+    li = li_;
+    const auto rf = rsrc_span(a.frames + hb * 32);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u, 0, IP);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rf, li * 32u + 16u, 0, IP);
+    f01 = make_uint4(v0[0], v0[1], v0[2], v0[3]);
+    f23 = make_uint4(v1[0], v1[1], v1[2], v1[3]);
+    const auto iy = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.iir_y + hb * 4), li * 16u, 0, LP);
+    // element copies before use (see kf6_load_in: an ext_vector element read through a bit cast
+    // miscompiled once)
+    iyw[0] = iy[0];
+    iyw[1] = iy[1];
+    iyw[2] = iy[2];
+    iyw[3] = iy[3];
+    sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
+    mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);
+    av = ld_span<uint64_t, LP>(rsrc_span(a.angle + hb * 4), li, 0);
+    pmv = ld_span<uint64_t, LP>(rsrc_span(a.prev_micro + hb * 4), li, 0);
+    pav = ld_span<uint64_t, LP>(rsrc_span(a.prev + hb * 4), li, 0);
+    const auto r_sm = rsrc_span(a.sum + hb);
+    const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+      sm[w] = SO ? ld_span<int64_t, LP>(r_sm, li, w * ps)
+                 : ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li);
+  }
+
+  __device__ __forceinline__ uint2 step(const CanArgs &a, bool live) {
+    const uint2 st = make_uint2((uint32_t)sv, (uint32_t)(sv >> 32));
+    const uint2 om = make_uint2((uint32_t)mv, (uint32_t)(mv >> 32)), oa = make_uint2((uint32_t)av, (uint32_t)(av >> 32));
+    const uint32_t fx[4] = {f01.x, f01.z, f23.x, f23.z}, fy[4] = {f01.y, f01.w, f23.y, f23.w};
+    const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
+    const uint32_t pmw[2] = {(uint32_t)pmv, (uint32_t)(pmv >> 32)}, paw[2] = {(uint32_t)pav, (uint32_t)(pav >> 32)};
+    uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0};
+    v4u32_t oy;
+    int64_t os[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const int sh = 16 * (w & 1);
+      const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
+                                   (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
+                                   (int16_t)(pmw[w >> 1] >> sh), (int16_t)(paw[w >> 1] >> sh),
+                                   __builtin_bit_cast(float, iyw[w]), sm[w]);
+      oy[w] = __builtin_bit_cast(uint32_t, o.iir_y);
+      os[w] = o.sum;
+      na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
+      nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
+      nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
+    }
+    if (live) {
+      const auto r_sm = rsrc_span(a.sum + hb);
+      const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        if constexpr (SO) st_span<int64_t, SP>(r_sm, li, w * ps, os[w]);
+        else st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li, os[w]);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(oy, rsrc_span(a.iir_y + hb * 4), li * 16u, 0, SP);
+      const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
+      st_span<uint64_t, SP>(rsrc_span(a.prev_micro + hb * 4), li, 0, mv);
+      st_span<uint64_t, SP>(rsrc_span(a.micro + hb * 4), li, 0, pk(st.x, st.y));
+      st_span<uint64_t, SP>(rsrc_span(a.angle + hb * 4), li, 0, pk(na[0], na[1]));
+      st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, av);
+      st_span<uint64_t, SP>(rsrc_span(a.rpm + hb * 4), li, 0, pk(nr[0], nr[1]));
+      st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
+    }
+    return make_uint2(nr[0], nr[1]);
+  }
+};
+
+}  // namespace fmskf

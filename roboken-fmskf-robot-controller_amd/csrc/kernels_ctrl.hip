@@ -12,6 +12,7 @@
 // expression keeps the reference's operation order (library built with -ffp-contract=off), so
 // results are bit-identical to oracle/fmskf_oracle.c, itself pinned to the reference's own
 // FF_PI_D (tests/golden/ctrl_ref.npz).  HBM-bound: ~370 B per robot-tick, no reuse.
+#include "can_lane.hpp"
 #include "ctrl_lane.hpp"
 #include "kf6_lane.hpp"
 #include "lane_rs.hpp"
@@ -114,24 +115,34 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
 // fmskf_control + fmskf_can_tx in sequence.  One robot per lane, the clamped-index form of
 // k_kf6t (lanes past N load instance N-1 and store nothing); every load of both steps is
 // issued before either computes.  CPC: the control planes' cache policy.
-template <class O, int CPC>
+// CAN (round 5, fmskf_isr_tick_can): the tick's four C610 frames per robot first
+// (MOTOR_IF_M2006::rx_callback, can_lane.hpp), their rpm handed to the tick and the wheel loops
+// in registers -- the firmware's CAN RX ISR and 1 kHz ISR in one launch, bit-identical to
+// fmskf_ingest_can + fmskf_isr_tick
+template <class O, int CPC, bool CAN = false>
 __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, CtrlDev c, CtrlPrm p,
-                                                   uint8_t *frames) {
+                                                   uint8_t *frames, CanArgs can) {
   const uint64_t n = a.n;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
   const uint32_t ic = live ? i : (uint32_t)n - 1u;
+  Can4Lane<false, true> cl;
+  if constexpr (CAN) {  // the block's 256-robot chunk (every block has a live lane)
+    const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
+    cl.load(can, hb, ic - hb);
+  }
   float x[6], P[21];
   __shared__ float wtab[O::LIBM ? 1 : kBlock / 64][O::LIBM ? 1 : kWaveTab];
   float *stab = wtab[O::LIBM ? 0 : threadIdx.x >> 6];
   WaveTable<O::LIBM> tv(a.in.sintab);
   kf6_load_state<O>(a.x, a.P, a.pitch, ic, x, P);
-  const Kf6In m = kf6_load_in<O>(a.in, n, 0, ic);
+  Kf6In m = kf6_load_in<O>(a.in, n, 0, ic);
   CtrlLane<true, CPC> L;
   L.load(c, ic);
   tv.store(stab);
   Kf6Lo<O> lo;  // O::COMP: the position low parts (FMSKF_CFG_COMP_POS)
   kf6_load_lo<O>(a.prm.lo, ic, lo);
+  if constexpr (CAN) m.rpm = cl.step(can, live);  // the rpm this tick's frames carried
   kf6_tick1<O>(m, stab, a.prm, x, P, lo);
   if (live) {
     kf6_store_state<O>(a.x, a.P, a.pitch, i, x, P);
@@ -275,34 +286,39 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
 // > 256 MiB) the control planes are non-temporal, as in k_isr_rs.
 template <bool LIBM, bool VALID, bool REC, bool COMP>
 static int isr_kf6_v(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
-                     bool nt, hipStream_t st) {
+                     bool nt, hipStream_t st, const CanArgs *can) {
   using O = Opt<LIBM, true, true, true, VALID, REC, false, false, COMP>;
-  if (nt) {
-    const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
-    k_isr_kf6<O, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames);
-  } else {
-    k_isr_kf6<O, 0><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames);
+  const unsigned lds = nt ? FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u) : 0u;
+  if constexpr (!REC) {  // with CAN the rpm comes from the frames, so the inputs are planes
+    if (can) {
+      if (nt) k_isr_kf6<O, kStateNT, true><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames, *can);
+      else k_isr_kf6<O, 0, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames, *can);
+      return (int)hipGetLastError();
+    }
   }
+  if (can) return (int)hipErrorNotSupported;
+  if (nt) k_isr_kf6<O, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames, CanArgs{});
+  else k_isr_kf6<O, 0><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames, CanArgs{});
   return (int)hipGetLastError();
 }
 
 template <bool COMP>
 static int isr_kf6_c(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames, bool nt,
-                     hipStream_t st, bool libm, bool valid, bool rec) {
+                     hipStream_t st, bool libm, bool valid, bool rec, const CanArgs *can) {
   if (libm) {
-    if (valid) return rec ? isr_kf6_v<true, true, true, COMP>(a, c, p, frames, nt, st)
-                          : isr_kf6_v<true, true, false, COMP>(a, c, p, frames, nt, st);
-    return rec ? isr_kf6_v<true, false, true, COMP>(a, c, p, frames, nt, st)
-               : isr_kf6_v<true, false, false, COMP>(a, c, p, frames, nt, st);
+    if (valid) return rec ? isr_kf6_v<true, true, true, COMP>(a, c, p, frames, nt, st, can)
+                          : isr_kf6_v<true, true, false, COMP>(a, c, p, frames, nt, st, can);
+    return rec ? isr_kf6_v<true, false, true, COMP>(a, c, p, frames, nt, st, can)
+               : isr_kf6_v<true, false, false, COMP>(a, c, p, frames, nt, st, can);
   }
-  if (valid) return rec ? isr_kf6_v<false, true, true, COMP>(a, c, p, frames, nt, st)
-                        : isr_kf6_v<false, true, false, COMP>(a, c, p, frames, nt, st);
-  return rec ? isr_kf6_v<false, false, true, COMP>(a, c, p, frames, nt, st)
-             : isr_kf6_v<false, false, false, COMP>(a, c, p, frames, nt, st);
+  if (valid) return rec ? isr_kf6_v<false, true, true, COMP>(a, c, p, frames, nt, st, can)
+                        : isr_kf6_v<false, true, false, COMP>(a, c, p, frames, nt, st, can);
+  return rec ? isr_kf6_v<false, false, true, COMP>(a, c, p, frames, nt, st, can)
+             : isr_kf6_v<false, false, false, COMP>(a, c, p, frames, nt, st, can);
 }
 
-int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
-                   const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+static int isr_kf6_l(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                     const CtrlPrm &p, uint8_t *frames, hipStream_t st, const CanArgs *can) {
   if (c.n == 0) return 0;
   const bool small_state = s.pitch * 84 < 0xFFFFFFFFull;
   const bool small_ctrl = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
@@ -314,8 +330,41 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
   const KfArgs<MdKF6, Kf6Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, kp};
   const bool nt = state_nt(ctrl_state_bytes(c) + s.n * sb);
   const bool valid = in.valid != nullptr, rec = in.rec != nullptr;
-  return kp.lo ? isr_kf6_c<true>(a, c, p, frames, nt, st, libm, valid, rec)
-               : isr_kf6_c<false>(a, c, p, frames, nt, st, libm, valid, rec);
+  return kp.lo ? isr_kf6_c<true>(a, c, p, frames, nt, st, libm, valid, rec, can)
+               : isr_kf6_c<false>(a, c, p, frames, nt, st, libm, valid, rec, can);
+}
+
+int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                   const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+  return isr_kf6_l(s, in, kp, libm, c, p, frames, st, nullptr);
+}
+
+// fmskf_isr_tick_can: the CAN RX of the tick's frames (every wheel present) fused into the KF6
+// ISR.  hipErrorNotSupported where the fused form does not apply (record inputs, the tick's
+// non-temporal regime, the motor state past the cached regime or its sum planes past 4 GiB,
+// unaligned frames / stamps): the caller then runs CAN RX and the ISR as two calls
+int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                       const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
+                       const int8_t dir[4], hipStream_t st) {
+  if (in.rec || !s.m_sum || state_nt(s.n * 66) || 4 * s.m_pitch * 8 > 0xFFFFFFFFull ||
+      ((uintptr_t)can_frames & 15) != 0 || ((uintptr_t)can_stamps & 7) != 0)
+    return (int)hipErrorNotSupported;
+  CanArgs ca{};
+  ca.n = s.n;
+  ca.frames = can_frames;
+  ca.stamps = can_stamps;
+  ca.present = nullptr;
+  for (int w = 0; w < 4; w++) ca.dir[w] = dir[w];
+  ca.micro = s.m_micro;
+  ca.angle = s.m_angle;
+  ca.prev = s.m_prev;
+  ca.prev_micro = s.m_prev_micro;
+  ca.rpm = s.m_rpm;
+  ca.curr = s.m_curr;
+  ca.sum = s.m_sum;
+  ca.sum_pitch = s.m_pitch;
+  ca.iir_y = s.m_iir_y;
+  return isr_kf6_l(s, in, kp, libm, c, p, frames, st, &ca);
 }
 
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {

@@ -143,6 +143,7 @@ SIGNATURES = {
     "fmskf_control": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_can_tx": (C.c_int, [_H, _P, C.c_uint32]),
     "fmskf_isr_tick": (C.c_int, [_H, _P, _P, C.c_uint32]),
+    "fmskf_isr_tick_can": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),
     "fmskf_save_state": (C.c_int, [_H, C.c_char_p]),
     "fmskf_load_state": (C.c_int, [_H, C.c_char_p]),
     "fmskf_get_ctrl": (C.c_int, [_H, _P, _P, _P, _P, C.c_uint32]),

@@ -495,6 +495,37 @@ class Engine:
               "isr_tick")
         return f
 
+    def isr_tick_can(self, can_frames, can_stamps, frames=True, out=None, **kw):
+        """The tick's CAN RX and the ISR in one call (fmskf_isr_tick_can): ingest_can(can_frames,
+        can_stamps) then isr_tick(**kw), one kernel for KF6.  can_frames [N, 4, 8] uint8,
+        can_stamps [N, 4] int16, both host arrays or both device tensors; the [N][8] TX frames
+        come back the same way (numpy, or the device tensor `out`), None with frames=False."""
+        a = _Args()
+        pf = a.ptr(can_frames, np.uint8)
+        ps = a.ptr(can_stamps, np.int16)
+        for name, v, per in (("can_frames", can_frames, 32), ("can_stamps", can_stamps, 4)):
+            have = v.numel() if _is_torch(v) else np.size(v)
+            if have < per * self.n:
+                raise ValueError(f"{name}: {have} elements, need {per}*N = {per * self.n}")
+        mem = MEM_HOST if a.mem is None else a.mem
+        ti, _keep = self._inputs(kw)
+        if not frames:
+            check(load().fmskf_isr_tick_can(self.h, pf, ps, C.byref(ti), None, mem), "isr_tick_can")
+            return None
+        if mem == MEM_DEVICE:
+            import torch
+            if out is None:
+                out = torch.empty((self.n, 8), dtype=torch.uint8, device=can_frames.device)
+            if not (_is_torch(out) and out.is_cuda):
+                raise TypeError("device CAN frames need a device `out`")
+            check(load().fmskf_isr_tick_can(self.h, pf, ps, C.byref(ti), C.c_void_p(out.data_ptr()), mem),
+                  "isr_tick_can")
+            return out
+        f = np.empty((self.n, 8), np.uint8)
+        check(load().fmskf_isr_tick_can(self.h, pf, ps, C.byref(ti), f.ctypes.data_as(C.c_void_p), mem),
+              "isr_tick_can")
+        return f
+
     def get_ctrl(self):
         vt = np.empty((3, self.n), np.float32)
         cur = np.empty((self.n, 4), np.int16)

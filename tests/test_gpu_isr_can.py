@@ -1,0 +1,103 @@
+"""fmskf_isr_tick_can: the tick's CAN RX and the firmware ISR in one call (one kernel for KF6,
+k_isr_kf6 with the C610 lane of can_lane.hpp in front) against the two calls it replaces,
+fmskf_ingest_can + fmskf_isr_tick, on random targets / power events.  Bar: bit-exact for the
+estimator state, the control state, the 0x200 frames and the whole motor state
+(MOTOR_IF_M2006::rx_callback, VD_motor_if_m2006.cpp; the two-call path is itself held to the
+oracle by test_gpu_parity / test_gpu_ctrl)."""
+import numpy as np
+import pytest
+
+import fmskf
+from fmskf import Engine
+from fmskf.synth import Trajectory
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+# kf6*: the fused kernel (planes, LIBM, validity mask, compensated positions, device-resident
+# frames, a ragged last block, the non-temporal control regime past the Infinity Cache);
+# kf6rpm / kf6rec / rs: the documented two-call fallback (a caller rpm or records, model RS)
+CASES = [("kf6", 4099, 40), ("kf6", 1, 20), ("kf6libm", 777, 20), ("kf6mask", 1001, 20),
+         ("kf6comp", 513, 20), ("kf6dev", 2048 + 5, 20), ("kf6rpm", 300, 12), ("kf6rec", 257, 12),
+         ("rs", 999, 12), ("kf6", (1 << 20) + 17, 3)]
+
+
+@pytest.mark.parametrize("case,n,T", CASES)
+def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
+    import torch
+    rng = np.random.default_rng(7 + n)
+    tr = Trajectory(n, T, seed=53)
+    trig = fmskf.TRIG_LIBM if case == "kf6libm" else fmskf.TRIG_TABLE512
+    flags = fmskf.CFG_COMP_POS if case == "kf6comp" else 0
+    model = "rs" if case == "rs" else "kf6"
+    yaw, gz, rpm = tr.kf6_inputs()
+    valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if case == "kf6mask" else None
+
+    def kw(t):
+        if case == "rs":
+            return dict(yaw_deg=yaw[t])  # sums and rpm: the device motor state
+        if case == "kf6rec":
+            return dict(kf6_rec=fmskf.kf6_records(yaw, gz, rpm)[t])
+        d = dict(yaw_deg=yaw[t], gyro_z_dps=gz[t])
+        if case == "kf6rpm":
+            d["rpm"] = rpm[t]
+        if valid is not None:
+            d["valid"] = valid[t]
+        return d
+
+    vel = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                    rng.uniform(-3, 3, n)]).astype(np.float32)
+    acl = np.full((3, n), 1000.0, np.float32)
+    jrk = np.full((3, n), 10000.0, np.float32)
+    with Engine(model, n, trig=trig, flags=flags) as a, Engine(model, n, trig=trig, flags=flags) as b:
+        on = (rng.random(n) < 0.9).astype(np.uint8)
+        for e in (a, b):
+            e.set_power(on)
+            e.set_target_vel(vel, acl, jrk)
+        for t in range(T):
+            f, s = tr.can_frames(t)
+            if case == "kf6dev":
+                f, s = (torch.from_numpy(np.ascontiguousarray(f)).cuda(),
+                        torch.from_numpy(np.ascontiguousarray(s)).cuda())
+            last = t == T - 1 or t % 5 == 1
+            fa = a.isr_tick_can(f, s, frames=last, **kw(t))
+            b.ingest_can(f, s)
+            if case != "kf6dev":
+                fb = b.isr_tick(frames=last, **kw(t))
+            elif last:
+                fb = b.isr_tick(out=torch.empty((n, 8), dtype=torch.uint8, device="cuda"), **kw(t)).cpu().numpy()
+                fa = fa.cpu().numpy()
+            else:
+                b.isr_tick(frames=False, **kw(t))
+            if last:
+                np.testing.assert_array_equal(fa, fb)
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        ga, gb = a.get_ctrl(), b.get_ctrl()
+        ma, mb = a.get_motors(), b.get_motors()
+    np.testing.assert_array_equal(bits(xa), bits(xb))
+    if Pa is not None:
+        np.testing.assert_array_equal(bits(Pa), bits(Pb))
+    for k in ("vel_tgt", "curr", "wheel_tgt", "wheel_ctrl"):
+        np.testing.assert_array_equal(bits(ga[k]), bits(gb[k]))
+    for k in ma:
+        np.testing.assert_array_equal(bits(ma[k]), bits(mb[k]), err_msg=k)
+
+
+def test_isr_tick_can_errors():
+    """null CAN buffers and a bad mem flag are refused before any launch (the handle stays usable)"""
+    import ctypes as C
+    n = 64
+    with Engine("kf6", n) as e:
+        L = fmskf._lib.load()
+        assert L.fmskf_isr_tick_can(e.h, None, None, None, None, fmskf.MEM_HOST) == fmskf._lib.EINVAL
+        f = np.zeros((n, 4, 8), np.uint8)
+        s = np.zeros((n, 4), np.int16)
+        assert L.fmskf_isr_tick_can(e.h, f.ctypes.data_as(C.c_void_p), s.ctypes.data_as(C.c_void_p),
+                                    None, None, 7) == fmskf._lib.EINVAL
+        e.isr_tick_can(f, s, frames=False)
