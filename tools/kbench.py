@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
     ap.add_argument("--can-desync", action="store_true",
                     help="--op can: one masked tick before timing (robots' ring heads out of step)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
@@ -90,7 +90,7 @@ def main():
         preps = [e.prepare(valid=vm[r], **kws[r]) for r in range(R)]
     if args.host:
         return bench_host(args, e, n, yaw, gz, rpm)
-    if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph"):
+    if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr"):
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
@@ -269,7 +269,19 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
     dy, dg, dr = yaw[0].clone(), gz[0].clone(), rpm[0].clone()
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
 
+    # isr_can: fmskf_isr_tick_can (the tick's CAN RX fused into the KF6 ISR); can_isr: the same
+    # work as fmskf_ingest_can + fmskf_isr_tick
+    cf = torch.randint(0, 256, (n, 4, 8), dtype=torch.uint8, device=dev)
+    cs = (torch.arange(4, device=dev, dtype=torch.int16) * 250).expand(n, 4).contiguous()
+
     def direct():
+        if args.op == "isr_can":
+            e.isr_tick_can(cf, cs, out=fr, yaw_deg=dy, gyro_z_dps=dg)
+            return
+        if args.op == "can_isr":
+            e.ingest_can(cf, cs)
+            e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg)
+            return
         if args.op.startswith("isr"):  # fmskf_isr_tick: one fused kernel for RS
             e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
             return
