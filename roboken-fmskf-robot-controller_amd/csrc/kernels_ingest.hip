@@ -151,8 +151,11 @@ struct Wt901Parser {
 // cache policies through buffer descriptors (same box, against 35.4-36.9 plain): `sc1` state
 // stores 36.0-36.3; `nt` poll-row loads 41.2-42.0, since a 16-byte load of 48-byte rows uses a
 // third of every line it touches and `nt` evicts the line before the next load reads the rest.
+#ifndef FMSKF_WT901_WPE
+#define FMSKF_WT901_WPE 8
+#endif
 template <bool VEC>
-__global__ __launch_bounds__(kBlock) void k_wt901(Wt901Args a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT901_WPE, 8))) void k_wt901(Wt901Args a) {
   const uint64_t n = a.n;
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
