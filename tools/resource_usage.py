@@ -9,7 +9,7 @@ import sys
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                      "-ffp-contract=off", "-fno-slp-vectorize", "-x", "hip", "-c", src, "-o", "/dev/null",
+                      "-ffp-contract=off", "-fno-slp-vectorize", *[a for a in sys.argv[3:]], "-x", "hip", "-c", src, "-o", "/dev/null",
                       "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
 cur = None
 rows = []
