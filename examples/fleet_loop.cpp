@@ -11,6 +11,9 @@
 // processes, the RCCL all-gather on the handle's side stream) and collected two records later.
 //
 //   fleet_loop [N] [ticks]
+//   FLEET_MODEL=kf6 fleet_loop ...    the 6-state KF instead of the reference's RS odometry
+//   FLEET_SPLIT_CAN=1 fleet_loop ...  CAN RX and the ISR as two calls (default: one,
+//       fmskf_isr_tick_can -- one kernel for KF6)
 //   FLEET_WORLD=W FLEET_RANK=r FLEET_ID=/path/id fleet_loop ...   one process per GPU: rank 0
 //       writes the communicator id to FLEET_ID, every rank reads it (device = rank, or
 //       FLEET_DEVICE)
@@ -18,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -43,7 +47,9 @@ int main(int argc, char **argv) {
   const int rank = getenv("FLEET_RANK") ? atoi(getenv("FLEET_RANK")) : 0;
   try {
     const int device = getenv("FLEET_DEVICE") ? atoi(getenv("FLEET_DEVICE")) : (world > 1 ? rank : 0);
-    fmskf::Robots robots(FMSKF_MODEL_RS, n, device);
+    const bool kf6 = getenv("FLEET_MODEL") && std::string(getenv("FLEET_MODEL")) == "kf6";
+    const bool split_can = getenv("FLEET_SPLIT_CAN") && atoi(getenv("FLEET_SPLIT_CAN")) != 0;
+    fmskf::Robots robots(kf6 ? FMSKF_MODEL_KF6 : FMSKF_MODEL_RS, n, device);
     if (world > 1) {  // the handle's RCCL communicator, its id passed through a file
       const char *path = getenv("FLEET_ID");
       if (!path) throw std::runtime_error("FLEET_ID must name the id file");
@@ -115,7 +121,7 @@ int main(int argc, char **argv) {
           stamps[i * 4 + w] = (int16_t)(((t + 1) * 1000 + 7 * w) & 0x7FFF);
         }
       }
-      motors.rx_callback(frames.data(), stamps.data());
+      if (split_can) motors.rx_callback(frames.data(), stamps.data());
       if (t % 10 == 0) {  // IMU task, 100 Hz: acc, gyro, angle (yaw = 30 deg), quaternion
         for (uint64_t i = 0; i < n; i++) {
           uint8_t *b = &bytes[i * stride];
@@ -127,8 +133,10 @@ int main(int argc, char **argv) {
         if (t == 0) imu.init(bytes.data(), stride, len.data());
         else imu.update(bytes.data(), stride, len.data());
       }
-      // correct + predict + wheel loops + 0x200 frames, device-resident inputs
-      robots.can_tx_routine(tx.data());
+      // correct + predict + wheel loops + 0x200 frames, device-resident inputs (with the
+      // tick's CAN RX in the same call unless split)
+      if (split_can) robots.can_tx_routine(tx.data());
+      else robots.can_rx_tx_routine(frames.data(), stamps.data(), tx.data());
       if (t % 17 == 16) fmskf::publish_vehicle_info(robots, info.data());  // ~60 Hz
       if (t % 16 == 15) {  // the fleet's ensemble record, collected two records later
         robots.ensemble_begin();

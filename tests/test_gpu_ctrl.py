@@ -196,6 +196,25 @@ def test_fleet_loop_cpp_host_program():
     assert abs(dlt - 2 * 3.1415926 / 8191 / 36) < 1e-6 * dlt, lines[4]
 
 
+@pytest.mark.parametrize("model", ["rs", "kf6"])
+def test_fleet_loop_cpp_fused_can_equals_split(model):
+    """examples/fleet_loop.cpp with the tick's CAN RX inside the ISR call (fmskf_isr_tick_can,
+    the default; one kernel for KF6) prints exactly what the split form (rx_callback, then
+    can_tx_routine) prints: poses, VehicleInfo, TX frame bytes, the ensemble and motor Status."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "fleet_loop")
+    outs = []
+    for split in ("0", "1"):
+        env = dict(os.environ, FLEET_MODEL=model, FLEET_SPLIT_CAN=split)
+        out = subprocess.run([exe, "3000", "120"], capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode == 0, out.stderr
+        outs.append(out.stdout.strip().splitlines()[1:])  # line 0: wall time
+    assert outs[0] == outs[1]
+    assert float(outs[0][0].split("x=")[1].split()[0]) > 0.0
+
+
 def test_reset_zeroes_control_state():
     n = 300
     with Engine("rs", n) as e:
