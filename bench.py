@@ -357,6 +357,9 @@ PATH_BYTES = {
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
     "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
+    # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
+    # CAN row's 216 + the ISR's 601 without its rpm read
+    "isr_can_kf6_2p20": 216 + (232 + 369 - 8 + 8) - 8,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
     "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
@@ -465,6 +468,9 @@ def path_rows(dev, stream, ticks: int, trig):
     e = driven("kf6")
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     timed("isr_kf6_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R], gyro_z_dps=gz[k % R], rpm=rpm[k % R]), e)
+    e = driven("kf6")
+    timed("isr_can_kf6_2p20", lambda k: e.isr_tick_can(frames[k % R], stamps[k % R], out=fr, yaw_deg=yaw[k % R],
+                                                       gyro_z_dps=gz[k % R]), e)
     # the whole firmware loop (VDT::can_tx_routine_intr with the CAN RX and IMU tasks feeding it):
     # four C610 frames per robot every tick, a WT901 poll every 10th tick, the fused ISR on the
     # ingested state; time per tick over a multiple of 10 ticks

@@ -93,7 +93,8 @@ def secondary(root, out):
 # neither read nor written); CAN RX, four
 # wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, sum read (120), those
 # state fields plus rpm and curr written (96); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
-# 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128).  The
+# 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128); the fused
+# ISR with and without the CAN RX (below).  The
 # counters are corrected with the KF6 calibration of profiles/pmc_traffic.json (the same
 # streaming dword / 8- / 16-byte lane accesses: FETCH_SIZE counts half, WRITE_SIZE exact).
 PATHS = [
@@ -102,6 +103,12 @@ PATHS = [
     ("wt901_ingest_2p20", "k_wt901", 60, 72),
     ("can_ingest_2p20", "k_can4", 120, 96),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
+    # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
+    # without its rpm (209) and writes (152), the 0x200 frame (8 w)
+    ("isr_kf6_2p20", "k_isr_kf6", 124 + 209, 108 + 152 + 8),
+    # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 120 / 96, the rpm
+    # plane no longer read
+    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 209 + 120, 108 + 152 + 8 + 96),
 ]
 
 

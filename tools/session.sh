@@ -8,7 +8,7 @@
 #   prof    rocprofv3 --kernel-trace --stats of the driver's bench command
 #   pmc     FETCH_SIZE / WRITE_SIZE passes of the headline kernel and its calibration pattern
 #   sec     the same for the HBM-regime secondary lines (cfg 3, cfg 5, KF6 2^24)
-#   paths   the same for the path rows at 2^20 (RS, WT901, CAN, COMP KF6)
+#   paths   the same for the path rows at 2^20 (RS, WT901, CAN, COMP KF6, the fused ISR with / without CAN)
 #   sq      wave-state counters (7 SQ + GRBM, one pass) of the tick and path-row kernels
 #   sqab    the same per SQ_LIST entry "name|VAR=v ...|kbench args" (';'-separated)
 #   mix     tools/membench.hip byte-mix streaming ceilings at 2^20 and 2^22
@@ -81,7 +81,9 @@ for s in $STEPS; do
            pmc2 pmc_path_rs_tick_2p20_padded_sums 120 --model rs --pad 512 --ticks 30
            pmc2 pmc_path_wt901_ingest_2p20 120 --op wt901 --ticks 30
            pmc2 pmc_path_can_ingest_2p20 120 --op can --ticks 30
-           pmc2 pmc_path_cfg2_kf6_comp_pos_2p20 120 --packed --comp --ticks 30 ;;
+           pmc2 pmc_path_cfg2_kf6_comp_pos_2p20 120 --packed --comp --ticks 30
+           pmc2 pmc_path_isr_kf6_2p20 120 --op isr --ticks 30
+           pmc2 pmc_path_isr_can_kf6_2p20 120 --op isr_can --ticks 30 ;;
     sq)    for ent in "kf6|--packed --ticks 30" "rs|--model rs --pad 512 --ticks 30" "wt901|--op wt901 --ticks 30" \
                       "can|--op can --ticks 30"; do
              IFS='|' read -r nm ka <<< "$ent"
