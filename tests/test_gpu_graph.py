@@ -100,6 +100,52 @@ def test_graph_isr_tick_kf6_fused(n):
             np.testing.assert_array_equal(a.get_ctrl()["curr"], e.get_ctrl()["curr"])
 
 
+def test_graph_isr_tick_can_kf6():
+    """fmskf_isr_tick_can (the tick's CAN RX fused into the KF6 ISR) captured with device CAN
+    buffers, input planes and frame buffer: each replay equals direct ingest_can + isr_tick,
+    frames, state and the motor state bit for bit."""
+    import torch
+    n, T = 4099, 12
+    tr = Trajectory(n, T, seed=79)
+    yaw, gz, _ = tr.kf6_inputs()
+    st = torch.cuda.Stream()
+    vel = np.zeros((3, n), np.float32)
+    vel[0] = 150.0
+    acl = np.full((3, n), 1000.0, np.float32)
+    jrk = np.full((3, n), 10000.0, np.float32)
+    with torch.cuda.stream(st), Engine("kf6", n) as a, Engine("kf6", n) as b:
+        for e in (a, b):
+            e.set_stream(st)
+            e.set_power(None)
+            e.set_target_vel(vel, acl, jrk)
+        dy = torch.empty(n, dtype=torch.float32, device="cuda")
+        dg = torch.empty(n, dtype=torch.float32, device="cuda")
+        df = torch.empty((n, 4, 8), dtype=torch.uint8, device="cuda")
+        ds = torch.empty((n, 4), dtype=torch.int16, device="cuda")
+        fa, fb = (torch.empty((n, 8), dtype=torch.uint8, device="cuda") for _ in range(2))
+        b.graph_begin()
+        b.isr_tick_can(df, ds, out=fb, yaw_deg=dy, gyro_z_dps=dg)
+        b.graph_end()
+        for t in range(T):
+            f, s = tr.can_frames(t)
+            df.copy_(torch.from_numpy(np.ascontiguousarray(f)))
+            ds.copy_(torch.from_numpy(np.ascontiguousarray(s)))
+            dy.copy_(torch.from_numpy(yaw[t]))
+            dg.copy_(torch.from_numpy(gz[t]))
+            a.ingest_can(df, ds)
+            a.isr_tick(out=fa, yaw_deg=dy, gyro_z_dps=dg)
+            b.graph_launch(1)
+            st.synchronize()
+            assert torch.equal(fa, fb), f"tick {t}: graph frames"
+        xa, Pa = a.get_state()
+        xb, Pb = b.get_state()
+        np.testing.assert_array_equal(xa.view(np.uint32), xb.view(np.uint32))
+        np.testing.assert_array_equal(Pa.view(np.uint32), Pb.view(np.uint32))
+        ma, mb = a.get_motors(), b.get_motors()
+        for k in ma:
+            np.testing.assert_array_equal(ma[k], mb[k], err_msg=k)
+
+
 def test_graph_errors():
     with Engine("kf6", 64) as e:
         with pytest.raises(fmskf.FmskfError):
