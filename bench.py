@@ -360,6 +360,12 @@ PATH_BYTES = {
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
     # CAN row's 216 + the ISR's 601 without its rpm read
     "isr_can_kf6_2p20": 216 + (232 + 369 - 8 + 8) - 8,
+    # the reference-semantics ISR (k_isr_rs) on the ingested motor state: the RS tick's 140 + the
+    # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
+    "isr_rs_2p20": 140 + 369 - 8 + 8,
+    # with the tick's CAN RX fused in: the CAN row's 216, the rpm and the four sums no longer read
+    # back (the CAN lane hands them over in registers)
+    "isr_can_rs_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
     "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
@@ -468,6 +474,11 @@ def path_rows(dev, stream, ticks: int, trig):
     e = driven("kf6")
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     timed("isr_kf6_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R], gyro_z_dps=gz[k % R], rpm=rpm[k % R]), e)
+    e = driven("rs")
+    e.ingest_can(frames[0], stamps[0])
+    timed("isr_rs_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R]), e)
+    e = driven("rs")
+    timed("isr_can_rs_2p20", lambda k: e.isr_tick_can(frames[k % R], stamps[k % R], out=fr, yaw_deg=yaw[k % R]), e)
     e = driven("kf6")
     timed("isr_can_kf6_2p20", lambda k: e.isr_tick_can(frames[k % R], stamps[k % R], out=fr, yaw_deg=yaw[k % R],
                                                        gyro_z_dps=gz[k % R]), e)

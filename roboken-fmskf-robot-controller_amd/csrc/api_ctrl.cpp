@@ -255,12 +255,16 @@ int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t 
     uint8_t *dst = !frames ? nullptr : mem == FMSKF_MEM_DEVICE ? frames : (uint8_t *)host_result(h, bytes);
     int fused = (int)hipErrorNotSupported;
     h->time_begin();
-    // one launch where the tick reads the rpm the frames carry (no caller rpm / records)
+    // one launch where the tick reads the rpm (RS: and the angle sums) the frames carry: no
+    // caller rpm / sums / records
     if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused() && !in->kf6_rec && !in->rpm) {
       fused = launch_isr_kf6_can(h->s, t, h->kf6, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
                                  (const int16_t *)s, h->cfg.motor_dir, h->stream);
-      if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr+can launch");
+    } else if (h->cfg.model == FMSKF_MODEL_RS && !in->rpm && !in->angle_sum) {
+      fused = launch_isr_rs_can(h->s, t, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+                                (const int16_t *)s, h->cfg.motor_dir, h->stream);
     }
+    if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr+can launch");
     if (fused == (int)hipErrorNotSupported) {  // CAN RX, then the ISR of fmskf_isr_tick
       launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, nullptr, h->cfg.motor_dir, h->stream),
                    "can launch");

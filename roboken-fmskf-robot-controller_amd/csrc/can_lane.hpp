@@ -96,7 +96,8 @@ __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t 
 // `nt` loads and stores.  SO: the sum array's wheel planes at soffset from one descriptor (the
 // launcher checks the 4 GiB span); else one clamped descriptor per plane.  load() issues every
 // load; step() computes the four wheels and stores (`live` lanes only: the fused ISR runs
-// clamped lanes past N) and returns the new rpm of the four wheels (s16_rawSpeedRpm) packed.
+// clamped lanes past N) and returns the new rpm of the four wheels (s16_rawSpeedRpm) packed;
+// sm[] then holds the new angle sums (get_rawAngleSum).
 template <bool NT, bool SO>
 struct Can4Lane {
   static constexpr int LP = NT ? kStateNT : 0, SP = st_pol(LP), IP = 2;  // IP: inputs nt
@@ -105,7 +106,7 @@ struct Can4Lane {
   uint4 f01, f23;
   uint32_t iyw[4];
   uint64_t sv, mv, av, pmv, pav;
-  int64_t sm[4];
+  int64_t sm[4];  // the wheels' angle sums: before step() the stored ones, after it the new ones
 
   __device__ __forceinline__ void load(const CanArgs &a, uint64_t hb_, uint32_t li_) {
     hb = hb_;
@@ -143,7 +144,6 @@ struct Can4Lane {
     const uint32_t pmw[2] = {(uint32_t)pmv, (uint32_t)(pmv >> 32)}, paw[2] = {(uint32_t)pav, (uint32_t)(pav >> 32)};
     uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0};
     v4u32_t oy;
-    int64_t os[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       const int sh = 16 * (w & 1);
@@ -152,7 +152,7 @@ struct Can4Lane {
                                    (int16_t)(pmw[w >> 1] >> sh), (int16_t)(paw[w >> 1] >> sh),
                                    __builtin_bit_cast(float, iyw[w]), sm[w]);
       oy[w] = __builtin_bit_cast(uint32_t, o.iir_y);
-      os[w] = o.sum;
+      sm[w] = o.sum;
       na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
       nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
       nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
@@ -162,8 +162,8 @@ struct Can4Lane {
       const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
 #pragma unroll
       for (int w = 0; w < 4; w++) {
-        if constexpr (SO) st_span<int64_t, SP>(r_sm, li, w * ps, os[w]);
-        else st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li, os[w]);
+        if constexpr (SO) st_span<int64_t, SP>(r_sm, li, w * ps, sm[w]);
+        else st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li, sm[w]);
       }
       __builtin_amdgcn_raw_buffer_store_b128(oy, rsrc_span(a.iir_y + hb * 4), li * 16u, 0, SP);
       const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };

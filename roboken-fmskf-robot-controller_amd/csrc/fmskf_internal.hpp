@@ -348,6 +348,9 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
 int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
                        const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
                        const int8_t dir[4], hipStream_t st);
+int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
+                      uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
+                      hipStream_t st);
 // the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
                   const CtrlPrm &p, uint8_t *frames, hipStream_t st);

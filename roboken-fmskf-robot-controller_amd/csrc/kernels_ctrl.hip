@@ -77,11 +77,19 @@ struct IsrRsArgs {
   const float *sintab;
   uint8_t *frames;
 };
-template <bool LIBM, bool SMALL, int CP = 0>
-__global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p) {
+// CAN (round 5, fmskf_isr_tick_can): the tick's four C610 frames per robot first (can_lane.hpp),
+// the new angle sums and rpm handed to the odometry and the wheel loops in registers instead of
+// read back from the motor state
+template <bool LIBM, bool SMALL, int CP = 0, bool CAN = false>
+__global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p, CanArgs can) {
   const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)n) return;
+  Can4Lane<false, true> cl;
+  if constexpr (CAN) {  // the block's 256-robot chunk
+    const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
+    cl.load(can, hb, i - hb);
+  }
   RsLane s;
   s.px = a.x[i];
   s.py = a.x[pp + i];
@@ -89,12 +97,20 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
 #pragma unroll
   for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
   const float yaw = a.yaw_deg[i];
-  const uint2 rw = reinterpret_cast<const uint2 *>(a.rpm)[i];
+  uint2 rw;
   int64_t sum[4];
+  if constexpr (!CAN) {
+    rw = reinterpret_cast<const uint2 *>(a.rpm)[i];
 #pragma unroll
-  for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * a.sum_pitch + i];
+    for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * a.sum_pitch + i];
+  }
   CtrlLane<SMALL, CP> L;
   L.load(c, i);
+  if constexpr (CAN) {
+    rw = cl.step(can, true);
+#pragma unroll
+    for (int w = 0; w < 4; w++) sum[w] = cl.sm[w];
+  }
   rs_tick1<LIBM, true, true>(s, yaw, rw, sum, a.sintab);
   const uint2 cw = L.step(c, p, i, rw);
   a.x[i] = s.px;
@@ -257,8 +273,9 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uin
   return (int)hipGetLastError();
 }
 
-int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
-                  const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+template <bool CAN>
+static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
+                    uint8_t *frames, hipStream_t st, const CanArgs &can) {
   if (c.n == 0) return 0;
   const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum, in.sum_pitch,
                     in.sintab, frames};
@@ -267,16 +284,21 @@ int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev 
   if (nt) {
     // 3 blocks per CU (48 KiB dynamic LDS): 2^20 75.7-76.5 -> 73.9 us (two passes)
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
-    if (libm) k_isr_rs<true, true, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p);
-    else k_isr_rs<false, true, kStateNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p);
+    if (libm) k_isr_rs<true, true, kStateNT, CAN><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
+    else k_isr_rs<false, true, kStateNT, CAN><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
   } else if (libm) {
-    if (small) k_isr_rs<true, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
-    else k_isr_rs<true, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+    if (small) k_isr_rs<true, true, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<true, false, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   } else {
-    if (small) k_isr_rs<false, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
-    else k_isr_rs<false, false><<<grid1(c.n), kBlock, 0, st>>>(a, c, p);
+    if (small) k_isr_rs<false, true, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<false, false, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   }
   return (int)hipGetLastError();
+}
+
+int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
+                  const CtrlPrm &p, uint8_t *frames, hipStream_t st) {
+  return isr_rs_l<false>(s, in, libm, c, p, frames, st, CanArgs{});
 }
 
 // The fused KF6 ISR where it applies: one tick of the default single-tick form (state in one
@@ -343,13 +365,15 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
 // ISR.  hipErrorNotSupported where the fused form does not apply (record inputs, the tick's
 // non-temporal regime, the motor state past the cached regime or its sum planes past 4 GiB,
 // unaligned frames / stamps): the caller then runs CAN RX and the ISR as two calls
-int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
-                       const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
-                       const int8_t dir[4], hipStream_t st) {
-  if (in.rec || !s.m_sum || state_nt(s.n * 66) || 4 * s.m_pitch * 8 > 0xFFFFFFFFull ||
-      ((uintptr_t)can_frames & 15) != 0 || ((uintptr_t)can_stamps & 7) != 0)
-    return (int)hipErrorNotSupported;
-  CanArgs ca{};
+// the CAN lane's arguments over the handle's motor state; false where the fused form does not
+// apply (the motor state past the cached regime or its sum planes past 4 GiB, unaligned frames /
+// stamps)
+static bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
+                     CanArgs &ca) {
+  if (!s.m_sum || state_nt(s.n * 66) || 4 * s.m_pitch * 8 > 0xFFFFFFFFull || ((uintptr_t)can_frames & 15) != 0 ||
+      ((uintptr_t)can_stamps & 7) != 0)
+    return false;
+  ca = CanArgs{};
   ca.n = s.n;
   ca.frames = can_frames;
   ca.stamps = can_stamps;
@@ -364,7 +388,25 @@ int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp,
   ca.sum = s.m_sum;
   ca.sum_pitch = s.m_pitch;
   ca.iir_y = s.m_iir_y;
+  return true;
+}
+
+int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
+                       const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
+                       const int8_t dir[4], hipStream_t st) {
+  CanArgs ca;
+  if (in.rec || !can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
   return isr_kf6_l(s, in, kp, libm, c, p, frames, st, &ca);
+}
+
+// the reference-semantics ISR with the tick's CAN RX fused in: the odometry reads the new sums
+// and rpm from the CAN lane (the caller passes no rpm / sums: TickIn's are the motor state's)
+int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
+                      uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
+                      hipStream_t st) {
+  CanArgs ca;
+  if (!can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  return isr_rs_l<true>(s, in, libm, c, p, frames, st, ca);
 }
 
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {

@@ -1,5 +1,5 @@
-"""fmskf_isr_tick_can: the tick's CAN RX and the firmware ISR in one call (one kernel for KF6,
-k_isr_kf6 with the C610 lane of can_lane.hpp in front) against the two calls it replaces,
+"""fmskf_isr_tick_can: the tick's CAN RX and the firmware ISR in one call (one kernel for RS and
+KF6, k_isr_rs / k_isr_kf6 with the C610 lane of can_lane.hpp in front) against the two calls it replaces,
 fmskf_ingest_can + fmskf_isr_tick, on random targets / power events.  Bar: bit-exact for the
 estimator state, the control state, the 0x200 frames and the whole motor state
 (MOTOR_IF_M2006::rx_callback, VD_motor_if_m2006.cpp; the two-call path is itself held to the
@@ -19,12 +19,13 @@ def bits(a):
     return a.view(np.uint32) if a.dtype == np.float32 else a
 
 
-# kf6*: the fused kernel (planes, LIBM, validity mask, compensated positions, device-resident
-# frames, a ragged last block, the non-temporal control regime past the Infinity Cache);
-# kf6rpm / kf6rec / rs: the documented two-call fallback (a caller rpm or records, model RS)
+# kf6* / rs*: the fused kernels (planes, LIBM, validity mask, compensated positions, device-
+# resident frames, a ragged last block, the non-temporal control regime past the Infinity Cache);
+# kf6rpm / kf6rec / rssum: the documented two-call fallback (a caller rpm, records, caller sums)
 CASES = [("kf6", 4099, 40), ("kf6", 1, 20), ("kf6libm", 777, 20), ("kf6mask", 1001, 20),
          ("kf6comp", 513, 20), ("kf6dev", 2048 + 5, 20), ("kf6rpm", 300, 12), ("kf6rec", 257, 12),
-         ("rs", 999, 12), ("kf6", (1 << 20) + 17, 3)]
+         ("rs", 999, 30), ("rs", 1, 12), ("rslibm", 700, 12), ("rssum", 333, 12),
+         ("kf6", (1 << 20) + 17, 3), ("rs", (1 << 20) + 17, 3)]
 
 
 @pytest.mark.parametrize("case,n,T", CASES)
@@ -32,14 +33,17 @@ def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
     import torch
     rng = np.random.default_rng(7 + n)
     tr = Trajectory(n, T, seed=53)
-    trig = fmskf.TRIG_LIBM if case == "kf6libm" else fmskf.TRIG_TABLE512
+    trig = fmskf.TRIG_LIBM if case.endswith("libm") else fmskf.TRIG_TABLE512
     flags = fmskf.CFG_COMP_POS if case == "kf6comp" else 0
-    model = "rs" if case == "rs" else "kf6"
+    model = "rs" if case.startswith("rs") else "kf6"
+    sums = np.ascontiguousarray(tr.rs_inputs()[1]) if case == "rssum" else None
     yaw, gz, rpm = tr.kf6_inputs()
     valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if case == "kf6mask" else None
 
     def kw(t):
-        if case == "rs":
+        if case == "rssum":  # the caller's sums: CAN RX, then the ISR on them
+            return dict(yaw_deg=yaw[t], angle_sum=sums[t])
+        if model == "rs":
             return dict(yaw_deg=yaw[t])  # sums and rpm: the device motor state
         if case == "kf6rec":
             return dict(kf6_rec=fmskf.kf6_records(yaw, gz, rpm)[t])

@@ -275,12 +275,13 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
     cs = (torch.arange(4, device=dev, dtype=torch.int16) * 250).expand(n, 4).contiguous()
 
     def direct():
+        imu = dict(yaw_deg=dy) if args.model == "rs" else dict(yaw_deg=dy, gyro_z_dps=dg)
         if args.op == "isr_can":
-            e.isr_tick_can(cf, cs, out=fr, yaw_deg=dy, gyro_z_dps=dg)
+            e.isr_tick_can(cf, cs, out=fr, **imu)
             return
         if args.op == "can_isr":
             e.ingest_can(cf, cs)
-            e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg)
+            e.isr_tick(out=fr, **imu)
             return
         if args.op.startswith("isr"):  # fmskf_isr_tick: one fused kernel for RS
             e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)

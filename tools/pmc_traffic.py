@@ -109,6 +109,10 @@ PATHS = [
     # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 120 / 96, the rpm
     # plane no longer read
     ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 209 + 120, 108 + 152 + 8 + 96),
+    # the reference-semantics ISR (k_isr_rs) on the motor state: the RS tick's 84 / 56 with the
+    # control step's 209 / 152 and the frame; with the CAN RX fused in, the rpm and sums not read
+    ("isr_rs_2p20", "k_isr_rs", 84 + 209, 56 + 152 + 8),
+    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 + 209 + 120, 56 + 152 + 8 + 96),
 ]
 
 
