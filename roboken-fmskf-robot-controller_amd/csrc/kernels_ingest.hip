@@ -151,8 +151,13 @@ struct Wt901Parser {
 // cache policies through buffer descriptors (same box, against 35.4-36.9 plain): `sc1` state
 // stores 36.0-36.3; `nt` poll-row loads 41.2-42.0, since a 16-byte load of 48-byte rows uses a
 // third of every line it touches and `nt` evicts the line before the next load reads the rest.
+// Occupancy (round 5): the kernel that loaded the magnetometer registers after parsing took 67
+// VGPRs, 7 waves per SIMD; capped at 64 (8 waves, no spills) it ran 29.2 -> 27.2 us per 2^20
+// polls.  With every unconditional load hoisted ahead of the parse (below) it takes 74 VGPRs:
+// 6 waves per SIMD, 27.0-27.2 -> 26.2-26.5 us at 2^20, 115.6-116.6 -> 109.9-110.6 at 2^22
+// (kbench, three passes, profiles/r5_ab.json); capped at 7 or 8 waves it spills (29.4, 34.8 us)
 #ifndef FMSKF_WT901_WPE
-#define FMSKF_WT901_WPE 8
+#define FMSKF_WT901_WPE 6
 #endif
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT901_WPE, 8))) void k_wt901(Wt901Args a) {
@@ -160,21 +165,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   Wt901Parser ps;
+  const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
+  // Every unconditional load first -- the count, flags, length, the poll row and the
+  // magnetometer registers -- so a wave waits for memory once before parsing (the parser words,
+  // read only when bytes are pending, and a non-standard poll's register reads come after)
+  const uint32_t cnt_in = a.cnt[i];
+  const uint32_t flags_in = a.flags[i];
+  const uint32_t len_in = a.len[i];
+  int16_t *reg = a.reg;
+  int16_t rm[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+  uint4 ch[4];
+  if constexpr (VEC) {
+    const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
+  }
   // The parser window holds exactly cnt bytes and is zero past them, so an empty window (the
   // state every poll of whole frames leaves) is all zero: its three words are read only when
   // bytes are pending, and written only when a window was or is now pending (round 5: the
   // standard poll moves 132 B instead of 157).
-  ps.cnt = a.cnt[i];
-  const uint32_t cnt_in = ps.cnt;
+  ps.cnt = cnt_in;
   ps.lo = 0;
   ps.hi = 0;
   if (cnt_in != 0) {
     ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
     ps.hi = (uint64_t)a.parser[2 * n + i];
   }
-  ps.flags = a.flags[i];
-  const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
-  const uint32_t len = a.len[i] < a.stride ? a.len[i] : a.stride;
+  ps.flags = flags_in;
+  const uint32_t len = len_in < a.stride ? len_in : a.stride;
   // the standard 10 ms poll (0x51 acc, 0x52 gyro, 0x53 angle, 0x59 quaternion)
   // taken by the fast path: every register updateData reads except the magnetometer's was
   // written by exactly one of its frames, so the Data page is built from the frame words
@@ -182,11 +203,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   bool std4 = false;
   uint32_t sw[4][4] = {};
   if constexpr (VEC) {
-    const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
-    uint4 ch[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      ch[c] = (uint32_t)c < nch ? reinterpret_cast<const uint4 *>(p)[c] : make_uint4(0, 0, 0, 0);
     // Whole-frame fast path.  With an empty parser window and a poll made of complete frames
     // (0x55 header and a valid checksum every 11 bytes), the byte-serial parser accepts frame
     // k at bytes 11k..11k+10 and never resyncs: dispatch the frames directly (static byte
@@ -272,7 +288,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   }
   uint64_t lo = ps.lo, hi = ps.hi;
   uint32_t cnt = ps.cnt, flags = ps.flags;
-  int16_t *reg = a.reg;
   // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
   const bool ok = (flags & F_QUAT) != 0;
   if (ok) flags = 0;
@@ -290,7 +305,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   // fmskf_get_imu and VehicleInfo form the page from them (imu_data_page), so a poll moves 157 B
   // instead of 197 (the 64-byte page written, q_init read; 132 B with the empty-window rule above).  Only a latching poll reads q_init,
   // to keep it (qprev) for the page of that very poll, which used the old one.
-  int16_t ra[3], rg[3], rr[3], rq[4], rm[3];
+  int16_t ra[3], rg[3], rr[3], rq[4];
   if (std4) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -309,9 +324,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
-  }
+    // any other poll may have carried a magnetometer frame: read the registers as it left them
 #pragma unroll
-  for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+    for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+  }
   a.yaw[i] = (float)rr[2] / 32768.0f * 180.0f;
   a.gz[i] = -((float)rg[2] / 32768.0f * 2000.0f);
   uint32_t snapf = kSnapValid;
