@@ -366,6 +366,9 @@ PATH_BYTES = {
     # with the tick's CAN RX fused in: the CAN row's 216, the rpm and the four sums no longer read
     # back (the CAN lane hands them over in registers)
     "isr_can_rs_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32,
+    # the reference-semantics firmware loop (VD_task_main.cpp:366-372 with its CAN RX and IMU
+    # tasks) on the fused call: CAN RX + the RS ISR in one kernel, a WT901 poll every 10th tick
+    "firmware_loop_rs_fused_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
     "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
@@ -503,6 +506,13 @@ def path_rows(dev, stream, ticks: int, trig):
             e.ingest_wt901(poll, lens, latch_qinit=(k == 0))
         e.isr_tick_can(frames[k % R], stamps[k % R], out=fr)
     timed("firmware_loop_kf6_fused_2p20", loop_fused, e)
+    e = driven("rs")
+
+    def loop_rs(k):
+        if k % 10 == 0:
+            e.ingest_wt901(poll, lens, latch_qinit=(k == 0))
+        e.isr_tick_can(frames[k % R], stamps[k % R], out=fr)
+    timed("firmware_loop_rs_fused_2p20", loop_rs, e)
     del yaw, gz, rpm, fr, frames, stamps, poll
     torch.cuda.empty_cache()
     return out

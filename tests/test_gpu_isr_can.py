@@ -25,6 +25,7 @@ def bits(a):
 CASES = [("kf6", 4099, 40), ("kf6", 1, 20), ("kf6libm", 777, 20), ("kf6mask", 1001, 20),
          ("kf6comp", 513, 20), ("kf6dev", 2048 + 5, 20), ("kf6rpm", 300, 12), ("kf6rec", 257, 12),
          ("rs", 999, 30), ("rs", 1, 12), ("rslibm", 700, 12), ("rssum", 333, 12),
+         ("kf6mixmem", 3000, 12), ("rsmixmem", 3000, 12),
          ("kf6", (1 << 20) + 17, 3), ("rs", (1 << 20) + 17, 3)]
 
 
@@ -36,6 +37,7 @@ def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
     trig = fmskf.TRIG_LIBM if case.endswith("libm") else fmskf.TRIG_TABLE512
     flags = fmskf.CFG_COMP_POS if case == "kf6comp" else 0
     model = "rs" if case.startswith("rs") else "kf6"
+    dev_in = case.endswith("mixmem")  # host CAN frames, device tick inputs: two staging flags
     sums = np.ascontiguousarray(tr.rs_inputs()[1]) if case == "rssum" else None
     yaw, gz, rpm = tr.kf6_inputs()
     valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if case == "kf6mask" else None
@@ -43,10 +45,15 @@ def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
     def kw(t):
         if case == "rssum":  # the caller's sums: CAN RX, then the ISR on them
             return dict(yaw_deg=yaw[t], angle_sum=sums[t])
-        if model == "rs":
+        if model == "rs" and not dev_in:
             return dict(yaw_deg=yaw[t])  # sums and rpm: the device motor state
         if case == "kf6rec":
             return dict(kf6_rec=fmskf.kf6_records(yaw, gz, rpm)[t])
+        if dev_in:
+            d = dict(yaw_deg=torch.from_numpy(yaw[t]).cuda())
+            if model == "kf6":
+                d["gyro_z_dps"] = torch.from_numpy(gz[t]).cuda()
+            return d
         d = dict(yaw_deg=yaw[t], gyro_z_dps=gz[t])
         if case == "kf6rpm":
             d["rpm"] = rpm[t]
