@@ -52,6 +52,10 @@ int main() {
     return 16;
   uint32_t rows = 0;
   if (fmskf_get_state_lo(nullptr, nullptr, &rows, FMSKF_MEM_HOST) != FMSKF_EINVAL) return 17;
+  // round 5: the fused CAN RX + ISR call refuses a null handle before anything else
+  if (fmskf_isr_tick_can(nullptr, nullptr, nullptr, nullptr, nullptr, FMSKF_MEM_HOST) != FMSKF_EINVAL) return 18;
+  float xms = 0.f;
+  if (fmskf_ensemble_exchange_ms(nullptr, &xms) != FMSKF_EINVAL) return 19;
   (void)strlen(fmskf_rccl_library());
   std::printf("api sanitize ok\n");
   return 0;
