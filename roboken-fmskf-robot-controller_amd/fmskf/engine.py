@@ -521,6 +521,8 @@ class Engine:
             check(load().fmskf_isr_tick_can(self.h, pf, ps, C.byref(ti), C.c_void_p(out.data_ptr()), mem),
                   "isr_tick_can")
             return out
+        if out is not None:  # one mem flag covers the CAN buffers and the TX frames
+            raise TypeError("host CAN frames: the TX frames come back as a numpy array (out=None)")
         f = np.empty((self.n, 8), np.uint8)
         check(load().fmskf_isr_tick_can(self.h, pf, ps, C.byref(ti), f.ctypes.data_as(C.c_void_p), mem),
               "isr_tick_can")

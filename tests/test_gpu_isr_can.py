@@ -112,3 +112,8 @@ def test_isr_tick_can_errors():
         assert L.fmskf_isr_tick_can(e.h, f.ctypes.data_as(C.c_void_p), s.ctypes.data_as(C.c_void_p),
                                     None, None, 7) == fmskf._lib.EINVAL
         e.isr_tick_can(f, s, frames=False)
+        import torch
+        with pytest.raises(TypeError):  # host CAN frames, device TX buffer: one mem flag covers both
+            e.isr_tick_can(f, s, out=torch.empty((n, 8), dtype=torch.uint8, device="cuda"))
+        with pytest.raises(ValueError):  # short CAN arrays are caught before the C call
+            e.isr_tick_can(f[: n // 2], s)
