@@ -34,23 +34,32 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_STEP = {"kf6": 2 * 6 * 4 + 2 * 21 * 4 + 16}
 
 
-def event_ms(stream, run, ticks: int, prequeue: int = 8) -> float:
-    """Average GPU time per call of `run(k)` over `ticks` back-to-back calls between two HIP events
-    on `stream` (the stream the kernels run on).  `prequeue` calls are queued before the first
-    event, so the GPU is already busy when it is recorded and the host's launch lag at the start
-    stays outside the timed span (round 4 recorded the first event on an idle stream: the
-    average then exceeded the step itself)."""
+EVENT_WINDOWS = 3
+
+
+def event_ms(stream, run, ticks: int, prequeue: int = 8, windows: int = EVENT_WINDOWS) -> float:
+    """GPU time per call of `run(k)`: the median over `windows` back-to-back windows of `ticks`
+    calls, each between two HIP events on `stream` (the stream the kernels run on).  `prequeue`
+    calls are queued before the first event, so the GPU is already busy when it is recorded and
+    the host's launch lag at the start stays outside the timed span (round 4 recorded the first
+    event on an idle stream: the average then exceeded the step itself); the median keeps one
+    window that a host hiccup left the GPU idle in (a round-5 world-1 run: 40.7 us against
+    37.0 us on the next measurement) out of the figure.  k runs on without a gap, so a
+    prequeue and window that are multiples of 10 keep a 10-tick cycle aligned."""
     import torch
     for k in range(prequeue):
         run(k)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for k in range(ticks):
-        run(prequeue + k)
-    e1.record(stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(windows + 1)]
+    ev[0].record(stream)
+    k = prequeue
+    for w in range(windows):
+        for _ in range(ticks):
+            run(k)
+            k += 1
+        ev[w + 1].record(stream)
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / ticks
+    per = sorted(ev[w].elapsed_time(ev[w + 1]) / ticks for w in range(windows))
+    return per[len(per) // 2]
 
 
 def mall_regime(state_and_input_bytes: float) -> str:
@@ -932,10 +941,10 @@ def main():
     torch.cuda.synchronize()
     region_ms = ev0.elapsed_time(ev1)
 
-    # the tick kernel's own average launch duration (the roofline's denominator): KT >= 200 more
-    # back-to-back plain ticks on the kernel's stream, no ensemble kernel and no collective in
-    # flight, 8 ticks queued before the first HIP event (rocprofv3's per-kernel average for the
-    # same command: profiles/)
+    # the tick kernel's own average launch duration (the roofline's denominator): the median of
+    # three windows of KT >= 200 more back-to-back plain ticks on the kernel's stream, no
+    # ensemble kernel and no collective in flight, 8 ticks queued before the first HIP event
+    # (rocprofv3's per-kernel average for the same command: profiles/)
     KT = max(200, args.steps)
     tick_ms = event_ms(stream, lambda k: tick(k % R), KT)
     # secondary: the same tick fed the three input planes (when the headline uses records)
@@ -1125,7 +1134,7 @@ def main():
                       "Opt<TABLE512, UPD, PRED, SMALL, !VALID" + (", REC>>" if krec is not None else ">>"),
             "timed_region_ms_per_step": region_ms / args.steps,
             "kernel_ms_plane_inputs": planes_ms,
-            "kernel_ticks_timed": KT,
+            "kernel_ticks_timed": KT, "kernel_windows": EVENT_WINDOWS,  # kernel_ms: the median window
             # 124 B per robot (the state read + the 16-byte record) against the 256 MiB
             # Infinity Cache: at 2^20 the state stays MALL-resident between ticks, so `achieved`
             # is HBM + MALL; secondary.cfg2_kf6_2p24 is the HBM-only figure
