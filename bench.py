@@ -930,14 +930,17 @@ def main():
     host_split = {"submit_ms": (t_sub - t0) * 1e3, "join_ms": (t_join - t_sub) * 1e3,
                   "sync_ms": (t1 - t_join) * 1e3}
     # the same K-step sequence once more between HIP events on the tick stream: the GPU-side
-    # duration of the timed region's work (diagnostic; `value` is the wall clock above)
+    # duration of the timed region's work on the tick stream (diagnostic; `value` is the wall
+    # clock above).  The second event is recorded before the pending results are collected:
+    # that collection is a host wait on the side stream, and recording after it counted the
+    # tick stream's idle time behind the wait (up to 3% of the span on a 20-step region)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for k in range(args.warmup + args.steps, args.warmup + 2 * args.steps):
         step(k)
-    join()
     ev1.record(stream)
+    join()
     torch.cuda.synchronize()
     region_ms = ev0.elapsed_time(ev1)
 
