@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--pad", type=int, default=0, help="input plane pitch padding (elements)")
     ap.add_argument("--can-desync", action="store_true",
                     help="--op can: one masked tick before timing (robots' ring heads out of step)")
-    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr"], default="tick")
+    ap.add_argument("--op", choices=["tick", "predict", "correct", "ensemble", "tick_ensemble", "ens_async", "control", "can_tx", "wt901", "can", "pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr", "isr_can_graph", "can_isr_graph"], default="tick")
     ap.add_argument("--trig", choices=["table512", "libm"], default="table512")
     ap.add_argument("--host", choices=["", "pageable", "pinned"], default="",
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
@@ -90,7 +90,8 @@ def main():
         preps = [e.prepare(valid=vm[r], **kws[r]) for r in range(R)]
     if args.host:
         return bench_host(args, e, n, yaw, gz, rpm)
-    if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr"):
+    if args.op in ("pipeline", "pipeline_graph", "isr", "isr_graph", "isr_can", "can_isr", "isr_can_graph",
+                   "can_isr_graph"):
         return bench_pipeline(args, e, n, yaw, gz, rpm, dev, st)
     if args.op in ("control", "can_tx", "wt901", "can"):
         return bench_io(args, e, n, R, dev, rpm, st)
@@ -276,10 +277,10 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
 
     def direct():
         imu = dict(yaw_deg=dy) if args.model == "rs" else dict(yaw_deg=dy, gyro_z_dps=dg)
-        if args.op == "isr_can":
+        if args.op.startswith("isr_can"):
             e.isr_tick_can(cf, cs, out=fr, **imu)
             return
-        if args.op == "can_isr":
+        if args.op.startswith("can_isr"):
             e.ingest_can(cf, cs)
             e.isr_tick(out=fr, **imu)
             return
