@@ -369,6 +369,10 @@ PATH_BYTES = {
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
     # CAN row's 216 + the ISR's 601 without its rpm read
     "isr_can_kf6_2p20": 216 + (232 + 369 - 8 + 8) - 8,
+    # the EKF9 ISR (k_isr_ekf9, round 5): the EKF9 tick's 448 (cfg 3's count; + 8 B with the
+    # heading's hidden low-part row) + the control step's 369 (its own rpm plane: the tick reads
+    # the raw record) + the 0x200 frame
+    "isr_ekf9_2p20": 448 + 369 + 8,
     # the reference-semantics ISR (k_isr_rs) on the ingested motor state: the RS tick's 140 + the
     # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
     "isr_rs_2p20": 140 + 369 - 8 + 8,
@@ -486,6 +490,12 @@ def path_rows(dev, stream, ticks: int, trig):
     e = driven("kf6")
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     timed("isr_kf6_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R], gyro_z_dps=gz[k % R], rpm=rpm[k % R]), e)
+    e = driven("ekf9")
+    raw = torch.cat([torch.round(yaw / 180.0 * 32768).to(torch.int16)[..., None],
+                     torch.round(-gz / 2000.0 * 32768).to(torch.int16)[..., None],
+                     torch.zeros(R, n, 2, dtype=torch.int16, device=dev), rpm], -1).contiguous()
+    timed("isr_ekf9_2p20", lambda k: e.isr_tick(out=fr, raw=raw[k % R], rpm=rpm[k % R]), e)
+    del raw
     e = driven("rs")
     e.ingest_can(frames[0], stamps[0])
     timed("isr_rs_2p20", lambda k: e.isr_tick(out=fr, yaw_deg=yaw[k % R]), e)

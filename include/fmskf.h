@@ -366,9 +366,9 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem);
  * VEHICLE_CTRL::update (estimator time update, then the control half on the same rpm record),
  * M_CAN.tx_routine.  Inputs as fmskf_tick (NULL planes = the device-resident ingest state);
  * frames [N][8] receives the 0x200 payloads (NULL: no frame, the current targets are still
- * kept).  Models RS and KF6 run as ONE kernel (one pass over the estimator state, the tick
- * inputs and the control state; KF6 with its state past the Infinity Cache: three); EKF9
- * and KF12D run their tick kernel, then the control step and the frame.  Results are
+ * kept).  Models RS, KF6 and EKF9 run as ONE kernel (one pass over the estimator state, the
+ * tick inputs and the control state; KF6 / EKF9 with their state past the Infinity Cache:
+ * three); KF12D runs its tick kernel, then the control step and the frame.  Results are
  * identical to fmskf_tick + fmskf_control + fmskf_can_tx in sequence. */
 int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem);
 /* The tick's CAN RX and the ISR in one call: fmskf_ingest_can(h, can_frames, can_stamps, NULL,

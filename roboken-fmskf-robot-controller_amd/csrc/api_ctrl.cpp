@@ -176,7 +176,7 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
   });
 }
 
-// FMSKF_ISR_FUSED=0: the KF6 ISR as three kernels (A/B, and the tests' cross-check)
+// FMSKF_ISR_FUSED=0: the KF6 and EKF9 ISRs as three kernels (A/B, and the tests' cross-check)
 static bool isr_kf6_fused() {
   static const bool v = [] {
     const char *e = getenv("FMSKF_ISR_FUSED");
@@ -193,6 +193,10 @@ static void isr_launches(fmskf_ctx *h, const TickIn &t, uint8_t *dst) {
   if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused()) {
     if (!t.rec && !t.rpm) ensure_motors(h);
     fused = launch_isr_kf6(h->s, t, h->kf6, libm, h->ctrl, p, dst, h->stream);
+    if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
+  } else if (h->cfg.model == FMSKF_MODEL_EKF9 && isr_kf6_fused()) {
+    if (!t.rpm) ensure_motors(h);
+    fused = launch_isr_ekf9(h->s, t, h->ekf9, libm, h->ctrl, p, t.rpm ? t.rpm : h->s.m_rpm, dst, h->stream);
     if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
   }
   if (h->cfg.model == FMSKF_MODEL_RS) {

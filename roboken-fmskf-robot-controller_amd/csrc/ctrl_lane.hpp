@@ -228,6 +228,9 @@ struct CtrlLane {
   }
 };
 
+// bytes of the per-robot control state the step streams (interpolators + wheel loops)
+inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * 4ull * (3 * kAxF + 4 * kPidF); }
+
 // C610 0x200 payload of one robot: bytes (hi, lo) per wheel -> swap the bytes of every 16-bit half
 __device__ __forceinline__ uint2 tx_frame(uint2 c) {
   auto sw = [](uint32_t v) { return ((v & 0x00FF00FFu) << 8) | ((v >> 8) & 0x00FF00FFu); };

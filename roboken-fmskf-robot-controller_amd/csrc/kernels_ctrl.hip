@@ -250,8 +250,6 @@ __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, ImuVie
 }
 
 static inline dim3 grid1(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
-// bytes of the per-robot control state the step streams (interpolators + wheel loops)
-static inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * 4ull * (3 * kAxF + 4 * kPidF); }
 
 int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
                            const uint8_t *mask, hipStream_t st) {

@@ -7,6 +7,7 @@
 // F / H / Q / R are shared: H and the sparsity of F are compile-time model traits
 // (kf_generic.hpp), Q / R / dt ride in the kernarg segment (scalar loads, SGPRs).
 // The 6-state headline kernel lives in kernels_kf6.hip.
+#include "ctrl_lane.hpp"
 #include "ens_device.hpp"
 #include "kf_generic.hpp"
 
@@ -258,6 +259,58 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
     for (int k = 0; k < N; k++) xs[0][k] = x[k];
     const bool lv[1] = {live};
     ens_epilogue<9, 1>(a.in, xs, lv, bid);
+  }
+}
+
+// The firmware ISR for the 9-state EKF in one pass (round 5; as k_isr_kf6 for KF6): the EKF9
+// tick of k_ekf9t (cached tiled state), then the control half of VEHICLE_CTRL::update on the
+// control step's rpm (the caller's plane or the ingested motor state, as fmskf_control reads
+// it), then the 0x200 frame; every load of both steps issued before either computes.  One robot
+// per lane, the clamped-index form.  Bit-identical to fmskf_tick + fmskf_control +
+// fmskf_can_tx.  CPC: the control planes' cache policy.
+template <bool LIBM, bool SEQ, int CPC, bool COMP>
+__global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> a, CtrlDev c, CtrlPrm p,
+                                                    uint8_t *frames, const int16_t *rpm) {
+  constexpr int N = 9, NP = 45;
+  const uint32_t bid = blockIdx.x;
+  __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
+  float *stab = wtab[LIBM ? 0 : threadIdx.x >> 6];
+  const uint64_t n = a.n;
+  const uint64_t i = (uint64_t)bid * kBlock + threadIdx.x;
+  const bool live = i < n;
+  const uint64_t ic = live ? i : n - 1;
+  float x[N], P[NP];
+  WaveTable<LIBM> tv(a.in.sintab);
+  const uint32_t sl = tile_slot(n, bid);
+  const TileRows<float, N, 0> tx(a.x, bid, sl, 0);
+  const TileRows<float, NP, 0> tp(a.P, bid, sl, 0);
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = tx.ld(k);
+#pragma unroll
+  for (int k = 0; k < NP; k++) P[k] = tp.ld(k);
+  const bool have = a.in.valid == nullptr || a.in.valid[ic];
+  const uint4 raw = ekf9_raw_at<false>(a.in.raw, ic);
+  const uint64_t hb0 = (uint64_t)bid * kBlock;
+  float lo = ld_chunk<float, 0>(a.prm.thlo, hb0, n, sl);
+  Ekf9Lo<COMP, 0> cl;
+  cl.load(a.prm.clo, bid, sl);
+  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[ic];
+  CtrlLane<true, CPC> L;
+  L.load(c, (uint32_t)ic);
+  tv.store(stab);
+  ekf9_tick1<LIBM, true, true, SEQ, COMP>(a, raw, have, stab, x, P, lo, cl.v);
+  if (live) {
+    st_chunk<float, st_pol(0)>(a.prm.thlo, hb0, n, sl, lo);
+    cl.store(a.prm.clo, bid, sl);
+#pragma unroll
+    for (int k = 0; k < N; k++) tx.st(k, x[k]);
+#pragma unroll
+    for (int k = 0; k < NP; k++) tp.st(k, P[k]);
+  }
+  nan_guard(x, P, a.counters, live);
+  if (live) {
+    const uint2 cw = L.step(c, p, (uint32_t)i, rw);
+    if (frames) reinterpret_cast<uint2 *>(frames)[i] = tx_frame(cw);
   }
 }
 
@@ -702,6 +755,48 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
                          : launch_ekf9_s<false, true>(a, s, in, libm, upd, pred, nt, st, ens_nb);
   return diag ? launch_ekf9_s<true, false>(a, s, in, libm, upd, pred, nt, st, ens_nb)
               : launch_ekf9_s<false, false>(a, s, in, libm, upd, pred, nt, st, ens_nb);
+}
+
+template <bool LIBM, bool SEQ, bool COMP>
+static int isr_ekf9_v(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
+                      const int16_t *rpm, bool nt, hipStream_t st) {
+  const dim3 g = grid_for(c.n);
+  if (nt) {
+    const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
+    k_isr_ekf9<LIBM, SEQ, kStateNT, COMP><<<g, kBlock, lds, st>>>(a, c, p, frames, rpm);
+  } else {
+    k_isr_ekf9<LIBM, SEQ, 0, COMP><<<g, kBlock, 0, st>>>(a, c, p, frames, rpm);
+  }
+  return (int)hipGetLastError();
+}
+
+template <bool SEQ, bool COMP>
+static int isr_ekf9_c(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
+                      const int16_t *rpm, bool nt, bool libm, hipStream_t st) {
+  return libm ? isr_ekf9_v<true, SEQ, COMP>(a, c, p, frames, rpm, nt, st)
+              : isr_ekf9_v<false, SEQ, COMP>(a, c, p, frames, rpm, nt, st);
+}
+
+// fmskf_isr_tick for EKF9 in one kernel where it applies: one tick, the tiled EKF9 state
+// cache-resident (past the Infinity Cache the tick kernel streams it non-temporal under its own
+// occupancy cap: three kernels, as for KF6), the control planes in one 4 GiB window.
+// hipErrorNotSupported otherwise
+int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
+                    const CtrlPrm &p, const int16_t *rpm, uint8_t *frames, hipStream_t st) {
+  if (c.n == 0) return 0;
+  const uint64_t sb = s.xlo ? 240 : 220;  // state bytes per robot (+ the compensation rows)
+  if (!FMSKF_TILED || !s.thlo || in.n_ticks != 1 || !in.raw || !rpm || state_nt(s.n * sb) ||
+      c.pitch * 4 * 3 * kAxF >= 0xFFFFFFFFull)
+    return (int)hipErrorNotSupported;
+  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, prm};
+  a.prm.thlo = s.thlo;
+  a.prm.clo = s.xlo;
+  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * sb);
+  const bool diag = ekf9_r_diagonal(prm.r);
+  if (s.xlo) return diag ? isr_ekf9_c<true, true>(a, c, p, frames, rpm, nt, libm, st)
+                         : isr_ekf9_c<false, true>(a, c, p, frames, rpm, nt, libm, st);
+  return diag ? isr_ekf9_c<true, false>(a, c, p, frames, rpm, nt, libm, st)
+              : isr_ekf9_c<false, false>(a, c, p, frames, rpm, nt, libm, st);
 }
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,

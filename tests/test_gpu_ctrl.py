@@ -231,12 +231,16 @@ def test_reset_zeroes_control_state():
         assert not e.get_ctrl()["curr"].any()
 
 
+# EKF9 (round 5): one fused kernel (k_isr_ekf9) while its state is cache-resident, with LIBM, a
+# mask, COMP_POS, one robot and 2^20 + 17 robots (the control planes non-temporal).
 # KF6: one fused kernel (k_isr_kf6) for planes / records, TABLE512 / LIBM, with or without a
 # validity mask; at 2^20 + 17 the KF6 + control state outgrows the Infinity Cache and the
 # fused kernel's control planes go non-temporal
 @pytest.mark.parametrize("model,n,T", [("rs", 3001, 200), ("rs", 1, 30), ("kf6", 1000, 60),
                                        ("kf6rec", 999, 40), ("kf6libm", 777, 30), ("kf6mask", 1001, 30),
-                                       ("kf6recmask", 1, 20), ("kf6rec", (1 << 20) + 17, 4)])
+                                       ("kf6recmask", 1, 20), ("kf6rec", (1 << 20) + 17, 4),
+                                       ("ekf9", 1000, 40), ("ekf9", 1, 20), ("ekf9libm", 513, 20),
+                                       ("ekf9mask", 777, 30), ("ekf9comp", 600, 20), ("ekf9", (1 << 20) + 17, 3)])
 def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
     """fmskf_isr_tick (the firmware ISR in one call; one fused kernel for RS and KF6) leaves
     the estimator state, the control state and the 0x200 frames bit-identical to fmskf_tick +
@@ -248,7 +252,14 @@ def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
     trig = fmskf.TRIG_LIBM if model.endswith("libm") else fmskf.TRIG_TABLE512
     valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if model.endswith("mask") else None
     vk = (lambda t: {}) if valid is None else (lambda t: dict(valid=valid[t]))  # noqa: E731
-    if model == "rs":
+    flags = 0
+    if model.startswith("ekf9"):  # the raw WT901 words + rpm; the control step reads the rpm plane
+        flags = fmskf.CFG_COMP_POS if model == "ekf9comp" else 0
+        raw = tr.ekf9_raw()
+        _, _, rpm = tr.kf6_inputs()
+        kw = [dict(raw=raw[t], rpm=rpm[t], **vk(t)) for t in range(T)]
+        model = "ekf9"
+    elif model == "rs":
         yaw, sums, rpm = tr.rs_inputs()
         kw = [dict(yaw_deg=yaw[t], angle_sum=sums[t], rpm=rpm[t]) for t in range(T)]
     elif not model.startswith("kf6rec"):
@@ -265,7 +276,7 @@ def test_isr_tick_equals_tick_control_can_tx(orc, model, n, T):
     pos = np.zeros((3, n), np.float32)
     vel = np.zeros((3, n), np.float32)
     prev = np.zeros((4, n), np.int64)
-    with Engine(model, n, trig=trig) as a, Engine(model, n, trig=trig) as b:
+    with Engine(model, n, trig=trig, flags=flags) as a, Engine(model, n, trig=trig, flags=flags) as b:
         for t in range(T):
             for kind, pl in ev.get(t, []):
                 for e in (a, b):

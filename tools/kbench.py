@@ -268,6 +268,10 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
     vel[0] = 150.0
     e.set_target_vel(vel, torch.full((3, n), 1000.0, device=dev), torch.full((3, n), 10000.0, device=dev))
     dy, dg, dr = yaw[0].clone(), gz[0].clone(), rpm[0].clone()
+    # EKF9 reads the raw WT901 words (+ rpm) instead of yaw / gyro planes
+    draw = torch.cat([torch.round(dy / 180.0 * 32768).to(torch.int16)[..., None],
+                      torch.round(-dg / 2000.0 * 32768).to(torch.int16)[..., None],
+                      torch.zeros(n, 2, dtype=torch.int16, device=dev), dr], -1).contiguous()
     fr = torch.empty((n, 8), dtype=torch.uint8, device=dev)
 
     # isr_can: fmskf_isr_tick_can (the tick's CAN RX fused into the KF6 ISR); can_isr: the same
@@ -284,8 +288,11 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
             e.ingest_can(cf, cs)
             e.isr_tick(out=fr, **imu)
             return
-        if args.op.startswith("isr"):  # fmskf_isr_tick: one fused kernel for RS
-            e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
+        if args.op.startswith("isr"):  # fmskf_isr_tick: one fused kernel for RS, KF6 and EKF9
+            if args.model == "ekf9":
+                e.isr_tick(out=fr, raw=draw, rpm=dr)
+            else:
+                e.isr_tick(out=fr, yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
             return
         e.tick(yaw_deg=dy, gyro_z_dps=dg, rpm=dr)
         e.control(dr)
