@@ -112,6 +112,10 @@ PATHS = [
     # the reference-semantics ISR (k_isr_rs) on the motor state: the RS tick's 84 / 56 with the
     # control step's 209 / 152 and the frame; with the CAN RX fused in, the rpm and sums not read
     ("isr_rs_2p20", "k_isr_rs", 84 + 209, 56 + 152 + 8),
+    # the EKF9 ISR (k_isr_ekf9): the tick's 232 / 216 (cfg 3's count; the heading's hidden row,
+    # 4 + 4 B, is traffic above it) with the control step's 217 / 152 (its own rpm plane) and the
+    # frame
+    ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 217, 216 + 152 + 8),
     ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 + 209 + 120, 56 + 152 + 8 + 96),
 ]
 
