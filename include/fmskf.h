@@ -374,10 +374,11 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
 /* The tick's CAN RX and the ISR in one call: fmskf_ingest_can(h, can_frames, can_stamps, NULL,
  * mem) -- the four C610 frames of every robot present, MOTOR_IF_M2006::rx_callback
  * (VD_motor_if_m2006.cpp) -- then fmskf_isr_tick(h, in, frames, mem).  can_frames [N][4][8],
- * can_stamps [N][4] as fmskf_ingest_can.  Models KF6 (no caller rpm / records in `in`) and
- * RS (no caller rpm / angle sums) run it as ONE kernel: the received rpm (RS: and the new angle
- * sums) feed the estimator and the four wheel loops from registers (otherwise, and where the
- * ISR itself is not one kernel, the two calls run).
+ * can_stamps [N][4] as fmskf_ingest_can.  Models KF6 (no caller rpm / records in `in`), EKF9
+ * (no caller rpm) and RS (no caller rpm / angle sums) run it as ONE kernel: the received rpm
+ * (RS: and the new angle sums) feed the estimator (EKF9: the wheel loops only, its measurement
+ * is the raw record) and the four wheel loops from registers (otherwise, and where the ISR
+ * itself is not one kernel, the two calls run).
  * Results are identical to the two calls in sequence. */
 int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t *can_stamps,
                        const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem);

@@ -264,6 +264,9 @@ int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t 
     if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused() && !in->kf6_rec && !in->rpm) {
       fused = launch_isr_kf6_can(h->s, t, h->kf6, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
                                  (const int16_t *)s, h->cfg.motor_dir, h->stream);
+    } else if (h->cfg.model == FMSKF_MODEL_EKF9 && isr_kf6_fused() && !in->rpm) {
+      fused = launch_isr_ekf9_can(h->s, t, h->ekf9, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+                                  (const int16_t *)s, h->cfg.motor_dir, h->stream);
     } else if (h->cfg.model == FMSKF_MODEL_RS && !in->rpm && !in->angle_sum) {
       fused = launch_isr_rs_can(h->s, t, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
                                 (const int16_t *)s, h->cfg.motor_dir, h->stream);

@@ -352,6 +352,9 @@ int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp,
 // the control step's [N][4] rpm (the caller's plane or the motor state)
 int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
                     const CtrlPrm &p, const int16_t *rpm, uint8_t *frames, hipStream_t st);
+int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
+                        const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
+                        const int8_t dir[4], hipStream_t st);
 int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                       uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
                       hipStream_t st);

@@ -363,32 +363,6 @@ int launch_isr_kf6(const DevState &s, const TickIn &in, const Kf6Params &kp, boo
 // ISR.  hipErrorNotSupported where the fused form does not apply (record inputs, the tick's
 // non-temporal regime, the motor state past the cached regime or its sum planes past 4 GiB,
 // unaligned frames / stamps): the caller then runs CAN RX and the ISR as two calls
-// the CAN lane's arguments over the handle's motor state; false where the fused form does not
-// apply (the motor state past the cached regime or its sum planes past 4 GiB, unaligned frames /
-// stamps)
-static bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
-                     CanArgs &ca) {
-  if (!s.m_sum || state_nt(s.n * 66) || 4 * s.m_pitch * 8 > 0xFFFFFFFFull || ((uintptr_t)can_frames & 15) != 0 ||
-      ((uintptr_t)can_stamps & 7) != 0)
-    return false;
-  ca = CanArgs{};
-  ca.n = s.n;
-  ca.frames = can_frames;
-  ca.stamps = can_stamps;
-  ca.present = nullptr;
-  for (int w = 0; w < 4; w++) ca.dir[w] = dir[w];
-  ca.micro = s.m_micro;
-  ca.angle = s.m_angle;
-  ca.prev = s.m_prev;
-  ca.prev_micro = s.m_prev_micro;
-  ca.rpm = s.m_rpm;
-  ca.curr = s.m_curr;
-  ca.sum = s.m_sum;
-  ca.sum_pitch = s.m_pitch;
-  ca.iir_y = s.m_iir_y;
-  return true;
-}
-
 int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp, bool libm, const CtrlDev &c,
                        const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
                        const int8_t dir[4], hipStream_t st) {

@@ -7,6 +7,7 @@
 // F / H / Q / R are shared: H and the sparsity of F are compile-time model traits
 // (kf_generic.hpp), Q / R / dt ride in the kernarg segment (scalar loads, SGPRs).
 // The 6-state headline kernel lives in kernels_kf6.hip.
+#include "can_lane.hpp"
 #include "ctrl_lane.hpp"
 #include "ens_device.hpp"
 #include "kf_generic.hpp"
@@ -267,10 +268,15 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 // control step's rpm (the caller's plane or the ingested motor state, as fmskf_control reads
 // it), then the 0x200 frame; every load of both steps issued before either computes.  One robot
 // per lane, the clamped-index form.  Bit-identical to fmskf_tick + fmskf_control +
-// fmskf_can_tx.  CPC: the control planes' cache policy.
-template <bool LIBM, bool SEQ, int CPC, bool COMP>
+// fmskf_can_tx.  CPC: the control planes' cache policy.  CAN (fmskf_isr_tick_can): the tick's
+// four C610 frames per robot first (can_lane.hpp), their rpm handed to the wheel loops in
+// registers instead of read back from the motor state (the EKF9 measurement keeps the raw record).
+// CNT: the motor state streamed non-temporal, so that it does not evict the cache-resident EKF9
+// state (2^20 robots: 220 + 66 B per robot outgrow the Infinity Cache; 194 -> 155.4-156.2 us per
+// tick against 195.8 for the two calls, kbench, two passes)
+template <bool LIBM, bool SEQ, int CPC, bool COMP, bool CAN = false, bool CNT = false>
 __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> a, CtrlDev c, CtrlPrm p,
-                                                    uint8_t *frames, const int16_t *rpm) {
+                                                    uint8_t *frames, const int16_t *rpm, CanArgs can) {
   constexpr int N = 9, NP = 45;
   const uint32_t bid = blockIdx.x;
   __shared__ float wtab[LIBM ? 1 : kBlock / 64][LIBM ? 1 : kWaveTab];
@@ -279,6 +285,8 @@ __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> 
   const uint64_t i = (uint64_t)bid * kBlock + threadIdx.x;
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
+  Can4Lane<CNT, true> cl4;
+  if constexpr (CAN) cl4.load(can, (uint64_t)bid * kBlock, (uint32_t)(ic - (uint64_t)bid * kBlock));
   float x[N], P[NP];
   WaveTable<LIBM> tv(a.in.sintab);
   const uint32_t sl = tile_slot(n, bid);
@@ -294,10 +302,12 @@ __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> 
   float lo = ld_chunk<float, 0>(a.prm.thlo, hb0, n, sl);
   Ekf9Lo<COMP, 0> cl;
   cl.load(a.prm.clo, bid, sl);
-  const uint2 rw = reinterpret_cast<const uint2 *>(rpm)[ic];
+  uint2 rw;
+  if constexpr (!CAN) rw = reinterpret_cast<const uint2 *>(rpm)[ic];
   CtrlLane<true, CPC> L;
   L.load(c, (uint32_t)ic);
   tv.store(stab);
+  if constexpr (CAN) rw = cl4.step(can, live);
   ekf9_tick1<LIBM, true, true, SEQ, COMP>(a, raw, have, stab, x, P, lo, cl.v);
   if (live) {
     st_chunk<float, st_pol(0)>(a.prm.thlo, hb0, n, sl, lo);
@@ -757,24 +767,55 @@ int launch_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &p, bool l
               : launch_ekf9_s<false, false>(a, s, in, libm, upd, pred, nt, st, ens_nb);
 }
 
-template <bool LIBM, bool SEQ, bool COMP>
-static int isr_ekf9_v(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
-                      const int16_t *rpm, bool nt, hipStream_t st) {
+template <bool LIBM, bool SEQ, bool COMP, bool CAN, bool CNT>
+static int isr_ekf9_w(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
+                      const int16_t *rpm, bool nt, hipStream_t st, const CanArgs &can) {
   const dim3 g = grid_for(c.n);
   if (nt) {
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
-    k_isr_ekf9<LIBM, SEQ, kStateNT, COMP><<<g, kBlock, lds, st>>>(a, c, p, frames, rpm);
+    k_isr_ekf9<LIBM, SEQ, kStateNT, COMP, CAN, CNT><<<g, kBlock, lds, st>>>(a, c, p, frames, rpm, can);
   } else {
-    k_isr_ekf9<LIBM, SEQ, 0, COMP><<<g, kBlock, 0, st>>>(a, c, p, frames, rpm);
+    k_isr_ekf9<LIBM, SEQ, 0, COMP, CAN, CNT><<<g, kBlock, 0, st>>>(a, c, p, frames, rpm, can);
   }
   return (int)hipGetLastError();
 }
 
-template <bool SEQ, bool COMP>
+template <bool LIBM, bool SEQ, bool COMP, bool CAN>
+static int isr_ekf9_v(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
+                      const int16_t *rpm, bool nt, hipStream_t st, const CanArgs &can) {
+  if constexpr (CAN) {
+    // the EKF9 state and the motor state together past the Infinity Cache: the motor state
+    // streams non-temporal and the EKF9 state stays resident
+    if (state_nt(a.n * ((a.prm.clo ? 240 : 220) + 66)))
+      return isr_ekf9_w<LIBM, SEQ, COMP, true, true>(a, c, p, frames, rpm, nt, st, can);
+  }
+  return isr_ekf9_w<LIBM, SEQ, COMP, CAN, false>(a, c, p, frames, rpm, nt, st, can);
+}
+
+template <bool SEQ, bool COMP, bool CAN>
 static int isr_ekf9_c(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, const CtrlPrm &p, uint8_t *frames,
-                      const int16_t *rpm, bool nt, bool libm, hipStream_t st) {
-  return libm ? isr_ekf9_v<true, SEQ, COMP>(a, c, p, frames, rpm, nt, st)
-              : isr_ekf9_v<false, SEQ, COMP>(a, c, p, frames, rpm, nt, st);
+                      const int16_t *rpm, bool nt, bool libm, hipStream_t st, const CanArgs &can) {
+  return libm ? isr_ekf9_v<true, SEQ, COMP, CAN>(a, c, p, frames, rpm, nt, st, can)
+              : isr_ekf9_v<false, SEQ, COMP, CAN>(a, c, p, frames, rpm, nt, st, can);
+}
+
+template <bool CAN>
+static int isr_ekf9_l(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
+                      const CtrlPrm &p, const int16_t *rpm, uint8_t *frames, hipStream_t st, const CanArgs &can) {
+  if (c.n == 0) return 0;
+  const uint64_t sb = s.xlo ? 240 : 220;  // state bytes per robot (+ the compensation rows)
+  if (!FMSKF_TILED || !s.thlo || in.n_ticks != 1 || !in.raw || (!CAN && !rpm) || state_nt(s.n * sb) ||
+      c.pitch * 4 * 3 * kAxF >= 0xFFFFFFFFull)
+    return (int)hipErrorNotSupported;
+  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, prm};
+  a.prm.thlo = s.thlo;
+  a.prm.clo = s.xlo;
+  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * sb);
+  const bool diag = ekf9_r_diagonal(prm.r);
+  if (s.xlo) return diag ? isr_ekf9_c<true, true, CAN>(a, c, p, frames, rpm, nt, libm, st, can)
+                         : isr_ekf9_c<false, true, CAN>(a, c, p, frames, rpm, nt, libm, st, can);
+  return diag ? isr_ekf9_c<true, false, CAN>(a, c, p, frames, rpm, nt, libm, st, can)
+              : isr_ekf9_c<false, false, CAN>(a, c, p, frames, rpm, nt, libm, st, can);
 }
 
 // fmskf_isr_tick for EKF9 in one kernel where it applies: one tick, the tiled EKF9 state
@@ -783,20 +824,16 @@ static int isr_ekf9_c(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, con
 // hipErrorNotSupported otherwise
 int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
                     const CtrlPrm &p, const int16_t *rpm, uint8_t *frames, hipStream_t st) {
-  if (c.n == 0) return 0;
-  const uint64_t sb = s.xlo ? 240 : 220;  // state bytes per robot (+ the compensation rows)
-  if (!FMSKF_TILED || !s.thlo || in.n_ticks != 1 || !in.raw || !rpm || state_nt(s.n * sb) ||
-      c.pitch * 4 * 3 * kAxF >= 0xFFFFFFFFull)
-    return (int)hipErrorNotSupported;
-  KfArgs<MdEKF9, Ekf9Params> a{s.n, s.pitch, (float *)s.x, (float *)s.P, in, s.counters, prm};
-  a.prm.thlo = s.thlo;
-  a.prm.clo = s.xlo;
-  const bool nt = state_nt(ctrl_state_bytes(c) + s.n * sb);
-  const bool diag = ekf9_r_diagonal(prm.r);
-  if (s.xlo) return diag ? isr_ekf9_c<true, true>(a, c, p, frames, rpm, nt, libm, st)
-                         : isr_ekf9_c<false, true>(a, c, p, frames, rpm, nt, libm, st);
-  return diag ? isr_ekf9_c<true, false>(a, c, p, frames, rpm, nt, libm, st)
-              : isr_ekf9_c<false, false>(a, c, p, frames, rpm, nt, libm, st);
+  return isr_ekf9_l<false>(s, in, prm, libm, c, p, rpm, frames, st, CanArgs{});
+}
+
+// the same with the tick's CAN RX fused in front (fmskf_isr_tick_can: no caller rpm)
+int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
+                        const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
+                        const int8_t dir[4], hipStream_t st) {
+  CanArgs ca;
+  if (!can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  return isr_ekf9_l<true>(s, in, prm, libm, c, p, nullptr, frames, st, ca);
 }
 
 int launch_kf12d(const DevState &s, const TickIn &in, const Kf12dParams &p, bool upd, bool pred,

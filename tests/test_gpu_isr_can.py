@@ -1,5 +1,5 @@
-"""fmskf_isr_tick_can: the tick's CAN RX and the firmware ISR in one call (one kernel for RS and
-KF6, k_isr_rs / k_isr_kf6 with the C610 lane of can_lane.hpp in front) against the two calls it replaces,
+"""fmskf_isr_tick_can: the tick's CAN RX and the firmware ISR in one call (one kernel for RS, KF6
+and EKF9, k_isr_rs / k_isr_kf6 / k_isr_ekf9 with the C610 lane of can_lane.hpp in front) against the two calls it replaces,
 fmskf_ingest_can + fmskf_isr_tick, on random targets / power events.  Bar: bit-exact for the
 estimator state, the control state, the 0x200 frames and the whole motor state
 (MOTOR_IF_M2006::rx_callback, VD_motor_if_m2006.cpp; the two-call path is itself held to the
@@ -19,13 +19,16 @@ def bits(a):
     return a.view(np.uint32) if a.dtype == np.float32 else a
 
 
-# kf6* / rs*: the fused kernels (planes, LIBM, validity mask, compensated positions, device-
-# resident frames, a ragged last block, the non-temporal control regime past the Infinity Cache);
-# kf6rpm / kf6rec / rssum: the documented two-call fallback (a caller rpm, records, caller sums)
+# kf6* / rs* / ekf9*: the fused kernels (planes, LIBM, validity mask, compensated positions,
+# device-resident frames, a ragged last block, the non-temporal control regime past the Infinity
+# Cache); kf6rpm / kf6rec / rssum / ekf9rpm: the documented two-call fallback (a caller rpm,
+# records, caller sums)
 CASES = [("kf6", 4099, 40), ("kf6", 1, 20), ("kf6libm", 777, 20), ("kf6mask", 1001, 20),
          ("kf6comp", 513, 20), ("kf6dev", 2048 + 5, 20), ("kf6rpm", 300, 12), ("kf6rec", 257, 12),
          ("rs", 999, 30), ("rs", 1, 12), ("rslibm", 700, 12), ("rssum", 333, 12),
          ("kf6mixmem", 3000, 12), ("rsmixmem", 3000, 12),
+         ("ekf9", 1000, 20), ("ekf9", 1, 12), ("ekf9libm", 513, 12), ("ekf9rpm", 400, 12),
+         ("ekf9", (1 << 20) + 17, 3),
          ("kf6", (1 << 20) + 17, 3), ("rs", (1 << 20) + 17, 3)]
 
 
@@ -36,13 +39,16 @@ def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
     tr = Trajectory(n, T, seed=53)
     trig = fmskf.TRIG_LIBM if case.endswith("libm") else fmskf.TRIG_TABLE512
     flags = fmskf.CFG_COMP_POS if case == "kf6comp" else 0
-    model = "rs" if case.startswith("rs") else "kf6"
+    model = "rs" if case.startswith("rs") else "ekf9" if case.startswith("ekf9") else "kf6"
+    raw = tr.ekf9_raw() if model == "ekf9" else None
     dev_in = case.endswith("mixmem")  # host CAN frames, device tick inputs: two staging flags
     sums = np.ascontiguousarray(tr.rs_inputs()[1]) if case == "rssum" else None
     yaw, gz, rpm = tr.kf6_inputs()
     valid = (rng.random((T, n)) > 0.25).astype(np.uint8) if case == "kf6mask" else None
 
     def kw(t):
+        if model == "ekf9":  # the raw WT901 words; ekf9rpm: the caller's rpm plane (two calls)
+            return dict(raw=raw[t], rpm=rpm[t]) if case == "ekf9rpm" else dict(raw=raw[t])
         if case == "rssum":  # the caller's sums: CAN RX, then the ISR on them
             return dict(yaw_deg=yaw[t], angle_sum=sums[t])
         if model == "rs" and not dev_in:

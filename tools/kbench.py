@@ -280,7 +280,8 @@ def bench_pipeline(args, e, n, yaw, gz, rpm, dev, st):
     cs = (torch.arange(4, device=dev, dtype=torch.int16) * 250).expand(n, 4).contiguous()
 
     def direct():
-        imu = dict(yaw_deg=dy) if args.model == "rs" else dict(yaw_deg=dy, gyro_z_dps=dg)
+        imu = dict(yaw_deg=dy) if args.model == "rs" else dict(raw=draw) if args.model == "ekf9" else \
+            dict(yaw_deg=dy, gyro_z_dps=dg)
         if args.op.startswith("isr_can"):
             e.isr_tick_can(cf, cs, out=fr, **imu)
             return
