@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
+#include "../../include/fmskf.h"
 
 namespace fmskf {
 
@@ -269,6 +270,17 @@ inline bool state_nt(uint64_t state_bytes) {
   }();
   if (force >= 0) return force != 0;
   return state_bytes > (256ull << 20);
+}
+
+// bytes per robot of the handle's estimator state (x, P and the hidden low-part rows): the part
+// of the working set the ingest kernels' cache policies have to leave room for
+inline uint64_t est_state_bytes(const DevState &s) {
+  switch (s.model) {
+    case FMSKF_MODEL_RS: return 56;
+    case FMSKF_MODEL_KF6: return s.xlo ? 128 : 108;
+    case FMSKF_MODEL_EKF9: return s.xlo ? 240 : 220;
+    default: return 90 * 8;  // KF12D
+  }
 }
 
 // Occupancy cap for the kernels that stream their state from HBM: dynamic LDS per block limits
