@@ -23,7 +23,9 @@ struct CanArgs {
   int64_t *sum;  // [4][sum_pitch]
   uint64_t sum_pitch;
   float *iir_y;  // [N][4] UTIL::IIR1 output state, also Status::flt_SpeedRadPS
+  bool nt;       // host side: the fused kernels' choice of a non-temporal motor state (can_nt)
 };
+inline bool can_nt_flag(const CanArgs &a) { return a.nt; }
 
 __device__ __forceinline__ int16_t s16_of(uint32_t h, uint32_t l) { return (int16_t)((h << 8) | l); }
 __device__ __forceinline__ int32_t mul_wrap(int32_t a, int32_t b) {
@@ -124,6 +126,15 @@ inline bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t
   return true;
 }
 
+
+// The motor state non-temporal (k_can4 and the fused kernels alike): once the motor state (66 B
+// per robot), the tick's CAN frames and stamps (40 B) and the estimator state together outgrow
+// the Infinity Cache, a cached motor state evicts the estimator state the tick reads next.
+// Measured (kbench, two passes, profiles/r5_ab.json): ingest_can + isr_tick EKF9 2^20 195 -> 163
+// us, KF6 2^21 299 -> 253-263; isr_tick_can KF6 2^21 306-307 -> 248-250, RS 2^21 255-256 ->
+// 216-217 (the 40 B of frames count: without them RS 2^21 stayed cached); unchanged where
+// everything fits (KF6 / RS 2^20)
+inline bool can_nt(const DevState &s) { return state_nt(s.n * (66 + 40 + est_state_bytes(s))); }
 
 template <bool NT, bool SO>
 struct Can4Lane {

@@ -80,12 +80,12 @@ struct IsrRsArgs {
 // CAN (round 5, fmskf_isr_tick_can): the tick's four C610 frames per robot first (can_lane.hpp),
 // the new angle sums and rpm handed to the odometry and the wheel loops in registers instead of
 // read back from the motor state
-template <bool LIBM, bool SMALL, int CP = 0, bool CAN = false>
+template <bool LIBM, bool SMALL, int CP = 0, bool CAN = false, bool CNT = false>
 __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p, CanArgs can) {
   const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)n) return;
-  Can4Lane<false, true> cl;
+  Can4Lane<CNT, true> cl;  // CNT: the motor state non-temporal (launchers: can_nt)
   if constexpr (CAN) {  // the block's 256-robot chunk
     const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
     cl.load(can, hb, i - hb);
@@ -135,14 +135,14 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
 // (MOTOR_IF_M2006::rx_callback, can_lane.hpp), their rpm handed to the tick and the wheel loops
 // in registers -- the firmware's CAN RX ISR and 1 kHz ISR in one launch, bit-identical to
 // fmskf_ingest_can + fmskf_isr_tick
-template <class O, int CPC, bool CAN = false>
+template <class O, int CPC, bool CAN = false, bool CNT = false>
 __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, CtrlDev c, CtrlPrm p,
                                                    uint8_t *frames, CanArgs can) {
   const uint64_t n = a.n;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
   const uint32_t ic = live ? i : (uint32_t)n - 1u;
-  Can4Lane<false, true> cl;
+  Can4Lane<CNT, true> cl;  // CNT: the motor state non-temporal (launchers: can_nt)
   if constexpr (CAN) {  // the block's 256-robot chunk (every block has a live lane)
     const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
     cl.load(can, hb, ic - hb);
@@ -271,7 +271,7 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uin
   return (int)hipGetLastError();
 }
 
-template <bool CAN>
+template <bool CAN, bool CNT = false>
 static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                     uint8_t *frames, hipStream_t st, const CanArgs &can) {
   if (c.n == 0) return 0;
@@ -282,14 +282,14 @@ static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDe
   if (nt) {
     // 3 blocks per CU (48 KiB dynamic LDS): 2^20 75.7-76.5 -> 73.9 us (two passes)
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
-    if (libm) k_isr_rs<true, true, kStateNT, CAN><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
-    else k_isr_rs<false, true, kStateNT, CAN><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
+    if (libm) k_isr_rs<true, true, kStateNT, CAN, CNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
+    else k_isr_rs<false, true, kStateNT, CAN, CNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
   } else if (libm) {
-    if (small) k_isr_rs<true, true, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
-    else k_isr_rs<true, false, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    if (small) k_isr_rs<true, true, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<true, false, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   } else {
-    if (small) k_isr_rs<false, true, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
-    else k_isr_rs<false, false, 0, CAN><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    if (small) k_isr_rs<false, true, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<false, false, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   }
   return (int)hipGetLastError();
 }
@@ -310,6 +310,11 @@ static int isr_kf6_v(const KfArgs<MdKF6, Kf6Params> &a, const CtrlDev &c, const 
   using O = Opt<LIBM, true, true, true, VALID, REC, false, false, COMP>;
   const unsigned lds = nt ? FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u) : 0u;
   if constexpr (!REC) {  // with CAN the rpm comes from the frames, so the inputs are planes
+    if (can && can_nt_flag(*can)) {
+      if (nt) k_isr_kf6<O, kStateNT, true, true><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames, *can);
+      else k_isr_kf6<O, 0, true, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames, *can);
+      return (int)hipGetLastError();
+    }
     if (can) {
       if (nt) k_isr_kf6<O, kStateNT, true><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, frames, *can);
       else k_isr_kf6<O, 0, true><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, frames, *can);
@@ -368,6 +373,7 @@ int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp,
                        const int8_t dir[4], hipStream_t st) {
   CanArgs ca;
   if (in.rec || !can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  ca.nt = can_nt(s);
   return isr_kf6_l(s, in, kp, libm, c, p, frames, st, &ca);
 }
 
@@ -378,6 +384,7 @@ int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const Ctrl
                       hipStream_t st) {
   CanArgs ca;
   if (!can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  if (can_nt(s)) return isr_rs_l<true, true>(s, in, libm, c, p, frames, st, ca);
   return isr_rs_l<true>(s, in, libm, c, p, frames, st, ca);
 }
 

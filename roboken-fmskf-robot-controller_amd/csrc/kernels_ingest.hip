@@ -482,9 +482,9 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
       return e ? atoi(e) : 1;
     }();
     const bool so = var != 0 && 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
-    // non-temporal once the motor state and the estimator state together outgrow the Infinity
-    // Cache: a cached motor state would evict the estimator state the next tick reads
-    if (state_nt(s.n * (66 + est_state_bytes(s)))) {
+    // non-temporal once the motor state, the frames and the estimator state together outgrow
+    // the Infinity Cache (can_nt, can_lane.hpp)
+    if (can_nt(s)) {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
       if (so) k_can4<true, true><<<g, kBlock, lds, st>>>(a);
       else k_can4<true, false><<<g, kBlock, lds, st>>>(a);

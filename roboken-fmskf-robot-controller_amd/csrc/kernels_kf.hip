@@ -272,8 +272,8 @@ __global__ __launch_bounds__(kBlock) void k_ekf9t(KfArgs<MdEKF9, Ekf9Params> a) 
 // four C610 frames per robot first (can_lane.hpp), their rpm handed to the wheel loops in
 // registers instead of read back from the motor state (the EKF9 measurement keeps the raw record).
 // CNT: the motor state streamed non-temporal, so that it does not evict the cache-resident EKF9
-// state (2^20 robots: 220 + 66 B per robot outgrow the Infinity Cache; 194 -> 155.4-156.2 us per
-// tick against 195.8 for the two calls, kbench, two passes)
+// state (can_nt; 2^20 robots: 194 -> 155.4-156.2 us per tick against 195.8 for the two calls,
+// kbench, two passes)
 template <bool LIBM, bool SEQ, int CPC, bool COMP, bool CAN = false, bool CNT = false>
 __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> a, CtrlDev c, CtrlPrm p,
                                                     uint8_t *frames, const int16_t *rpm, CanArgs can) {
@@ -786,8 +786,7 @@ static int isr_ekf9_v(const KfArgs<MdEKF9, Ekf9Params> &a, const CtrlDev &c, con
   if constexpr (CAN) {
     // the EKF9 state and the motor state together past the Infinity Cache: the motor state
     // streams non-temporal and the EKF9 state stays resident
-    if (state_nt(a.n * ((a.prm.clo ? 240 : 220) + 66)))
-      return isr_ekf9_w<LIBM, SEQ, COMP, true, true>(a, c, p, frames, rpm, nt, st, can);
+    if (can_nt_flag(can)) return isr_ekf9_w<LIBM, SEQ, COMP, true, true>(a, c, p, frames, rpm, nt, st, can);
   }
   return isr_ekf9_w<LIBM, SEQ, COMP, CAN, false>(a, c, p, frames, rpm, nt, st, can);
 }
@@ -833,6 +832,7 @@ int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &p
                         const int8_t dir[4], hipStream_t st) {
   CanArgs ca;
   if (!can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  ca.nt = can_nt(s);
   return isr_ekf9_l<true>(s, in, prm, libm, c, p, nullptr, frames, st, ca);
 }
 
