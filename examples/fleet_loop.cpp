@@ -13,7 +13,7 @@
 //   fleet_loop [N] [ticks]
 //   FLEET_MODEL=kf6 fleet_loop ...    the 6-state KF instead of the reference's RS odometry
 //   FLEET_SPLIT_CAN=1 fleet_loop ...  CAN RX and the ISR as two calls (default: one,
-//       fmskf_isr_tick_can -- one kernel for RS and KF6)
+//       fmskf_isr_tick_can -- one kernel for RS, KF6 and EKF9)
 //   FLEET_WORLD=W FLEET_RANK=r FLEET_ID=/path/id fleet_loop ...   one process per GPU: rank 0
 //       writes the communicator id to FLEET_ID, every rank reads it (device = rank, or
 //       FLEET_DEVICE)

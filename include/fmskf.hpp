@@ -100,7 +100,7 @@ class Robots {
     else check(fmskf_tick(h_, &in), "fmskf_tick");
   }
   // the tick's CAN RX (MOTOR_IF_M2006::rx_callback of every wheel: frames [N][4][8], stamps
-  // [N][4]) and can_tx_routine in one call -- one kernel for RS and KF6 (fmskf_isr_tick_can)
+  // [N][4]) and can_tx_routine in one call -- one kernel for RS, KF6 and EKF9 (fmskf_isr_tick_can)
   void can_rx_tx_routine(const uint8_t *frames, const int16_t *stamps, uint8_t *tx_frames,
                          uint32_t mem = FMSKF_MEM_HOST) {
     fmskf_tick_inputs in{};

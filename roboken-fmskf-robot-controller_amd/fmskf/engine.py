@@ -497,7 +497,7 @@ class Engine:
 
     def isr_tick_can(self, can_frames, can_stamps, frames=True, out=None, **kw):
         """The tick's CAN RX and the ISR in one call (fmskf_isr_tick_can): ingest_can(can_frames,
-        can_stamps) then isr_tick(**kw), one kernel for RS and KF6.  can_frames [N, 4, 8] uint8,
+        can_stamps) then isr_tick(**kw), one kernel for RS, KF6 and EKF9.  can_frames [N, 4, 8] uint8,
         can_stamps [N, 4] int16, both host arrays or both device tensors; the [N][8] TX frames
         come back the same way (numpy, or the device tensor `out`), None with frames=False."""
         a = _Args()
