@@ -199,7 +199,7 @@ def test_fleet_loop_cpp_host_program():
 @pytest.mark.parametrize("model", ["rs", "kf6"])
 def test_fleet_loop_cpp_fused_can_equals_split(model):
     """examples/fleet_loop.cpp with the tick's CAN RX inside the ISR call (fmskf_isr_tick_can,
-    the default; one kernel for RS and KF6) prints exactly what the split form (rx_callback, then
+    the default; one kernel for RS, KF6 and EKF9) prints exactly what the split form (rx_callback, then
     can_tx_routine) prints: poses, VehicleInfo, TX frame bytes, the ensemble and motor Status."""
     import os
     import subprocess
