@@ -373,6 +373,9 @@ PATH_BYTES = {
     # heading's hidden low-part row) + the control step's 369 (its own rpm plane: the tick reads
     # the raw record) + the 0x200 frame
     "isr_ekf9_2p20": 448 + 369 + 8,
+    # with the tick's CAN RX fused in (fmskf_isr_tick_can): the CAN row's 216, the control step's
+    # rpm no longer read back
+    "isr_can_ekf9_2p20": 216 + (448 + 369 + 8) - 8,
     # the reference-semantics ISR (k_isr_rs) on the ingested motor state: the RS tick's 140 + the
     # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
     "isr_rs_2p20": 140 + 369 - 8 + 8,
@@ -495,6 +498,8 @@ def path_rows(dev, stream, ticks: int, trig):
                      torch.round(-gz / 2000.0 * 32768).to(torch.int16)[..., None],
                      torch.zeros(R, n, 2, dtype=torch.int16, device=dev), rpm], -1).contiguous()
     timed("isr_ekf9_2p20", lambda k: e.isr_tick(out=fr, raw=raw[k % R], rpm=rpm[k % R]), e)
+    e = driven("ekf9")
+    timed("isr_can_ekf9_2p20", lambda k: e.isr_tick_can(frames[k % R], stamps[k % R], out=fr, raw=raw[k % R]), e)
     del raw
     e = driven("rs")
     e.ingest_can(frames[0], stamps[0])
