@@ -242,7 +242,13 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
  * the last two angles), flt_SpeedRadPS.  Any pointer may be NULL. */
 int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle, int16_t *rpm,
                            int16_t *curr, float *dlt_out_angle_rad, float *speed_radps, uint32_t mem);
-/* counters: [0] = instances whose state went non-finite (NaN/Inf guard) */
+/* counters: [0] = instances whose state went non-finite (NaN/Inf guard); [1] = calls of
+ * fmskf_isr_tick_can that ran the CAN RX as a kernel of its own before the ISR (a caller rpm /
+ * angle sums / KF6 records, CAN buffers not 16-byte (frames) / 8-byte (stamps) aligned, or a
+ * regime where the ISR is not one kernel); [2] = ISRs (fmskf_isr_tick or fmskf_isr_tick_can)
+ * that ran as the estimator tick, the control step and the 0x200 frame in three kernels instead
+ * of one (KF12D; KF6 / EKF9 past the Infinity Cache).  Results are identical either way; [1] and
+ * [2] count since create / reset and are not checkpointed. */
 int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters);
 
 /* ---- ensemble statistics (mean / covariance of x across instances) --------- */
@@ -305,8 +311,9 @@ int fmskf_ensemble_stats(fmskf_handle h, double *mean, double *cov_packed);
  *   fmskf_ensemble_begin: the stand-alone record of the current state (no tick);
  *   the record's fold rides in the next begin's tick kernel (extra blocks past its tick
  *   blocks), or runs ahead of the next fmskf_tick, or at fmskf_ensemble_end when nothing
- *   came first; with a communicator of fmskf_comm_init, ncclAllGather and the copy of the
- *   gathered records to pinned host memory then run on the handle's side stream.  No tick on
+ *   came first; with a communicator of fmskf_comm_init of more than one rank, ncclAllGather
+ *   and the copy of the gathered records to pinned host memory then run on the handle's side
+ *   stream (one rank: the gather is the identity, the fold writes the pinned slot).  No tick on
  *   the handle's stream waits for the gather, and no call waits on the host.
  *   fmskf_ensemble_end: waits for the OLDEST pending begin and returns its mean [n] and
  *     covariance packed [n(n+1)/2] (unbiased, rank-order fold: identical on every rank,
@@ -324,8 +331,9 @@ int fmskf_ensemble_end_count(fmskf_handle h, double *mean, double *cov_packed, d
 /* How long the exchange of the result the last fmskf_ensemble_end / _end_count collected took on
  * the handle's side stream: ncclAllGather of the record plus the copy of the gathered records to
  * pinned host memory, between two timing events recorded around them (ms).  -1 when that result
- * needed no exchange (no communicator: the fold wrote the pinned slot itself) or none was
- * collected yet.  Lets an N > 1 run say what its collective costs beside the tick. */
+ * needed no exchange (no communicator, or one of a single rank: the fold wrote the pinned slot
+ * itself) or none was collected yet.  Lets an N > 1 run say what its collective costs beside the
+ * tick. */
 int fmskf_ensemble_exchange_ms(fmskf_handle h, float *ms);
 
 /* ---- vehicle control step -------------------------- */

@@ -174,6 +174,9 @@ int fmskf_save_state(fmskf_handle h, const char *path) {
     memcpy(hd.magic, kCkMagic, 8);
     ck_layout(h, &hd);
     hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
+    rs_prev_materialize(h);  // the file holds the odometry's previous sums in the prev planes
+    // and the whole WT901 register file in its planes (no row-resident registers)
+    launch_check(launch_wt901_regs_sync(h->s, h->stream), "register file sync");
     hip_check(hipStreamSynchronize(h->stream), "save sync");
     File f(path, "wb");
     f.write(&hd, sizeof(hd));  // rewritten with the body size and checksum at the end
@@ -272,6 +275,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (!(hd.groups & 2) && h->s.imu_reg) zero_imu(h);
     if (!(hd.groups & 4) && h->s.m_sum) zero_motors(h);
     if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
+    h->rs_prev_synced = h->rs_prev_stale = false;  // the prev planes come from the file
     hip_check(hipStreamSynchronize(h->stream), "load sync");
     // pass 2: stream each section to the device in bounded chunks
     for (const CkSection &c : secs) {

@@ -18,14 +18,20 @@ namespace capi {
 // stand-alone): with a communicator the side stream all-gathers the record over xGMI and copies
 // the gathered records into the slot's pinned buffer behind it; on one GPU the fold wrote the
 // pinned buffer itself.  Then the slot's `done` event.
-double *ens_fold_dst(const fmskf_ctx *h, const fmskf_ctx::EnsSlot &S) { return h->comm ? S.rec : S.host_dev; }
+// A communicator of one rank exchanges nothing: the all-gather of one record is that record.  So
+// the side stream runs only with world > 1; at world 1 the fold writes the pinned slot as on a
+// handle without a communicator.  Round 6, kbench ens_async (K = 1, 2^20 KF6, one box): the
+// side-stream RCCL copy + D2H took the per-tick time from 39.2 to 82.6-91.7 us on the null
+// stream (the bench line's own stream: 46.2 against 39.1 in round 5).
+bool ens_exchanges(const fmskf_ctx *h) { return h->comm && h->world > 1; }
+double *ens_fold_dst(const fmskf_ctx *h, const fmskf_ctx::EnsSlot &S) { return ens_exchanges(h) ? S.rec : S.host_dev; }
 void ens_gather_async(fmskf_ctx *h, fmskf_ctx::EnsSlot &S);  // with the RCCL entry points below
 // One GPU: the event behind the fold (the fold stored the record into the pinned slot with
 // system-scope stores, ens_fold_block).  Waiting on the pinned slot itself instead of an event
 // (a signalling-NaN sentinel polled by fmskf_ensemble_end) measured slower: K = 1 at 2^20
 // 41.8-41.9 us per tick against 40.0-40.2 (kbench ens_async, two passes each, one box).
 void ens_fold_queued(fmskf_ctx *h, fmskf_ctx::EnsSlot &S) {
-  if (h->comm) ens_gather_async(h, S);
+  if (ens_exchanges(h)) ens_gather_async(h, S);
   else hip_check(hipEventRecord(S.done, h->stream), "hipEventRecord");
   h->ens_carry = -1;
 }
@@ -95,7 +101,12 @@ bool elf_exports(const char *path, const char *name) {
     return false;
   Elf64_Ehdr eh;
   memcpy(&eh, img.data(), sizeof(eh));
-  if (eh.e_shentsize != sizeof(Elf64_Shdr) || eh.e_shoff + (uint64_t)eh.e_shnum * sizeof(Elf64_Shdr) > img.size())
+  // every extent is checked field by field against the image, never as a sum that could wrap
+  // past 2^64 (a header with e_shoff or sh_offset near 2^64 is refused, not read out of bounds)
+  const uint64_t size = img.size();
+  auto within = [size](uint64_t off, uint64_t len) { return off <= size && len <= size - off; };
+  if (eh.e_shentsize != sizeof(Elf64_Shdr) || eh.e_shoff > size ||
+      eh.e_shnum > (size - eh.e_shoff) / sizeof(Elf64_Shdr))
     return false;
   auto shdr = [&](uint32_t k) {
     Elf64_Shdr sh;
@@ -105,13 +116,13 @@ bool elf_exports(const char *path, const char *name) {
   const size_t nlen = strlen(name);
   for (uint32_t k = 0; k < eh.e_shnum; k++) {
     const Elf64_Shdr sy = shdr(k);
-    if (sy.sh_type != SHT_DYNSYM || sy.sh_link >= eh.e_shnum || sy.sh_offset + sy.sh_size > img.size()) continue;
+    if (sy.sh_type != SHT_DYNSYM || sy.sh_link >= eh.e_shnum || !within(sy.sh_offset, sy.sh_size)) continue;
     const Elf64_Shdr st = shdr(sy.sh_link);
-    if (st.sh_offset + st.sh_size > img.size()) continue;
+    if (!within(st.sh_offset, st.sh_size)) continue;
     for (uint64_t o = 0; o + sizeof(Elf64_Sym) <= sy.sh_size; o += sizeof(Elf64_Sym)) {
       Elf64_Sym sym;
       memcpy(&sym, img.data() + sy.sh_offset + o, sizeof(sym));
-      if (sym.st_shndx == SHN_UNDEF || sym.st_name + nlen >= st.sh_size) continue;
+      if (sym.st_shndx == SHN_UNDEF || sym.st_name >= st.sh_size || nlen >= st.sh_size - sym.st_name) continue;
       if (memcmp(img.data() + st.sh_offset + sym.st_name, name, nlen + 1) == 0) return true;
     }
   }
@@ -185,20 +196,26 @@ void fmskf::capi::ens_gather_async(fmskf_ctx *h, fmskf_ctx::EnsSlot &S) {
     hip_check(hipEventCreateWithFlags(&h->ens_ticked, kSyncEvent), "hipEventCreate");
   }
   const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
-  if (!S.x0) {  // timing events on the side stream only (the tick stream records none)
+  // FMSKF_ENS_XTIME=0: no timing events around the exchange (A/B of their cost; then
+  // fmskf_ensemble_exchange_ms reports -1)
+  static const bool xtime = [] {
+    const char *e = getenv("FMSKF_ENS_XTIME");
+    return !e || atoi(e) != 0;
+  }();
+  if (xtime && !S.x0) {  // timing events on the side stream only (the tick stream records none)
     hip_check(hipEventCreate(&S.x0), "hipEventCreate");
     hip_check(hipEventCreate(&S.x1), "hipEventCreate");
   }
   hip_check(hipEventRecord(h->ens_ticked, h->stream), "hipEventRecord");
   hip_check(hipStreamWaitEvent(h->ens_stream, h->ens_ticked, 0), "hipStreamWaitEvent");
-  hip_check(hipEventRecord(S.x0, h->ens_stream), "hipEventRecord");
+  if (xtime) hip_check(hipEventRecord(S.x0, h->ens_stream), "hipEventRecord");
   nccl_check(need_rccl().all_gather(S.rec, S.gather, len, ncclFloat64, h->comm, h->ens_stream),
              "ncclAllGather");
   hip_check(hipMemcpyAsync(S.host, S.gather, (size_t)S.ranks * len * 8, hipMemcpyDeviceToHost, h->ens_stream),
             "D2H");
-  hip_check(hipEventRecord(S.x1, h->ens_stream), "hipEventRecord");
+  if (xtime) hip_check(hipEventRecord(S.x1, h->ens_stream), "hipEventRecord");
   hip_check(hipEventRecord(S.done, h->ens_stream), "hipEventRecord");
-  S.exchanged = true;
+  S.exchanged = xtime;
 }
 
 
@@ -316,7 +333,7 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
     fail(FMSKF_EINVAL, "four ensemble results pending: call fmskf_ensemble_end first");
   DeviceGuard g(h->cfg.device);
   const uint32_t nx = h->d.nx, len = 1 + nx + nx * (nx + 1) / 2;
-  const int ranks = h->comm ? h->world : 1;
+  const int ranks = ens_exchanges(h) ? h->world : 1;
   const int si = (h->ens_head + h->ens_pending) % fmskf_ctx::kEnsSlots;
   fmskf_ctx::EnsSlot &S = h->eslot[si];
   if (!S.blocks) {
@@ -350,7 +367,7 @@ void ens_async_begin(fmskf_ctx *h, const fmskf_tick_inputs *in) {
       t.fold_nb = (uint32_t)C->nb;
       t.fold_out = ens_fold_dst(h, *C);
       // one GPU, untimed: the carrying kernel's own completion records C's event
-      if (!h->comm && !h->timing) t.ens_done = C->done;
+      if (!ens_exchanges(h) && !h->timing) t.ens_done = C->done;
     }
     const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
     h->time_begin();

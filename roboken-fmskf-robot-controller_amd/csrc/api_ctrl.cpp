@@ -177,6 +177,15 @@ int fmskf_can_tx(fmskf_handle h, uint8_t *frames, uint32_t mem) {
 }
 
 // FMSKF_ISR_FUSED=0: the KF6 and EKF9 ISRs as three kernels (A/B, and the tests' cross-check)
+// FMSKF_RS_PREV_SKIP=0: the fused RS CAN ISR always reads and writes the prev planes (A/B)
+static bool rs_prev_skip() {
+  static const bool v = [] {
+    const char *e = getenv("FMSKF_RS_PREV_SKIP");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 static bool isr_kf6_fused() {
   static const bool v = [] {
     const char *e = getenv("FMSKF_ISR_FUSED");
@@ -200,8 +209,11 @@ static void isr_launches(fmskf_ctx *h, const TickIn &t, uint8_t *dst) {
     if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr launch");
   }
   if (h->cfg.model == FMSKF_MODEL_RS) {
+    rs_prev_materialize(h);
     launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
+    h->rs_prev_synced = t.angle_sum == h->s.m_sum;
   } else if (fused == (int)hipErrorNotSupported) {  // estimator tick, then the control step and the frame (three launches)
+    h->isr_ctrl_split++;
     int e = 0;
     switch (h->cfg.model) {
       case FMSKF_MODEL_KF6: e = launch_kf6(h->s, t, h->kf6, libm, true, true, h->stream); break;
@@ -268,11 +280,22 @@ int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t 
       fused = launch_isr_ekf9_can(h->s, t, h->ekf9, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
                                   (const int16_t *)s, h->cfg.motor_dir, h->stream);
     } else if (h->cfg.model == FMSKF_MODEL_RS && !in->rpm && !in->angle_sum) {
+      // the previous sums are the stored ones: take them from the CAN lane, skip the prev planes
+      // (not inside a capture: a replay may start from another state)
+      const bool ps = h->rs_prev_synced && !h->capturing && rs_prev_skip();
+      if (!ps) rs_prev_materialize(h);
       fused = launch_isr_rs_can(h->s, t, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
-                                (const int16_t *)s, h->cfg.motor_dir, h->stream);
+                                (const int16_t *)s, h->cfg.motor_dir, ps, h->stream);
+      if (fused != (int)hipErrorNotSupported) {
+        h->rs_prev_synced = true;  // the odometry's previous sums are the new motor sums
+        h->rs_prev_stale = h->rs_prev_stale || ps;
+      }
     }
     if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr+can launch");
     if (fused == (int)hipErrorNotSupported) {  // CAN RX, then the ISR of fmskf_isr_tick
+      h->isr_can_split++;
+      rs_prev_materialize(h);  // the CAN RX rewrites the motor sums
+      h->rs_prev_synced = false;
       launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, nullptr, h->cfg.motor_dir, h->stream),
                    "can launch");
       isr_launches(h, t, dst);

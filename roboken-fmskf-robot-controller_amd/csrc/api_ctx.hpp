@@ -164,6 +164,16 @@ struct fmskf_ctx {
   fmskf::Kf6Params kf6{};
   fmskf::Ekf9Params ekf9{};
   fmskf::Kf12dParams kf12{};
+  // which launch form the firmware-ISR calls took (fmskf_get_counters [1], [2]): calls of
+  // fmskf_isr_tick_can that ran the CAN RX as its own kernel before the ISR, and ISRs (of either
+  // call) that ran as the tick, control-step and frame kernels instead of one fused kernel
+  uint64_t isr_can_split = 0, isr_ctrl_split = 0;
+  // RS: where the odometry's previous encoder sums (s64_rawAngleSumPrev) are.  rs_prev_synced:
+  // they equal the motor state's sums (the last predict read those, and nothing changed them
+  // since); rs_prev_stale: the prev planes are behind, the fused RS CAN ISR took the previous sums
+  // from the motor state and wrote no prev (k_isr_rs PS).  stale implies synced.  Every reader of
+  // the prev planes and every writer of the motor sums calls rs_prev_materialize first.
+  bool rs_prev_synced = false, rs_prev_stale = false;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // pooled per-launch events (fmskf_kernel_time_total)
@@ -353,6 +363,8 @@ void zero_imu(fmskf_ctx *h);
 void zero_motors(fmskf_ctx *h);
 void ensure_imu(fmskf_ctx *h);
 void ensure_motors(fmskf_ctx *h);
+// RS: copy the motor state's sums into the prev planes if they are behind (rs_prev_stale)
+void rs_prev_materialize(fmskf_ctx *h);
 // extra: more host planes of the same call staged together with the tick inputs (one pinned
 // slot per call: two staging rounds in one call would release the first slot before the
 // kernel that reads it is queued); they must share in->mem

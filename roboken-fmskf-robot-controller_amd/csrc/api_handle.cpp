@@ -146,6 +146,15 @@ void ensure_imu(fmskf_ctx *h) {
   s.imu_qprev = h->alloc<float>(4 * n);
   zero_imu(h);
 }
+void rs_prev_materialize(fmskf_ctx *h) {
+  if (!h->rs_prev_stale) return;
+  const DevState &s = h->s;
+  hip_check(hipMemcpy2DAsync(s.prev_sum, s.pitch * 8, s.m_sum, s.m_pitch * 8, s.n * 8, 4, hipMemcpyDeviceToDevice,
+                             h->stream),
+            "previous sums");
+  h->rs_prev_stale = false;
+}
+
 void ensure_motors(fmskf_ctx *h) {
   DevState &s = h->s;
   if (s.m_sum) return;
@@ -224,6 +233,8 @@ void do_reset(fmskf_ctx *h) {
     hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, st), "reset ctrl");
   }
   hip_check(hipMemsetAsync(s.counters, 0, 8 * 8, st), "reset counters");
+  h->isr_can_split = h->isr_ctrl_split = 0;
+  h->rs_prev_synced = h->rs_prev_stale = false;  // the prev planes were zeroed above
   h->ens_shift_ok = false;
 }
 
@@ -333,6 +344,8 @@ void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, ui
   // whatever the slot holds then
   if (!h->capturing) ens_flush(h);
   const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
+  const bool rs_pred = h->cfg.model == FMSKF_MODEL_RS && pred;
+  if (rs_pred) rs_prev_materialize(h);  // the predict reads the prev planes
   h->time_begin();
   int e = 0;
   switch (h->cfg.model) {
@@ -342,6 +355,8 @@ void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, ui
     case FMSKF_MODEL_KF12D: e = launch_kf12d(h->s, t, h->kf12, upd, pred, h->stream); break;
   }
   launch_check(e, "tick kernel launch");
+  // the predict stored the sums it read as the previous ones
+  if (rs_pred) h->rs_prev_synced = t.angle_sum == h->s.m_sum;
   h->time_end();
 }
 
@@ -560,6 +575,10 @@ int fmskf_graph_begin(fmskf_handle h) {
     ensure_motors(h);
     ensure_ctrl(h);
     ensure_shift(h);
+    // a replay starts from whatever state the handle is in then: captured RS ISRs keep the prev
+    // planes themselves (no PS form inside a capture), so they must be current before it
+    rs_prev_materialize(h);
+    h->rs_prev_synced = false;
     hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
               "hipStreamBeginCapture");
     h->capturing = true;
@@ -572,6 +591,7 @@ int fmskf_graph_end(fmskf_handle h) {
     if (!h->capturing) fail(FMSKF_EINVAL, "no capture open");
     DeviceGuard g(h->cfg.device);
     h->capturing = false;
+    h->rs_prev_synced = false;  // the captured calls moved host-side flags the replays do not
     hipGraph_t gnew = nullptr;
     hip_check(hipStreamEndCapture(h->stream, &gnew), "hipStreamEndCapture");
     if (h->graph_exec) hip_check(hipGraphExecDestroy(h->graph_exec), "hipGraphExecDestroy");
@@ -591,6 +611,7 @@ int fmskf_graph_launch(fmskf_handle h, uint32_t times) {
     DeviceGuard g(h->cfg.device);
     for (uint32_t k = 0; k < times; k++)
       hip_check(hipGraphLaunch(h->graph_exec, h->stream), "hipGraphLaunch");
+    h->rs_prev_synced = false;
   });
 }
 
@@ -647,9 +668,11 @@ int fmskf_ingest_can(fmskf_handle h, const uint8_t *frames, const int16_t *stamp
     sg.add(&s, n * 8);
     sg.add(&p, n);
     sg.run();
+    rs_prev_materialize(h);  // the previous sums leave the motor state now
     launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, (const uint8_t *)p,
                             h->cfg.motor_dir, h->stream),
                  "can launch");
+    h->rs_prev_synced = false;
   });
 }
 

@@ -11,6 +11,7 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem) {
   return guarded([&] {
     check_handle(h);
     if (!h->s.prev_sum) fail(FMSKF_ENOTSUP, "prev_sum exists in the RS model only");
+    rs_prev_materialize(h);
     DeviceGuard g(h->cfg.device);
     copy_planes_out(h, prev, h->s.prev_sum, h->s.n * 8, h->s.pitch * 8, 4, mem);
     finish_out(h, mem);
@@ -38,6 +39,7 @@ int fmskf_get_imu_regs(fmskf_handle h, int16_t *regs, uint8_t *pending, uint32_t
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     ensure_imu(h);
+    launch_check(launch_wt901_regs_sync(h->s, h->stream), "register file sync");
     copy_out(h, regs, h->s.imu_reg, 0x90 * h->s.n * 2, mem);
     copy_out(h, pending, h->s.imu_cnt, h->s.n, mem);
     finish_out(h, mem);
@@ -150,6 +152,8 @@ int fmskf_get_counters(fmskf_handle h, uint64_t *counters, uint32_t n_counters) 
     unsigned long long tmp[8];
     hip_check(hipMemcpyAsync(tmp, h->s.counters, sizeof(tmp), hipMemcpyDeviceToHost, h->stream), "D2H");
     hip_check(hipStreamSynchronize(h->stream), "sync");
+    tmp[1] = h->isr_can_split;  // host-side counters: the launch forms the ISR calls took
+    tmp[2] = h->isr_ctrl_split;
     for (uint32_t k = 0; k < n_counters && k < 8; k++) counters[k] = tmp[k];
   });
 }

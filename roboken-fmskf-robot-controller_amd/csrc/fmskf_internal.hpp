@@ -367,9 +367,12 @@ int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, 
 int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
                         const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
                         const int8_t dir[4], hipStream_t st);
+// the WT901 register file made whole: the row-resident registers written back from the
+// snapshot rows of the robots whose standard poll kept them there (kernels_ingest.hip F_ROWREGS)
+int launch_wt901_regs_sync(const DevState &s, hipStream_t st);
 int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                       uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
-                      hipStream_t st);
+                      bool prev_in_sums, hipStream_t st);
 // the firmware ISR, reference semantics: RS tick + control step + TX frame in one kernel
 int launch_isr_rs(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c,
                   const CtrlPrm &p, uint8_t *frames, hipStream_t st);

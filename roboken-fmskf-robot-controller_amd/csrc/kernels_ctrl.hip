@@ -79,9 +79,16 @@ struct IsrRsArgs {
 };
 // CAN (round 5, fmskf_isr_tick_can): the tick's four C610 frames per robot first (can_lane.hpp),
 // the new angle sums and rpm handed to the odometry and the wheel loops in registers instead of
-// read back from the motor state
-template <bool LIBM, bool SMALL, int CP = 0, bool CAN = false, bool CNT = false>
+// read back from the motor state.
+// PS (round 6, CAN only): the previous sums live in the motor state.  When the last predict read
+// the motor state's sums and nothing changed them since (the host tracks it: fmskf_ctx
+// rs_prev_synced), s64_rawAngleSumPrev equals the sums the CAN lane loads anyway, so the odometry
+// takes those and the prev planes are neither read nor written (64 B per robot-tick: 685 -> 621 B);
+// the host copies the sums into the prev planes before anything else reads them
+// (rs_prev_materialize).  Mrad is the same int64 difference, so the result is bit-identical.
+template <bool LIBM, bool SMALL, int CP = 0, bool CAN = false, bool CNT = false, bool PS = false>
 __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlPrm p, CanArgs can) {
+  static_assert(CAN || !PS, "the previous sums come from the CAN lane");
   const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)n) return;
@@ -94,8 +101,10 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   s.px = a.x[i];
   s.py = a.x[pp + i];
   s.th = 0.f;  // overwritten by the correct step
+  if constexpr (!PS) {
 #pragma unroll
-  for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
+    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
+  }
   const float yaw = a.yaw_deg[i];
   uint2 rw;
   int64_t sum[4];
@@ -107,6 +116,10 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   CtrlLane<SMALL, CP> L;
   L.load(c, i);
   if constexpr (CAN) {
+    if constexpr (PS) {  // the stored sums are the previous ones (before step() updates sm[])
+#pragma unroll
+      for (int w = 0; w < 4; w++) s.prev[w] = cl.sm[w];
+    }
     rw = cl.step(can, true);
 #pragma unroll
     for (int w = 0; w < 4; w++) sum[w] = cl.sm[w];
@@ -119,8 +132,10 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   a.x[3 * pp + i] = s.vx;
   a.x[4 * pp + i] = s.vy;
   a.x[5 * pp + i] = s.vth;
+  if constexpr (!PS) {
 #pragma unroll
-  for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+  }
   if (a.frames) reinterpret_cast<uint2 *>(a.frames)[i] = tx_frame(cw);
 }
 
@@ -271,7 +286,7 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uin
   return (int)hipGetLastError();
 }
 
-template <bool CAN, bool CNT = false>
+template <bool CAN, bool CNT = false, bool PS = false>
 static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                     uint8_t *frames, hipStream_t st, const CanArgs &can) {
   if (c.n == 0) return 0;
@@ -282,14 +297,14 @@ static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDe
   if (nt) {
     // 3 blocks per CU (48 KiB dynamic LDS): 2^20 75.7-76.5 -> 73.9 us (two passes)
     const unsigned lds = FMSKF_LDS_CAP("FMSKF_ISR_LDS", true, 48u * 1024u);
-    if (libm) k_isr_rs<true, true, kStateNT, CAN, CNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
-    else k_isr_rs<false, true, kStateNT, CAN, CNT><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
+    if (libm) k_isr_rs<true, true, kStateNT, CAN, CNT, PS><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
+    else k_isr_rs<false, true, kStateNT, CAN, CNT, PS><<<grid1(c.n), kBlock, lds, st>>>(a, c, p, can);
   } else if (libm) {
-    if (small) k_isr_rs<true, true, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
-    else k_isr_rs<true, false, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    if (small) k_isr_rs<true, true, 0, CAN, CNT, PS><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<true, false, 0, CAN, CNT, PS><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   } else {
-    if (small) k_isr_rs<false, true, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
-    else k_isr_rs<false, false, 0, CAN, CNT><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    if (small) k_isr_rs<false, true, 0, CAN, CNT, PS><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
+    else k_isr_rs<false, false, 0, CAN, CNT, PS><<<grid1(c.n), kBlock, 0, st>>>(a, c, p, can);
   }
   return (int)hipGetLastError();
 }
@@ -378,12 +393,17 @@ int launch_isr_kf6_can(const DevState &s, const TickIn &in, const Kf6Params &kp,
 }
 
 // the reference-semantics ISR with the tick's CAN RX fused in: the odometry reads the new sums
-// and rpm from the CAN lane (the caller passes no rpm / sums: TickIn's are the motor state's)
+// and rpm from the CAN lane (the caller passes no rpm / sums: TickIn's are the motor state's).
+// prev_in_sums: the previous sums equal the motor state's stored sums (k_isr_rs PS)
 int launch_isr_rs_can(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                       uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
-                      hipStream_t st) {
+                      bool prev_in_sums, hipStream_t st) {
   CanArgs ca;
   if (!can_args(s, can_frames, can_stamps, dir, ca)) return (int)hipErrorNotSupported;
+  if (prev_in_sums) {
+    if (can_nt(s)) return isr_rs_l<true, true, true>(s, in, libm, c, p, frames, st, ca);
+    return isr_rs_l<true, false, true>(s, in, libm, c, p, frames, st, ca);
+  }
   if (can_nt(s)) return isr_rs_l<true, true>(s, in, libm, c, p, frames, st, ca);
   return isr_rs_l<true>(s, in, libm, c, p, frames, st, ca);
 }

@@ -29,6 +29,34 @@ enum : uint32_t {
 };
 // imu_if_wt901c.cpp:10-15
 enum : uint32_t { F_ACC = 0x01, F_GYRO = 0x02, F_ANGLE = 0x04, F_MAG = 0x08, F_QUAT = 0x10, F_READ = 0x80 };
+// not a firmware flag (round 6): the robot's row-resident registers -- AX AY AZ GX GY Roll Pitch
+// Q0-Q3, the eleven words the snapshot row holds besides the magnetometer's -- live in its
+// snapshot row, and their sReg planes are behind (the standard poll writes them once, into the
+// row).  Any other poll, fmskf_get_imu_regs and a checkpoint write them back first (row_regs_out).
+enum : uint32_t { F_ROWREGS = 0x40 };
+// bit k of a register's row-resident index (AX AY AZ GX GY Roll Pitch Q0-Q3 -> 0..10), or 0
+__device__ __forceinline__ uint32_t rowreg_bit(uint32_t r) {
+  return r >= R_AX && r < R_GZ ? 1u << (r - R_AX)
+         : r == R_ROLL || r == R_ROLL + 1 ? 1u << (5 + r - R_ROLL)
+         : r >= R_Q0 && r <= R_Q3 ? 1u << (7 + r - R_Q0) : 0u;
+}
+// the row-resident registers in snapshot-row word order (words 0-4, 8-13 of imu_data_page's row)
+// written back to sReg, except those in `skip` (rowreg_bit mask: registers written since)
+__device__ __forceinline__ void row_regs_out(const int16_t *snap, int16_t *reg, uint64_t n, uint64_t i,
+                                             uint32_t skip = 0) {
+  const uint4 r0 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[0];
+  const uint4 r1 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[1];
+  const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};  // word k in w[k / 2]
+  // (register, snapshot word) of the eleven, in rowreg_bit order
+  constexpr uint32_t kReg[11] = {R_AX, R_AX + 1, R_AX + 2, R_GX, R_GX + 1, R_ROLL, R_ROLL + 1,
+                                 R_Q0, R_Q0 + 1, R_Q0 + 2, R_Q0 + 3};
+  constexpr int kWord[11] = {0, 1, 2, 3, 4, 8, 9, 10, 11, 12, 13};
+#pragma unroll
+  for (int k = 0; k < 11; k++) {
+    const uint32_t v = w[kWord[k] / 2];
+    if (!((skip >> k) & 1u)) reg[kReg[k] * n + i] = (int16_t)(kWord[k] & 1 ? v >> 16 : v & 0xFFFFu);
+  }
+}
 
 // SensorDataUpdata for registers [r0, r0 + len)
 __device__ __forceinline__ uint32_t flags_of(uint32_t r0, uint32_t len) {
@@ -64,6 +92,7 @@ struct Wt901Args {
 struct Wt901Parser {
   uint64_t lo, hi;
   uint32_t cnt, flags;
+  uint32_t roww;  // rowreg_bit mask of the row-resident registers this poll's frames wrote
   // CopeWitData on a validated 11-byte window (bytes 0-7 in w0, 8-10 in w1)
   __device__ __forceinline__ void dispatch(uint64_t w0, uint64_t w1, const Wt901Args &a, uint64_t i) {
     const uint64_t n = a.n;
@@ -91,7 +120,10 @@ struct Wt901Parser {
       default: known = false; break;
     }
     if (known) {
-      for (uint32_t k = 0; k < len1; k++) reg[(reg1 + k) * n + i] = (int16_t)d[k];
+      for (uint32_t k = 0; k < len1; k++) {
+        reg[(reg1 + k) * n + i] = (int16_t)d[k];
+        roww |= rowreg_bit(reg1 + k);
+      }
       flags |= flags_of(reg1, len1);
       if (len2) {
         reg[reg2 * n + i] = (int16_t)d[3];
@@ -190,11 +222,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   ps.cnt = cnt_in;
   ps.lo = 0;
   ps.hi = 0;
+  ps.roww = 0;
   if (cnt_in != 0) {
     ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
     ps.hi = (uint64_t)a.parser[2 * n + i];
   }
-  ps.flags = flags_in;
+  ps.flags = flags_in & ~F_ROWREGS;
+  const bool row_regs = (flags_in & F_ROWREGS) != 0;
   const uint32_t len = len_in < a.stride ? len_in : a.stride;
   // the standard 10 ms poll (0x51 acc, 0x52 gyro, 0x53 angle, 0x59 quaternion)
   // taken by the fast path: every register updateData reads except the magnetometer's was
@@ -246,17 +280,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
         sw[f][2] = (uint32_t)(w0[f] >> 48) & 0xFFFFu;
         sw[f][3] = (uint32_t)w1[f] & 0xFFFFu;
       }
+      // round 6: of the 15 registers the four frames write, the eleven the snapshot row holds
+      // (AX AY AZ GX GY Roll Pitch Q0-Q3) are written once, into the row below (F_ROWREGS);
+      // GZ and Yaw (the row carries them as the tick's floats), TEMP and VERSION go to sReg
       int16_t *reg = a.reg;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        reg[(R_AX + k) * n + i] = (int16_t)sw[0][k];
-        reg[(R_GX + k) * n + i] = (int16_t)sw[1][k];
-        reg[(R_ROLL + k) * n + i] = (int16_t)sw[2][k];
-      }
+      reg[R_GZ * n + i] = (int16_t)sw[1][2];
+      reg[R_YAW * n + i] = (int16_t)sw[2][2];
       reg[R_TEMP * n + i] = (int16_t)sw[0][3];
       reg[R_VERSION * n + i] = (int16_t)sw[2][3];
-#pragma unroll
-      for (int k = 0; k < 4; k++) reg[(R_Q0 + k) * n + i] = (int16_t)sw[3][k];
       ps.flags |= flags_of(R_AX, 3) | flags_of(R_TEMP, 1) | flags_of(R_GX, 3) | flags_of(R_ROLL, 3) |
                   flags_of(R_VERSION, 1) | flags_of(R_Q0, 4);
     } else if (fast) {
@@ -286,12 +317,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   } else {
     for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);
   }
+  // any other poll worked on the register file itself: the row-resident registers its frames did
+  // not write are brought back from the row now (after the parse, when the poll row's registers
+  // are dead; frames only write registers, so the order is immaterial).  Rare: a damaged or
+  // non-standard poll
+  if (!std4 && row_regs) row_regs_out(a.snap, a.reg, n, i, ps.roww);
   uint64_t lo = ps.lo, hi = ps.hi;
   uint32_t cnt = ps.cnt, flags = ps.flags;
   // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
   const bool ok = (flags & F_QUAT) != 0;
   if (ok) flags = 0;
   a.err[i] = ok ? 0 : 1;
+  // the standard poll (always a successful one) leaves its row-resident registers in the row
+  if (std4) flags |= F_ROWREGS;
   if (cnt_in != 0 || cnt != 0) {
     a.parser[i] = (uint32_t)lo;
     a.parser[n + i] = (uint32_t)(lo >> 32);
@@ -343,6 +381,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   uint4 *row = reinterpret_cast<uint4 *>(a.snap + (uint64_t)kSnapWords * i);
   row[0] = make_uint4(u(ra[0], ra[1]), u(ra[2], rg[0]), u(rg[1], rm[0]), u(rm[1], rm[2]));
   row[1] = make_uint4(u(rr[0], rr[1]), u(rq[0], rq[1]), u(rq[2], rq[3]), snapf);
+}
+
+// the register file made whole (fmskf_get_imu_regs, a checkpoint): robots whose row-resident
+// registers live in their snapshot row (F_ROWREGS) get them written back into sReg
+__global__ __launch_bounds__(kBlock) void k_wt901_regs_sync(const int16_t *snap, int16_t *reg, uint8_t *flags,
+                                                            uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = flags[i];
+  if (!(f & F_ROWREGS)) return;
+  row_regs_out(snap, reg, n, i);
+  flags[i] = (uint8_t)(f & ~F_ROWREGS);
+}
+
+int launch_wt901_regs_sync(const DevState &s, hipStream_t st) {
+  if (s.n == 0 || !s.imu_reg) return 0;
+  k_wt901_regs_sync<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_reg,
+                                                                                      s.imu_flags, s.n);
+  return (int)hipGetLastError();
 }
 
 // IMU_IF::Data [16][N] of every robot from its snapshot (fmskf_get_imu): zeros until the first

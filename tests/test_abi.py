@@ -230,3 +230,39 @@ def test_rccl_override_refused_before_load(tmp_path):
                          env=dict(os.environ, FMSKF_RCCL_LIBRARY=str(so)))
     assert "before ''" in out.stdout and "refused 4" in out.stdout, out.stdout + out.stderr
     assert not marker.exists(), "the refused library's constructor ran"
+
+
+def test_rccl_override_malformed_elf_refused(tmp_path):
+    """the ELF check that vets a FMSKF_RCCL_LIBRARY file reads every extent against the file size
+    field by field: a truncated file and headers whose section offsets sit near 2^64 (so an
+    offset + size sum would wrap past the check) are refused as FMSKF_ERCCL, without reading out
+    of bounds or crashing the process"""
+    import struct
+    import subprocess
+    import sys
+    loop = os.path.join(ROOT, "build", "libloopback_rccl.so")
+    assert os.path.exists(loop), "build() makes build/libloopback_rccl.so"
+    img = bytearray(open(loop, "rb").read())
+    e_shoff, = struct.unpack_from("<Q", img, 0x28)
+    e_shnum, = struct.unpack_from("<H", img, 0x3C)
+    cases = {"truncated": bytes(img[: len(img) // 3])}
+    wrap = bytearray(img)  # e_shoff near 2^64: e_shoff + e_shnum * 64 wraps to a small number
+    struct.pack_into("<Q", wrap, 0x28, (1 << 64) - 64 * max(e_shnum, 1) + 8)
+    cases["shoff_wraps"] = bytes(wrap)
+    sect = bytearray(img)  # every section's offset near 2^64 with a size that wraps the sum
+    for k in range(e_shnum):
+        base = e_shoff + 64 * k
+        struct.pack_into("<Q", sect, base + 0x18, (1 << 64) - 16)   # sh_offset
+        struct.pack_into("<Q", sect, base + 0x20, 32)               # sh_size
+    cases["sh_offset_wraps"] = bytes(sect)
+    pkg = os.path.join(ROOT, "roboken-fmskf-robot-controller_amd")
+    script = ("import sys\nsys.path.insert(0, sys.argv[1])\nimport fmskf\n"
+              "try:\n    fmskf.comm_unique_id()\n    print('ok')\n"
+              "except fmskf.FmskfError as e:\n    print('refused', e.code, e)\n")
+    for name, data in cases.items():
+        so = tmp_path / f"lib_{name}.so"
+        so.write_bytes(data)
+        out = subprocess.run([sys.executable, "-c", script, pkg], capture_output=True, text=True, timeout=120,
+                             env=dict(os.environ, FMSKF_RCCL_LIBRARY=str(so), LOOPBACK_RCCL_DIR="/tmp"))
+        assert out.returncode == 0, (name, out.returncode, out.stderr)
+        assert out.stdout.startswith("refused 4") and "fmskf_rccl_stand_in" in out.stdout, (name, out.stdout)

@@ -32,6 +32,9 @@ CASES = [("kf6", 4099, 40), ("kf6", 1, 20), ("kf6libm", 777, 20), ("kf6mask", 10
          ("kf6", (1 << 20) + 17, 3), ("rs", (1 << 20) + 17, 3)]
 
 
+FALLBACK = ("kf6rpm", "kf6rec", "rssum", "ekf9rpm")
+
+
 @pytest.mark.parametrize("case,n,T", CASES)
 def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
     import torch
@@ -97,6 +100,15 @@ def test_isr_tick_can_equals_ingest_then_isr(case, n, T):
         xb, Pb = b.get_state()
         ga, gb = a.get_ctrl(), b.get_ctrl()
         ma, mb = a.get_motors(), b.get_motors()
+        ca, cb = a.get_counters(), b.get_counters()
+    # which launch form ran (fmskf_get_counters [1]: CAN RX as its own kernel, [2]: the ISR as
+    # three kernels): the fused cases really ran one kernel per tick, the documented fallbacks
+    # (a caller rpm / records / sums) ran the two calls every tick
+    if case in FALLBACK:
+        assert ca[1] == T, (case, ca[:3])
+    else:
+        assert ca[1] == 0 and ca[2] == 0, (case, ca[:3])
+    assert cb[1] == 0 and cb[2] == ca[2], (case, ca[:3], cb[:3])
     np.testing.assert_array_equal(bits(xa), bits(xb))
     if Pa is not None:
         np.testing.assert_array_equal(bits(Pa), bits(Pb))
@@ -123,3 +135,126 @@ def test_isr_tick_can_errors():
             e.isr_tick_can(f, s, out=torch.empty((n, 8), dtype=torch.uint8, device="cuda"))
         with pytest.raises(ValueError):  # short CAN arrays are caught before the C call
             e.isr_tick_can(f[: n // 2], s)
+
+
+def test_isr_tick_can_kf12d_counts_three_kernels():
+    """KF12D has no fused ISR: fmskf_isr_tick_can runs CAN RX, the tick, the control step and the
+    frame as separate kernels, and the handle's counters say so"""
+    n, T = 300, 3
+    tr = Trajectory(n, T, seed=5)
+    z = tr.kf12d_z()
+    with Engine("kf12d", n) as e:
+        for t in range(T):
+            f, s = tr.can_frames(t)
+            e.isr_tick_can(f, s, frames=False, z=z[t])
+        c = e.get_counters()
+    assert c[1] == T and c[2] == T, c[:3]
+
+
+# the scripted sequence of test_rs_prev_in_motor_sums: every transition of where the RS
+# odometry's previous sums live (fmskf_ctx rs_prev_synced / rs_prev_stale)
+RS_OPS = (["fused"] * 3 + ["prev"] + ["split"] + ["fused"] * 2 + ["caller_sums"] + ["fused"] * 2 + ["ckpt"]
+          + ["fused"] * 2 + ["graph"] + ["fused"] + ["predict_only"] + ["fused"] * 2 + ["prev", "fused", "reset"]
+          + ["fused"] * 3 + ["ingest_only", "fused", "fused", "prev"])
+
+
+def test_rs_prev_in_motor_sums(orc, tmp_path):
+    """fmskf_isr_tick_can, reference semantics: once the last predict read the motor state's sums,
+    the fused kernel takes the previous sums (s64_rawAngleSumPrev) from the motor state and skips
+    the prev planes (k_isr_rs PS); every other reader / writer brings them back first.  A scripted
+    mix of fused ticks, the two-call form, a tick on caller sums, a checkpoint round trip, a graph
+    capture and replay, a predict on the motor sums, a stand-alone CAN RX and a reset, against the
+    oracle (orc_m2006_rx + orc_rs_tick, VD_motor_if_m2006.cpp:32-72, VD_vehicle_controller.cpp:
+    36-51): the pose after every step and the previous sums at the `prev` steps, bit for bit."""
+    import torch
+    n = 1001
+    T = len(RS_OPS) + 2
+    tr = Trajectory(n, T, seed=77)
+    yaw = tr.kf6_inputs()[0]
+    csum = tr.rs_inputs()[1]  # [T][4][N] sums unrelated to the motor state's
+    rpm_c = tr.rs_inputs()[2]
+    mb = orc.MotorBatch(n)
+    pos, vel, prev = np.zeros((3, n), np.float32), np.zeros((3, n), np.float32), np.zeros((4, n), np.int64)
+    prev_stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # graph capture needs a real stream; the copies below queue on it too
+    torch.cuda.set_stream(stream)
+    e = Engine("rs", n)
+    e.set_stream(stream)
+
+    def oracle_tick(t, sums=None, rpm=None, correct=True):
+        r = mb.field("rpm") if rpm is None else rpm
+        s = np.ascontiguousarray(mb.field("angle_sum").T) if sums is None else np.ascontiguousarray(sums)
+        orc.rs_tick(pos, vel, prev, yaw[t], s, r, do_correct=correct)
+
+    t = 0
+    try:
+        for op in RS_OPS:
+            f, s = tr.can_frames(t)
+            if op == "fused":
+                e.isr_tick_can(f, s, frames=False, yaw_deg=yaw[t])
+                mb.rx(f, s)
+                oracle_tick(t)
+            elif op == "split":
+                e.ingest_can(f, s)
+                e.isr_tick(frames=False, yaw_deg=yaw[t])
+                mb.rx(f, s)
+                oracle_tick(t)
+            elif op == "caller_sums":  # the odometry on the caller's sums: prev = those
+                e.ingest_can(f, s)
+                e.tick(yaw_deg=yaw[t], angle_sum=csum[t], rpm=rpm_c[t])
+                mb.rx(f, s)
+                oracle_tick(t, csum[t], rpm_c[t])
+            elif op == "predict_only":  # predict on the motor state's sums (no correct)
+                e.ingest_can(f, s)
+                e.predict()
+                mb.rx(f, s)
+                oracle_tick(t, correct=False)
+            elif op == "ingest_only":  # CAN RX with no tick: the motor sums move ahead of prev
+                e.ingest_can(f, s)
+                mb.rx(f, s)
+                t += 1
+                continue
+            elif op == "ckpt":
+                path = str(tmp_path / "rs.ck")
+                e.save_state(path)
+                e.close()
+                e = Engine("rs", n)
+                e.set_stream(stream)
+                e.load_state(path)
+                e.isr_tick_can(f, s, frames=False, yaw_deg=yaw[t])
+                mb.rx(f, s)
+                oracle_tick(t)
+            elif op == "graph":  # capture one fused call on device buffers, replay it twice
+                fd = torch.from_numpy(np.ascontiguousarray(f)).cuda()
+                sd = torch.from_numpy(np.ascontiguousarray(s)).cuda()
+                yd = torch.from_numpy(np.ascontiguousarray(yaw[t])).cuda()
+                e.graph_begin()
+                e.isr_tick_can(fd, sd, frames=False, yaw_deg=yd)
+                e.graph_end()
+                for k in range(2):
+                    f2, s2 = tr.can_frames(t + k)
+                    fd.copy_(torch.from_numpy(np.ascontiguousarray(f2)))
+                    sd.copy_(torch.from_numpy(np.ascontiguousarray(s2)))
+                    yd.copy_(torch.from_numpy(np.ascontiguousarray(yaw[t + k])))
+                    e.graph_launch(1)
+                    mb.rx(f2, s2)
+                    oracle_tick(t + k)
+                t += 1
+            elif op == "reset":
+                e.reset()
+                mb = orc.MotorBatch(n)
+                pos[:], vel[:], prev[:] = 0, 0, 0
+                t += 1
+                continue
+            elif op == "prev":
+                np.testing.assert_array_equal(e.get_prev_sum(), prev, err_msg=f"previous sums after tick {t}")
+                continue
+            x, _ = e.get_state()
+            np.testing.assert_array_equal(bits(x[:3]), bits(pos), err_msg=f"pose after {op} at tick {t}")
+            np.testing.assert_array_equal(bits(x[3:]), bits(vel), err_msg=f"velocity after {op} at tick {t}")
+            t += 1
+        m = e.get_motors()
+        np.testing.assert_array_equal(m["angle_sum"], mb.field("angle_sum").T)
+    finally:
+        e.close()
+        torch.cuda.set_stream(prev_stream)

@@ -243,3 +243,116 @@ def test_firmware_pipeline_60000_ticks(orc, model):
             np.testing.assert_array_equal(m["angle_sum"], mb.field("angle_sum").T, err_msg=f"angle sums at tick {t}")
             np.testing.assert_array_equal(m["rpm"], mb.field("rpm"), err_msg=f"rpm at tick {t}")
         assert e.get_counters()[0] == 0
+
+
+def _motor_state(e, mb, t):
+    """the whole C610 state (MOTOR_IF_M2006, VD_motor_if_m2006.cpp:32-72) against the oracle's:
+    the int64 angle sums, every Status field (get_status_latest) incl. the IIR speed"""
+    m = e.get_motors()
+    st = e.get_motor_status()
+    np.testing.assert_array_equal(m["angle_sum"], mb.field("angle_sum").T, err_msg=f"angle sums at tick {t}")
+    for k, f in (("microsec_id", "micro"), ("angle", "angle"), ("rpm", "rpm"), ("curr", "curr")):
+        np.testing.assert_array_equal(st[k], mb.field(f), err_msg=f"{k} at tick {t}")
+    _bits(st["dlt_out_angle_rad"], mb.field("dlt_out_angle_rad"), "flt_dltOutAngle_rad", t)
+    _bits(st["speed_radps"], mb.field("speed_radps"), "flt_SpeedRadPS", t)
+
+
+@pytest.mark.parametrize("model", ["rs", "kf6", "ekf9"])
+def test_isr_tick_can_firmware_60000_ticks(orc, model):
+    """The default firmware call, fmskf_isr_tick_can (the millisecond's four C610 rx_callbacks and
+    the whole ISR, can_tx_routine_intr, VD_task_main.cpp:366-372, in ONE kernel: k_isr_rs /
+    k_isr_kf6 / k_isr_ekf9 with the C610 lane in front), over BASELINE configs[0]'s horizon
+    against the oracle directly -- not against the library's own two-call path.  2048 robots,
+    device-resident CAN frames every tick, a 44-byte WT901 poll every 10 ticks (RS, KF6: the
+    tick reads the ingested yaw / gyro page; EKF9 reads its raw record), power and target events
+    every few seconds.  At every 1000th tick, bit for bit: the motor state (orc_m2006_rx), the
+    estimator state (orc_rs_tick / kf6_tick / ekf9_tick), the control state and currents
+    (CtrlBatch) and the 0x200 frames (orc_can_tx).  The handle's launch-form counters show every
+    tick ran as the one fused kernel."""
+    import torch
+    n = 2048
+    rng = np.random.default_rng(0xF05ED ^ len(model))
+    tr = Trajectory(n, CHUNK, seed=0x464D534B ^ 31)
+    frames = np.stack([tr.can_frames(k)[0] for k in range(CHUNK)])          # [T, N, 4, 8]
+    frames_d = torch.from_numpy(frames).cuda()
+    wb, mb, ref = orc.Wt901Batch(n), orc.MotorBatch(n), orc.CtrlBatch(n)
+    if model == "ekf9":
+        raw = tr.ekf9_raw()
+        raw_d = torch.from_numpy(raw).cuda()
+        cfg = fmskf.default_config("ekf9", n)
+        prm = orc.ekf9_params(cfg.dt, np.array(cfg.q[:45]), np.array(cfg.r[:21]), orc.TRIG_TABLE512)
+        xo = np.zeros((10, n), np.float32)  # row 9: the heading's low part
+        Po = np.repeat(np.float32(np.array(cfg.p0[:45]))[:, None], n, 1).copy()
+    else:
+        polls = [tr.wt901_poll_rows(k) for k in range(0, CHUNK, 10)]
+        polls_d = [(torch.from_numpy(r).cuda(), torch.from_numpy(ln).cuda()) for r, ln in polls]
+        if model == "rs":
+            pos, vel = np.zeros((3, n), np.float32), np.zeros((3, n), np.float32)
+            prev = np.zeros((4, n), np.int64)
+        else:
+            cfg = fmskf.default_config("kf6", n)
+            prm = orc.kf6_params(cfg.dt, np.array(cfg.q[:21]), np.array(cfg.r[:10]), orc.TRIG_TABLE512)
+            xo = np.zeros((6, n), np.float32)
+            Po = np.repeat(np.float32(np.array(cfg.p0[:21]))[:, None], n, 1).copy()
+    out_d = torch.empty((n, 8), dtype=torch.uint8, device="cuda")
+    with Engine(model, n) as e:
+        e.set_stream(torch.cuda.current_stream())
+        for t0 in range(0, T_LONG, CHUNK):
+            if t0 % 6000 == 0:  # new targets (C_ACCEL / JERK_MAX_MOVE, VD_task_main.cpp:29-38)
+                vel_t = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                                  rng.uniform(-6 * np.pi, 6 * np.pi, n)]).astype(np.float32)
+                acl = np.array([[1000.0], [1000.0], [30.0]], np.float32).repeat(n, 1)
+                jrk = np.array([[10000.0], [10000.0], [300.0]], np.float32).repeat(n, 1)
+                e.set_target_vel(vel_t, acl, jrk)
+                ref.set_target_vel(vel_t, acl, jrk)
+            if t0 % 9000 == 0:  # power: most robots on, some off, changing every 9 s
+                on = (rng.random(n) < 0.85).astype(np.uint8)
+                e.set_power(on)
+                ref.set_power(on)
+            g = t0 + np.arange(CHUNK)
+            stamps = (((g[:, None, None] + 1) * 1000 + np.arange(4)[None, None, :] * 7) & 0x7FFF).astype(np.int16)
+            stamps = np.ascontiguousarray(np.broadcast_to(stamps, (CHUNK, n, 4)))
+            stamps_d = torch.from_numpy(stamps).cuda()
+            for k in range(CHUNK):
+                t = t0 + k
+                if model != "ekf9" and k % 10 == 0:  # the IMU task's 10 ms poll
+                    rows_d, lens_d = polls_d[k // 10]
+                    e.ingest_wt901(rows_d, lens_d, latch_qinit=(t == 0))
+                    wb.update(*polls[k // 10], latch_qinit=(t == 0))
+                last = k == CHUNK - 1
+                kw = dict(raw=raw_d[k]) if model == "ekf9" else {}
+                e.isr_tick_can(frames_d[k], stamps_d[k], frames=last, out=out_d if last else None, **kw)
+                mb.rx(frames[k], stamps[k])
+                rpm = mb.field("rpm")
+                if model == "rs":
+                    d = wb.data
+                    orc.rs_tick(pos, vel, prev, np.ascontiguousarray(d[11]),
+                                np.ascontiguousarray(mb.field("angle_sum").T), rpm)
+                elif model == "kf6":
+                    d = wb.data
+                    orc.kf6_tick(xo, Po, np.ascontiguousarray(d[11]), np.ascontiguousarray(d[5]), rpm, None, prm,
+                                 nthreads=0)
+                else:
+                    orc.ekf9_tick(xo, Po, raw[k], None, prm, nthreads=0)
+                ref.step(rpm)
+            t = t0 + CHUNK - 1
+            x, P = e.get_state()
+            if model == "rs":
+                _bits(x[:3], pos, "pose", t)
+                _bits(x[3:], vel, "velocity", t)
+                np.testing.assert_array_equal(e.get_prev_sum(), prev, err_msg=f"previous sums at tick {t}")
+            else:
+                _bits(x, xo[:x.shape[0]], "x", t)
+                _bits(P, Po, "P", t)
+            _motor_state(e, mb, t)
+            gc = e.get_ctrl()
+            cur = ref.curr()
+            np.testing.assert_array_equal(gc["curr"], cur, err_msg=f"currents at tick {t}")
+            _bits(gc["wheel_ctrl"], ref.wheel("ctrl"), "FF_PI_D output", t)
+            _bits(gc["wheel_tgt"], ref.wheel("tgt"), "FF_PI_D target", t)
+            _bits(gc["vel_tgt"], ref.vel_tgt(), "velocity target", t)
+            np.testing.assert_array_equal(out_d.cpu().numpy(), orc.can_tx(cur), err_msg=f"0x200 frames at tick {t}")
+        c = e.get_counters()
+        assert c[0] == 0, c[:3]
+        assert c[1] == 0 and c[2] == 0, f"not every tick ran as the fused kernel: {c[:3]}"
+    assert np.abs(cur).max() > 0  # the loops drove the wheels

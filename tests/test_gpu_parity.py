@@ -556,7 +556,10 @@ def test_wt901_data_page_across_latches(orc, stride):
     5): after EVERY poll it equals the oracle's eagerly written page bit for bit -- before the
     first successful poll (all zeros), on the poll that latches q_init (its page uses the OLD
     q_init, kept as qprev), on the polls after it, across a second latch, and for robots whose
-    poll failed (the page of their last success stays).  VehicleInfo reads the same page."""
+    poll failed (the page of their last success stays).  VehicleInfo reads the same page.  The
+    register file too, on every third poll: the standard poll writes eleven registers into the
+    snapshot row only (round 6), and a failed poll, a 0x5F register reply (Q0-Q3) or another
+    frame mix after it must see them (wit_c_sdk.c:90-130)."""
     n, polls = 1537, 9
     rng = np.random.default_rng(41 + stride)
     orcs = [orc.Wt901(0x51) for _ in range(n)]
@@ -573,6 +576,8 @@ def test_wt901_data_page_across_latches(orc, stride):
                     ts = (0x51, 0x52, 0x53, 0x59)
                 elif r < 0.85:  # no quaternion frame: the poll fails, the page stays
                     ts = (0x51, 0x53)
+                elif r < 0.92:  # a register-read reply (0x5F at imu_read_reg 0x51: Q0-Q3) alone
+                    ts = (0x5F,)
                 else:  # a quaternion frame among others, through the parser
                     ts = (0x54, 0x59, 0x52)
                 b = np.frombuffer(b"".join(wt901_frame(t, rng.integers(0, 65536, 4)) for t in ts), np.uint8)
@@ -584,6 +589,12 @@ def test_wt901_data_page_across_latches(orc, stride):
             for i in range(n):
                 assert err[i] == orcs[i].is_error
                 bits_equal(data[:, i], orcs[i].data, f"data {i} poll {k}")
+            if k % 3 == 1:  # the register file (round 6: the standard poll keeps eleven of its
+                # registers in the snapshot row only; the readout writes them back), on some polls,
+                # so that later polls also start from row-resident registers
+                regs, _ = e.get_imu_regs()
+                for i in range(0, n, 3):
+                    np.testing.assert_array_equal(regs[:, i], orcs[i].regs, err_msg=f"regs {i} poll {k}")
         vi = e.export_vehicle_info()
     for i in range(0, n, 5):
         d = orcs[i].data

@@ -34,6 +34,8 @@ def main():
                     help="KF6 tick with host-resident inputs staged over PCIe per call")
     ap.add_argument("--valid", action="store_true", help="a validity mask per tick (9 in 10 robots valid)")
     ap.add_argument("--comp", action="store_true", help="KF6 with FMSKF_CFG_COMP_POS (compensated positions)")
+    ap.add_argument("--comm", action="store_true",
+                    help="--op ens_async: a world-1 RCCL communicator on the handle (fmskf_comm_init)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -157,13 +159,18 @@ def main():
             while pend:
                 e.ensemble_end()
                 pend -= 1
+        if args.comm:  # the real RCCL at world 1: the side-stream exchange of every result
+            e.comm_init(fmskf.comm_unique_id(), 0, 1)
+            res["comm"] = fmskf.rccl_library()
         for kind in ("tick", "tick_ev", "tick_ev3", "tick_evnf", "sync", "async", "async3") * 2:
             loop(kind, 8)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             loop(kind, args.ticks)
+            t1 = time.perf_counter()  # the host's submission of every call (and the result waits)
             torch.cuda.synchronize()
             res[kind + "_us"] = min(res.get(kind + "_us", 1e9), (time.perf_counter() - t0) * 1e6 / args.ticks)
+            res[kind + "_host_us"] = min(res.get(kind + "_host_us", 1e9), (t1 - t0) * 1e6 / args.ticks)
         # the bench's K = 16 region shape: 20 ticks, one event at tick 10, its result collected
         # at the end (end() then synchronize, or synchronize then end()), against 20 plain ticks
         def region(kind):

@@ -682,6 +682,92 @@ __global__ __launch_bounds__(256) void k_mix_wt901_pair(const uint4 *rows, const
     reinterpret_cast<float2 *>(data + k * n)[j] = make_float2(q[k & 3].x + (float)(m & 7) * (float)k, q[k & 3].y);
 }
 
+// round 6 probes (membench LG 1 r6): the RS tick and CAN RX byte mixes at the kernels' exact
+// access widths, with the int64 encoder sums / previous sums as [4][pitch] planes (8-byte
+// accesses, one per wheel) against [N][4] rows (two 16-byte accesses per robot).  RS: yaw f32,
+// rpm u64 and the four sums from a 16-slot ring (SUMROWS: rows; else planes at sum pitch sp);
+// px, py read, six state floats written, prev (PREVROWS: rows) read and written.  140 B.
+template <bool SUMROWS, bool PREVROWS>
+__global__ __launch_bounds__(256) void k_rsmix(float *x, int64_t *prev, const float *yaw, const uint64_t *rpm,
+                                               const int64_t *sums, uint64_t n, uint64_t pp, uint64_t sp) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t sm[4], pv[4];
+  if constexpr (SUMROWS) {
+    const longlong2 a = reinterpret_cast<const longlong2 *>(sums)[2 * i], b = reinterpret_cast<const longlong2 *>(sums)[2 * i + 1];
+    sm[0] = a.x, sm[1] = a.y, sm[2] = b.x, sm[3] = b.y;
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; w++) sm[w] = __builtin_nontemporal_load(sums + w * sp + i);
+  }
+  const float y = __builtin_nontemporal_load(yaw + i);
+  const uint64_t r = __builtin_nontemporal_load(rpm + i);
+  const float px = x[i], py = x[pp + i];
+  if constexpr (PREVROWS) {
+    const longlong2 a = reinterpret_cast<const longlong2 *>(prev)[2 * i], b = reinterpret_cast<const longlong2 *>(prev)[2 * i + 1];
+    pv[0] = a.x, pv[1] = a.y, pv[2] = b.x, pv[3] = b.y;
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; w++) pv[w] = prev[w * pp + i];
+  }
+  float d = y + (float)(r & 7);
+#pragma unroll
+  for (int w = 0; w < 4; w++) d += (float)(sm[w] - pv[w]);
+  x[i] = px + d;
+  x[pp + i] = py - d;
+#pragma unroll
+  for (int k = 2; k < 6; k++) x[k * pp + i] = d * (float)k;
+  if constexpr (PREVROWS) {
+    reinterpret_cast<longlong2 *>(prev)[2 * i] = make_longlong2(sm[0], sm[1]);
+    reinterpret_cast<longlong2 *>(prev)[2 * i + 1] = make_longlong2(sm[2], sm[3]);
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; w++) prev[w * pp + i] = sm[w];
+  }
+}
+
+// CAN RX (k_can4's accesses, 216 B): the robot's 32 frame bytes (two 16-byte loads) and four
+// stamps (8 B) from a 16-slot ring; micro, angle, previous angle, previous micro ([N][4] int16,
+// 8 B each) and the IIR output ([N][4] f32, 16 B) read and written; the four int64 sums read
+// and written (SUMROWS: two 16-byte accesses each way, else four [4][pp] planes); rpm and curr
+// ([N][4] int16) written
+template <bool SUMROWS>
+__global__ __launch_bounds__(256) void k_canmix(const uint4 *frames, const uint64_t *stamps, uint64_t *st16,
+                                                uint4 *iir, int64_t *sums, uint64_t n, uint64_t pp) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint4 f0 = frames[2 * i], f1 = frames[2 * i + 1];
+  const uint64_t stp = __builtin_nontemporal_load(stamps + i);
+  uint64_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) v[k] = st16[k * n + i];
+  uint4 y = iir[i];
+  int64_t sm[4];
+  if constexpr (SUMROWS) {
+    const longlong2 a = reinterpret_cast<const longlong2 *>(sums)[2 * i], b = reinterpret_cast<const longlong2 *>(sums)[2 * i + 1];
+    sm[0] = a.x, sm[1] = a.y, sm[2] = b.x, sm[3] = b.y;
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; w++) sm[w] = sums[w * pp + i];
+  }
+  const uint32_t m = f0.x ^ f0.y ^ f0.z ^ f0.w ^ f1.x ^ f1.y ^ f1.z ^ f1.w ^ (uint32_t)stp;
+#pragma unroll
+  for (int w = 0; w < 4; w++) sm[w] += (int16_t)(m >> (4 * w));
+  y.x ^= m;
+  iir[i] = y;
+#pragma unroll
+  for (int k = 0; k < 4; k++) st16[k * n + i] = v[k] ^ (uint64_t)m;
+  st16[4 * n + i] = (uint64_t)m * 3u;
+  st16[5 * n + i] = (uint64_t)m * 5u;
+  if constexpr (SUMROWS) {
+    reinterpret_cast<longlong2 *>(sums)[2 * i] = make_longlong2(sm[0], sm[1]);
+    reinterpret_cast<longlong2 *>(sums)[2 * i + 1] = make_longlong2(sm[2], sm[3]);
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; w++) sums[w * pp + i] = sm[w];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -718,6 +804,104 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'r' && argv[3][1] == '6') {
+    // membench LG 1 r6: the RS tick and CAN RX mixes with int64 sum planes against [N][4] rows
+    // (k_rsmix, k_canmix), and the KF6 2^24-shape tiled pattern fed a ring of 16-byte records
+    // (`kf6ring`: 1, 4 and 16 ticks of records at LG + 4) -- two passes, random data
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    const uint64_t pp = ((n + 511) / 512) * 512 + 256;
+    constexpr int kRing = 16;
+    float *xs;
+    int64_t *pv, *sm;
+    uint8_t *ring;
+    uint64_t *st16;
+    uint4 *iir;
+    CK(hipMalloc(&xs, 6 * pp * 4));
+    CK(hipMalloc(&pv, 4 * pp * 8));
+    CK(hipMalloc(&sm, 4 * pp * 8));
+    CK(hipMalloc(&st16, 6 * n * 8));
+    CK(hipMalloc(&iir, n * 16));
+    const size_t slot = (size_t)48 * pp;  // RS: yaw 4 + rpm 8 + sums 32 (planes at pitch pp or n); CAN: 40
+    CK(hipMalloc(&ring, kRing * slot));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)xs, 6 * pp, 1);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)pv, 8 * pp, 2);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sm, 8 * pp, 3);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)st16, 12 * n, 4);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)iir, 4 * n, 5);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ring, kRing * slot / 4, 6);
+    CK(hipDeviceSynchronize());
+    int tick = 0;
+    auto tm = [&](const char *name, int bpr, auto launch) {
+      for (int w = 0; w < 2 * kRing; w++) launch(ring + (size_t)(tick++ % kRing) * slot);
+      for (int rep = 0; rep < 2; rep++) {
+        CK(hipEventRecord(f0));
+        for (int it = 0; it < 64; it++) launch(ring + (size_t)(tick++ % kRing) * slot);
+        CK(hipEventRecord(f1));
+        CK(hipEventSynchronize(f1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, f0, f1));
+        const double us = ms * 1e3 / 64;
+        printf("{\"n\": %llu, \"mix\": \"%s\", \"bytes_per_robot\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+               (unsigned long long)n, name, bpr, us, (double)bpr * n / (us * 1e-6) / 1e9);
+      }
+    };
+    const unsigned g1 = (unsigned)((n + 255) / 256);
+    auto rs = [&](auto kern, uint64_t sp) {
+      return [=](uint8_t *in) {
+        kern<<<g1, 256>>>(xs, pv, (const float *)in, (const uint64_t *)(in + 4 * pp), (const int64_t *)(in + 12 * pp),
+                          n, pp, sp);
+      };
+    };
+    for (int rep = 0; rep < 2; rep++) {
+      tm("rs_sums_planes_dense_prev_planes", 140, rs(k_rsmix<false, false>, n));
+      tm("rs_sums_planes_padded_prev_planes", 140, rs(k_rsmix<false, false>, pp));
+      tm("rs_sums_planes_dense_prev_rows", 140, rs(k_rsmix<false, true>, n));
+      tm("rs_sums_planes_padded_prev_rows", 140, rs(k_rsmix<false, true>, pp));
+      tm("rs_sums_rows_prev_planes", 140, rs(k_rsmix<true, false>, n));
+      tm("rs_sums_rows_prev_rows", 140, rs(k_rsmix<true, true>, n));
+      tm("can_sums_planes", 216, [&](uint8_t *in) {
+        k_canmix<false><<<g1, 256>>>((const uint4 *)in, (const uint64_t *)(in + 32 * pp), st16, iir, sm, n, pp);
+      });
+      tm("can_sums_rows", 216, [&](uint8_t *in) {
+        k_canmix<true><<<g1, 256>>>((const uint4 *)in, (const uint64_t *)(in + 32 * pp), st16, iir, sm, n, pp);
+      });
+    }
+    CK(hipFree(xs));
+    CK(hipFree(pv));
+    CK(hipFree(sm));
+    CK(hipFree(st16));
+    CK(hipFree(iir));
+    CK(hipFree(ring));
+    // the KF6 tick's 2^24 pattern (27 tiled non-temporal rows, 2048-wide tiles, 448 FMAs, the
+    // 48 KiB cap) with its 16-byte records taken from a ring of R ticks, as the bench feeds it
+    const uint64_t n6 = n << 4;
+    float *sb;
+    uint4 *rb;
+    CK(hipMalloc(&sb, (size_t)27 * n6 * 4));
+    CK(hipMalloc(&rb, (size_t)16 * n6 * 16));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sb, (uint64_t)27 * n6, 7);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)rb, (uint64_t)16 * n6 * 4, 8);
+    CK(hipDeviceSynchronize());
+    const unsigned g6 = (unsigned)(n6 / 256);
+    for (int rep = 0; rep < 2; rep++)
+      for (int R : {1, 4, 16}) {
+        int k = 0;
+        auto launch = [&] { k_tiled_delay<27, 448, 2048><<<g6, 256, 48 * 1024>>>(sb, rb + (size_t)(k++ % R) * n6, n6, 0.f); };
+        for (int w = 0; w < 3; w++) launch();
+        CK(hipEventRecord(f0));
+        for (int it = 0; it < 16; it++) launch();
+        CK(hipEventRecord(f1));
+        CK(hipEventSynchronize(f1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, f0, f1));
+        const double us = ms * 1e3 / 16;
+        printf("{\"n\": %llu, \"kernel\": \"kf6ring_t2048_fma448_lds48\", \"ring\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+               (unsigned long long)n6, R, us, 232.0 * n6 / (us * 1e-6) / 1e9);
+      }
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'd') {
     // membench LG 1 d: the KF12D-shaped pattern (90 fp64 rows, non-temporal) with fp64 compute
     // phases of increasing length, at 2 blocks per CU (the kernel's 2 waves per SIMD) and uncapped
