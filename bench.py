@@ -338,6 +338,8 @@ def secondary_configs(dev, stream, ticks: int, trig):
     return out
 
 
+# the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20)
+WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 8 + 6 + 32 + 8
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
     # RS tick: pos (x, y) 8 r + (x, y, th) 12 w -- theta is overwritten by the correct, so it is
@@ -347,11 +349,13 @@ PATH_BYTES = {
     "rs_tick_2p20_padded_sums": 140,
     "rs_tick_2p20_device_state": 140,
     # WT901 standard poll: row 48 + len 4, the parser count and update flags 2 r, flags and error
-    # 2 w, 15 registers 30 w, magnetometer 6 r, the snapshot row 32 w (the words updateData
+    # 2 w, 4 registers 8 w (GZ, Yaw, TEMP, VERSION: the other eleven the poll writes live in the
+    # snapshot row, round 6), magnetometer 6 r, the snapshot row 32 w (the words updateData
     # reads: the Data page is formed at readout), yaw and gyro z 8 w; the parser window is empty
     # before and after such a poll, so its words are neither read nor written (round 4: 197 B,
-    # with the window words, q_init read and the 64-byte page written)
-    "wt901_ingest_2p20": 48 + 4 + 2 + 2 + 30 + 6 + 32 + 8,
+    # with the window words, q_init read and the 64-byte page written; round 5: 132 B, the 15
+    # registers written to sReg as well as to the row)
+    "wt901_ingest_2p20": WT901_POLL_BYTES,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
     # output y, int64 sum read and written; rpm and curr written (the speed is the IIR state y;
     # Status's dlt is formed at readout from the angle and the previous one; the IIR input state
@@ -365,7 +369,7 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
+    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + WT901_POLL_BYTES / 10,
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
     # CAN row's 216 + the ISR's 601 without its rpm read
     "isr_can_kf6_2p20": 216 + (232 + 369 - 8 + 8) - 8,
@@ -380,14 +384,15 @@ PATH_BYTES = {
     # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
     "isr_rs_2p20": 140 + 369 - 8 + 8,
     # with the tick's CAN RX fused in: the CAN row's 216, the rpm and the four sums no longer read
-    # back (the CAN lane hands them over in registers)
-    "isr_can_rs_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32,
+    # back (the CAN lane hands them over in registers), and (round 6) the previous sums neither
+    # read nor written while they equal the motor state's stored sums (k_isr_rs PS: 64 B)
+    "isr_can_rs_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 - 64,
     # the reference-semantics firmware loop (VD_task_main.cpp:366-372 with its CAN RX and IMU
     # tasks) on the fused call: CAN RX + the RS ISR in one kernel, a WT901 poll every 10th tick
-    "firmware_loop_rs_fused_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
+    "firmware_loop_rs_fused_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
-    "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + (48 + 4 + 2 + 2 + 30 + 6 + 32 + 8) / 10,
+    "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + WT901_POLL_BYTES / 10,
 }
 
 

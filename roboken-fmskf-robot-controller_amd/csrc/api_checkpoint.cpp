@@ -33,8 +33,13 @@ struct CkHeader {
   uint32_t tile, elem, groups, ctrl_tile;  // ctrl_tile: control arrays' tile width (0 = planar)
   uint64_t m_pitch, ctrl_pitch;            // motor sum planes' pitch, control state's pitch
   uint64_t body_bytes, checksum;           // what follows the header, and its hash
-  uint32_t flags, reserved;                // fmskf_config.flags (FMSKF_CFG_*)
+  uint32_t flags;                          // fmskf_config.flags (FMSKF_CFG_*)
+  // layout bits of format 5 (0 in round-5 files): bit 0, the RS previous sums in 64-robot tiles
+  // of wheel pairs (round 6, lane_rs.hpp rs_prev_at; [4][pitch] planes before), so a round-5 RS
+  // file is refused instead of loaded scrambled
+  uint32_t layout;
 };
+constexpr uint32_t kCkPrevRows = 1u;
 struct CkSection {
   void *dev;
   size_t bytes;
@@ -93,6 +98,7 @@ void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->elem = h->d.elem;
   hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
   hd->m_pitch = plane_pitch(h->s.n);
+  hd->layout = h->s.prev_sum ? kCkPrevRows : 0u;
   const uint64_t w = tile_w_elem(4);
   hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
 }
@@ -231,6 +237,8 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
         hd.tile != me.tile || hd.elem != me.elem || hd.flags != me.flags || (hd.groups & ~15u))
       fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, flags, N or layout)");
     if ((hd.groups & 4) && hd.m_pitch != me.m_pitch) fail(FMSKF_EINVAL, "checkpoint motor layout differs");
+    if (hd.layout != me.layout)
+      fail(FMSKF_EINVAL, "checkpoint layout differs (a round-5 RS file keeps its previous sums as [4][pitch] planes)");
     if ((hd.groups & 8) && (hd.ctrl_tile != me.ctrl_tile || hd.ctrl_pitch != me.ctrl_pitch))
       fail(FMSKF_EINVAL, "checkpoint control layout differs (tiling / pitch)");
     if (!(hd.groups & 1u)) fail(FMSKF_EINVAL, "checkpoint holds no estimator state");

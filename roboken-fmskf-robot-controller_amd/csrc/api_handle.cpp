@@ -149,9 +149,7 @@ void ensure_imu(fmskf_ctx *h) {
 void rs_prev_materialize(fmskf_ctx *h) {
   if (!h->rs_prev_stale) return;
   const DevState &s = h->s;
-  hip_check(hipMemcpy2DAsync(s.prev_sum, s.pitch * 8, s.m_sum, s.m_pitch * 8, s.n * 8, 4, hipMemcpyDeviceToDevice,
-                             h->stream),
-            "previous sums");
+  launch_check(launch_sums_rows(s.m_sum, s.prev_sum, s.n, s.m_pitch, true, h->stream), "previous sums");
   h->rs_prev_stale = false;
 }
 

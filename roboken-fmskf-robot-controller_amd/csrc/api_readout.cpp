@@ -11,9 +11,15 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem) {
   return guarded([&] {
     check_handle(h);
     if (!h->s.prev_sum) fail(FMSKF_ENOTSUP, "prev_sum exists in the RS model only");
-    rs_prev_materialize(h);
     DeviceGuard g(h->cfg.device);
-    copy_planes_out(h, prev, h->s.prev_sum, h->s.n * 8, h->s.pitch * 8, 4, mem);
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
+    rs_prev_materialize(h);
+    if (!prev) return;
+    // the tick's tiled layout on the device -> the ABI's [4][N] planes
+    const uint64_t n = h->s.n;
+    int64_t *dense = mem == FMSKF_MEM_DEVICE ? prev : (int64_t *)h->out_for((size_t)4 * n * 8);
+    launch_check(launch_sums_rows(h->s.prev_sum, dense, n, n, false, h->stream), "previous sums");
+    if (mem == FMSKF_MEM_HOST) copy_out(h, prev, dense, (size_t)4 * n * 8, mem);
     finish_out(h, mem);
   });
 }

@@ -33,7 +33,7 @@ struct DevState {
   // RS: x = (px, py, th, vx, vy, vth) floats
   void *x = nullptr;
   void *P = nullptr;
-  int64_t *prev_sum = nullptr;  // RS: s64_rawAngleSumPrev [4][N]
+  int64_t *prev_sum = nullptr;  // RS: s64_rawAngleSumPrev, 64-robot tiles of wheel pairs (lane_rs.hpp rs_prev_at)
   float *thlo = nullptr;        // EKF9: the heading's low part [N] (compensated heading)
   // KF6 with FMSKF_CFG_COMP_POS: the low parts of px, py, P[0][0], P[1][0], P[1][1], tiled like
   // x and P ([N/2048][5][2048])
@@ -367,6 +367,9 @@ int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, 
 int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
                         const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
                         const int8_t dir[4], hipStream_t st);
+// RS previous sums: the tick's tiled layout (lane_rs.hpp rs_prev_at) <-> [4][pitch] planes
+// (to_rows: planes -> tiles)
+int launch_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch, bool to_rows, hipStream_t st);
 // the WT901 register file made whole: the row-resident registers written back from the
 // snapshot rows of the robots whose standard poll kept them there (kernels_ingest.hip F_ROWREGS)
 int launch_wt901_regs_sync(const DevState &s, hipStream_t st);

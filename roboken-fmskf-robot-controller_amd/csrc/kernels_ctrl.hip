@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, cons
 struct IsrRsArgs {
   uint64_t pitch;
   float *x;
-  int64_t *prev;
+  int64_t *prev;  // [N][4] rows
   const float *yaw_deg;
   const int16_t *rpm;
   const int64_t *angle_sum;  // [4][sum_pitch]
@@ -101,10 +101,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   s.px = a.x[i];
   s.py = a.x[pp + i];
   s.th = 0.f;  // overwritten by the correct step
-  if constexpr (!PS) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
-  }
+  if constexpr (!PS) rs_prev_load(a.prev, i, s.prev);
   const float yaw = a.yaw_deg[i];
   uint2 rw;
   int64_t sum[4];
@@ -132,10 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   a.x[3 * pp + i] = s.vx;
   a.x[4 * pp + i] = s.vy;
   a.x[5 * pp + i] = s.vth;
-  if constexpr (!PS) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
-  }
+  if constexpr (!PS) rs_prev_store(a.prev, i, s.prev);
   if (a.frames) reinterpret_cast<uint2 *>(a.frames)[i] = tx_frame(cw);
 }
 

@@ -13,6 +13,7 @@
 
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
+#include "lane_rs.hpp"
 #include "ens_device.hpp"
 
 #pragma clang fp contract(off)
@@ -238,6 +239,35 @@ int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint3
   const dim3 g((unsigned)((n + kBlock - 1) / kBlock), rows);
   if (elem == 8) k_retile<double, false><<<g, kBlock, 0, st>>>((const double *)dense, (double *)tiled, rows, n);
   else k_retile<float, false><<<g, kBlock, 0, st>>>((const float *)dense, (float *)tiled, rows, n);
+  return (int)hipGetLastError();
+}
+
+// RS s64_rawAngleSumPrev in the tick's layout (64-robot tiles of 16-byte wheel pairs,
+// lane_rs.hpp rs_prev_at) <-> [4][pitch] int64 planes (the motor state's sums, the ABI's [4][N]
+// readout).  Grid-stride.
+template <bool TO_ROWS>
+__global__ __launch_bounds__(kBlock) void k_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    if constexpr (TO_ROWS) {
+      reinterpret_cast<longlong2 *>(dst)[rs_prev_at(i, 0)] = make_longlong2(src[i], src[pitch + i]);
+      reinterpret_cast<longlong2 *>(dst)[rs_prev_at(i, 1)] = make_longlong2(src[2 * pitch + i], src[3 * pitch + i]);
+    } else {
+      const longlong2 a = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 0)];
+      const longlong2 b = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 1)];
+      dst[i] = a.x;
+      dst[pitch + i] = a.y;
+      dst[2 * pitch + i] = b.x;
+      dst[3 * pitch + i] = b.y;
+    }
+  }
+}
+
+int launch_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch, bool to_rows, hipStream_t st) {
+  if (n == 0) return 0;
+  const uint64_t b = (n + kBlock - 1) / kBlock;
+  const dim3 g((unsigned)(b < (1u << 20) ? b : (1u << 20)));
+  if (to_rows) k_sums_rows<true><<<g, kBlock, 0, st>>>(src, dst, n, pitch);
+  else k_sums_rows<false><<<g, kBlock, 0, st>>>(src, dst, n, pitch);
   return (int)hipGetLastError();
 }
 

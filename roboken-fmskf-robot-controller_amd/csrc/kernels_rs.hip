@@ -20,9 +20,9 @@ namespace fmskf {
 
 struct RsArgs {
   uint64_t n;
-  uint64_t pitch;    // plane pitch of x and prev (elements)
+  uint64_t pitch;    // plane pitch of x (elements)
   float *x;          // [6][pitch]: px, py, th, vx, vy, vth
-  int64_t *prev;     // [4][pitch]
+  int64_t *prev;     // 64-robot tiles of 16-byte wheel pairs (lane_rs.hpp rs_prev_at)
   TickIn in;
 };
 
@@ -36,10 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   s.py = a.x[pp + i];
   s.th = CORR ? 0.f : a.x[2 * pp + i];  // correct overwrites theta before any use
   s.vx = s.vy = s.vth = 0.f;
-  if (PRED) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) s.prev[w] = a.prev[w * pp + i];
-  }
+  if (PRED) rs_prev_load(a.prev, i, s.prev);
   const uint64_t st = a.in.stride;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t j = (uint64_t)t * st + i;
@@ -60,8 +57,7 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
     a.x[3 * pp + i] = s.vx;
     a.x[4 * pp + i] = s.vy;
     a.x[5 * pp + i] = s.vth;
-#pragma unroll
-    for (int w = 0; w < 4; w++) a.prev[w * pp + i] = s.prev[w];
+    rs_prev_store(a.prev, i, s.prev);
   }
   if (CORR) a.x[2 * pp + i] = s.th;
 }
@@ -129,18 +125,24 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     if (i >= n) return;
     RsLane s;
     constexpr int SP = st_pol(CP);
-    const auto rx = rsrc_span(a.x + hb[r]), rp = rsrc_span(a.prev + hb[r]);
-    const uint32_t px4 = (uint32_t)(pp * 4), pp8 = (uint32_t)(pp * 8);
+    // prev: the chunk's four 64-robot tiles (lane_rs.hpp rs_prev_at), each half of a wave's
+    // tile one 1 KiB run (round 6)
+    const auto rx = rsrc_span(a.x + hb[r]), rp = rsrc_span(a.prev + hb[r] * 4);
+    const uint32_t po = (li[r] & ~63u) * 32u + (li[r] & 63u) * 16u;
+    const uint32_t px4 = (uint32_t)(pp * 4);
     if constexpr (SO) {
       s.px = ld_span<float, CP>(rx, li[r], 0);
       s.py = ld_span<float, CP>(rx, li[r], px4);
-#pragma unroll
-      for (int w = 0; w < 4; w++) s.prev[w] = ld_span<int64_t, CP>(rp, li[r], w * pp8);
     } else {
       s.px = ld_chunk<float, CP>(a.x, hb[r], n, li[r]);
       s.py = ld_chunk<float, CP>(a.x + pp, hb[r], n, li[r]);
+    }
 #pragma unroll
-      for (int w = 0; w < 4; w++) s.prev[w] = ld_chunk<int64_t, CP>(a.prev + w * pp, hb[r], n, li[r]);
+    for (int h2 = 0; h2 < 2; h2++) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, po + 1024u * h2, 0, CP);
+      const uint32_t w0 = v[0], w1 = v[1], w2 = v[2], w3 = v[3];  // element copies (see kf6_load_in)
+      s.prev[2 * h2] = (int64_t)(((uint64_t)w1 << 32) | w0);
+      s.prev[2 * h2 + 1] = (int64_t)(((uint64_t)w3 << 32) | w2);
     }
     s.th = 0.f;
     rs_tick1<LIBM, true, true>(s, yaw[r], rw[r], sum[r], tab);
@@ -148,13 +150,18 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     if constexpr (SO) {
 #pragma unroll
       for (int k = 0; k < 6; k++) st_span<float, SP>(rx, li[r], k * px4, xs[k]);
-#pragma unroll
-      for (int w = 0; w < 4; w++) st_span<int64_t, SP>(rp, li[r], w * pp8, s.prev[w]);
     } else {
 #pragma unroll
       for (int k = 0; k < 6; k++) st_chunk<float, SP>(a.x + k * pp, hb[r], n, li[r], xs[k]);
+    }
 #pragma unroll
-      for (int w = 0; w < 4; w++) st_chunk<int64_t, SP>(a.prev + w * pp, hb[r], n, li[r], s.prev[w]);
+    for (int h2 = 0; h2 < 2; h2++) {
+      v4u32_t w;
+      w[0] = (uint32_t)s.prev[2 * h2];
+      w[1] = (uint32_t)((uint64_t)s.prev[2 * h2] >> 32);
+      w[2] = (uint32_t)s.prev[2 * h2 + 1];
+      w[3] = (uint32_t)((uint64_t)s.prev[2 * h2 + 1] >> 32);
+      __builtin_amdgcn_raw_buffer_store_b128(w, rp, po + 1024u * h2, 0, SP);
     }
   }
 }
@@ -178,8 +185,7 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
       const char *e = getenv("FMSKF_RS_VARIANT");
       return e ? atoi(e) : 1;
     }();
-    const bool so = var != 0 && 6 * s.pitch * 4 <= 0xFFFFFFFFull && 4 * s.pitch * 8 <= 0xFFFFFFFFull &&
-                    4 * in.sum_pitch * 8 <= 0xFFFFFFFFull;
+    const bool so = var != 0 && 6 * s.pitch * 4 <= 0xFFFFFFFFull && 4 * in.sum_pitch * 8 <= 0xFFFFFFFFull;
     if (state_nt(s.n * 124)) {
       if (so) {
         if (libm) k_rs2<true, kStateNT, true><<<g2, kBlock, lds, st>>>(a);

@@ -17,6 +17,28 @@ struct RsLane {
   int64_t prev[4];
 };
 
+// s64_rawAngleSumPrev (round 6): 16-byte pairs (wheels 0-1, wheels 2-3) in 64-robot tiles,
+// [N/64][2][64] x 16 B, so a wave's 64 robots move each half as one 1 KiB run of whole lines:
+// two 16-byte accesses per robot instead of one 8-byte access per wheel plane.  (Plain [N][4]
+// rows, 32 B per lane, left every line half-written by each store and measured 30% slower with
+// the memory-side `sc1` stores of the cache-resident tick: 25.8 -> 33.5 us at 2^20.)
+// rs_prev_at: the pair of wheels 2h, 2h + 1 of robot i, in 16-byte units
+__host__ __device__ __forceinline__ uint64_t rs_prev_at(uint64_t i, int h) {
+  return (i >> 6) * 128 + (uint64_t)h * 64 + (i & 63);
+}
+__device__ __forceinline__ void rs_prev_load(const int64_t *prev, uint64_t i, int64_t (&pv)[4]) {
+  const longlong2 a = reinterpret_cast<const longlong2 *>(prev)[rs_prev_at(i, 0)];
+  const longlong2 b = reinterpret_cast<const longlong2 *>(prev)[rs_prev_at(i, 1)];
+  pv[0] = a.x;
+  pv[1] = a.y;
+  pv[2] = b.x;
+  pv[3] = b.y;
+}
+__device__ __forceinline__ void rs_prev_store(int64_t *prev, uint64_t i, const int64_t (&pv)[4]) {
+  reinterpret_cast<longlong2 *>(prev)[rs_prev_at(i, 0)] = make_longlong2(pv[0], pv[1]);
+  reinterpret_cast<longlong2 *>(prev)[rs_prev_at(i, 1)] = make_longlong2(pv[2], pv[3]);
+}
+
 template <bool LIBM, bool CORR, bool PRED>
 __device__ __forceinline__ void rs_tick1(RsLane &s, float yaw_deg, uint2 rpm, const int64_t (&sum)[4],
                                          const float *tab) {

@@ -431,11 +431,14 @@ def test_checkpoint_resume_bitexact(tmp_path, model):
     v2 = b"FMSKFCK2" + blob[8:]  # format 2 kept the dlt / speed motor planes
     v3 = b"FMSKFCK3" + blob[8:]  # format 3 had no previous motor angles (ABI 2)
     v4 = b"FMSKFCK4" + blob[8:]  # format 4 kept the motor IIR state as [4][N] planes
+    cases = [("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2), ("v3", v3),
+             ("v4", v4)]
+    if model == "rs":  # a round-5 RS file: header layout word 0, the previous sums as [4][N] planes
+        cases.append(("rs_r5", blob[:84] + b"\0\0\0\0" + blob[88:]))
     with Engine(model, n) as e:
         e.load_state(ck)
         before = readout(e)
-        for name, data in (("cut", blob[:-5]), ("long", blob + b"\0"), ("flip", flipped), ("v1", v1), ("v2", v2),
-                           ("v3", v3), ("v4", v4)):
+        for name, data in cases:
             bad = tmp_path / name
             bad.write_bytes(data)
             with pytest.raises(fmskf.FmskfError):

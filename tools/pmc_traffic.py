@@ -89,8 +89,8 @@ def secondary(root, out):
 # The rows either side of the tick at 2^20 (bench path_rows): (bench key, kernel substring,
 # kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
 # written (56); WT901 standard poll: row, len, parser count / flags, magnetometer read (60),
-# flags, error, 15 registers, snapshot row, yaw / gyro z written (72; the empty parser window is
-# neither read nor written); CAN RX, four
+# flags, error, 4 registers (round 6: the other eleven only in the snapshot row), snapshot row,
+# yaw / gyro z written (50; the empty parser window is neither read nor written); CAN RX, four
 # wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, sum read (120), those
 # state fields plus rpm and curr written (96); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128); the fused
@@ -100,7 +100,7 @@ def secondary(root, out):
 PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
-    ("wt901_ingest_2p20", "k_wt901", 60, 72),
+    ("wt901_ingest_2p20", "k_wt901", 60, 50),
     ("can_ingest_2p20", "k_can4", 120, 96),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
     # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
@@ -116,7 +116,11 @@ PATHS = [
     # 4 + 4 B, is traffic above it) with the control step's 217 / 152 (its own rpm plane) and the
     # frame
     ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 217, 216 + 152 + 8),
-    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 + 209 + 120, 56 + 152 + 8 + 96),
+    # round 6: the previous sums neither read nor written while they equal the motor sums (PS)
+    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 209 + 120, 56 - 32 + 152 + 8 + 96),
+    # the EKF9 ISR with the tick's CAN RX fused in: + the CAN row's 120 / 96, the control step's
+    # rpm plane no longer read
+    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 217 - 8 + 120, 216 + 152 + 8 + 96),
 ]
 
 

@@ -86,7 +86,8 @@ for s in $STEPS; do
            pmc2 pmc_path_isr_can_kf6_2p20 120 --op isr_can --ticks 30
            pmc2 pmc_path_isr_rs_2p20 120 --model rs --op isr --ticks 30
            pmc2 pmc_path_isr_can_rs_2p20 120 --model rs --op isr_can --ticks 30
-           pmc2 pmc_path_isr_ekf9_2p20 120 --model ekf9 --op isr --ticks 30 ;;
+           pmc2 pmc_path_isr_ekf9_2p20 120 --model ekf9 --op isr --ticks 30
+           pmc2 pmc_path_isr_can_ekf9_2p20 120 --model ekf9 --op isr_can --ticks 30 ;;
     sq)    for ent in "kf6|--packed --ticks 30" "rs|--model rs --pad 512 --ticks 30" "wt901|--op wt901 --ticks 30" \
                       "can|--op can --ticks 30"; do
              IFS='|' read -r nm ka <<< "$ent"
