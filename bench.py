@@ -338,8 +338,10 @@ def secondary_configs(dev, stream, ticks: int, trig):
     return out
 
 
-# the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20)
+# the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20) and the C610 RX of four wheels
+# (can_ingest_2p20)
 WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 8 + 6 + 32 + 8
+CAN_RX_BYTES = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
     # RS tick: pos (x, y) 8 r + (x, y, th) 12 w -- theta is overwritten by the correct, so it is
@@ -357,10 +359,11 @@ PATH_BYTES = {
     # registers written to sReg as well as to the row)
     "wt901_ingest_2p20": WT901_POLL_BYTES,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
-    # output y, int64 sum read and written; rpm and curr written (the speed is the IIR state y;
-    # Status's dlt is formed at readout from the angle and the previous one; the IIR input state
-    # x is formed from the previous frame's angle and stamp (round 5: 224 -> 216 B))
-    "can_ingest_2p20": 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 8) + 2 + 2),
+    # output y and the low word of the int64 sum read and written (round 6: the high word only on
+    # a carry across 2^32); rpm and curr written (the speed is the IIR state y; Status's dlt is
+    # formed at readout from the angle and the previous one; the IIR input state x is formed from
+    # the previous frame's angle and stamp (round 5: 224 -> 216 B; round 6: 216 -> 184 B))
+    "can_ingest_2p20": CAN_RX_BYTES,
     # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
     "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
     # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
@@ -369,30 +372,30 @@ PATH_BYTES = {
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
     # the WT901 poll
-    "firmware_loop_kf6_2p20": 216 + (232 + 369 - 8 + 8) + WT901_POLL_BYTES / 10,
+    "firmware_loop_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) + WT901_POLL_BYTES / 10,
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
-    # CAN row's 216 + the ISR's 601 without its rpm read
-    "isr_can_kf6_2p20": 216 + (232 + 369 - 8 + 8) - 8,
+    # CAN row's 184 + the ISR's 601 without its rpm read
+    "isr_can_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8,
     # the EKF9 ISR (k_isr_ekf9, round 5): the EKF9 tick's 448 (cfg 3's count; + 8 B with the
     # heading's hidden low-part row) + the control step's 369 (its own rpm plane: the tick reads
     # the raw record) + the 0x200 frame
     "isr_ekf9_2p20": 448 + 369 + 8,
-    # with the tick's CAN RX fused in (fmskf_isr_tick_can): the CAN row's 216, the control step's
+    # with the tick's CAN RX fused in (fmskf_isr_tick_can): the CAN row's 184, the control step's
     # rpm no longer read back
-    "isr_can_ekf9_2p20": 216 + (448 + 369 + 8) - 8,
+    "isr_can_ekf9_2p20": CAN_RX_BYTES + (448 + 369 + 8) - 8,
     # the reference-semantics ISR (k_isr_rs) on the ingested motor state: the RS tick's 140 + the
     # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
     "isr_rs_2p20": 140 + 369 - 8 + 8,
-    # with the tick's CAN RX fused in: the CAN row's 216, the rpm and the four sums no longer read
+    # with the tick's CAN RX fused in: the CAN row's 184, the rpm and the four sums no longer read
     # back (the CAN lane hands them over in registers), and (round 6) the previous sums neither
     # read nor written while they equal the motor state's stored sums (k_isr_rs PS: 64 B)
-    "isr_can_rs_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 - 64,
+    "isr_can_rs_2p20": CAN_RX_BYTES + (140 + 369 - 8 + 8) - 8 - 32 - 64,
     # the reference-semantics firmware loop (VD_task_main.cpp:366-372 with its CAN RX and IMU
     # tasks) on the fused call: CAN RX + the RS ISR in one kernel, a WT901 poll every 10th tick
-    "firmware_loop_rs_fused_2p20": 216 + (140 + 369 - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
+    "firmware_loop_rs_fused_2p20": CAN_RX_BYTES + (140 + 369 - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
-    "firmware_loop_kf6_fused_2p20": 216 + (232 + 369 - 8 + 8) - 8 + WT901_POLL_BYTES / 10,
+    "firmware_loop_kf6_fused_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8 + WT901_POLL_BYTES / 10,
 }
 
 

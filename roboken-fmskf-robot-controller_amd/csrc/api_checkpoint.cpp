@@ -31,15 +31,16 @@ struct CkHeader {
   uint32_t abi, model;
   uint64_t n, pitch;
   uint32_t tile, elem, groups, ctrl_tile;  // ctrl_tile: control arrays' tile width (0 = planar)
-  uint64_t m_pitch, ctrl_pitch;            // motor sum planes' pitch, control state's pitch
+  uint64_t m_pitch, ctrl_pitch;            // (round 5: the motor sum planes' pitch), control state's pitch
   uint64_t body_bytes, checksum;           // what follows the header, and its hash
   uint32_t flags;                          // fmskf_config.flags (FMSKF_CFG_*)
-  // layout bits of format 5 (0 in round-5 files): bit 0, the RS previous sums in 64-robot tiles
-  // of wheel pairs (round 6, lane_rs.hpp rs_prev_at; [4][pitch] planes before), so a round-5 RS
-  // file is refused instead of loaded scrambled
+  // layout bits of format 5 (0 in round-5 files), so a round-5 file is refused instead of loaded
+  // scrambled: bit 0, the RS previous sums in 64-robot tiles of wheel pairs (round 6, lane_rs.hpp
+  // rs_prev_at; [4][pitch] planes before); bit 1, the motor group's angle sums as split low /
+  // high words (round 6, fmskf_internal.hpp m_sum_lo; int64 [4][pitch] planes before)
   uint32_t layout;
 };
-constexpr uint32_t kCkPrevRows = 1u;
+constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u;
 struct CkSection {
   void *dev;
   size_t bytes;
@@ -73,7 +74,8 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_prev_micro,
                     (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
-    v.push_back({s.m_sum, (size_t)4 * s.m_pitch * 8});
+    v.push_back({s.m_sum_lo, (size_t)4 * n * 4});
+    v.push_back({s.m_sum_hi, (size_t)4 * n * 4});
     v.push_back({s.m_iir_y, (size_t)4 * n * 4});
   }
   if (groups & 8) {
@@ -98,7 +100,7 @@ void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->elem = h->d.elem;
   hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
   hd->m_pitch = plane_pitch(h->s.n);
-  hd->layout = h->s.prev_sum ? kCkPrevRows : 0u;
+  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit;
   const uint64_t w = tile_w_elem(4);
   hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
 }
@@ -179,7 +181,7 @@ int fmskf_save_state(fmskf_handle h, const char *path) {
     CkHeader hd{};
     memcpy(hd.magic, kCkMagic, 8);
     ck_layout(h, &hd);
-    hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
+    hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum_lo ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
     rs_prev_materialize(h);  // the file holds the odometry's previous sums in the prev planes
     // and the whole WT901 register file in its planes (no row-resident registers)
     launch_check(launch_wt901_regs_sync(h->s, h->stream), "register file sync");
@@ -238,7 +240,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
       fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, flags, N or layout)");
     if ((hd.groups & 4) && hd.m_pitch != me.m_pitch) fail(FMSKF_EINVAL, "checkpoint motor layout differs");
     if (hd.layout != me.layout)
-      fail(FMSKF_EINVAL, "checkpoint layout differs (a round-5 RS file keeps its previous sums as [4][pitch] planes)");
+      fail(FMSKF_EINVAL, "checkpoint layout differs (a round-5 file: int64 motor sum planes, RS previous sums as planes)");
     if ((hd.groups & 8) && (hd.ctrl_tile != me.ctrl_tile || hd.ctrl_pitch != me.ctrl_pitch))
       fail(FMSKF_EINVAL, "checkpoint control layout differs (tiling / pitch)");
     if (!(hd.groups & 1u)) fail(FMSKF_EINVAL, "checkpoint holds no estimator state");
@@ -281,7 +283,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     f.seek(first, SEEK_SET);
     // groups the checkpoint does not hold were never used by the saving handle: reset them here
     if (!(hd.groups & 2) && h->s.imu_reg) zero_imu(h);
-    if (!(hd.groups & 4) && h->s.m_sum) zero_motors(h);
+    if (!(hd.groups & 4) && h->s.m_sum_lo) zero_motors(h);
     if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
     h->rs_prev_synced = h->rs_prev_stale = false;  // the prev planes come from the file
     hip_check(hipStreamSynchronize(h->stream), "load sync");

@@ -211,7 +211,7 @@ static void isr_launches(fmskf_ctx *h, const TickIn &t, uint8_t *dst) {
   if (h->cfg.model == FMSKF_MODEL_RS) {
     rs_prev_materialize(h);
     launch_check(launch_isr_rs(h->s, t, libm, h->ctrl, p, dst, h->stream), "isr launch");
-    h->rs_prev_synced = t.angle_sum == h->s.m_sum;
+    h->rs_prev_synced = t.msum_lo != nullptr;
   } else if (fused == (int)hipErrorNotSupported) {  // estimator tick, then the control step and the frame (three launches)
     h->isr_ctrl_split++;
     int e = 0;

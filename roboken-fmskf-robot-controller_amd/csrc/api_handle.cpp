@@ -124,7 +124,8 @@ void zero_motors(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.m_prev, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_rpm, 0, 4 * n * 2, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_curr, 0, 4 * n * 2, st), "reset motors");
-  hip_check(hipMemsetAsync(s.m_sum, 0, 4 * s.m_pitch * 8, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_sum_lo, 0, 4 * n * 4, st), "reset motors");
+  hip_check(hipMemsetAsync(s.m_sum_hi, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_iir_y, 0, 4 * n * 4, st), "reset motors");
   hip_check(hipMemsetAsync(s.m_prev_micro, 0, 4 * n * 2, st), "reset motors");
 }
@@ -149,13 +150,13 @@ void ensure_imu(fmskf_ctx *h) {
 void rs_prev_materialize(fmskf_ctx *h) {
   if (!h->rs_prev_stale) return;
   const DevState &s = h->s;
-  launch_check(launch_sums_rows(s.m_sum, s.prev_sum, s.n, s.m_pitch, true, h->stream), "previous sums");
+  launch_check(launch_motor_sums(s.m_sum_lo, s.m_sum_hi, s.prev_sum, s.n, 0, true, h->stream), "previous sums");
   h->rs_prev_stale = false;
 }
 
 void ensure_motors(fmskf_ctx *h) {
   DevState &s = h->s;
-  if (s.m_sum) return;
+  if (s.m_sum_lo) return;
   if (h->capturing) fail(FMSKF_EINVAL, "motor state first used inside a graph capture");
   const uint64_t n = s.n;
   s.m_micro = h->alloc<int16_t>(4 * n);
@@ -163,8 +164,8 @@ void ensure_motors(fmskf_ctx *h) {
   s.m_prev = h->alloc<int16_t>(4 * n);
   s.m_rpm = h->alloc<int16_t>(4 * n);
   s.m_curr = h->alloc<int16_t>(4 * n);
-  s.m_pitch = plane_pitch(n);
-  s.m_sum = h->alloc<int64_t>(4 * s.m_pitch);
+  s.m_sum_lo = h->alloc<uint32_t>(4 * n);
+  s.m_sum_hi = h->alloc<int32_t>(4 * n);
   s.m_iir_y = h->alloc<float>(4 * n);
   s.m_prev_micro = h->alloc<int16_t>(4 * n);
   zero_motors(h);
@@ -221,7 +222,7 @@ void do_reset(fmskf_ctx *h) {
   if (s.thlo) hip_check(hipMemsetAsync(s.thlo, 0, n * 4, st), "reset heading low part");
   if (s.xlo) hip_check(hipMemsetAsync(s.xlo, 0, (size_t)kKf6LoRows * pp * 4, st), "reset position low parts");
   if (s.imu_reg) zero_imu(h);
-  if (s.m_sum) zero_motors(h);
+  if (s.m_sum_lo) zero_motors(h);
   if (h->ctrl_ready) {  // the control objects are static in the firmware too: zero, power off
     const CtrlDev &c = h->ctrl;
     hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, st), "reset ctrl");
@@ -303,9 +304,9 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.angle_sum, "angle_sum");
         if (!t.rpm || !t.angle_sum) ensure_motors(h);
         if (!t.rpm) t.rpm = s.m_rpm;
-        if (!t.angle_sum) {
-          t.angle_sum = s.m_sum;
-          t.sum_pitch = s.m_pitch;
+        if (!t.angle_sum) {  // the motor state's split sums (fmskf_internal.hpp m_sum_lo)
+          t.msum_lo = s.m_sum_lo;
+          t.msum_hi = s.m_sum_hi;
         }
       }
       break;
@@ -354,7 +355,7 @@ void run_tick(fmskf_ctx *h, const fmskf_tick_inputs *in, bool upd, bool pred, ui
   }
   launch_check(e, "tick kernel launch");
   // the predict stored the sums it read as the previous ones
-  if (rs_pred) h->rs_prev_synced = t.angle_sum == h->s.m_sum;
+  if (rs_pred) h->rs_prev_synced = t.msum_lo != nullptr;
   h->time_end();
 }
 

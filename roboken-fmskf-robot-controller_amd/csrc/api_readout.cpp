@@ -18,7 +18,7 @@ int fmskf_get_prev_sum(fmskf_handle h, int64_t *prev, uint32_t mem) {
     // the tick's tiled layout on the device -> the ABI's [4][N] planes
     const uint64_t n = h->s.n;
     int64_t *dense = mem == FMSKF_MEM_DEVICE ? prev : (int64_t *)h->out_for((size_t)4 * n * 8);
-    launch_check(launch_sums_rows(h->s.prev_sum, dense, n, n, false, h->stream), "previous sums");
+    launch_check(launch_prev_out(h->s.prev_sum, dense, n, n, h->stream), "previous sums");
     if (mem == FMSKF_MEM_HOST) copy_out(h, prev, dense, (size_t)4 * n * 8, mem);
     finish_out(h, mem);
   });
@@ -57,12 +57,17 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
   return guarded([&] {
     check_handle(h);
     DeviceGuard g(h->cfg.device);
+    if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
     const uint64_t n = h->s.n;
     ensure_motors(h);
     copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
-    copy_planes_out(h, angle_sum, h->s.m_sum, n * 8, h->s.m_pitch * 8, 4, mem);
+    if (angle_sum) {  // the split sums as whole int64 [4][N] planes
+      int64_t *dense = mem == FMSKF_MEM_DEVICE ? angle_sum : (int64_t *)h->out_for((size_t)4 * n * 8);
+      launch_check(launch_motor_sums(h->s.m_sum_lo, h->s.m_sum_hi, dense, n, n, false, h->stream), "motor sums");
+      if (mem == FMSKF_MEM_HOST) copy_out(h, angle_sum, dense, (size_t)4 * n * 8, mem);
+    }
     // Status::flt_SpeedRadPS is the IIR1 output, i.e. its state y (VD_motor_if_m2006.cpp:63):
     // [4][N] planes out of the device's [N][4] rows
     if (speed_radps) {

@@ -20,8 +20,8 @@ struct CanArgs {
   int16_t *micro, *angle, *rpm, *curr;
   int16_t *prev;  // [N][4] the angle before this frame (Status::flt_dltOutAngle_rad at readout)
   int16_t *prev_micro;  // [N][4] the stamp before this frame (the IIR1's previous sample, speed_x)
-  int64_t *sum;  // [4][sum_pitch]
-  uint64_t sum_pitch;
+  uint32_t *sum_lo;  // [N][4] s64_rawAngleSum, low 32 bits (fmskf_internal.hpp m_sum_lo)
+  int32_t *sum_hi;   // [N][4] high 32 bits (written only when a frame's delta carries)
   float *iir_y;  // [N][4] UTIL::IIR1 output state, also Status::flt_SpeedRadPS
   bool nt;       // host side: the fused kernels' choice of a non-temporal motor state (can_nt)
 };
@@ -41,15 +41,23 @@ __device__ __forceinline__ int32_t sdiv_arm(int32_t a, int32_t b) {
 }
 
 // one wheel's rx_callback on its 8-byte frame and microsecond stamp (VD_motor_if_m2006.cpp:
-// 32-72): the decoded fields, the IIR1 speed state and the int64 sum.  The Status ring's head
+// 32-72): the decoded fields, the IIR1 speed state and the wrapped angle step the int64 sum
+// takes (:66-69; the caller adds it to the split sum, sum_add).  The Status ring's head
 // (:33-34, 71) is not kept: both readers, get_status_latest and get_status_estimate
 // (VD_motor_if_m2006.hpp:44-47, .cpp:11-24), read only the newest entry, which is what the
 // engine stores, so the head selects nothing that can be observed (round 4: 232 -> 224 B)
 struct CanWheel {
   int16_t angle, rpm, curr;
   float iir_y;
-  int64_t sum;
+  int32_t d;  // s64_rawAngleSum += d (|d| <= 4096)
 };
+// s64_rawAngleSum += d on the split halves: the low word wraps, the carry (-1, 0, +1) goes to the
+// high word
+__device__ __forceinline__ uint32_t sum_add(uint32_t lo, int32_t d, int32_t &carry) {
+  const int64_t t = (int64_t)lo + d;
+  carry = (int32_t)(t >> 32);
+  return (uint32_t)t;
+}
 // the speed sample rx_callback feeds the IIR1 (VD_motor_if_m2006.cpp:49-63): the wrapped angle
 // step over the wrapped microsecond step, with the M7's wrapping MUL and SDIV x/0 = 0
 __device__ __forceinline__ float speed_x(int16_t new_angle, int16_t old_angle, int16_t micro, int16_t old_micro) {
@@ -70,7 +78,7 @@ __device__ __forceinline__ float speed_x(int16_t new_angle, int16_t old_angle, i
 // zero-initialised filter's prev_X_.
 __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t micro, int dir,
                                               int16_t old_micro, int16_t old_angle, int16_t prev_micro,
-                                              int16_t prev_angle, float py, int64_t sum) {
+                                              int16_t prev_angle, float py) {
   const uint32_t b0 = fx & 0xFF, b1 = (fx >> 8) & 0xFF, b2 = (fx >> 16) & 0xFF, b3 = fx >> 24;
   const uint32_t b4 = fy & 0xFF, b5 = (fy >> 8) & 0xFF;
   CanWheel o;
@@ -86,27 +94,27 @@ __device__ __forceinline__ CanWheel can_wheel(uint32_t fx, uint32_t fy, int16_t 
   // the previous one, which the caller stores (k_motor_dlt)
   int16_t d = (int16_t)(new_angle - old_angle);
   d = (d > 4096) ? (int16_t)(d - 8192) : ((d < -4096) ? (int16_t)(d + 8192) : d);
-  o.sum = sum + d;
+  o.d = d;
   return o;
 }
 
 // One robot per lane, every wheel present: the robot's 32 frame bytes, its four stamps and its
-// [N][4] int16 / float state in single 16- and 8-byte accesses, and each [4][N] sum plane row
-// coalesced across the wave, every access through a scalar descriptor at the block's 256-robot
-// chunk hb (wave-uniform) with the KF6 tick's cache policies: the frames and stamps (read once)
-// `nt`, the state stored `sc1` while cache-resident; NT: the motor state streams from HBM,
-// `nt` loads and stores.  SO: the sum array's wheel planes at soffset from one descriptor (the
-// launcher checks the 4 GiB span); else one clamped descriptor per plane.  load() issues every
-// load; step() computes the four wheels and stores (`live` lanes only: the fused ISR runs
-// clamped lanes past N) and returns the new rpm of the four wheels (s16_rawSpeedRpm) packed;
-// sm[] then holds the new angle sums (get_rawAngleSum).
+// [N][4] int16 / float / uint32 state in single 8- and 16-byte accesses, every access through a
+// scalar descriptor at the block's 256-robot chunk hb (wave-uniform) with the KF6 tick's cache
+// policies: the frames and stamps (read once) `nt`, the state stored `sc1` while cache-resident;
+// NT: the motor state streams from HBM, `nt` loads and stores.  The angle sums move as their low
+// words (one 16-byte row); the high words are read only with FULL (a consumer of the whole new
+// sums: the RS odometry on its prev planes) and written only by a wheel whose delta carries.
+// load() issues every load; step() computes the four wheels and stores (`live` lanes only: the
+// fused ISR runs clamped lanes past N) and returns the new rpm of the four wheels
+// (s16_rawSpeedRpm) packed; d[] then holds the four sum deltas and, with FULL, sm[] the new sums
+// (get_rawAngleSum).
 // the CAN lane's arguments over the handle's motor state; false where the fused form does not
 // apply (the motor state past the cached regime or its sum planes past 4 GiB, unaligned frames /
 // stamps)
 inline bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t *can_stamps, const int8_t dir[4],
                      CanArgs &ca) {
-  if (!s.m_sum || state_nt(s.n * 66) || 4 * s.m_pitch * 8 > 0xFFFFFFFFull || ((uintptr_t)can_frames & 15) != 0 ||
-      ((uintptr_t)can_stamps & 7) != 0)
+  if (!s.m_sum_lo || state_nt(s.n * 66) || ((uintptr_t)can_frames & 15) != 0 || ((uintptr_t)can_stamps & 7) != 0)
     return false;
   ca = CanArgs{};
   ca.n = s.n;
@@ -120,8 +128,8 @@ inline bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t
   ca.prev_micro = s.m_prev_micro;
   ca.rpm = s.m_rpm;
   ca.curr = s.m_curr;
-  ca.sum = s.m_sum;
-  ca.sum_pitch = s.m_pitch;
+  ca.sum_lo = s.m_sum_lo;
+  ca.sum_hi = s.m_sum_hi;
   ca.iir_y = s.m_iir_y;
   return true;
 }
@@ -136,15 +144,18 @@ inline bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t
 // everything fits (KF6 / RS 2^20)
 inline bool can_nt(const DevState &s) { return state_nt(s.n * (66 + 40 + est_state_bytes(s))); }
 
-template <bool NT, bool SO>
+template <bool NT, bool FULL = false>
 struct Can4Lane {
   static constexpr int LP = NT ? kStateNT : 0, SP = st_pol(LP), IP = 2;  // IP: inputs nt
   uint64_t hb;
   uint32_t li;
   uint4 f01, f23;
-  uint32_t iyw[4];
+  uint32_t iyw[4], slo[4];
+  int32_t shi[4];
   uint64_t sv, mv, av, pmv, pav;
-  int64_t sm[4];  // the wheels' angle sums: before step() the stored ones, after it the new ones
+  int32_t d[4];   // after step(): the wheels' sum deltas (s64_rawAngleSum += d)
+  int64_t sm[4];  // FULL: before step() the stored sums, after it the new ones
+  uint32_t cmask; // after step(): wheel w's carry into the high word, 2 bits each (1: +1, 3: -1)
 
   __device__ __forceinline__ void load(const CanArgs &a, uint64_t hb_, uint32_t li_) {
     hb = hb_;
@@ -161,17 +172,25 @@ struct Can4Lane {
     iyw[1] = iy[1];
     iyw[2] = iy[2];
     iyw[3] = iy[3];
+    const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.sum_lo + hb * 4), li * 16u, 0, LP);
+    slo[0] = lw[0];
+    slo[1] = lw[1];
+    slo[2] = lw[2];
+    slo[3] = lw[3];
+    if constexpr (FULL) {
+      const auto hw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.sum_hi + hb * 4), li * 16u, 0, LP);
+      shi[0] = (int32_t)hw[0];
+      shi[1] = (int32_t)hw[1];
+      shi[2] = (int32_t)hw[2];
+      shi[3] = (int32_t)hw[3];
+#pragma unroll
+      for (int w = 0; w < 4; w++) sm[w] = (int64_t)(((uint64_t)(uint32_t)shi[w] << 32) | slo[w]);
+    }
     sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
     mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);
     av = ld_span<uint64_t, LP>(rsrc_span(a.angle + hb * 4), li, 0);
     pmv = ld_span<uint64_t, LP>(rsrc_span(a.prev_micro + hb * 4), li, 0);
     pav = ld_span<uint64_t, LP>(rsrc_span(a.prev + hb * 4), li, 0);
-    const auto r_sm = rsrc_span(a.sum + hb);
-    const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-      sm[w] = SO ? ld_span<int64_t, LP>(r_sm, li, w * ps)
-                 : ld_chunk<int64_t, LP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li);
   }
 
   __device__ __forceinline__ uint2 step(const CanArgs &a, bool live) {
@@ -181,28 +200,27 @@ struct Can4Lane {
     const uint32_t sw[2] = {st.x, st.y}, mw[2] = {om.x, om.y}, aw[2] = {oa.x, oa.y};
     const uint32_t pmw[2] = {(uint32_t)pmv, (uint32_t)(pmv >> 32)}, paw[2] = {(uint32_t)pav, (uint32_t)(pav >> 32)};
     uint32_t na[2] = {0, 0}, nr[2] = {0, 0}, nc[2] = {0, 0};
-    v4u32_t oy;
+    v4u32_t oy, ol;
+    cmask = 0;
 #pragma unroll
     for (int w = 0; w < 4; w++) {
       const int sh = 16 * (w & 1);
       const CanWheel o = can_wheel(fx[w], fy[w], (int16_t)(sw[w >> 1] >> sh), a.dir[w],
                                    (int16_t)(mw[w >> 1] >> sh), (int16_t)(aw[w >> 1] >> sh),
                                    (int16_t)(pmw[w >> 1] >> sh), (int16_t)(paw[w >> 1] >> sh),
-                                   __builtin_bit_cast(float, iyw[w]), sm[w]);
+                                   __builtin_bit_cast(float, iyw[w]));
       oy[w] = __builtin_bit_cast(uint32_t, o.iir_y);
-      sm[w] = o.sum;
+      d[w] = o.d;
+      int32_t cy;
+      ol[w] = sum_add(slo[w], o.d, cy);
+      cmask |= ((uint32_t)cy & 3u) << (2 * w);
+      if constexpr (FULL) sm[w] += o.d;
       na[w >> 1] |= (uint32_t)(uint16_t)o.angle << sh;
       nr[w >> 1] |= (uint32_t)(uint16_t)o.rpm << sh;
       nc[w >> 1] |= (uint32_t)(uint16_t)o.curr << sh;
     }
     if (live) {
-      const auto r_sm = rsrc_span(a.sum + hb);
-      const uint32_t ps = (uint32_t)(a.sum_pitch * 8);
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-        if constexpr (SO) st_span<int64_t, SP>(r_sm, li, w * ps, sm[w]);
-        else st_chunk<int64_t, SP>(a.sum + (uint64_t)w * a.sum_pitch, hb, a.n, li, sm[w]);
-      }
+      __builtin_amdgcn_raw_buffer_store_b128(ol, rsrc_span(a.sum_lo + hb * 4), li * 16u, 0, SP);
       __builtin_amdgcn_raw_buffer_store_b128(oy, rsrc_span(a.iir_y + hb * 4), li * 16u, 0, SP);
       const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
       st_span<uint64_t, SP>(rsrc_span(a.prev_micro + hb * 4), li, 0, mv);
@@ -213,6 +231,22 @@ struct Can4Lane {
       st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
     }
     return make_uint2(nr[0], nr[1]);
+  }
+
+  // the high word of a wheel whose low word carried (a wheel crossing a multiple of 2^32 counts:
+  // rare).  Called last in the kernel: a read-modify-write through a plain pointer that may alias
+  // any other array, kept out of the way of the kernel's own loads and stores (issued inside
+  // step() it cost the fused EKF9 ISR 40 VGPRs and a spill)
+  __device__ __forceinline__ void finish(const CanArgs &a, bool live) {
+    if (!live || cmask == 0) return;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const uint32_t c = (cmask >> (2 * w)) & 3u;
+      if (c) {
+        int32_t *hp = a.sum_hi + (hb + li) * 4 + w;
+        *hp = (FULL ? shi[w] : *hp) + (c == 1u ? 1 : -1);
+      }
+    }
   }
 };
 

@@ -58,10 +58,13 @@ struct DevState {
                                // flt_dltOutAngle_rad is formed from the two at readout
   int16_t *m_rpm = nullptr;    // [N][4]
   int16_t *m_curr = nullptr;   // [N][4]
-  int64_t *m_sum = nullptr;    // [4][m_pitch]: the encoder sums the RS tick reads, at a padded
-                               // plane pitch (a power-of-two stride N aliases: RS tick 2^20
-                               // 27.5-27.8 us from [4][2^20] sums, 24.7 from [4][2^20 + 512])
-  uint64_t m_pitch = 0;
+  // s64_rawAngleSum of the four wheels, split (round 6): the low 32 bits [N][4] (one 16-byte access
+  // per robot), which every frame updates, and the high 32 bits [N][4], which a frame touches only
+  // when its delta (|d| <= 4096) carries across 2^32.  The CAN RX moves 16 + 16 B of sums per robot
+  // instead of 32 + 32; readers of the whole sum (the RS tick on the motor state, the readouts)
+  // load both halves (motor_sum_load).  m_sum_lo doubles as "the motor state exists".
+  uint32_t *m_sum_lo = nullptr;
+  int32_t *m_sum_hi = nullptr;
   float *m_iir_y = nullptr;    // [N][4] (one 16-byte access per robot in k_can4)
   int16_t *m_prev_micro = nullptr;  // [N][4] the stamp of the frame before (the IIR1's previous
                                     // sample x is formed from it: kernels_ingest.hip can_wheel)
@@ -82,7 +85,10 @@ struct TickIn {
   const uint32_t *rec;       // KF6 [N] x 16-byte records {yaw, gz, rpm[4]} or null
   const float *sintab;       // 513-entry TABLE512 sine table (device)
   uint64_t stride;
-  uint64_t sum_pitch;  // plane stride of angle_sum: the caller's stride, or the ingested m_pitch
+  uint64_t sum_pitch;  // plane stride of angle_sum (the caller's)
+  // the RS tick on the motor state's sums (angle_sum NULL): their [N][4] low / high halves
+  const uint32_t *msum_lo;
+  const int32_t *msum_hi;
   uint32_t n_ticks;
   // fmskf_tick_ensemble: the tick kernel also writes its blocks' ensemble records of the
   // post-tick state ([LEN][grid], ens_device.hpp) against the shift vector; null otherwise
@@ -367,9 +373,12 @@ int launch_isr_ekf9(const DevState &s, const TickIn &in, const Ekf9Params &prm, 
 int launch_isr_ekf9_can(const DevState &s, const TickIn &in, const Ekf9Params &prm, bool libm, const CtrlDev &c,
                         const CtrlPrm &p, uint8_t *frames, const uint8_t *can_frames, const int16_t *can_stamps,
                         const int8_t dir[4], hipStream_t st);
-// RS previous sums: the tick's tiled layout (lane_rs.hpp rs_prev_at) <-> [4][pitch] planes
-// (to_rows: planes -> tiles)
-int launch_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch, bool to_rows, hipStream_t st);
+// RS previous sums: the tick's tiled layout (lane_rs.hpp rs_prev_at) -> [4][pitch] planes
+int launch_prev_out(const int64_t *prev, int64_t *dst, uint64_t n, uint64_t pitch, hipStream_t st);
+// the motor state's split sums as int64: into the RS previous-sum tiles (to_prev), or [4][pitch]
+// planes
+int launch_motor_sums(const uint32_t *lo, const int32_t *hi, int64_t *dst, uint64_t n, uint64_t pitch, bool to_prev,
+                      hipStream_t st);
 // the WT901 register file made whole: the row-resident registers written back from the
 // snapshot rows of the robots whose standard poll kept them there (kernels_ingest.hip F_ROWREGS)
 int launch_wt901_regs_sync(const DevState &s, hipStream_t st);

@@ -69,11 +69,13 @@ __global__ __launch_bounds__(kBlock) void k_ctrl_step(CtrlDev c, CtrlPrm p, cons
 struct IsrRsArgs {
   uint64_t pitch;
   float *x;
-  int64_t *prev;  // [N][4] rows
+  int64_t *prev;  // 64-robot tiles of wheel pairs (lane_rs.hpp rs_prev_at)
   const float *yaw_deg;
   const int16_t *rpm;
-  const int64_t *angle_sum;  // [4][sum_pitch]
+  const int64_t *angle_sum;  // [4][sum_pitch]: the caller's sums, or NULL: the motor state's
   uint64_t sum_pitch;
+  const uint32_t *msum_lo;  // the motor state's sums, split (fmskf_internal.hpp m_sum_lo)
+  const int32_t *msum_hi;
   const float *sintab;
   uint8_t *frames;
 };
@@ -92,7 +94,8 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   const uint64_t n = c.n, pp = a.pitch;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint32_t)n) return;
-  Can4Lane<CNT, true> cl;  // CNT: the motor state non-temporal (launchers: can_nt)
+  Can4Lane<CNT, CAN && !PS> cl;  // CNT: the motor state non-temporal (launchers: can_nt); the whole
+                                  // new sums only where the odometry needs them (not PS)
   if constexpr (CAN) {  // the block's 256-robot chunk
     const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
     cl.load(can, hb, i - hb);
@@ -107,19 +110,29 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   int64_t sum[4];
   if constexpr (!CAN) {
     rw = reinterpret_cast<const uint2 *>(a.rpm)[i];
+    if (a.msum_lo) {  // the motor state's sums (wave-uniform)
+      motor_sum_load(a.msum_lo, a.msum_hi, i, sum);
+    } else {
 #pragma unroll
-    for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * a.sum_pitch + i];
+      for (int w = 0; w < 4; w++) sum[w] = a.angle_sum[w * a.sum_pitch + i];
+    }
   }
   CtrlLane<SMALL, CP> L;
   L.load(c, i);
   if constexpr (CAN) {
-    if constexpr (PS) {  // the stored sums are the previous ones (before step() updates sm[])
-#pragma unroll
-      for (int w = 0; w < 4; w++) s.prev[w] = cl.sm[w];
-    }
     rw = cl.step(can, true);
+    if constexpr (PS) {
+      // the previous sums are the stored ones, so sum - prev is this frame's delta: the odometry
+      // takes (d, 0), the same int64 difference, without the whole sums
 #pragma unroll
-    for (int w = 0; w < 4; w++) sum[w] = cl.sm[w];
+      for (int w = 0; w < 4; w++) {
+        s.prev[w] = 0;
+        sum[w] = cl.d[w];
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; w++) sum[w] = cl.sm[w];
+    }
   }
   rs_tick1<LIBM, true, true>(s, yaw, rw, sum, a.sintab);
   const uint2 cw = L.step(c, p, i, rw);
@@ -131,6 +144,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   a.x[5 * pp + i] = s.vth;
   if constexpr (!PS) rs_prev_store(a.prev, i, s.prev);
   if (a.frames) reinterpret_cast<uint2 *>(a.frames)[i] = tx_frame(cw);
+  if constexpr (CAN) cl.finish(can, true);
 }
 
 // The firmware ISR in one pass for the 6-state KF: the KF6 tick (correct with the IMU yaw /
@@ -151,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, 
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const bool live = i < (uint32_t)n;
   const uint32_t ic = live ? i : (uint32_t)n - 1u;
-  Can4Lane<CNT, true> cl;  // CNT: the motor state non-temporal (launchers: can_nt)
+  Can4Lane<CNT> cl;  // CNT: the motor state non-temporal (launchers: can_nt)
   if constexpr (CAN) {  // the block's 256-robot chunk (every block has a live lane)
     const uint32_t hb = __builtin_amdgcn_readfirstlane(i) & ~(uint32_t)(kBlock - 1);
     cl.load(can, hb, ic - hb);
@@ -178,6 +192,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_kf6(KfArgs<MdKF6, Kf6Params> a, 
     const uint2 cw = L.step(c, p, i, m.rpm);
     if (frames) reinterpret_cast<uint2 *>(frames)[i] = tx_frame(cw);
   }
+  if constexpr (CAN) cl.finish(can, live);
 }
 
 // CAN_CTRL::tx_routine, VD_can_controller.hpp:43-55: frames [N][8], big-endian raw currents
@@ -285,7 +300,7 @@ static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDe
                     uint8_t *frames, hipStream_t st, const CanArgs &can) {
   if (c.n == 0) return 0;
   const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum, in.sum_pitch,
-                    in.sintab, frames};
+                    in.msum_lo, in.msum_hi, in.sintab, frames};
   const bool small = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   const bool nt = small && state_nt(ctrl_state_bytes(c) + s.n * 56);
   if (nt) {

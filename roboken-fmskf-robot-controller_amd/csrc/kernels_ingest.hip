@@ -458,11 +458,12 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   const int w = (int)(g & 3);
   if (a.present && !((a.present[i] >> w) & 1)) return;
   const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
-  const uint64_t ps = (uint64_t)w * a.sum_pitch + i;
   const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g], a.prev_micro[g],
-                               a.prev[g], a.iir_y[g], a.sum[ps]);
+                               a.prev[g], a.iir_y[g]);
   a.iir_y[g] = o.iir_y;
-  a.sum[ps] = o.sum;
+  int32_t cy;
+  a.sum_lo[g] = sum_add(a.sum_lo[g], o.d, cy);
+  if (cy != 0) a.sum_hi[g] += cy;
   a.prev_micro[g] = a.micro[g];
   a.micro[g] = a.stamps[g];
   a.prev[g] = a.angle[g];
@@ -481,9 +482,8 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
 }
 
 // one robot per lane, every wheel present (no mask): the robot's 32 frame bytes, its four
-// stamps and its [N][4] int16 / float state in single 16- and 8-byte accesses, and each [4][N]
-// sum plane row coalesced across the wave (the per-wheel kernel moves 64 B half-lines: 2^20
-// 57.4-57.7 -> 42.1-44.1 us, 2^22 232-239 -> 211).  Every access goes through a scalar
+// stamps and its [N][4] int16 / float / uint32 state in single 16- and 8-byte accesses (the
+// per-wheel kernel moves 64 B half-lines: 2^20 57.4-57.7 -> 42.1-44.1 us, 2^22 232-239 -> 211).  Every access goes through a scalar
 // descriptor at the block's 256-robot chunk with the KF6 tick's cache policies: the frames and
 // stamps (read once) `nt`, the state stored `sc1` while cache-resident; NT: the motor state
 // streams from HBM (past the Infinity Cache), `nt` loads and stores.  Plain global accesses
@@ -492,9 +492,9 @@ __global__ __launch_bounds__(kBlock) void k_can(CanArgs a) {
 // [4][N] planes took 4 dword loads and stores per array: measured neutral, 39.3-41.0 against
 // 40.0-40.1 us at 2^20, profiles/r5_kb_can_iir_ab.jsonl, issue-wait 0.78 either way), and the
 // IIR1 state x formed again from the previous frame (can_wheel): 224 -> 216 B per robot.
-// SO: the sum array's wheel planes reached through soffset from one descriptor (the launcher
-// checks the 4 GiB span); else one clamped descriptor per plane.
-template <bool NT, bool SO>
+// Round 6: the angle sums as their low words (one 16-byte access each way; the high words only on
+// a carry): 216 -> 184 B per robot.
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -502,9 +502,10 @@ __global__ __launch_bounds__(kBlock) void k_can4(CanArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint64_t hb = (uint64_t)(__builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1));
-  Can4Lane<NT, SO> L;
+  Can4Lane<NT> L;
   L.load(a, hb, (uint32_t)(i - hb));
   (void)L.step(a, true);
+  L.finish(a, true);
 }
 
 int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
@@ -520,8 +521,8 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.prev = s.m_prev;
   a.rpm = s.m_rpm;
   a.curr = s.m_curr;
-  a.sum = s.m_sum;
-  a.sum_pitch = s.m_pitch;
+  a.sum_lo = s.m_sum_lo;
+  a.sum_hi = s.m_sum_hi;
   a.iir_y = s.m_iir_y;
   a.prev_micro = s.m_prev_micro;
   // every wheel present and the caller's frames / stamps aligned for the wide loads: one robot
@@ -531,24 +532,14 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
     // 132 B of motor state per robot.  Non-temporal with 2 blocks per CU once it is well past
     // the Infinity Cache; measured (kbench, two passes): 2^22 plain 191.6-192.8 us, nt
     // 183.9-187.2, nt + 64 KiB cap 176.7-179.8; at 2^21 (277 MB) plain 83.3-85.1, nt 87.5-87.9
-    // the sum array's wheel planes through soffset while they lie within 4 GiB of a chunk base;
-    // FMSKF_CAN_VARIANT=0 forces one clamped descriptor per sum plane (the form past that, so
-    // the tests check it at small N)
-    static const int var = [] {
-      const char *e = getenv("FMSKF_CAN_VARIANT");
-      return e ? atoi(e) : 1;
-    }();
-    const bool so = var != 0 && 4 * s.m_pitch * 8 <= 0xFFFFFFFFull;
     // non-temporal once the motor state, the frames and the estimator state together outgrow
     // the Infinity Cache (can_nt, can_lane.hpp)
     if (can_nt(s)) {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", true, 64u * 1024u);
-      if (so) k_can4<true, true><<<g, kBlock, lds, st>>>(a);
-      else k_can4<true, false><<<g, kBlock, lds, st>>>(a);
+      k_can4<true><<<g, kBlock, lds, st>>>(a);
     } else {
       const unsigned lds = FMSKF_LDS_CAP("FMSKF_CAN_LDS", false, 0u);
-      if (so) k_can4<false, true><<<g, kBlock, lds, st>>>(a);
-      else k_can4<false, false><<<g, kBlock, lds, st>>>(a);
+      k_can4<false><<<g, kBlock, lds, st>>>(a);
     }
   } else {
     const uint64_t blocks = (4 * s.n + kBlock - 1) / kBlock;

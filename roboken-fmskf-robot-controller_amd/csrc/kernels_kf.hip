@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> 
   const uint64_t i = (uint64_t)bid * kBlock + threadIdx.x;
   const bool live = i < n;
   const uint64_t ic = live ? i : n - 1;
-  Can4Lane<CNT, true> cl4;
+  Can4Lane<CNT> cl4;
   if constexpr (CAN) cl4.load(can, (uint64_t)bid * kBlock, (uint32_t)(ic - (uint64_t)bid * kBlock));
   float x[N], P[NP];
   WaveTable<LIBM> tv(a.in.sintab);
@@ -322,6 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_ekf9(KfArgs<MdEKF9, Ekf9Params> 
     const uint2 cw = L.step(c, p, (uint32_t)i, rw);
     if (frames) reinterpret_cast<uint2 *>(frames)[i] = tx_frame(cw);
   }
+  if constexpr (CAN) cl4.finish(can, live);
 }
 
 // Two robots per lane (256-robot chunks b and b + G of the tiled state, G the tick blocks):

@@ -243,31 +243,50 @@ int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint3
 }
 
 // RS s64_rawAngleSumPrev in the tick's layout (64-robot tiles of 16-byte wheel pairs,
-// lane_rs.hpp rs_prev_at) <-> [4][pitch] int64 planes (the motor state's sums, the ABI's [4][N]
-// readout).  Grid-stride.
-template <bool TO_ROWS>
-__global__ __launch_bounds__(kBlock) void k_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch) {
+// lane_rs.hpp rs_prev_at) -> [4][pitch] int64 planes (the ABI's [4][N] readout).  Grid-stride.
+__global__ __launch_bounds__(kBlock) void k_prev_out(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch) {
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    if constexpr (TO_ROWS) {
-      reinterpret_cast<longlong2 *>(dst)[rs_prev_at(i, 0)] = make_longlong2(src[i], src[pitch + i]);
-      reinterpret_cast<longlong2 *>(dst)[rs_prev_at(i, 1)] = make_longlong2(src[2 * pitch + i], src[3 * pitch + i]);
+    const longlong2 a = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 0)];
+    const longlong2 b = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 1)];
+    dst[i] = a.x;
+    dst[pitch + i] = a.y;
+    dst[2 * pitch + i] = b.x;
+    dst[3 * pitch + i] = b.y;
+  }
+}
+// the motor state's split sums (fmskf_internal.hpp m_sum_lo / m_sum_hi) as whole int64 sums:
+// TO_PREV into the RS previous-sum tiles, else into [4][pitch] planes (get_rawAngleSum readout)
+template <bool TO_PREV>
+__global__ __launch_bounds__(kBlock) void k_motor_sums(const uint32_t *lo, const int32_t *hi, int64_t *dst, uint64_t n,
+                                                       uint64_t pitch) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    int64_t s[4];
+    motor_sum_load(lo, hi, i, s);
+    if constexpr (TO_PREV) {
+      rs_prev_store(dst, i, s);
     } else {
-      const longlong2 a = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 0)];
-      const longlong2 b = reinterpret_cast<const longlong2 *>(src)[rs_prev_at(i, 1)];
-      dst[i] = a.x;
-      dst[pitch + i] = a.y;
-      dst[2 * pitch + i] = b.x;
-      dst[3 * pitch + i] = b.y;
+#pragma unroll
+      for (int w = 0; w < 4; w++) dst[w * pitch + i] = s[w];
     }
   }
 }
 
-int launch_sums_rows(const int64_t *src, int64_t *dst, uint64_t n, uint64_t pitch, bool to_rows, hipStream_t st) {
-  if (n == 0) return 0;
+static inline dim3 grid_stride(uint64_t n) {
   const uint64_t b = (n + kBlock - 1) / kBlock;
-  const dim3 g((unsigned)(b < (1u << 20) ? b : (1u << 20)));
-  if (to_rows) k_sums_rows<true><<<g, kBlock, 0, st>>>(src, dst, n, pitch);
-  else k_sums_rows<false><<<g, kBlock, 0, st>>>(src, dst, n, pitch);
+  return dim3((unsigned)(b < (1u << 20) ? b : (1u << 20)));
+}
+
+int launch_prev_out(const int64_t *prev, int64_t *dst, uint64_t n, uint64_t pitch, hipStream_t st) {
+  if (n == 0) return 0;
+  k_prev_out<<<grid_stride(n), kBlock, 0, st>>>(prev, dst, n, pitch);
+  return (int)hipGetLastError();
+}
+
+int launch_motor_sums(const uint32_t *lo, const int32_t *hi, int64_t *dst, uint64_t n, uint64_t pitch, bool to_prev,
+                      hipStream_t st) {
+  if (n == 0) return 0;
+  if (to_prev) k_motor_sums<true><<<grid_stride(n), kBlock, 0, st>>>(lo, hi, dst, n, pitch);
+  else k_motor_sums<false><<<grid_stride(n), kBlock, 0, st>>>(lo, hi, dst, n, pitch);
   return (int)hipGetLastError();
 }
 

@@ -45,9 +45,13 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
     int64_t sum[4] = {0, 0, 0, 0};
     if (PRED) {
       r = reinterpret_cast<const uint2 *>(a.in.rpm)[j];
-      const int64_t *sp = a.in.angle_sum + (uint64_t)t * st * 4;
+      if (a.in.msum_lo) {  // the motor state's sums (single tick; wave-uniform)
+        motor_sum_load(a.in.msum_lo, a.in.msum_hi, i, sum);
+      } else {
+        const int64_t *sp = a.in.angle_sum + (uint64_t)t * st * 4;
 #pragma unroll
-      for (int w = 0; w < 4; w++) sum[w] = sp[w * a.in.sum_pitch + i];
+        for (int w = 0; w < 4; w++) sum[w] = sp[w * a.in.sum_pitch + i];
+      }
     }
     rs_tick1<LIBM, CORR, PRED>(s, yaw, r, sum, a.in.sintab);
   }
@@ -102,7 +106,17 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
     li[r] = (uint32_t)(i - hb[r]);
     uint64_t rv;
-    if constexpr (SO) {
+    if (a.in.msum_lo) {  // the motor state's sums: [N][4] low and high words (wave-uniform branch)
+      yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
+      rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
+      const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_lo + hb[r] * 4), li[r] * 16u, 0, CP);
+      const auto hw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_hi + hb[r] * 4), li[r] * 16u, 0, CP);
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const uint32_t l = lw[w], h = hw[w];  // element copies (see kf6_load_in)
+        sum[r][w] = (int64_t)(((uint64_t)h << 32) | l);
+      }
+    } else if constexpr (SO) {
       yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
       rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
       const auto rs = rsrc_span(a.in.angle_sum + hb[r]);

@@ -34,6 +34,15 @@ __device__ __forceinline__ void rs_prev_load(const int64_t *prev, uint64_t i, in
   pv[2] = b.x;
   pv[3] = b.y;
 }
+// the motor state's s64_rawAngleSum of robot i from its split halves (fmskf_internal.hpp m_sum_lo)
+__device__ __forceinline__ void motor_sum_load(const uint32_t *lo, const int32_t *hi, uint64_t i, int64_t (&s)[4]) {
+  const uint4 l = reinterpret_cast<const uint4 *>(lo)[i];
+  const int4 h = reinterpret_cast<const int4 *>(hi)[i];
+  s[0] = (int64_t)(((uint64_t)(uint32_t)h.x << 32) | l.x);
+  s[1] = (int64_t)(((uint64_t)(uint32_t)h.y << 32) | l.y);
+  s[2] = (int64_t)(((uint64_t)(uint32_t)h.z << 32) | l.z);
+  s[3] = (int64_t)(((uint64_t)(uint32_t)h.w << 32) | l.w);
+}
 __device__ __forceinline__ void rs_prev_store(int64_t *prev, uint64_t i, const int64_t (&pv)[4]) {
   reinterpret_cast<longlong2 *>(prev)[rs_prev_at(i, 0)] = make_longlong2(pv[0], pv[1]);
   reinterpret_cast<longlong2 *>(prev)[rs_prev_at(i, 1)] = make_longlong2(pv[2], pv[3]);

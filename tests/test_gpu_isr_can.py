@@ -258,3 +258,117 @@ def test_rs_prev_in_motor_sums(orc, tmp_path):
     finally:
         e.close()
         torch.cuda.set_stream(prev_stream)
+
+
+# ---- the split angle sums across 2^32 (round 6: low words every frame, high words on a carry)
+_M64 = (1 << 64) - 1
+
+
+def _ck_hash(body: bytes) -> int:
+    """api_checkpoint.cpp CkHash: 64-bit multiply-xor over 8-byte little-endian words, the tail
+    zero-padded, xor the length"""
+    h = 0x9E3779B97F4A7C15
+    pad = body + b"\0" * (-len(body) % 8)
+    for (w,) in __import__("struct").iter_unpack("<Q", pad):
+        h = ((h ^ w) * 0x100000001B3) & _M64
+        h ^= h >> 29
+    return h ^ len(body)
+
+
+def _patch_motor_sums(path, n, sums):
+    """rewrite the motor group's angle sums of an RS checkpoint (groups 1 | 4 | 8) to `sums`
+    ([N][4] int64) and fix the checksum: a test-side forge of the split low / high words"""
+    import struct
+    from fmskf._lib import Config, CtrlParams
+    blob = bytearray(open(path, "rb").read())
+    groups = struct.unpack_from("<I", blob, 40)[0]
+    assert groups == 1 | 4 | 8, groups
+    pos = 88 + C_sizeof(Config) + C_sizeof(CtrlParams)
+    secs = []
+    while pos < len(blob):
+        b = struct.unpack_from("<Q", blob, pos)[0]
+        secs.append((pos + 8, b))
+        pos += 8 + b
+    # estimator group (RS: x, prev sums, counters), then the motor group: micro, angle, prev,
+    # prev_micro, rpm, curr, sum_lo, sum_hi, iir_y
+    (lo_off, lo_b), (hi_off, hi_b) = secs[3 + 6], secs[3 + 7]
+    assert lo_b == hi_b == 16 * n
+    u = np.asarray(sums, np.int64).reshape(n, 4).view(np.uint64)
+    blob[lo_off:lo_off + lo_b] = (u & 0xFFFFFFFF).astype(np.uint32).tobytes()
+    blob[hi_off:hi_off + hi_b] = (u >> 32).astype(np.uint32).tobytes()
+    body = bytes(blob[88:])
+    struct.pack_into("<QQ", blob, 64, len(body), _ck_hash(body))
+    open(path, "wb").write(bytes(blob))
+
+
+def C_sizeof(t):
+    import ctypes
+    return ctypes.sizeof(t)
+
+
+def test_angle_sums_carry_across_2p32(orc, tmp_path):
+    """s64_rawAngleSum (VD_motor_if_m2006.cpp:66-69) is kept as low / high 32-bit words and a frame
+    writes the high word only when its delta carries.  Sums forged next to every carry boundary
+    (2^32 and 0 of the low word, negative and positive high words) are driven across it for a
+    dozen ticks by +-3000..4000-count steps through every CAN path -- the fused RS CAN+ISR (its PS
+    and whole-sum forms), fmskf_ingest_can (k_can4) with the RS tick on the motor state, and the
+    masked wheel-per-lane kernel -- against the oracle's int64 sums, the previous sums and the
+    pose, bit for bit."""
+    n, T = 515, 14
+    rng = np.random.default_rng(2032)
+    dirs = np.array([1, 1, -1, -1])
+    raw0 = rng.integers(0, 8192, (n, 4))
+    step = rng.choice([4000, -4000, 3000, -3500], (n, 4))
+
+    def frames(t):
+        raw = (raw0 + t * step) % 8192
+        fr = np.zeros((n, 4, 8), np.uint8)
+        for k, v in enumerate((raw, rng.integers(-900, 900, (n, 4)) * dirs, np.full((n, 4), 100))):
+            u = np.asarray(v, np.int64) & 0xFFFF
+            fr[:, :, 2 * k] = (u >> 8).astype(np.uint8)
+            fr[:, :, 2 * k + 1] = (u & 0xFF).astype(np.uint8)
+        st = np.ascontiguousarray(np.broadcast_to(((t + 1) * 1000 + np.arange(4) * 7) & 0x7FFF, (n, 4))).astype(np.int16)
+        return fr, st
+
+    yaw = rng.uniform(-180, 180, (T + 2, n)).astype(np.float32)
+    mb = orc.MotorBatch(n)
+    ck = str(tmp_path / "rs.ck")
+    with Engine("rs", n) as e:  # two warm-up ticks, then the checkpoint
+        for t in range(2):
+            f, s = frames(t)
+            e.isr_tick_can(f, s, frames=False, yaw_deg=yaw[t])
+            mb.rx(f, s)
+        e.save_state(ck)
+    lo = rng.choice([(1 << 32) - 6000, 6000, (1 << 31) - 5000, (1 << 31) + 5000], (n, 4)).astype(np.int64)
+    hi = rng.integers(-3, 3, (n, 4)).astype(np.int64)
+    sums = (hi << 32) + lo
+    _patch_motor_sums(ck, n, sums)
+    orc._struct_view(mb.m, orc.M2006State)["angle_sum"][:] = sums.reshape(-1)
+    pos, vel = np.zeros((3, n), np.float32), np.zeros((3, n), np.float32)
+    with Engine("rs", n) as e:
+        e.load_state(ck)
+        x, _ = e.get_state()
+        pos[:], vel[:] = x[:3], x[3:]
+        prev = e.get_prev_sum()
+        np.testing.assert_array_equal(e.get_motors()["angle_sum"], sums.T)
+        for t in range(2, T):
+            f, s = frames(t)
+            kind = t % 4
+            if kind in (0, 1):  # the fused call (whole sums on its first tick, PS after)
+                e.isr_tick_can(f, s, frames=False, yaw_deg=yaw[t])
+                mb.rx(f, s)
+            elif kind == 2:  # k_can4, then the RS tick on the motor state's sums
+                e.ingest_can(f, s)
+                mb.rx(f, s)
+                e.tick(yaw_deg=yaw[t])
+            else:  # the masked wheel-per-lane kernel (every wheel present), then the ISR
+                e.ingest_can(f, s, present=np.full(n, 15, np.uint8))
+                mb.rx(f, s)
+                e.isr_tick(frames=False, yaw_deg=yaw[t])
+            orc.rs_tick(pos, vel, prev, yaw[t], np.ascontiguousarray(mb.field("angle_sum").T), mb.field("rpm"))
+            np.testing.assert_array_equal(e.get_motors()["angle_sum"], mb.field("angle_sum").T, err_msg=f"tick {t}")
+            x, _ = e.get_state()
+            np.testing.assert_array_equal(bits(x[:3]), bits(pos), err_msg=f"pose tick {t}")
+        np.testing.assert_array_equal(e.get_prev_sum(), prev)
+    moved = mb.field("angle_sum") >> 32 != hi
+    assert moved.sum() > n // 2, moved.sum()  # many wheels carried into another high word

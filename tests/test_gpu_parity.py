@@ -1146,9 +1146,9 @@ def test_wt901_wave_patterns_bitexact():
 
 
 def test_can_rs_per_plane_descriptor_forms_bitexact():
-    """The per-plane descriptor forms of k_can4 and k_rs2 (FMSKF_CAN_VARIANT=0,
-    FMSKF_RS_VARIANT=0; the default reaches every plane of an array through one descriptor and
-    soffset) in a child process: the CAN ingest and RS tick parity tests against the oracle."""
+    """The per-plane descriptor form of k_rs2 (FMSKF_RS_VARIANT=0; the default reaches every plane
+    of an array through one descriptor and soffset) in a child process: the RS tick parity tests
+    against the oracle, with the CAN ingest tests beside them (round 6: k_can4 has one form)."""
     import os
     import subprocess
     import sys
@@ -1163,7 +1163,7 @@ def test_can_rs_per_plane_descriptor_forms_bitexact():
         "T.test_rs_tick_bitexact(orc, T.TABLE)\n"
         "T.test_rs_tick_bitexact(orc, T.LIBM)\n"
         "print('planes ok')\n")
-    env = dict(os.environ, FMSKF_CAN_VARIANT="0", FMSKF_RS_VARIANT="0")
+    env = dict(os.environ, FMSKF_RS_VARIANT="0")
     out = subprocess.run([sys.executable, "-c", script, root,
                           os.path.join(root, "roboken-fmskf-robot-controller_amd"),
                           os.path.join(root, "tests")],

@@ -91,8 +91,9 @@ def secondary(root, out):
 # written (56); WT901 standard poll: row, len, parser count / flags, magnetometer read (60),
 # flags, error, 4 registers (round 6: the other eleven only in the snapshot row), snapshot row,
 # yaw / gyro z written (50; the empty parser window is neither read nor written); CAN RX, four
-# wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, sum read (120), those
-# state fields plus rpm and curr written (96); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
+# wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, the sums' low words read
+# (104), those state fields plus rpm and curr written (80; round 6: the sums' high words only on
+# a carry); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128); the fused
 # ISR with and without the CAN RX (below).  The
 # counters are corrected with the KF6 calibration of profiles/pmc_traffic.json (the same
@@ -101,14 +102,14 @@ PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 60, 50),
-    ("can_ingest_2p20", "k_can4", 120, 96),
+    ("can_ingest_2p20", "k_can4", 104, 80),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
     # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
     # without its rpm (209) and writes (152), the 0x200 frame (8 w)
     ("isr_kf6_2p20", "k_isr_kf6", 124 + 209, 108 + 152 + 8),
     # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 120 / 96, the rpm
     # plane no longer read
-    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 209 + 120, 108 + 152 + 8 + 96),
+    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 209 + 104, 108 + 152 + 8 + 80),
     # the reference-semantics ISR (k_isr_rs) on the motor state: the RS tick's 84 / 56 with the
     # control step's 209 / 152 and the frame; with the CAN RX fused in, the rpm and sums not read
     ("isr_rs_2p20", "k_isr_rs", 84 + 209, 56 + 152 + 8),
@@ -117,10 +118,10 @@ PATHS = [
     # frame
     ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 217, 216 + 152 + 8),
     # round 6: the previous sums neither read nor written while they equal the motor sums (PS)
-    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 209 + 120, 56 - 32 + 152 + 8 + 96),
+    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 209 + 104, 56 - 32 + 152 + 8 + 80),
     # the EKF9 ISR with the tick's CAN RX fused in: + the CAN row's 120 / 96, the control step's
     # rpm plane no longer read
-    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 217 - 8 + 120, 216 + 152 + 8 + 96),
+    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 217 - 8 + 104, 216 + 152 + 8 + 80),
 ]
 
 
