@@ -6,6 +6,7 @@
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
 #include "kf_generic.hpp"
+#include "lane_rs.hpp"
 
 #pragma clang fp contract(off)
 
@@ -51,13 +52,18 @@ struct CanWheel {
   float iir_y;
   int32_t d;  // s64_rawAngleSum += d (|d| <= 4096)
 };
-// s64_rawAngleSum += d on the split halves: the low word wraps, the carry (-1, 0, +1) goes to the
-// high word
+// s64_rawAngleSum += d on the split halves (fmskf_internal.hpp m_sum_lo: sum = hi * 2^32 + the
+// low word read as int32): the low word wraps, the carry (-1, 0, +1) goes to the high word.  A
+// signed low word carries only where the sum crosses an odd multiple of 2^31, so a wheel that
+// turns back and forth around its start (sum near 0) never does; an unsigned one carried at every
+// crossing of 0 and measured 8% slower at 2^22 robots on random frames
 __device__ __forceinline__ uint32_t sum_add(uint32_t lo, int32_t d, int32_t &carry) {
-  const int64_t t = (int64_t)lo + d;
-  carry = (int32_t)(t >> 32);
-  return (uint32_t)t;
+  const int64_t t = (int64_t)(int32_t)lo + d;
+  const int32_t nl = (int32_t)(uint32_t)t;
+  carry = (int32_t)((t - nl) >> 32);
+  return (uint32_t)nl;
 }
+
 // the speed sample rx_callback feeds the IIR1 (VD_motor_if_m2006.cpp:49-63): the wrapped angle
 // step over the wrapped microsecond step, with the M7's wrapping MUL and SDIV x/0 = 0
 __device__ __forceinline__ float speed_x(int16_t new_angle, int16_t old_angle, int16_t micro, int16_t old_micro) {
@@ -184,7 +190,7 @@ struct Can4Lane {
       shi[2] = (int32_t)hw[2];
       shi[3] = (int32_t)hw[3];
 #pragma unroll
-      for (int w = 0; w < 4; w++) sm[w] = (int64_t)(((uint64_t)(uint32_t)shi[w] << 32) | slo[w]);
+      for (int w = 0; w < 4; w++) sm[w] = motor_sum_join(shi[w], slo[w]);
     }
     sv = ld_span<uint64_t, IP>(rsrc_span(a.stamps + hb * 4), li, 0);
     mv = ld_span<uint64_t, LP>(rsrc_span(a.micro + hb * 4), li, 0);

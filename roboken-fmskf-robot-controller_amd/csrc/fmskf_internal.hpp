@@ -58,11 +58,13 @@ struct DevState {
                                // flt_dltOutAngle_rad is formed from the two at readout
   int16_t *m_rpm = nullptr;    // [N][4]
   int16_t *m_curr = nullptr;   // [N][4]
-  // s64_rawAngleSum of the four wheels, split (round 6): the low 32 bits [N][4] (one 16-byte access
-  // per robot), which every frame updates, and the high 32 bits [N][4], which a frame touches only
-  // when its delta (|d| <= 4096) carries across 2^32.  The CAN RX moves 16 + 16 B of sums per robot
-  // instead of 32 + 32; readers of the whole sum (the RS tick on the motor state, the readouts)
-  // load both halves (motor_sum_load).  m_sum_lo doubles as "the motor state exists".
+  // s64_rawAngleSum of the four wheels, split (round 6): sum = hi * 2^32 + lo read as int32.  The
+  // low words [N][4] (one 16-byte access per robot) change with every frame, the high words [N][4]
+  // only when a frame's delta (|d| <= 4096) carries the low word out of the int32 range (the sum
+  // crossing an odd multiple of 2^31: never for a wheel near its start).  The CAN RX moves 16 + 16 B
+  // of sums per robot instead of 32 + 32; readers of the whole sum (the RS tick on the motor state,
+  // the readouts) load both halves (lane_rs.hpp motor_sum_load).  m_sum_lo doubles as "the motor
+  // state exists"; all-zero is the reset state.
   uint32_t *m_sum_lo = nullptr;
   int32_t *m_sum_hi = nullptr;
   float *m_iir_y = nullptr;    // [N][4] (one 16-byte access per robot in k_can4)

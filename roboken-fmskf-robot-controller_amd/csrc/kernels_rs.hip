@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
 #pragma unroll
       for (int w = 0; w < 4; w++) {
         const uint32_t l = lw[w], h = hw[w];  // element copies (see kf6_load_in)
-        sum[r][w] = (int64_t)(((uint64_t)h << 32) | l);
+        sum[r][w] = motor_sum_join((int32_t)h, l);
       }
     } else if constexpr (SO) {
       yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);

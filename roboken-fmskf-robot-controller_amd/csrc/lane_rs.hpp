@@ -34,14 +34,19 @@ __device__ __forceinline__ void rs_prev_load(const int64_t *prev, uint64_t i, in
   pv[2] = b.x;
   pv[3] = b.y;
 }
-// the motor state's s64_rawAngleSum of robot i from its split halves (fmskf_internal.hpp m_sum_lo)
+// one s64_rawAngleSum from its split halves: hi * 2^32 + the low word read as int32
+// (fmskf_internal.hpp m_sum_lo)
+__host__ __device__ __forceinline__ int64_t motor_sum_join(int32_t hi, uint32_t lo) {
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) + (uint64_t)(int64_t)(int32_t)lo);
+}
+// the motor state's s64_rawAngleSum of robot i from its split halves
 __device__ __forceinline__ void motor_sum_load(const uint32_t *lo, const int32_t *hi, uint64_t i, int64_t (&s)[4]) {
   const uint4 l = reinterpret_cast<const uint4 *>(lo)[i];
   const int4 h = reinterpret_cast<const int4 *>(hi)[i];
-  s[0] = (int64_t)(((uint64_t)(uint32_t)h.x << 32) | l.x);
-  s[1] = (int64_t)(((uint64_t)(uint32_t)h.y << 32) | l.y);
-  s[2] = (int64_t)(((uint64_t)(uint32_t)h.z << 32) | l.z);
-  s[3] = (int64_t)(((uint64_t)(uint32_t)h.w << 32) | l.w);
+  s[0] = motor_sum_join(h.x, l.x);
+  s[1] = motor_sum_join(h.y, l.y);
+  s[2] = motor_sum_join(h.z, l.z);
+  s[3] = motor_sum_join(h.w, l.w);
 }
 __device__ __forceinline__ void rs_prev_store(int64_t *prev, uint64_t i, const int64_t (&pv)[4]) {
   reinterpret_cast<longlong2 *>(prev)[rs_prev_at(i, 0)] = make_longlong2(pv[0], pv[1]);

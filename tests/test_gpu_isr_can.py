@@ -275,6 +275,13 @@ def _ck_hash(body: bytes) -> int:
     return h ^ len(body)
 
 
+def _split_sums(sums):
+    """fmskf_internal.hpp m_sum_lo / m_sum_hi: sum = hi * 2^32 + lo read as int32"""
+    s = np.asarray(sums, np.int64)
+    lo = ((s + (1 << 31)) & 0xFFFFFFFF) - (1 << 31)  # the signed low word
+    return lo.astype(np.int32), ((s - lo) >> 32).astype(np.int32)
+
+
 def _patch_motor_sums(path, n, sums):
     """rewrite the motor group's angle sums of an RS checkpoint (groups 1 | 4 | 8) to `sums`
     ([N][4] int64) and fix the checksum: a test-side forge of the split low / high words"""
@@ -293,9 +300,9 @@ def _patch_motor_sums(path, n, sums):
     # prev_micro, rpm, curr, sum_lo, sum_hi, iir_y
     (lo_off, lo_b), (hi_off, hi_b) = secs[3 + 6], secs[3 + 7]
     assert lo_b == hi_b == 16 * n
-    u = np.asarray(sums, np.int64).reshape(n, 4).view(np.uint64)
-    blob[lo_off:lo_off + lo_b] = (u & 0xFFFFFFFF).astype(np.uint32).tobytes()
-    blob[hi_off:hi_off + hi_b] = (u >> 32).astype(np.uint32).tobytes()
+    lo, hi = _split_sums(sums)
+    blob[lo_off:lo_off + lo_b] = lo.reshape(n, 4).tobytes()
+    blob[hi_off:hi_off + hi_b] = hi.reshape(n, 4).tobytes()
     body = bytes(blob[88:])
     struct.pack_into("<QQ", blob, 64, len(body), _ck_hash(body))
     open(path, "wb").write(bytes(blob))
@@ -307,11 +314,12 @@ def C_sizeof(t):
 
 
 def test_angle_sums_carry_across_2p32(orc, tmp_path):
-    """s64_rawAngleSum (VD_motor_if_m2006.cpp:66-69) is kept as low / high 32-bit words and a frame
-    writes the high word only when its delta carries.  Sums forged next to every carry boundary
-    (2^32 and 0 of the low word, negative and positive high words) are driven across it for a
-    dozen ticks by +-3000..4000-count steps through every CAN path -- the fused RS CAN+ISR (its PS
-    and whole-sum forms), fmskf_ingest_can (k_can4) with the RS tick on the motor state, and the
+    """s64_rawAngleSum (VD_motor_if_m2006.cpp:66-69) is kept as a signed low 32-bit word and a high
+    word, and a frame writes the high word only when its delta carries the low word out of the
+    int32 range.  Sums forged next to the carry boundaries (odd multiples of 2^31, with negative
+    and positive high words) and next to 0 and 2^32 (no carry) are driven across them for a dozen
+    ticks by +-3000..4000-count steps through every CAN path -- the fused RS CAN+ISR (its PS and
+    whole-sum forms), fmskf_ingest_can (k_can4) with the RS tick on the motor state, and the
     masked wheel-per-lane kernel -- against the oracle's int64 sums, the previous sums and the
     pose, bit for bit."""
     n, T = 515, 14
@@ -370,5 +378,5 @@ def test_angle_sums_carry_across_2p32(orc, tmp_path):
             x, _ = e.get_state()
             np.testing.assert_array_equal(bits(x[:3]), bits(pos), err_msg=f"pose tick {t}")
         np.testing.assert_array_equal(e.get_prev_sum(), prev)
-    moved = mb.field("angle_sum") >> 32 != hi
+    moved = _split_sums(mb.field("angle_sum"))[1] != _split_sums(sums)[1]
     assert moved.sum() > n // 2, moved.sum()  # many wheels carried into another high word
