@@ -9,6 +9,8 @@
 //
 // Algorithmic bytes per instance-tick: pos 12 B r+w, prev 32 B r+w,
 // sums 32 B, yaw 4 B, rpm 8 B, vel 12 B w  -> 12*2 + 32*2 + 32 + 4 + 8 + 12 = 144 B.
+#include <type_traits>
+
 #include "fmskf_device.hpp"
 #include "fmskf_internal.hpp"
 #include "kf_generic.hpp"
@@ -83,7 +85,10 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 // SO (round 4): one span descriptor per array and robot slot (rsrc_span) with the planes of
 // x, prev and the encoder sums reached through soffset, instead of one clamped descriptor per
 // plane (16 -> 5 per slot; the launcher checks the 4 GiB span).
-template <bool LIBM, int CP = 0, bool SO = false>
+// MS: the sums are the motor state's split words (a.in.msum_lo / msum_hi; a compile-time choice:
+// a run-time branch between the two load forms slowed both, 25.4 -> 26.4 us on caller sums and
+// 20.7 -> 23.5 on the motor state at 2^20)
+template <bool LIBM, int CP = 0, bool SO = false, bool MS = false>
 __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   extern __shared__ double occ_cap[];
   (void)occ_cap;
@@ -106,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     hb[r] = __builtin_amdgcn_readfirstlane((uint32_t)i) & ~(uint32_t)(kBlock - 1);
     li[r] = (uint32_t)(i - hb[r]);
     uint64_t rv;
-    if (a.in.msum_lo) {  // the motor state's sums: [N][4] low and high words (wave-uniform branch)
+    if constexpr (MS) {  // the motor state's sums: [N][4] low and high words
       yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
       rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
       const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_lo + hb[r] * 4), li[r] * 16u, 0, CP);
@@ -200,22 +205,25 @@ int launch_rs(const DevState &s, const TickIn &in, bool libm, bool correct, bool
       return e ? atoi(e) : 1;
     }();
     const bool so = var != 0 && 6 * s.pitch * 4 <= 0xFFFFFFFFull && 4 * in.sum_pitch * 8 <= 0xFFFFFFFFull;
+    const bool ms = in.msum_lo != nullptr;
+    auto go = [&](auto cp, auto so_, auto ms_) {
+      constexpr int C = decltype(cp)::value;
+      constexpr bool S = decltype(so_)::value, M = decltype(ms_)::value;
+      if (libm) k_rs2<true, C, S, M><<<g2, kBlock, lds, st>>>(a);
+      else k_rs2<false, C, S, M><<<g2, kBlock, lds, st>>>(a);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    using NT = std::integral_constant<int, kStateNT>;
+    using C0 = std::integral_constant<int, 0>;
     if (state_nt(s.n * 124)) {
-      if (so) {
-        if (libm) k_rs2<true, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
-        else k_rs2<false, kStateNT, true><<<g2, kBlock, lds, st>>>(a);
-      } else {
-        if (libm) k_rs2<true, kStateNT><<<g2, kBlock, lds, st>>>(a);
-        else k_rs2<false, kStateNT><<<g2, kBlock, lds, st>>>(a);
-      }
+      if (ms) go(NT{}, T{}, T{});
+      else if (so) go(NT{}, T{}, F{});
+      else go(NT{}, F{}, F{});
     } else {
-      if (so) {
-        if (libm) k_rs2<true, 0, true><<<g2, kBlock, lds, st>>>(a);
-        else k_rs2<false, 0, true><<<g2, kBlock, lds, st>>>(a);
-      } else {
-        if (libm) k_rs2<true><<<g2, kBlock, lds, st>>>(a);
-        else k_rs2<false><<<g2, kBlock, lds, st>>>(a);
-      }
+      if (ms) go(C0{}, T{}, T{});
+      else if (so) go(C0{}, T{}, F{});
+      else go(C0{}, F{}, F{});
     }
     return (int)hipGetLastError();
   }
