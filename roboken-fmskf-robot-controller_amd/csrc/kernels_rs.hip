@@ -82,6 +82,10 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
 #ifndef FMSKF_IN_CPOL
 #define FMSKF_IN_CPOL 2
 #endif
+// the cache policy of the motor state's sums in the MS form (-1: the state's, CP)
+#ifndef FMSKF_MS_CPOL
+#define FMSKF_MS_CPOL 2
+#endif
 // SO (round 4): one span descriptor per array and robot slot (rsrc_span) with the planes of
 // x, prev and the encoder sums reached through soffset, instead of one clamped descriptor per
 // plane (16 -> 5 per slot; the launcher checks the 4 GiB span).
@@ -114,8 +118,9 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     if constexpr (MS) {  // the motor state's sums: [N][4] low and high words
       yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
       rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
-      const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_lo + hb[r] * 4), li[r] * 16u, 0, CP);
-      const auto hw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_hi + hb[r] * 4), li[r] * 16u, 0, CP);
+      constexpr int MP = FMSKF_MS_CPOL < 0 ? CP : FMSKF_MS_CPOL;
+      const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_lo + hb[r] * 4), li[r] * 16u, 0, MP);
+      const auto hw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_hi + hb[r] * 4), li[r] * 16u, 0, MP);
 #pragma unroll
       for (int w = 0; w < 4; w++) {
         const uint32_t l = lw[w], h = hw[w];  // element copies (see kf6_load_in)
