@@ -340,7 +340,7 @@ def secondary_configs(dev, stream, ticks: int, trig):
 
 # the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20) and the C610 RX of four wheels
 # (can_ingest_2p20)
-WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 8 + 6 + 32 + 8
+WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4
 CAN_RX_BYTES = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
@@ -351,12 +351,14 @@ PATH_BYTES = {
     "rs_tick_2p20_padded_sums": 140,
     "rs_tick_2p20_device_state": 140,
     # WT901 standard poll: row 48 + len 4, the parser count and update flags 2 r, flags and error
-    # 2 w, 4 registers 8 w (GZ, Yaw, TEMP, VERSION: the other eleven the poll writes live in the
-    # snapshot row, round 6), magnetometer 6 r, the snapshot row 32 w (the words updateData
-    # reads: the Data page is formed at readout), yaw and gyro z 8 w; the parser window is empty
+    # 2 w, 2 registers 4 w (TEMP, VERSION: of the other thirteen the poll writes, eleven live in
+    # the snapshot row and GZ / Yaw in the Yaw / GZ dword, round 6), magnetometer 6 r, the
+    # snapshot row 32 w (the words updateData reads: the Data page is formed at readout), the Yaw
+    # / GZ words 4 w (what the tick reads as its yaw and gyro z); the parser window is empty
     # before and after such a poll, so its words are neither read nor written (round 4: 197 B,
     # with the window words, q_init read and the 64-byte page written; round 5: 132 B, the 15
-    # registers written to sReg as well as to the row)
+    # registers written to sReg as well as to the row; round 6: 110 B with GZ / Yaw in sReg and
+    # the yaw / gyro z floats, then 102)
     "wt901_ingest_2p20": WT901_POLL_BYTES,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
     # output y and the low word of the int64 sum read and written (round 6: the high word only on
@@ -370,9 +372,9 @@ PATH_BYTES = {
     # loads it once) + the 8-byte 0x200 frame
     "isr_kf6_2p20": 232 + 369 - 8 + 8,
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
-    # ingested yaw / gyro page and wheel rpm (the same 16 B as a record), and every 10th tick
-    # the WT901 poll
-    "firmware_loop_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) + WT901_POLL_BYTES / 10,
+    # ingested Yaw / GZ words (one dword for the record's two floats, round 6) and wheel rpm, and
+    # every 10th tick the WT901 poll
+    "firmware_loop_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 4 + WT901_POLL_BYTES / 10,
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
     # CAN row's 184 + the ISR's 601 without its rpm read
     "isr_can_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8,
@@ -395,7 +397,7 @@ PATH_BYTES = {
     "firmware_loop_rs_fused_2p20": CAN_RX_BYTES + (140 + 369 - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
-    "firmware_loop_kf6_fused_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8 + WT901_POLL_BYTES / 10,
+    "firmware_loop_kf6_fused_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8 - 4 + WT901_POLL_BYTES / 10,
 }
 
 

@@ -37,10 +37,12 @@ struct CkHeader {
   // layout bits of format 5 (0 in round-5 files), so a round-5 file is refused instead of loaded
   // scrambled: bit 0, the RS previous sums in 64-robot tiles of wheel pairs (round 6, lane_rs.hpp
   // rs_prev_at; [4][pitch] planes before); bit 1, the motor group's angle sums as split low /
-  // high words (round 6, fmskf_internal.hpp m_sum_lo; int64 [4][pitch] planes before)
+  // high words (round 6, fmskf_internal.hpp m_sum_lo; int64 [4][pitch] planes before); bit 2, the
+  // IMU group's yaw / gyro z as the Yaw / GZ register words (round 6, DevState::imu_yg; two float
+  // planes before)
   uint32_t layout;
 };
-constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u;
+constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u, kCkImuYg = 4u;
 struct CkSection {
   void *dev;
   size_t bytes;
@@ -66,8 +68,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_err, (size_t)n});
     v.push_back({s.imu_qinit, (size_t)4 * n * 4});
     v.push_back({s.imu_snap, (size_t)kSnapWords * n * 2});
-    v.push_back({s.imu_yaw, (size_t)n * 4});
-    v.push_back({s.imu_gz, (size_t)n * 4});
+    v.push_back({s.imu_yg, (size_t)n * 4});
     v.push_back({s.imu_qprev, (size_t)4 * n * 4});
   }
   if (groups & 4) {
@@ -100,7 +101,7 @@ void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->elem = h->d.elem;
   hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
   hd->m_pitch = plane_pitch(h->s.n);
-  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit;
+  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit | kCkImuYg;
   const uint64_t w = tile_w_elem(4);
   hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
 }
@@ -240,7 +241,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
       fail(FMSKF_EINVAL, "checkpoint does not match this handle (ABI, model, flags, N or layout)");
     if ((hd.groups & 4) && hd.m_pitch != me.m_pitch) fail(FMSKF_EINVAL, "checkpoint motor layout differs");
     if (hd.layout != me.layout)
-      fail(FMSKF_EINVAL, "checkpoint layout differs (a round-5 file: int64 motor sum planes, RS previous sums as planes)");
+      fail(FMSKF_EINVAL, "checkpoint layout differs (an older file: int64 motor sum planes, RS previous sums as planes, IMU yaw / gyro z floats)");
     if ((hd.groups & 8) && (hd.ctrl_tile != me.ctrl_tile || hd.ctrl_pitch != me.ctrl_pitch))
       fail(FMSKF_EINVAL, "checkpoint control layout differs (tiling / pitch)");
     if (!(hd.groups & 1u)) fail(FMSKF_EINVAL, "checkpoint holds no estimator state");

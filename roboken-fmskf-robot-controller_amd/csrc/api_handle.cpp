@@ -111,8 +111,7 @@ void zero_imu(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_snap, 0, kSnapWords * n * 2, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_yaw, 0, n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_gz, 0, n * 4, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_yg, 0, n * 4, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_qprev, 0, 4 * n * 4, st), "reset imu");
 }
 void zero_motors(fmskf_ctx *h) {
@@ -142,8 +141,7 @@ void ensure_imu(fmskf_ctx *h) {
   s.imu_err = h->alloc<uint8_t>(n);
   s.imu_qinit = h->alloc<float>(4 * n);
   s.imu_snap = h->alloc<int16_t>(kSnapWords * n);
-  s.imu_yaw = h->alloc<float>(n);
-  s.imu_gz = h->alloc<float>(n);
+  s.imu_yg = h->alloc<uint32_t>(n);
   s.imu_qprev = h->alloc<float>(4 * n);
   zero_imu(h);
 }
@@ -296,7 +294,8 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.yaw_deg, "yaw_deg");
         if (!t.yaw_deg) {
           ensure_imu(h);
-          t.yaw_deg = s.imu_yaw;  // IMT::get_status_now_yaw: Data.angle[2]
+          t.yaw_deg = (const float *)s.imu_yg;  // IMT::get_status_now_yaw: Data.angle[2], its Yaw word
+          t.imu_words |= 1u;
         }
       }
       if (need_pred) {
@@ -317,8 +316,15 @@ TickIn resolve_inputs(fmskf_ctx *h, const fmskf_tick_inputs *in, bool need_upd, 
         dev_default(t.rpm, "rpm");
         if (!t.yaw_deg || !t.gyro_z) ensure_imu(h);
         if (!t.rpm) ensure_motors(h);
-        if (!t.yaw_deg) t.yaw_deg = s.imu_yaw;  // Data.angle[2]
-        if (!t.gyro_z) t.gyro_z = s.imu_gz;     // Data.gyro[2]
+        // Data.angle[2] / Data.gyro[2]: a NULL plane reads the IMU state's Yaw / GZ word
+        if (!t.yaw_deg) {
+          t.yaw_deg = (const float *)s.imu_yg;
+          t.imu_words |= 1u;
+        }
+        if (!t.gyro_z) {
+          t.gyro_z = (const float *)s.imu_yg;
+          t.imu_words |= 2u;
+        }
         if (!t.rpm) t.rpm = s.m_rpm;
       }
       break;

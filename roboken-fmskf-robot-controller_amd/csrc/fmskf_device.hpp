@@ -148,14 +148,36 @@ __device__ __forceinline__ double wrap_innov(double a) {
 // ---------------------------------------------------------------------------
 // IMU_IF_WT901C::Data, formed where it is read.  updateData (imu_if_wt901c.cpp:91-129) is a
 // pure function of 16 register words and q_init, so the WT901 kernel keeps the words of the
-// last successful poll (the snapshot row) and the two values the tick consumes (yaw, gyro z),
+// last successful poll (the snapshot row, and the Yaw / GZ words the tick consumes: imu_yg),
 // and the readers (fmskf_get_imu, VehicleInfo) form the page from them.  Snapshot row [N][16]
 // int16: accel x y z (0-2), gyro x y (3-4), mag x y z (5-7), roll, pitch (8-9), q0-q3 (10-13),
 // word 14 the flags below, word 15 zero.
 // (the row's flags and width: fmskf_internal.hpp kSnapValid / kSnapLatched / kSnapWords)
 
+// Data.angle[2] and Data.gyro[2] from the Yaw (low half) / GZ (high half) register words of
+// DevState::imu_yg, with updateData's operations (imu_if_wt901c.cpp:91-129): the readers form the
+// same floats the WT901 kernel stored before round 6.
+__host__ __device__ __forceinline__ float imu_yaw_deg(uint32_t yg) {
+  return (float)(int16_t)(yg & 0xFFFFu) / 32768.0f * 180.0f;
+}
+__host__ __device__ __forceinline__ float imu_gz_dps(uint32_t yg) {
+  return -((float)(int16_t)(yg >> 16) / 32768.0f * 2000.0f);
+}
+// A tick's yaw / gyro z from the dword its lane loaded: the IMU state's word when the call left
+// the plane NULL (`word`, wave-uniform: TickIn::imu_words), else the caller's float.  Both are
+// [N] dwords, so a kernel loads the same way either way and selects the conversion -- with a mask,
+// not `?:`: the compiler turned the uniform select into a branch around the conversion, whose
+// s_waitcnt vmcnt(0) stalled the KF6 plane-input tick behind every load it had issued (37.7-38.6
+// -> 42.3 us at 2^20)
+__device__ __forceinline__ float tick_word_sel(bool word, uint32_t w, float conv) {
+  const uint32_t m = 0u - (uint32_t)word;
+  return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, conv) & m) | (w & ~m));
+}
+__device__ __forceinline__ float tick_yaw(bool word, uint32_t w) { return tick_word_sel(word, w, imu_yaw_deg(w)); }
+__device__ __forceinline__ float tick_gz(bool word, uint32_t w) { return tick_word_sel(word, w, imu_gz_dps(w)); }
+
 // the Data page of a snapshot row (same operations and order as updateData): yaw = angle[2]
-// and gz = gyro[2] as the kernel stored them; qi: q_init as it was when the poll ran
+// and gz = gyro[2] from the Yaw / GZ words; qi: q_init as it was when the poll ran
 __device__ __forceinline__ void imu_data_page(const int16_t *w, float yaw, float gz, const float qi[4],
                                               float d[16]) {
   float acc[3], gyr[2], mag[3], ang[2], q[4];

@@ -48,8 +48,11 @@ struct DevState {
   // IMU_IF::Data is not stored: the WT901 kernel keeps the register words updateData reads
   // (fmskf_device.hpp imu_data_page), and the readers form the page
   int16_t *imu_snap = nullptr;    // snapshot rows [N][16] of the last successful poll
-  float *imu_yaw = nullptr;       // Data.angle[2] [N] (deg): what the tick reads as its yaw
-  float *imu_gz = nullptr;        // Data.gyro[2] [N] (deg/s, negated as Data publishes it)
+  // the Yaw (low half) and GZ (high half) register words of the last successful poll [N]: what
+  // the tick reads as its yaw and gyro z (Data.angle[2], Data.gyro[2]: fmskf_device.hpp
+  // imu_yaw_deg / imu_gz_dps, exact both ways).  Round 6: one dword plane instead of the two
+  // float planes, and while F_ROWREGS is set (kernels_ingest.hip) also the live GZ / Yaw registers
+  uint32_t *imu_yg = nullptr;
   float *imu_qprev = nullptr;     // [4][N] q_init before a poll that latched it (kSnapLatched)
   // MOTOR_IF_M2006 x 4 wheels
   int16_t *m_micro = nullptr;  // [N][4]
@@ -105,7 +108,12 @@ struct TickIn {
   double *fold_out;
   // host side only (never read by a kernel): the event the fused ENS launch attaches to the
   // kernel's own completion signal (launch_signal), or null
-  hipEvent_t ens_done;
+  hipEvent_t ens_done;  // bit 0: yaw_deg points at the IMU state's Yaw words, bit 1: gyro_z at its GZ words (both
+  // DevState::imu_yg, fmskf_device.hpp tick_yaw / tick_gz) -- a NULL plane of the call.  The host
+  // resolves the pointer: selecting it in the kernel took the KF6 plane-input k_kf6t from 64 to 87
+  // VGPRs (and a field inserted before the others, which moved their kernel-argument offsets, did
+  // the same).
+  uint32_t imu_words;
 };
 
 // k<<<g, kBlock, lds, st>>>(a); with `done`, the dispatch's own completion signal records the

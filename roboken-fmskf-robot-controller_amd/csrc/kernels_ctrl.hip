@@ -70,7 +70,7 @@ struct IsrRsArgs {
   uint64_t pitch;
   float *x;
   int64_t *prev;  // 64-robot tiles of wheel pairs (lane_rs.hpp rs_prev_at)
-  const float *yaw_deg;
+  const float *yaw_deg;      // the caller's plane, or the IMU state's Yaw words (yaw_word)
   const int16_t *rpm;
   const int64_t *angle_sum;  // [4][sum_pitch]: the caller's sums, or NULL: the motor state's
   uint64_t sum_pitch;
@@ -78,6 +78,7 @@ struct IsrRsArgs {
   const int32_t *msum_hi;
   const float *sintab;
   uint8_t *frames;
+  uint32_t yaw_word;  // TickIn::imu_words bit 0 (fmskf_device.hpp tick_yaw)
 };
 // CAN (round 5, fmskf_isr_tick_can): the tick's four C610 frames per robot first (can_lane.hpp),
 // the new angle sums and rpm handed to the odometry and the wheel loops in registers instead of
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kBlock) void k_isr_rs(IsrRsArgs a, CtrlDev c, CtrlP
   s.py = a.x[pp + i];
   s.th = 0.f;  // overwritten by the correct step
   if constexpr (!PS) rs_prev_load(a.prev, i, s.prev);
-  const float yaw = a.yaw_deg[i];
+  const float yaw = tick_yaw(a.yaw_word != 0u, reinterpret_cast<const uint32_t *>(a.yaw_deg)[i]);
   uint2 rw;
   int64_t sum[4];
   if constexpr (!CAN) {
@@ -208,7 +209,8 @@ __global__ __launch_bounds__(kBlock) void k_can_tx(const int16_t *curr, uint64_t
 constexpr int kViWords = 21;
 struct ImuView {  // the IMU state VehicleInfo reads (the snapshot: fmskf_device.hpp imu_data_page)
   const int16_t *snap;
-  const float *yaw, *gz, *qinit, *qprev;
+  const uint32_t *yg;  // the snapshot's Yaw / GZ words (DevState::imu_yg)
+  const float *qinit, *qprev;
   const uint8_t *err;
 };
 __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, ImuView im, uint64_t n,
@@ -248,7 +250,8 @@ __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, ImuVie
     if (!err && (w[14] & kSnapValid)) {
       const float *q = (w[14] & kSnapLatched) ? im.qprev : im.qinit;
       const float qi[4] = {q[i], q[n + i], q[2 * n + i], q[3 * n + i]};
-      imu_data_page(w, im.yaw[i], im.gz[i], qi, d);
+      const uint32_t g = im.yg[i];
+      imu_data_page(w, imu_yaw_deg(g), imu_gz_dps(g), qi, d);
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) r[7 + k] = err ? 0u : __builtin_bit_cast(uint32_t, d[12 + k]);
@@ -300,7 +303,7 @@ static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDe
                     uint8_t *frames, hipStream_t st, const CanArgs &can) {
   if (c.n == 0) return 0;
   const IsrRsArgs a{s.pitch, (float *)s.x, s.prev_sum, in.yaw_deg, in.rpm, in.angle_sum, in.sum_pitch,
-                    in.msum_lo, in.msum_hi, in.sintab, frames};
+                    in.msum_lo, in.msum_hi, in.sintab, frames, in.imu_words & 1u};
   const bool small = c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull;
   const bool nt = small && state_nt(ctrl_state_bytes(c) + s.n * 56);
   if (nt) {
@@ -426,7 +429,7 @@ int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st) {
 int launch_vehicle_info(const DevState &s, const float *readout, void *out, const uint8_t *floor,
                         const float *cam_pitch, const uint32_t *fault, hipStream_t st) {
   if (s.n == 0) return 0;
-  const ImuView im{s.imu_snap, s.imu_yaw, s.imu_gz, s.imu_qinit, s.imu_qprev, s.imu_err};
+  const ImuView im{s.imu_snap, s.imu_yg, s.imu_qinit, s.imu_qprev, s.imu_err};
   k_vehicle_info<<<grid1(s.n), kBlock, 0, st>>>(readout, im, s.n, (uint32_t *)out, floor, cam_pitch, fault);
   return (int)hipGetLastError();
 }

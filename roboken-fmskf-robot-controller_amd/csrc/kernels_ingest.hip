@@ -30,20 +30,24 @@ enum : uint32_t {
 // imu_if_wt901c.cpp:10-15
 enum : uint32_t { F_ACC = 0x01, F_GYRO = 0x02, F_ANGLE = 0x04, F_MAG = 0x08, F_QUAT = 0x10, F_READ = 0x80 };
 // not a firmware flag (round 6): the robot's row-resident registers -- AX AY AZ GX GY Roll Pitch
-// Q0-Q3, the eleven words the snapshot row holds besides the magnetometer's -- live in its
-// snapshot row, and their sReg planes are behind (the standard poll writes them once, into the
-// row).  Any other poll, fmskf_get_imu_regs and a checkpoint write them back first (row_regs_out).
+// Q0-Q3, the eleven words the snapshot row holds besides the magnetometer's, and GZ and Yaw, the
+// two words of its imu_yg dword -- live there, and their sReg planes are behind (the standard
+// poll writes them once, into the row and the dword).  Any other poll, fmskf_get_imu_regs and a
+// checkpoint write them back first (row_regs_out).
 enum : uint32_t { F_ROWREGS = 0x40 };
-// bit k of a register's row-resident index (AX AY AZ GX GY Roll Pitch Q0-Q3 -> 0..10), or 0
+// bit k of a register's row-resident index (AX AY AZ GX GY Roll Pitch Q0-Q3 -> 0..10, GZ 11,
+// Yaw 12), or 0
 __device__ __forceinline__ uint32_t rowreg_bit(uint32_t r) {
   return r >= R_AX && r < R_GZ ? 1u << (r - R_AX)
          : r == R_ROLL || r == R_ROLL + 1 ? 1u << (5 + r - R_ROLL)
-         : r >= R_Q0 && r <= R_Q3 ? 1u << (7 + r - R_Q0) : 0u;
+         : r >= R_Q0 && r <= R_Q3 ? 1u << (7 + r - R_Q0)
+         : r == R_GZ ? 1u << 11 : r == R_YAW ? 1u << 12 : 0u;
 }
-// the row-resident registers in snapshot-row word order (words 0-4, 8-13 of imu_data_page's row)
-// written back to sReg, except those in `skip` (rowreg_bit mask: registers written since)
-__device__ __forceinline__ void row_regs_out(const int16_t *snap, int16_t *reg, uint64_t n, uint64_t i,
-                                             uint32_t skip = 0) {
+// the row-resident registers (words 0-4, 8-13 of imu_data_page's row in snapshot-row order, then
+// the imu_yg dword's GZ and Yaw) written back to sReg, except those in `skip` (rowreg_bit mask:
+// registers written since)
+__device__ __forceinline__ void row_regs_out(const int16_t *snap, const uint32_t *yg, int16_t *reg, uint64_t n,
+                                             uint64_t i, uint32_t skip = 0) {
   const uint4 r0 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[0];
   const uint4 r1 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[1];
   const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};  // word k in w[k / 2]
@@ -56,6 +60,9 @@ __device__ __forceinline__ void row_regs_out(const int16_t *snap, int16_t *reg, 
     const uint32_t v = w[kWord[k] / 2];
     if (!((skip >> k) & 1u)) reg[kReg[k] * n + i] = (int16_t)(kWord[k] & 1 ? v >> 16 : v & 0xFFFFu);
   }
+  const uint32_t g = yg[i];
+  if (!((skip >> 11) & 1u)) reg[R_GZ * n + i] = (int16_t)(g >> 16);
+  if (!((skip >> 12) & 1u)) reg[R_YAW * n + i] = (int16_t)(g & 0xFFFFu);
 }
 
 // SensorDataUpdata for registers [r0, r0 + len)
@@ -83,7 +90,7 @@ struct Wt901Args {
   uint8_t *err;
   float *qinit;
   int16_t *snap;  // [N][16] snapshot rows (fmskf_device.hpp imu_data_page)
-  float *yaw, *gz;
+  uint32_t *yg;   // [N] Yaw / GZ words of the snapshot (DevState::imu_yg)
   float *qprev;
 };
 
@@ -187,7 +194,10 @@ struct Wt901Parser {
 // VGPRs, 7 waves per SIMD; capped at 64 (8 waves, no spills) it ran 29.2 -> 27.2 us per 2^20
 // polls.  With every unconditional load hoisted ahead of the parse (below) it takes 74 VGPRs:
 // 6 waves per SIMD, 27.0-27.2 -> 26.2-26.5 us at 2^20, 115.6-116.6 -> 109.9-110.6 at 2^22
-// (kbench, three passes, profiles/r5_ab.json); capped at 7 or 8 waves it spills (29.4, 34.8 us)
+// (kbench, three passes, profiles/r5_ab.json); capped at 7 or 8 waves it spills (29.4, 34.8 us).
+// Round 6, the bytes read from the chunk registers where used (62 VGPRs, 103 SGPRs: 7 waves per
+// SIMD): 6 here (7 waves) against 8 (63 VGPRs, 78 SGPRs, 8 waves) 21.3 / 21.3-21.6 us at 2^20,
+// 84.3 / 86.4 at 2^22 (two passes, one box)
 #ifndef FMSKF_WT901_WPE
 #define FMSKF_WT901_WPE 6
 #endif
@@ -235,65 +245,54 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   // written by exactly one of its frames, so the Data page is built from the frame words
   // instead of reading the register file back
   bool std4 = false;
-  uint32_t sw[4][4] = {};
+  // byte o (a compile-time offset) of the poll row, from the chunk registers
+  const auto rb = [&](int o) -> uint32_t {
+    if (o >= 64) return 0u;
+    const uint4 c = ch[o / 16];
+    const uint32_t w = (o % 16) / 4 == 0 ? c.x : (o % 16) / 4 == 1 ? c.y : (o % 16) / 4 == 2 ? c.z : c.w;
+    return (w >> (8 * (o % 4))) & 0xFFu;
+  };
+  // data word k of frame f (CopeWitData's usData[k]: bytes 2 + 2k, 3 + 2k, little-endian)
+  const auto fw = [&](int f, int k) -> uint32_t { return rb(f * 11 + 2 + 2 * k) | (rb(f * 11 + 3 + 2 * k) << 8); };
   if constexpr (VEC) {
     // Whole-frame fast path.  With an empty parser window and a poll made of complete frames
     // (0x55 header and a valid checksum every 11 bytes), the byte-serial parser accepts frame
     // k at bytes 11k..11k+10 and never resyncs: dispatch the frames directly (static byte
     // offsets -> register selects).  Anything else takes the byte-serial path from the start.
+    // Every byte is taken from the chunk registers where it is used (round 6: the frames were
+    // first copied into ten 64-bit window registers; 75 -> 62 VGPRs, 22.4 -> 21.3 us per 2^20
+    // standard polls, 90.6 -> 84.3 at 2^22, profiles/r6_ab.json `wt901_chunk_bytes`)
     const uint32_t nfr = len / 11;
     bool fast = ps.cnt == 0 && len == nfr * 11 && len <= 55;
-    uint64_t w0[5], w1[5];
 #pragma unroll
     for (int f = 0; f < 5; f++) {
-      uint32_t b[11];
-#pragma unroll
-      for (int k = 0; k < 11; k++) {
-        const int o = f * 11 + k;  // compile-time byte offset
-        if (o < 64) {
-          const uint4 c = ch[o / 16];
-          const uint32_t w = (o % 16) / 4 == 0 ? c.x : (o % 16) / 4 == 1 ? c.y : (o % 16) / 4 == 2 ? c.z : c.w;
-          b[k] = (w >> (8 * (o % 4))) & 0xFFu;
-        } else {
-          b[k] = 0;
-        }
-      }
       uint32_t sum = 0;
 #pragma unroll
-      for (int k = 0; k < 10; k++) sum += b[k];
-      const bool ok = b[0] == 0x55u && (sum & 0xFFu) == b[10];
+      for (int k = 0; k < 10; k++) sum += rb(f * 11 + k);
+      const bool ok = rb(f * 11) == 0x55u && (sum & 0xFFu) == rb(f * 11 + 10);
       if ((uint32_t)f < nfr) fast = fast && ok;
-      w0[f] = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) w0[f] |= (uint64_t)b[k] << (8 * k);
-      w1[f] = (uint64_t)b[8] | ((uint64_t)b[9] << 8) | ((uint64_t)b[10] << 16);
     }
-    const auto ftype = [](uint64_t w) { return (uint32_t)(w >> 8) & 0xFFu; };
-    std4 = fast && nfr == 4 && ftype(w0[0]) == 0x51u && ftype(w0[1]) == 0x52u &&
-           ftype(w0[2]) == 0x53u && ftype(w0[3]) == 0x59u;
+    std4 = fast && nfr == 4 && rb(1) == 0x51u && rb(12) == 0x52u && rb(23) == 0x53u && rb(34) == 0x59u;
     if (std4) {
-      // CopeWitData of the four frames with their register runs known statically
-#pragma unroll
-      for (int f = 0; f < 4; f++) {
-        sw[f][0] = (uint32_t)(w0[f] >> 16) & 0xFFFFu;
-        sw[f][1] = (uint32_t)(w0[f] >> 32) & 0xFFFFu;
-        sw[f][2] = (uint32_t)(w0[f] >> 48) & 0xFFFFu;
-        sw[f][3] = (uint32_t)w1[f] & 0xFFFFu;
-      }
-      // round 6: of the 15 registers the four frames write, the eleven the snapshot row holds
-      // (AX AY AZ GX GY Roll Pitch Q0-Q3) are written once, into the row below (F_ROWREGS);
-      // GZ and Yaw (the row carries them as the tick's floats), TEMP and VERSION go to sReg
+      // CopeWitData of the four frames with their register runs known statically.  Round 6: of
+      // the 15 registers the four frames write, thirteen are written once (F_ROWREGS): AX AY AZ
+      // GX GY Roll Pitch Q0-Q3 into the snapshot row, GZ and Yaw into the imu_yg dword (below);
+      // TEMP and VERSION go to sReg
       int16_t *reg = a.reg;
-      reg[R_GZ * n + i] = (int16_t)sw[1][2];
-      reg[R_YAW * n + i] = (int16_t)sw[2][2];
-      reg[R_TEMP * n + i] = (int16_t)sw[0][3];
-      reg[R_VERSION * n + i] = (int16_t)sw[2][3];
+      reg[R_TEMP * n + i] = (int16_t)fw(0, 3);
+      reg[R_VERSION * n + i] = (int16_t)fw(2, 3);
       ps.flags |= flags_of(R_AX, 3) | flags_of(R_TEMP, 1) | flags_of(R_GX, 3) | flags_of(R_ROLL, 3) |
                   flags_of(R_VERSION, 1) | flags_of(R_Q0, 4);
     } else if (fast) {
 #pragma unroll
       for (int f = 0; f < 5; f++)
-        if ((uint32_t)f < nfr) ps.dispatch(w0[f], w1[f], a, i);
+        if ((uint32_t)f < nfr) {
+          uint64_t w0 = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) w0 |= (uint64_t)rb(f * 11 + k) << (8 * k);
+          const uint64_t w1 = (uint64_t)rb(f * 11 + 8) | ((uint64_t)rb(f * 11 + 9) << 8) | ((uint64_t)rb(f * 11 + 10) << 16);
+          ps.dispatch(w0, w1, a, i);
+        }
     } else {
     // one parser body: the next chunk's bytes are consumed from the bottom of a 128-bit
     // shift register
@@ -321,7 +320,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   // not write are brought back from the row now (after the parse, when the poll row's registers
   // are dead; frames only write registers, so the order is immaterial).  Rare: a damaged or
   // non-standard poll
-  if (!std4 && row_regs) row_regs_out(a.snap, a.reg, n, i, ps.roww);
+  if (!std4 && row_regs) row_regs_out(a.snap, a.yg, a.reg, n, i, ps.roww);
   uint64_t lo = ps.lo, hi = ps.hi;
   uint32_t cnt = ps.cnt, flags = ps.flags;
   // isComComp / update, imu_if_wt901c.cpp:83-89,132-143
@@ -344,15 +343,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   // instead of 197 (the 64-byte page written, q_init read; 132 B with the empty-window rule above).  Only a latching poll reads q_init,
   // to keep it (qprev) for the page of that very poll, which used the old one.
   int16_t ra[3], rg[3], rr[3], rq[4];
-  if (std4) {
+  if (std4) {  // (VEC only: the chunk registers still hold the poll)
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      ra[k] = (int16_t)sw[0][k];
-      rg[k] = (int16_t)sw[1][k];
-      rr[k] = (int16_t)sw[2][k];
+      ra[k] = (int16_t)fw(0, k);
+      rg[k] = (int16_t)fw(1, k);
+      rr[k] = (int16_t)fw(2, k);
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) rq[k] = (int16_t)sw[3][k];
+    for (int k = 0; k < 4; k++) rq[k] = (int16_t)fw(3, k);
   } else {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -366,8 +365,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
 #pragma unroll
     for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
   }
-  a.yaw[i] = (float)rr[2] / 32768.0f * 180.0f;
-  a.gz[i] = -((float)rg[2] / 32768.0f * 2000.0f);
+  // Data.angle[2] / Data.gyro[2] as their register words (fmskf_device.hpp imu_yaw_deg)
+  a.yg[i] = (uint32_t)(uint16_t)rr[2] | ((uint32_t)(uint16_t)rg[2] << 16);
   uint32_t snapf = kSnapValid;
   if (a.latch_qinit) {
     snapf |= kSnapLatched;
@@ -385,28 +384,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
 
 // the register file made whole (fmskf_get_imu_regs, a checkpoint): robots whose row-resident
 // registers live in their snapshot row (F_ROWREGS) get them written back into sReg
-__global__ __launch_bounds__(kBlock) void k_wt901_regs_sync(const int16_t *snap, int16_t *reg, uint8_t *flags,
-                                                            uint64_t n) {
+__global__ __launch_bounds__(kBlock) void k_wt901_regs_sync(const int16_t *snap, const uint32_t *yg, int16_t *reg,
+                                                            uint8_t *flags, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint32_t f = flags[i];
   if (!(f & F_ROWREGS)) return;
-  row_regs_out(snap, reg, n, i);
+  row_regs_out(snap, yg, reg, n, i);
   flags[i] = (uint8_t)(f & ~F_ROWREGS);
 }
 
 int launch_wt901_regs_sync(const DevState &s, hipStream_t st) {
   if (s.n == 0 || !s.imu_reg) return 0;
-  k_wt901_regs_sync<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_reg,
-                                                                                      s.imu_flags, s.n);
+  k_wt901_regs_sync<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_yg,
+                                                                                      s.imu_reg, s.imu_flags, s.n);
   return (int)hipGetLastError();
 }
 
 // IMU_IF::Data [16][N] of every robot from its snapshot (fmskf_get_imu): zeros until the first
 // successful poll, like the firmware's zero-initialised page
-__global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const float *yaw, const float *gz,
-                                                     const float *qinit, const float *qprev, uint64_t n,
-                                                     float *out) {
+__global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const uint32_t *yg, const float *qinit,
+                                                     const float *qprev, uint64_t n, float *out) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   int16_t w[kSnapWords];
@@ -422,7 +420,8 @@ __global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const 
   if (w[14] & kSnapValid) {
     const float *q = (w[14] & kSnapLatched) ? qprev : qinit;
     const float qi[4] = {q[i], q[n + i], q[2 * n + i], q[3 * n + i]};
-    imu_data_page(w, yaw[i], gz[i], qi, d);
+    const uint32_t g = yg[i];
+    imu_data_page(w, imu_yaw_deg(g), imu_gz_dps(g), qi, d);
   } else {
 #pragma unroll
     for (int k = 0; k < 16; k++) d[k] = 0.0f;
@@ -433,16 +432,16 @@ __global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const 
 
 int launch_imu_data(const DevState &s, float *out, hipStream_t st) {
   if (s.n == 0) return 0;
-  k_imu_data<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_yaw, s.imu_gz,
-                                                                                s.imu_qinit, s.imu_qprev, s.n, out);
+  k_imu_data<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_yg, s.imu_qinit,
+                                                                                s.imu_qprev, s.n, out);
   return (int)hipGetLastError();
 }
 
 int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
                  int latch_qinit, uint32_t read_reg_index, hipStream_t st) {
   Wt901Args a{s.n,       bytes,      stride,   len,        latch_qinit,  read_reg_index, s.imu_reg,
-              s.imu_parser, s.imu_cnt, s.imu_flags, s.imu_err, s.imu_qinit, s.imu_snap, s.imu_yaw,
-              s.imu_gz,  s.imu_qprev};
+              s.imu_parser, s.imu_cnt, s.imu_flags, s.imu_err, s.imu_qinit, s.imu_snap, s.imu_yg,
+              s.imu_qprev};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   const bool vec = stride % 16 == 0 && stride <= 64 && ((uintptr_t)bytes & 15) == 0;
   if (vec) k_wt901<true><<<g, kBlock, 0, st>>>(a);

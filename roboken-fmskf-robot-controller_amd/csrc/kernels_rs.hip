@@ -42,7 +42,7 @@ __global__ __launch_bounds__(kBlock) void k_rs(RsArgs a) {
   const uint64_t st = a.in.stride;
   for (uint32_t t = 0; t < a.in.n_ticks; t++) {
     const uint64_t j = (uint64_t)t * st + i;
-    const float yaw = CORR ? a.in.yaw_deg[j] : 0.f;
+    const float yaw = CORR ? tick_yaw(a.in.imu_words & 1u, reinterpret_cast<const uint32_t *>(a.in.yaw_deg)[j]) : 0.f;
     uint2 r = make_uint2(0u, 0u);
     int64_t sum[4] = {0, 0, 0, 0};
     if (PRED) {
@@ -104,6 +104,9 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
   WaveTable<!WT> tv(a.in.sintab);
   const float *tab = WT ? wtab[threadIdx.x >> 6] : a.in.sintab;
   float yaw[2];
+  // the yaw plane, or the IMU state's Yaw words (fmskf_device.hpp tick_yaw): one dword either way
+  const bool yp = (a.in.imu_words & 1u) != 0;
+  const uint32_t *ys = reinterpret_cast<const uint32_t *>(a.in.yaw_deg);
   uint2 rw[2];
   int64_t sum[2][4];
   uint64_t hb[2];
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
     li[r] = (uint32_t)(i - hb[r]);
     uint64_t rv;
     if constexpr (MS) {  // the motor state's sums: [N][4] low and high words
-      yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
+      yaw[r] = tick_yaw(yp, ld_span<uint32_t, FMSKF_IN_CPOL>(rsrc_span(ys + hb[r]), li[r], 0));
       rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
       constexpr int MP = FMSKF_MS_CPOL < 0 ? CP : FMSKF_MS_CPOL;
       const auto lw = __builtin_amdgcn_raw_buffer_load_b128(rsrc_span(a.in.msum_lo + hb[r] * 4), li[r] * 16u, 0, MP);
@@ -127,14 +130,14 @@ __global__ __launch_bounds__(kBlock) void k_rs2(RsArgs a) {
         sum[r][w] = motor_sum_join((int32_t)h, l);
       }
     } else if constexpr (SO) {
-      yaw[r] = ld_span<float, FMSKF_IN_CPOL>(rsrc_span(a.in.yaw_deg + hb[r]), li[r], 0);
+      yaw[r] = tick_yaw(yp, ld_span<uint32_t, FMSKF_IN_CPOL>(rsrc_span(ys + hb[r]), li[r], 0));
       rv = ld_span<uint64_t, FMSKF_IN_CPOL>(rsrc_span(a.in.rpm + hb[r] * 4), li[r], 0);
       const auto rs = rsrc_span(a.in.angle_sum + hb[r]);
 #pragma unroll
       for (int w = 0; w < 4; w++)
         sum[r][w] = ld_span<int64_t, FMSKF_IN_CPOL>(rs, li[r], w * (uint32_t)(a.in.sum_pitch * 8));
     } else {
-      yaw[r] = ld_chunk<float, FMSKF_IN_CPOL>(a.in.yaw_deg, hb[r], n, li[r]);
+      yaw[r] = tick_yaw(yp, ld_chunk<uint32_t, FMSKF_IN_CPOL>(ys, hb[r], n, li[r]));
       rv = ld_chunk<uint64_t, FMSKF_IN_CPOL>(reinterpret_cast<const uint64_t *>(a.in.rpm), hb[r], n, li[r]);
 #pragma unroll
       for (int w = 0; w < 4; w++)

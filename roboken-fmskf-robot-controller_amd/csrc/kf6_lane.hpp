@@ -85,10 +85,13 @@ __device__ __forceinline__ Kf6In kf6_load_in(const TickIn &in, uint64_t n, uint6
     m.valid = O::VALID ? (uint32_t)in.valid[tb + i] : 1u;
     return m;
   }
-  m.yaw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                        rsrc(in.yaw_deg + base, left * 4), li * 4u, 0, FMSKF_IN_CPOL));
-  m.gz = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                       rsrc(in.gyro_z + base, left * 4), li * 4u, 0, FMSKF_IN_CPOL));
+  // the yaw / gyro z planes, or for a NULL one the IMU state's Yaw / GZ words (fmskf_device.hpp
+  // tick_yaw): one dword per lane either way (with both from the IMU state, the same dword twice)
+  const bool yw = (in.imu_words & 1u) != 0, gw = (in.imu_words & 2u) != 0;
+  m.yaw = tick_yaw(yw, __builtin_amdgcn_raw_buffer_load_b32(rsrc(in.yaw_deg + base, left * 4), li * 4u, 0,
+                                                            FMSKF_IN_CPOL));
+  m.gz = tick_gz(gw, __builtin_amdgcn_raw_buffer_load_b32(rsrc(in.gyro_z + base, left * 4), li * 4u, 0,
+                                                          FMSKF_IN_CPOL));
   const auto rr = __builtin_amdgcn_raw_buffer_load_b64(rsrc(in.rpm + base * 4, left * 8), li * 8u, 0,
                                                        FMSKF_IN_CPOL);
   m.rpm = make_uint2(rr[0], rr[1]);

@@ -559,12 +559,15 @@ def test_wt901_data_page_across_latches(orc, stride):
     poll failed (the page of their last success stays).  VehicleInfo reads the same page.  The
     register file too, on every third poll: the standard poll writes eleven registers into the
     snapshot row only (round 6), and a failed poll, a 0x5F register reply (Q0-Q3) or another
-    frame mix after it must see them (wit_c_sdk.c:90-130)."""
+    frame mix after it must see them (wit_c_sdk.c:90-130).  And the tick's yaw: an RS handle fed
+    the same polls takes Data.angle[2] from the Yaw / GZ words (round 6) in its correct step
+    (theta = deg2rad(yaw), VD_task_main.cpp:368), so theta follows the page, not the register."""
     n, polls = 1537, 9
     rng = np.random.default_rng(41 + stride)
     orcs = [orc.Wt901(0x51) for _ in range(n)]
     latch = {1, 5}
-    with Engine("kf6", n) as e:
+    deg2rad = np.float32(np.float32(3.14159265358979) / np.float32(180.0))  # util_mymath.hpp:14
+    with Engine("kf6", n) as e, Engine("rs", n) as rs:
         for k in range(polls):
             buf = np.zeros((n, stride), np.uint8)
             lens = np.zeros(n, np.uint32)
@@ -585,10 +588,15 @@ def test_wt901_data_page_across_latches(orc, stride):
                 lens[i] = b.size
                 orcs[i].update(b, latch_qinit=(k in latch))
             e.ingest_wt901(buf, lens, latch_qinit=(k in latch))
+            rs.ingest_wt901(buf, lens, latch_qinit=(k in latch))
+            rs.correct()  # NULL yaw plane: the ingested Data.angle[2]
+            th = rs.get_pose()[2]
             data, err = e.get_imu()
             for i in range(n):
                 assert err[i] == orcs[i].is_error
                 bits_equal(data[:, i], orcs[i].data, f"data {i} poll {k}")
+            yaw = np.array([orcs[i].data[11] for i in range(n)], np.float32)
+            bits_equal(th, yaw * deg2rad, f"theta poll {k}")
             if k % 3 == 1:  # the register file (round 6: the standard poll keeps eleven of its
                 # registers in the snapshot row only; the readout writes them back), on some polls,
                 # so that later polls also start from row-resident registers

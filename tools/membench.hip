@@ -768,6 +768,55 @@ __global__ __launch_bounds__(256) void k_canmix(const uint4 *frames, const uint6
   }
 }
 
+// the round-6 standard WT901 poll's exact accesses with no parsing (membench LG 1 w6, 110 B):
+// the 48-byte poll row (three 16-byte loads) and its length from a 16-slot ring; the count and
+// flags byte planes read; the three magnetometer int16 registers read (MAG); GZ, Yaw, TEMP and
+// VERSION int16 registers written; the error and flags bytes written; the yaw / gyro z floats
+// written (FLT 1: two float planes; 2: one [N][2] float plane; 3: instead of the floats and the GZ
+// / Yaw registers, their raw words as one dword plane: 102 B); the 32-byte snapshot row written as
+// two 16-byte stores.  PACK: count, flags and error in one dword plane read and written (114 B)
+template <bool MAG, int FLT, bool PACK>
+__global__ __launch_bounds__(256) void k_wt901mix6(const uint4 *rows, const uint32_t *len, uint8_t *cnt, uint8_t *flg,
+                                                   uint8_t *err, uint32_t *packed, int16_t *reg, float *yaw,
+                                                   float *gz, uint4 *snap, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t st;
+  if constexpr (PACK) st = packed[i];
+  else st = cnt[i] | ((uint32_t)flg[i] << 8);
+  const uint32_t l = len[i];
+  int16_t h[3] = {0, 0, 0};
+  if constexpr (MAG) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) h[k] = reg[(0x3a + k) * n + i];
+  }
+  const uint4 a = rows[3 * i], b = rows[3 * i + 1], c = rows[3 * i + 2];
+  const uint32_t m = a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ l ^ st;
+  if constexpr (FLT != 3) {
+    reg[0x39 * n + i] = (int16_t)m;
+    reg[0x3f * n + i] = (int16_t)(m >> 3);
+  }
+  reg[0x40 * n + i] = (int16_t)(m >> 5);
+  reg[0x2e * n + i] = (int16_t)(m >> 7);
+  if constexpr (PACK) packed[i] = (st & 0xFF00FFu) ^ (m & 0xFF0000u);
+  else {
+    err[i] = (uint8_t)m;
+    flg[i] = (uint8_t)(st >> 8);
+  }
+  const float fy = (float)(int16_t)(a.y >> 16) / 32768.0f * 180.0f;
+  const float fg = (float)(int16_t)(b.x >> 8) / 32768.0f * 2000.0f;
+  if constexpr (FLT == 1) {
+    yaw[i] = fy;
+    gz[i] = fg;
+  } else if constexpr (FLT == 2) {
+    reinterpret_cast<float2 *>(yaw)[i] = make_float2(fy, fg);
+  } else if constexpr (FLT == 3) {
+    reinterpret_cast<uint32_t *>(yaw)[i] = (a.y >> 16) | (b.x << 16);
+  }
+  snap[2 * i] = make_uint4(a.x ^ m, b.y, (uint32_t)(uint16_t)h[0] | (c.x << 16), (uint32_t)(uint16_t)h[1] | ((uint32_t)(uint16_t)h[2] << 16));
+  snap[2 * i + 1] = make_uint4(c.y, c.z ^ m, a.w, 1u);
+}
+
 __global__ __launch_bounds__(256) void k_copy4(const float4 *a, float4 *b, uint64_t nv) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * 256)
     b[i] = a[i];
@@ -804,6 +853,64 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&cb, bytes / 2));
   CK(hipMemset(ca, 0, bytes / 2));
   const bool zeros = argc > 2 && atoi(argv[2]) == 0;  // membench LG 0 -> all-zero buffers
+  if (argc > 3 && argv[3][0] == 'w' && argv[3][1] == '6') {
+    // membench LG 1 w6: the round-6 standard WT901 poll's byte mix (k_wt901mix6) and what each
+    // of its parts costs -- two passes, random data, rows and lengths from a 16-slot ring
+    hipEvent_t f0, f1;
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    constexpr int kRing = 16;
+    uint8_t *ring, *b3;
+    uint32_t *pk;
+    int16_t *rg;
+    float *yw, *gzz;
+    uint4 *sn;
+    const size_t slot = (size_t)52 * n;  // [n][48] rows + [n] lengths
+    CK(hipMalloc(&ring, kRing * slot));
+    CK(hipMalloc(&b3, 3 * n));
+    CK(hipMalloc(&pk, 4 * n));
+    CK(hipMalloc(&rg, (size_t)0x41 * n * 2));
+    CK(hipMalloc(&yw, 8 * n));
+    CK(hipMalloc(&gzz, 4 * n));
+    CK(hipMalloc(&sn, 32 * n));
+    k_fill_rand<<<4096, 256>>>((uint32_t *)ring, kRing * slot / 4, 1);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)rg, (uint64_t)0x41 * n / 2, 2);
+    k_fill_rand<<<4096, 256>>>((uint32_t *)sn, 8 * n, 3);
+    k_fill_rand<<<4096, 256>>>(pk, n, 4);
+    CK(hipMemset(b3, 0, 3 * n));
+    CK(hipDeviceSynchronize());
+    int tick = 0;
+    const unsigned g1 = (unsigned)((n + 255) / 256);
+    auto tm = [&](const char *name, int bpr, auto kern) {
+      auto launch = [&] {
+        const uint8_t *in = ring + (size_t)(tick++ % kRing) * slot;
+        kern<<<g1, 256>>>((const uint4 *)in, (const uint32_t *)(in + 48 * n), b3, b3 + n, b3 + 2 * n, pk, rg, yw,
+                          gzz, sn, n);
+      };
+      for (int w = 0; w < 2 * kRing; w++) launch();
+      for (int rep = 0; rep < 2; rep++) {
+        CK(hipEventRecord(f0));
+        for (int it = 0; it < 64; it++) launch();
+        CK(hipEventRecord(f1));
+        CK(hipEventSynchronize(f1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, f0, f1));
+        const double us = ms * 1e3 / 64;
+        printf("{\"n\": %llu, \"mix\": \"%s\", \"bytes_per_robot\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+               (unsigned long long)n, name, bpr, us, (double)bpr * n / (us * 1e-6) / 1e9);
+      }
+    };
+    for (int rep = 0; rep < 2; rep++) {
+      tm("wt901_r6_exact", 110, k_wt901mix6<true, 1, false>);
+      tm("wt901_r6_no_mag", 104, k_wt901mix6<false, 1, false>);
+      tm("wt901_r6_no_floats", 102, k_wt901mix6<true, 0, false>);
+      tm("wt901_r6_packed_bytes", 114, k_wt901mix6<true, 1, true>);
+      tm("wt901_r6_no_mag_no_floats", 96, k_wt901mix6<false, 0, false>);
+      tm("wt901_r6_float2_plane", 110, k_wt901mix6<true, 2, false>);
+      tm("wt901_r6_raw_gz_yaw_dword", 102, k_wt901mix6<true, 3, false>);
+    }
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'r' && argv[3][1] == '6') {
     // membench LG 1 r6: the RS tick and CAN RX mixes with int64 sum planes against [N][4] rows
     // (k_rsmix, k_canmix), and the KF6 2^24-shape tiled pattern fed a ring of 16-byte records

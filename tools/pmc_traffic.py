@@ -101,7 +101,7 @@ def secondary(root, out):
 PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
-    ("wt901_ingest_2p20", "k_wt901", 60, 50),
+    ("wt901_ingest_2p20", "k_wt901", 60, 42),
     ("can_ingest_2p20", "k_can4", 104, 80),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
     # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
