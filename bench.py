@@ -342,6 +342,10 @@ def secondary_configs(dev, stream, ticks: int, trig):
 # (can_ingest_2p20)
 WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4
 CAN_RX_BYTES = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)
+# the vehicle control step (control_step_2p20): power 1, interpolators 144, FF_PI_D 64, rpm 8
+# read; interpolator time / speed / accel 36, FF_PI_D value / integral / LPF 64, currents 8 written
+# (369 before round 6, with vel_tgt and FF_PI_D now_tgt / now_ctrl stored by every step)
+CTRL_STEP_BYTES = 1 + 144 + 64 + 8 + 36 + 64 + 8
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
     # RS tick: pos (x, y) 8 r + (x, y, th) 12 w -- theta is overwritten by the correct, so it is
@@ -366,38 +370,39 @@ PATH_BYTES = {
     # formed at readout from the angle and the previous one; the IIR input state x is formed from
     # the previous frame's angle and stamp (round 5: 224 -> 216 B; round 6: 216 -> 184 B))
     "can_ingest_2p20": CAN_RX_BYTES,
-    # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 96 + 12 + 8 w
-    "control_step_2p20": 1 + 144 + 64 + 8 + 36 + 96 + 12 + 8,
-    # fused KF6 ISR: the tick's 232 + the control step's 369 without its rpm read (the tick
+    # control step: power 1, interpolators 144, FF_PI_D 64, rpm 8 r; 36 + 64 + 8 w (round 6: the
+    # outputs nothing reads back -- vel_tgt 12, FF_PI_D now_tgt / now_ctrl 32 -- formed on demand)
+    "control_step_2p20": CTRL_STEP_BYTES,
+    # fused KF6 ISR: the tick's 232 + the control step's CTRL_STEP_BYTES without its rpm read (the tick
     # loads it once) + the 8-byte 0x200 frame
-    "isr_kf6_2p20": 232 + 369 - 8 + 8,
+    "isr_kf6_2p20": 232 + CTRL_STEP_BYTES - 8 + 8,
     # the firmware loop per tick on device-resident state: CAN RX, the fused KF6 ISR reading the
     # ingested Yaw / GZ words (one dword for the record's two floats, round 6) and wheel rpm, and
     # every 10th tick the WT901 poll
-    "firmware_loop_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 4 + WT901_POLL_BYTES / 10,
+    "firmware_loop_kf6_2p20": CAN_RX_BYTES + (232 + CTRL_STEP_BYTES - 8 + 8) - 4 + WT901_POLL_BYTES / 10,
     # fmskf_isr_tick_can alone (the tick's CAN RX fused into the KF6 ISR, yaw / gyro planes): the
     # CAN row's 184 + the ISR's 601 without its rpm read
-    "isr_can_kf6_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8,
+    "isr_can_kf6_2p20": CAN_RX_BYTES + (232 + CTRL_STEP_BYTES - 8 + 8) - 8,
     # the EKF9 ISR (k_isr_ekf9, round 5): the EKF9 tick's 448 (cfg 3's count; + 8 B with the
-    # heading's hidden low-part row) + the control step's 369 (its own rpm plane: the tick reads
+    # heading's hidden low-part row) + the control step's CTRL_STEP_BYTES (its own rpm plane: the tick reads
     # the raw record) + the 0x200 frame
-    "isr_ekf9_2p20": 448 + 369 + 8,
+    "isr_ekf9_2p20": 448 + CTRL_STEP_BYTES + 8,
     # with the tick's CAN RX fused in (fmskf_isr_tick_can): the CAN row's 184, the control step's
     # rpm no longer read back
-    "isr_can_ekf9_2p20": CAN_RX_BYTES + (448 + 369 + 8) - 8,
+    "isr_can_ekf9_2p20": CAN_RX_BYTES + (448 + CTRL_STEP_BYTES + 8) - 8,
     # the reference-semantics ISR (k_isr_rs) on the ingested motor state: the RS tick's 140 + the
     # control step's 369 without its rpm read (the tick loads it once) + the 0x200 frame
-    "isr_rs_2p20": 140 + 369 - 8 + 8,
+    "isr_rs_2p20": 140 + CTRL_STEP_BYTES - 8 + 8,
     # with the tick's CAN RX fused in: the CAN row's 184, the rpm and the four sums no longer read
     # back (the CAN lane hands them over in registers), and (round 6) the previous sums neither
     # read nor written while they equal the motor state's stored sums (k_isr_rs PS: 64 B)
-    "isr_can_rs_2p20": CAN_RX_BYTES + (140 + 369 - 8 + 8) - 8 - 32 - 64,
+    "isr_can_rs_2p20": CAN_RX_BYTES + (140 + CTRL_STEP_BYTES - 8 + 8) - 8 - 32 - 64,
     # the reference-semantics firmware loop (VD_task_main.cpp:366-372 with its CAN RX and IMU
     # tasks) on the fused call: CAN RX + the RS ISR in one kernel, a WT901 poll every 10th tick
-    "firmware_loop_rs_fused_2p20": CAN_RX_BYTES + (140 + 369 - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
+    "firmware_loop_rs_fused_2p20": CAN_RX_BYTES + (140 + CTRL_STEP_BYTES - 8 + 8) - 8 - 32 - 64 + WT901_POLL_BYTES / 10,
     # the same loop with the CAN RX fused into the ISR (fmskf_isr_tick_can): the ISR no longer
     # reads the rpm plane back (the CAN lane hands it over in registers); everything else stays
-    "firmware_loop_kf6_fused_2p20": CAN_RX_BYTES + (232 + 369 - 8 + 8) - 8 - 4 + WT901_POLL_BYTES / 10,
+    "firmware_loop_kf6_fused_2p20": CAN_RX_BYTES + (232 + CTRL_STEP_BYTES - 8 + 8) - 8 - 4 + WT901_POLL_BYTES / 10,
 }
 
 

@@ -184,6 +184,7 @@ int fmskf_save_state(fmskf_handle h, const char *path) {
     ck_layout(h, &hd);
     hd.groups = 1u | (h->s.imu_reg ? 2u : 0u) | (h->s.m_sum_lo ? 4u : 0u) | (h->ctrl_ready ? 8u : 0u);
     rs_prev_materialize(h);  // the file holds the odometry's previous sums in the prev planes
+    ctrl_materialize(h);     // and the control step's outputs
     // and the whole WT901 register file in its planes (no row-resident registers)
     launch_check(launch_wt901_regs_sync(h->s, h->stream), "register file sync");
     hip_check(hipStreamSynchronize(h->stream), "save sync");
@@ -287,6 +288,7 @@ int fmskf_load_state(fmskf_handle h, const char *path) {
     if (!(hd.groups & 4) && h->s.m_sum_lo) zero_motors(h);
     if (!(hd.groups & 8) && h->ctrl_ready) zero_ctrl(h);
     h->rs_prev_synced = h->rs_prev_stale = false;  // the prev planes come from the file
+    h->ctrl_derived_stale = false;                  // and the control outputs
     hip_check(hipStreamSynchronize(h->stream), "load sync");
     // pass 2: stream each section to the device in bounded chunks
     for (const CkSection &c : secs) {

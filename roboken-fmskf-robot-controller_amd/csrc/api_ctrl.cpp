@@ -46,10 +46,31 @@ CtrlPrm make_ctrl_prm(const fmskf_ctx *h) {
   return p;
 }
 
+// the parameter block of a control-step launch: outside a capture the step leaves its derived
+// outputs to be formed on demand, with these parameters (ctrl_materialize); inside one it stores
+// them itself
+CtrlPrm ctrl_step_prm(fmskf_ctx *h) {
+  CtrlPrm p = make_ctrl_prm(h);
+  p.store_derived = h->capturing ? 1u : 0u;
+  if (h->capturing) {
+    h->graph_has_ctrl = true;
+  } else {
+    h->ctrl_prm_last = p;
+    h->ctrl_derived_stale = true;
+  }
+  return p;
+}
+
 }  // namespace
 
 namespace fmskf {
 namespace capi {
+
+void ctrl_materialize(fmskf_ctx *h) {
+  if (!h->ctrl_ready || !h->ctrl_derived_stale) return;
+  launch_check(launch_ctrl_derive(h->ctrl, h->ctrl_prm_last, h->stream), "control outputs");
+  h->ctrl_derived_stale = false;
+}
 
 void zero_ctrl(fmskf_ctx *h) {
   CtrlDev &c = h->ctrl;
@@ -59,6 +80,7 @@ void zero_ctrl(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
   hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, h->stream), "ctrl init");
   ctrl_params_defaults(&h->cprm);
+  h->ctrl_derived_stale = false;
 }
 
 void ensure_ctrl(fmskf_ctx *h) {
@@ -106,6 +128,7 @@ int fmskf_set_power(fmskf_handle h, const uint8_t *on, uint32_t mem) {
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     ensure_ctrl(h);
+    ctrl_materialize(h);  // the last step's outputs are formed with the power flags it ran with
     const uint64_t n = h->s.n;
     if (!on) {
       hip_check(hipMemsetAsync(h->ctrl.power, 1, n, h->stream), "power");
@@ -156,7 +179,7 @@ int fmskf_control(fmskf_handle h, const int16_t *rpm, uint32_t mem) {
       r = h->s.m_rpm;
     }
     h->time_begin();
-    launch_check(launch_ctrl_step(h->ctrl, make_ctrl_prm(h), (const int16_t *)r, 1, h->stream),
+    launch_check(launch_ctrl_step(h->ctrl, ctrl_step_prm(h), (const int16_t *)r, 1, h->stream),
                  "control launch");
     h->time_end();
   });
@@ -197,7 +220,7 @@ static bool isr_kf6_fused() {
 // the ISR's launches for resolved inputs `t` (frames into `dst`, or none)
 static void isr_launches(fmskf_ctx *h, const TickIn &t, uint8_t *dst) {
   const bool libm = h->cfg.trig == FMSKF_TRIG_LIBM;
-  const CtrlPrm p = make_ctrl_prm(h);
+  const CtrlPrm p = ctrl_step_prm(h);
   int fused = (int)hipErrorNotSupported;
   if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused()) {
     if (!t.rec && !t.rpm) ensure_motors(h);
@@ -274,17 +297,17 @@ int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t 
     // one launch where the tick reads the rpm (RS: and the angle sums) the frames carry: no
     // caller rpm / sums / records
     if (h->cfg.model == FMSKF_MODEL_KF6 && isr_kf6_fused() && !in->kf6_rec && !in->rpm) {
-      fused = launch_isr_kf6_can(h->s, t, h->kf6, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+      fused = launch_isr_kf6_can(h->s, t, h->kf6, libm, h->ctrl, ctrl_step_prm(h), dst, (const uint8_t *)f,
                                  (const int16_t *)s, h->cfg.motor_dir, h->stream);
     } else if (h->cfg.model == FMSKF_MODEL_EKF9 && isr_kf6_fused() && !in->rpm) {
-      fused = launch_isr_ekf9_can(h->s, t, h->ekf9, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+      fused = launch_isr_ekf9_can(h->s, t, h->ekf9, libm, h->ctrl, ctrl_step_prm(h), dst, (const uint8_t *)f,
                                   (const int16_t *)s, h->cfg.motor_dir, h->stream);
     } else if (h->cfg.model == FMSKF_MODEL_RS && !in->rpm && !in->angle_sum) {
       // the previous sums are the stored ones: take them from the CAN lane, skip the prev planes
       // (not inside a capture: a replay may start from another state)
       const bool ps = h->rs_prev_synced && !h->capturing && rs_prev_skip();
       if (!ps) rs_prev_materialize(h);
-      fused = launch_isr_rs_can(h->s, t, libm, h->ctrl, make_ctrl_prm(h), dst, (const uint8_t *)f,
+      fused = launch_isr_rs_can(h->s, t, libm, h->ctrl, ctrl_step_prm(h), dst, (const uint8_t *)f,
                                 (const int16_t *)s, h->cfg.motor_dir, ps, h->stream);
       if (fused != (int)hipErrorNotSupported) {
         h->rs_prev_synced = true;  // the odometry's previous sums are the new motor sums
@@ -311,6 +334,7 @@ int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *whe
     check_handle(h);
     DeviceGuard g(h->cfg.device);
     ensure_ctrl(h);
+    ctrl_materialize(h);
     const CtrlDev &c = h->ctrl;
     const size_t row = c.n * 4, pb = c.pitch * 4;
     copy_planes_out(h, vel_tgt, c.vel_tgt, row, pb, 3, mem);

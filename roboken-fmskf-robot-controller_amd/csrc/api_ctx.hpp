@@ -174,6 +174,14 @@ struct fmskf_ctx {
   // from the motor state and wrote no prev (k_isr_rs PS).  stale implies synced.  Every reader of
   // the prev planes and every writer of the motor sums calls rs_prev_materialize first.
   bool rs_prev_synced = false, rs_prev_stale = false;
+  // The control step's outputs nothing reads back (vel_tgt, FF_PI_D now_tgt / now_ctrl) are
+  // formed on demand (round 6, ctrl_lane.hpp ctrl_derive_lane): ctrl_derived_stale says the last
+  // step left them to be formed, with its parameters ctrl_prm_last.  fmskf_get_ctrl and a
+  // checkpoint form them first (ctrl_materialize), and so does fmskf_set_power, since the forming
+  // reads the power flags the step ran with.  Inside a graph capture the step stores them itself
+  // (the host cannot follow the replays): graph_has_ctrl marks a captured sequence with a step.
+  bool ctrl_derived_stale = false, graph_has_ctrl = false;
+  fmskf::CtrlPrm ctrl_prm_last{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // pooled per-launch events (fmskf_kernel_time_total)
@@ -390,6 +398,8 @@ bool fused_record(const fmskf_ctx *h);
 // api_ctrl.cpp
 void ensure_ctrl(fmskf_ctx *h);
 void zero_ctrl(fmskf_ctx *h);
+// form the control step's derived outputs if the last step left them (ctrl_derived_stale)
+void ctrl_materialize(fmskf_ctx *h);
 
 }  // namespace capi
 }  // namespace fmskf

@@ -232,6 +232,7 @@ void do_reset(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.counters, 0, 8 * 8, st), "reset counters");
   h->isr_can_split = h->isr_ctrl_split = 0;
   h->rs_prev_synced = h->rs_prev_stale = false;  // the prev planes were zeroed above
+  h->ctrl_derived_stale = false;                  // and the control outputs
   h->ens_shift_ok = false;
 }
 
@@ -584,6 +585,10 @@ int fmskf_graph_begin(fmskf_handle h) {
     // planes themselves (no PS form inside a capture), so they must be current before it
     rs_prev_materialize(h);
     h->rs_prev_synced = false;
+    // captured control steps store their derived outputs themselves (ctrl_step_prm); the ones
+    // before the capture are formed now, while the host still knows their parameters
+    ctrl_materialize(h);
+    h->graph_has_ctrl = false;
     hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
               "hipStreamBeginCapture");
     h->capturing = true;
@@ -617,6 +622,7 @@ int fmskf_graph_launch(fmskf_handle h, uint32_t times) {
     for (uint32_t k = 0; k < times; k++)
       hip_check(hipGraphLaunch(h->graph_exec, h->stream), "hipGraphLaunch");
     h->rs_prev_synced = false;
+    if (h->graph_has_ctrl && times > 0) h->ctrl_derived_stale = false;  // the replayed steps stored them
   });
 }
 

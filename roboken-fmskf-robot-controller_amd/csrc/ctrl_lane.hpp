@@ -73,6 +73,23 @@ __device__ __forceinline__ float interp_update(Interp &s, float ts) {
   return f[IV_V];
 }
 
+// conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
+__device__ __forceinline__ void vdir_to_mdir(const float v[3], float mt[4]) {
+  mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+  mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+}
+// FF_PI_D::update's output (util_controller.hpp:104-120,171-177) from the loop's new target,
+// value, integral and LPF output: the step and ctrl_derive form it with these same operations
+__device__ __forceinline__ float ffpid_out(const CtrlPrm &p, float tgt, float val, float integ, float ly) {
+  const float err = tgt - val;
+  float ctrl = p.p_gain * err + integ - p.d_gain * ly;
+  float ff = tgt * p.ff_gain;
+  ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
+  return ctrl + ff;
+}
+
 // ARM VCVT.S32.F32: truncate, saturate, NaN -> 0 (fmskf_device.hpp)
 __device__ __forceinline__ int32_t f2i32_arm(float f) { return cvt_i32_arm(f); }
 
@@ -157,12 +174,8 @@ struct CtrlLane {
     float v[3];
 #pragma unroll
     for (int a = 0; a < 3; a++) v[a] = interp_update(ax[a], p.ts);
-    // conv_Vdir_to_Mdir, VD_vehicle_controller.cpp:113-118 (FL, BL, BR, FR)
     float mt[4];
-    mt[0] = (v[0] - v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[1] = (v[0] + v[1] - K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[2] = (v[0] - v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
-    mt[3] = (v[0] + v[1] + K::sqrtf2 * K::wheel_l * v[2] * 4.0f) / K::wheel_r;
+    vdir_to_mdir(v, mt);
     const int16_t r[4] = {(int16_t)(rw.x & 0xFFFFu), (int16_t)(rw.x >> 16),
                           (int16_t)(rw.y & 0xFFFFu), (int16_t)(rw.y >> 16)};
     float po[4][kPidF];
@@ -178,10 +191,7 @@ struct CtrlLane {
         const float ly = p.a1 * pv[w][PD_LY] + p.b0 * lx + p.b1 * pv[w][PD_LX];
         float integ = pv[w][PD_INTEG] + p.i_gain * p.dt * err;
         integ = (integ >= p.i_limit) ? p.i_limit : ((integ <= -p.i_limit) ? -p.i_limit : integ);
-        float ctrl = p.p_gain * err + integ - p.d_gain * ly;
-        float ff = tgt * p.ff_gain;
-        ff = (ff >= p.ff_limit) ? p.ff_limit : ((ff <= -p.ff_limit) ? -p.ff_limit : ff);
-        ctrl = ctrl + ff;
+        const float ctrl = ffpid_out(p, tgt, val, integ, ly);
         po[w][PD_VAL] = val;
         po[w][PD_INTEG] = integ;
         po[w][PD_LY] = ly;
@@ -215,18 +225,66 @@ struct CtrlLane {
 #pragma unroll
         for (int k = 0; k < IV_DT; k++) AX.st(a * kAxF + k, i, 0.0f);
     }
+    // the loop state the next step reads; now_tgt, now_ctrl and vel_tgt only where they cannot
+    // be formed later from that state (power off: the reset erased the interpolators' output) or
+    // when asked to (p.store_derived)
 #pragma unroll
     for (int w = 0; w < 4; w++)
 #pragma unroll
-      for (int k = 0; k < kPidF; k++) PD.st(w * kPidF + k, i, po[w][k]);
+      for (int k = 0; k < PD_TGT; k++) PD.st(w * kPidF + k, i, po[w][k]);
+    if (p.store_derived) {
 #pragma unroll
-    for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
+      for (int w = 0; w < 4; w++) {
+        PD.st(w * kPidF + PD_TGT, i, po[w][PD_TGT]);
+        PD.st(w * kPidF + PD_CTRL, i, po[w][PD_CTRL]);
+      }
+    }
+    if (!on || p.store_derived) {
+#pragma unroll
+      for (int a = 0; a < 3; a++) c.vel_tgt[a * pp + i] = v[a];
+    }
     const uint2 cw = make_uint2((uint32_t)(uint16_t)cur[0] | ((uint32_t)(uint16_t)cur[1] << 16),
                                 (uint32_t)(uint16_t)cur[2] | ((uint32_t)(uint16_t)cur[3] << 16));
     reinterpret_cast<uint2 *>(c.curr)[i] = cw;
     return cw;
   }
 };
+
+// now_vhcl_vel_tgt_mmps, FF_PI_D now_tgt and now_ctrl of robot i formed from the state the last
+// step left (ctrl_derive_out is the kernel): with the power on, the interpolators' output is the
+// stored vel_now and the loops' new value / integral / LPF output are stored, so the same
+// operations as the step give the same bits; with it off the step reset everything, stored
+// vel_tgt itself, and the loops' target and output are 0.  Valid while the power flags and the
+// parameters are those of that step (the host materialises before set_power; p: the step's)
+template <bool SMALL>
+__device__ __forceinline__ void ctrl_derive_lane(const CtrlDev &c, const CtrlPrm &p, uint32_t i) {
+  const Planes<SMALL> AX(c.ax, c.pitch, 3 * kAxF, i), PD(c.pid, c.pitch, 4 * kPidF, i);
+  if (!c.power[i]) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      PD.st(w * kPidF + PD_TGT, i, 0.0f);
+      PD.st(w * kPidF + PD_CTRL, i, 0.0f);
+    }
+    return;
+  }
+  float v[3], mt[4];
+#pragma unroll
+  for (int a = 0; a < 3; a++) v[a] = AX.ld(a * kAxF + IV_V, i);
+  float pv[4][3];
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) pv[w][k] = PD.ld(w * kPidF + k, i);  // PD_VAL, PD_INTEG, PD_LY
+  vdir_to_mdir(v, mt);
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const float tgt = mt[w] * 36.0f;
+    PD.st(w * kPidF + PD_TGT, i, tgt);
+    PD.st(w * kPidF + PD_CTRL, i, ffpid_out(p, tgt, pv[w][PD_VAL], pv[w][PD_INTEG], pv[w][PD_LY]));
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++) c.vel_tgt[a * c.pitch + i] = v[a];
+}
 
 // bytes of the per-robot control state the step streams (interpolators + wheel loops)
 inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * 4ull * (3 * kAxF + 4 * kPidF); }

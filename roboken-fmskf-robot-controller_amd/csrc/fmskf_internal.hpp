@@ -222,6 +222,10 @@ inline bool ekf9_r_diagonal(const float *r21) {
 //   pid [4 wheels][6][pitch]: FF_PI_D (now_val == prev_val, Integ, LPF now_Y, LPF prev_X,
 //                            now_tgt, now_ctrl)
 //   vel_tgt [3][pitch]       : now_vhcl_vel_tgt_mmps
+// Round 6: the step's outputs nothing reads back -- vel_tgt, now_tgt, now_ctrl, 44 B per robot --
+// are formed from the state it leaves when a reader asks (ctrl_lane.hpp ctrl_derive, host flag
+// fmskf_ctx::ctrl_derived_stale), except for robots whose power was off (vel_tgt is the
+// interpolators' last output, which their reset erased: the step stores it).
 //   curr [N][4] int16        : MOTOR_IF_M2006::s16_rawCurr_tgt (one 8-byte access per robot)
 //   power [N] u8             : isPowerOn
 struct CtrlDev {
@@ -238,6 +242,9 @@ struct CtrlPrm {
   float freq, dt, ff_gain, p_gain, i_gain, d_gain, i_limit, ff_limit, a1, b0, b1, ts;
   int32_t curr_limit;
   int32_t dir[4];
+  // 1: the step also stores vel_tgt, now_tgt and now_ctrl (inside a graph capture: the replay's
+  // readers cannot be brought up to date by the host); 0: they are formed on demand (ctrl_derive)
+  uint32_t store_derived;
 };
 
 // x / P plane pitch for N instances: N rounded up to 512, plus 256 -> an odd multiple of
@@ -364,6 +371,7 @@ int ensemble_nblocks(uint64_t n);
 // vehicle control step, TX frames, VehicleInfo export (kernels_ctrl.hip)
 int launch_ctrl_set_target(const CtrlDev &c, const float *vel, const float *acl, const float *jrk,
                            const uint8_t *mask, hipStream_t st);
+int launch_ctrl_derive(const CtrlDev &c, const CtrlPrm &p, hipStream_t st);
 int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uint32_t rstride,
                      hipStream_t st);
 int launch_can_tx(const CtrlDev &c, uint8_t *frames, hipStream_t st);

@@ -298,6 +298,22 @@ int launch_ctrl_step(const CtrlDev &c, const CtrlPrm &p, const int16_t *rpm, uin
   return (int)hipGetLastError();
 }
 
+// the step outputs nothing reads back, formed when a reader needs them (ctrl_lane.hpp
+// ctrl_derive_lane; host: fmskf_ctx::ctrl_derived_stale)
+template <bool SMALL>
+__global__ __launch_bounds__(kBlock) void k_ctrl_derive(CtrlDev c, CtrlPrm p) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (uint32_t)c.n) return;
+  ctrl_derive_lane<SMALL>(c, p, i);
+}
+
+int launch_ctrl_derive(const CtrlDev &c, const CtrlPrm &p, hipStream_t st) {
+  if (c.n == 0) return 0;
+  if (c.pitch * 4 * 3 * kAxF < 0xFFFFFFFFull) k_ctrl_derive<true><<<grid1(c.n), kBlock, 0, st>>>(c, p);
+  else k_ctrl_derive<false><<<grid1(c.n), kBlock, 0, st>>>(c, p);
+  return (int)hipGetLastError();
+}
+
 template <bool CAN, bool CNT = false, bool PS = false>
 static int isr_rs_l(const DevState &s, const TickIn &in, bool libm, const CtrlDev &c, const CtrlPrm &p,
                     uint8_t *frames, hipStream_t st, const CanArgs &can) {

@@ -90,6 +90,95 @@ def test_control_custom_params_and_d_term(orc):
     np.testing.assert_array_equal(bits(got["wheel_ctrl"]), bits(ref.wheel("ctrl")))
 
 
+def test_control_outputs_formed_on_demand(orc, tmp_path):
+    """Round 6: the step leaves vel_tgt and FF_PI_D now_tgt / now_ctrl to be formed when read
+    (ctrl_lane.hpp ctrl_derive_lane).  A readout still returns the LAST step's outputs after the
+    parameters change, after the power flags and targets change, after graph replays whose
+    captured steps ran with parameters changed since, and through a checkpoint; robots switched
+    off keep the interpolators' last output (VD_vehicle_controller.cpp, FF_PI_D reset)."""
+    import torch
+    n = 1537
+    rng = np.random.default_rng(77)
+    kw_b = dict(ctrl_freq_hz=1000.0, ff_gain=0.01, p_gain=0.05, i_gain=0.2, d_gain=0.004,
+                i_limit=0.8, lpf_freq_hz=25.0, ff_limit=0.7, interp_ts=np.float32(0.001),
+                curr_limit_raw=2500)
+    prm_b = orc.ctrl_params(c_freq=1000.0, ff=0.01, pg=0.05, ig=0.2, dg=0.004, ilim=0.8, lpf=25.0,
+                            fflim=0.7, ts=np.float32(0.001), clim=2500)
+    prm_a = orc.ctrl_params()
+    ref = orc.CtrlBatch(n, prm_a)
+
+    def targets():
+        vel = np.stack([rng.uniform(-400, 400, n), rng.uniform(-400, 400, n),
+                        rng.uniform(-6, 6, n)]).astype(np.float32)
+        return vel, np.full((3, n), 1000.0, np.float32), np.full((3, n), 10000.0, np.float32)
+
+    def rpm():
+        return rng.integers(-900, 900, (n, 4)).astype(np.int16)
+
+    def check(e, what):
+        got = e.get_ctrl()
+        np.testing.assert_array_equal(got["curr"], ref.curr(), err_msg=what)
+        np.testing.assert_array_equal(bits(got["vel_tgt"]), bits(ref.vel_tgt()), err_msg=what)
+        np.testing.assert_array_equal(bits(got["wheel_tgt"]), bits(ref.wheel("tgt")), err_msg=what)
+        np.testing.assert_array_equal(bits(got["wheel_ctrl"]), bits(ref.wheel("ctrl")), err_msg=what)
+
+    st = torch.cuda.Stream()
+    with Engine("kf6", n) as e:
+        e.set_stream(st)
+        pw = (rng.random(n) < 0.8).astype(np.uint8)
+        e.set_power(pw)
+        ref.set_power(pw)
+        tv = targets()
+        e.set_target_vel(*tv)
+        ref.set_target_vel(*tv)
+        for _ in range(6):
+            r = rpm()
+            e.control(r)
+            ref.step(r)
+        e.set_ctrl_params(**kw_b)  # the last step ran with the defaults
+        check(e, "after set_ctrl_params")
+        ref.p = prm_b
+        r = rpm()
+        e.control(r)
+        ref.step(r)
+        pw = (rng.random(n) < 0.5).astype(np.uint8)  # power and targets change after the step
+        e.set_power(pw)
+        ref.set_power(pw)
+        tv = targets()
+        e.set_target_vel(*tv)
+        ref.set_target_vel(*tv)
+        check(e, "after set_power / set_target_vel")
+        for _ in range(2):  # steps with robots just switched off (their outputs are stored)
+            r = rpm()
+            e.control(r)
+            ref.step(r)
+        check(e, "power-off robots")
+        # a graph of two steps captured with parameters B, replayed after switching to A
+        rr = [rpm() for _ in range(2)]
+        dev = [torch.from_numpy(x).cuda() for x in rr]
+        torch.cuda.synchronize()
+        e.graph_begin()
+        for d in dev:
+            e.control(d)
+        e.graph_end()
+        e.set_ctrl_params()  # defaults (A) from now on; the replays keep B
+        e.graph_launch(3)
+        for _ in range(3):
+            for x in rr:
+                ref.step(x)
+        st.synchronize()
+        check(e, "graph replays")
+        ref.p = prm_a
+        r = rpm()
+        e.control(r)  # a direct step with A after the replays
+        ref.step(r)
+        e.save_state(tmp_path / "ctrl.ck")  # a checkpoint right after a step
+        with Engine("kf6", n) as b:
+            b.load_state(tmp_path / "ctrl.ck")
+            check(b, "checkpoint")
+        check(e, "direct step after the replays")
+
+
 def test_control_reads_ingested_motor_state():
     n = 513
     T = 6
