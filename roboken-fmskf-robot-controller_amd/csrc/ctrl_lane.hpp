@@ -156,10 +156,12 @@ struct CtrlLane {
   __device__ __forceinline__ void load(const CtrlDev &c, uint32_t i) {
     const Planes<SMALL, CP> AX(c.ax, c.pitch, 3 * kAxF, i), PD(c.pid, c.pitch, 4 * kPidF, i);
     on = c.power[i];
+    // every interpolator field but acl_now, which update() writes before any use (round 6: 12 B
+    // less per robot; only set_target_params reads it, as acl_ini)
 #pragma unroll
     for (int a = 0; a < 3; a++)
 #pragma unroll
-      for (int k = 0; k < kAxF; k++) ax[a].f[k] = AX.ld(a * kAxF + k, i);
+      for (int k = 0; k < kAxF; k++) ax[a].f[k] = k == IV_A ? 0.0f : AX.ld(a * kAxF + k, i);
 #pragma unroll
     for (int w = 0; w < 4; w++)
 #pragma unroll
