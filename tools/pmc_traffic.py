@@ -103,6 +103,9 @@ PATHS = [
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 60, 42),
     ("can_ingest_2p20", "k_can4", 104, 80),
+    # the control step (k_ctrl_step): power 1, interpolators 132, FF_PI_D 64, rpm 8 read; the
+    # interpolators' time / speed / accel 36, FF_PI_D 64 and the currents 8 written (round 6)
+    ("control_step_2p20", "k_ctrl_step", 1 + 132 + 64 + 8, 36 + 64 + 8),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
     # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
     # without its rpm (197; 209 before round 6 also read the interpolators' acceleration) and

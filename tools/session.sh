@@ -81,6 +81,7 @@ for s in $STEPS; do
            pmc2 pmc_path_rs_tick_2p20_padded_sums 120 --model rs --pad 512 --ticks 30
            pmc2 pmc_path_wt901_ingest_2p20 120 --op wt901 --ticks 30
            pmc2 pmc_path_can_ingest_2p20 120 --op can --ticks 30
+           pmc2 pmc_path_control_step_2p20 120 --op control --ticks 30
            pmc2 pmc_path_cfg2_kf6_comp_pos_2p20 120 --packed --comp --ticks 30
            pmc2 pmc_path_isr_kf6_2p20 120 --op isr --ticks 30
            pmc2 pmc_path_isr_can_kf6_2p20 120 --op isr_can --ticks 30
