@@ -391,8 +391,12 @@ int fmskf_isr_tick(fmskf_handle h, const fmskf_tick_inputs *in, uint8_t *frames,
 int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t *can_stamps,
                        const fmskf_tick_inputs *in, uint8_t *frames, uint32_t mem);
 /* readout: vel_tgt [3][N] (get_vehicle_vel_tgt_mmps_latest), curr_raw [N][4]
- * (get_rawCurr_tgt), wheel_tgt / wheel_ctrl [4][N] (FF_PI_D get_target / last output).
- * Any pointer may be NULL. */
+ * (get_rawCurr_tgt), wheel_tgt / wheel_ctrl [4][N] (FF_PI_D get_target / last output), all as
+ * the last control step (fmskf_control or an ISR call) left them.  Any pointer may be NULL.
+ * The step itself stores only the state its next tick reads and the currents: the first readout
+ * (or checkpoint, or fmskf_set_power) after a step forms vel_tgt / wheel_tgt / wheel_ctrl from
+ * that state with the step's parameters, one small kernel on the handle's stream; changing the
+ * parameters, targets or power flags after a step does not change what this returns. */
 int fmskf_get_ctrl(fmskf_handle h, float *vel_tgt, int16_t *curr_raw, float *wheel_tgt,
                    float *wheel_ctrl, uint32_t mem);
 
