@@ -343,9 +343,11 @@ def secondary_configs(dev, stream, ticks: int, trig):
 WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4
 CAN_RX_BYTES = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)
 # the vehicle control step (control_step_2p20): power 1, interpolators 132 (every field but the
-# acceleration, which update() writes before it reads it), FF_PI_D 64, rpm 8 read; interpolator time / speed / accel 36, FF_PI_D value / integral / LPF 64, currents 8 written
-# (369 before round 6, with vel_tgt and FF_PI_D now_tgt / now_ctrl stored by every step)
-CTRL_STEP_BYTES = 1 + 132 + 64 + 8 + 36 + 64 + 8
+# acceleration, which update() writes before it reads it), FF_PI_D integral / LPF 48, the last
+# step's rpm 8 (FF_PI_D now_val is formed from it), rpm 8 read; interpolator time / speed / accel
+# 36, FF_PI_D 48, the rpm 8 and the currents 8 written (369 before round 6, with vel_tgt and
+# FF_PI_D now_tgt / now_ctrl stored by every step and now_val as four floats)
+CTRL_STEP_BYTES = 1 + 132 + 48 + 8 + 8 + 36 + 48 + 8 + 8
 # algorithmic bytes per robot of the rows either side of the tick
 PATH_BYTES = {
     # RS tick: pos (x, y) 8 r + (x, y, th) 12 w -- theta is overwritten by the correct, so it is
@@ -370,7 +372,7 @@ PATH_BYTES = {
     # formed at readout from the angle and the previous one; the IIR input state x is formed from
     # the previous frame's angle and stamp (round 5: 224 -> 216 B; round 6: 216 -> 184 B))
     "can_ingest_2p20": CAN_RX_BYTES,
-    # control step: power 1, interpolators 132, FF_PI_D 64, rpm 8 r; 36 + 64 + 8 w (round 6: the
+    # control step: power 1, interpolators 132, FF_PI_D 48 + 8, rpm 8 r; 36 + 48 + 8 + 8 w (round 6: the
     # outputs nothing reads back -- vel_tgt 12, FF_PI_D now_tgt / now_ctrl 32 -- formed on demand)
     "control_step_2p20": CTRL_STEP_BYTES,
     # fused KF6 ISR: the tick's 232 + the control step's CTRL_STEP_BYTES without its rpm read (the tick

@@ -39,10 +39,10 @@ struct CkHeader {
   // rs_prev_at; [4][pitch] planes before); bit 1, the motor group's angle sums as split low /
   // high words (round 6, fmskf_internal.hpp m_sum_lo; int64 [4][pitch] planes before); bit 2, the
   // IMU group's yaw / gyro z as the Yaw / GZ register words (round 6, DevState::imu_yg; two float
-  // planes before)
+  // planes before); bit 3, the control group's rpm of the last step (round 6, CtrlDev::rpm_prev)
   uint32_t layout;
 };
-constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u, kCkImuYg = 4u;
+constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u, kCkImuYg = 4u, kCkRpmPrev = 8u;
 struct CkSection {
   void *dev;
   size_t bytes;
@@ -84,6 +84,7 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({c.ax, (size_t)3 * kAxF * c.pitch * 4});
     v.push_back({c.pid, (size_t)4 * kPidF * c.pitch * 4});
     v.push_back({c.vel_tgt, (size_t)3 * c.pitch * 4});
+    v.push_back({c.rpm_prev, (size_t)4 * c.n * 2});
     v.push_back({c.curr, (size_t)4 * c.n * 2});
     v.push_back({c.power, (size_t)c.n});
   }
@@ -101,7 +102,7 @@ void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->elem = h->d.elem;
   hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
   hd->m_pitch = plane_pitch(h->s.n);
-  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit | kCkImuYg;
+  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit | kCkImuYg | kCkRpmPrev;
   const uint64_t w = tile_w_elem(4);
   hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
 }

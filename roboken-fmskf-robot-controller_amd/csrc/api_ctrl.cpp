@@ -77,6 +77,7 @@ void zero_ctrl(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, h->stream), "ctrl init");
   hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, h->stream), "ctrl init");
   hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, h->stream), "ctrl init");
+  hip_check(hipMemsetAsync(c.rpm_prev, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
   hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, h->stream), "ctrl init");
   hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, h->stream), "ctrl init");
   ctrl_params_defaults(&h->cprm);
@@ -93,6 +94,7 @@ void ensure_ctrl(fmskf_ctx *h) {
   c.ax = h->alloc<float>((size_t)3 * kAxF * c.pitch);
   c.pid = h->alloc<float>((size_t)4 * kPidF * c.pitch);
   c.vel_tgt = h->alloc<float>((size_t)3 * c.pitch);
+  c.rpm_prev = h->alloc<int16_t>((size_t)4 * c.n);
   c.curr = h->alloc<int16_t>((size_t)4 * c.n);
   c.power = h->alloc<uint8_t>((size_t)c.n);
   zero_ctrl(h);

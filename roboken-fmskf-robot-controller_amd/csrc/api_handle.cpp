@@ -226,6 +226,7 @@ void do_reset(fmskf_ctx *h) {
     hip_check(hipMemsetAsync(c.ax, 0, (size_t)3 * kAxF * c.pitch * 4, st), "reset ctrl");
     hip_check(hipMemsetAsync(c.pid, 0, (size_t)4 * kPidF * c.pitch * 4, st), "reset ctrl");
     hip_check(hipMemsetAsync(c.vel_tgt, 0, (size_t)3 * c.pitch * 4, st), "reset ctrl");
+    hip_check(hipMemsetAsync(c.rpm_prev, 0, (size_t)4 * c.n * 2, st), "reset ctrl");
     hip_check(hipMemsetAsync(c.curr, 0, (size_t)4 * c.n * 2, st), "reset ctrl");
     hip_check(hipMemsetAsync(c.power, 0, (size_t)c.n, st), "reset ctrl");
   }

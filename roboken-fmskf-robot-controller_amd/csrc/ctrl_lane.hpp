@@ -162,10 +162,17 @@ struct CtrlLane {
     for (int a = 0; a < 3; a++)
 #pragma unroll
       for (int k = 0; k < kAxF; k++) ax[a].f[k] = k == IV_A ? 0.0f : AX.ld(a * kAxF + k, i);
+    // now_val from the rpm the last step ran on (CtrlDev::rpm_prev), the other loop fields from
+    // their planes
+    const uint2 rp = reinterpret_cast<const uint2 *>(c.rpm_prev)[i];
+    const int16_t r[4] = {(int16_t)(rp.x & 0xFFFFu), (int16_t)(rp.x >> 16), (int16_t)(rp.y & 0xFFFFu),
+                          (int16_t)(rp.y >> 16)};
 #pragma unroll
-    for (int w = 0; w < 4; w++)
+    for (int w = 0; w < 4; w++) {
+      pv[w][PD_VAL] = rpm_to_mvel(r[w]) * 36.0f;
 #pragma unroll
-      for (int k = 0; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
+      for (int k = PD_INTEG; k < 4; k++) pv[w][k] = PD.ld(w * kPidF + k, i);
+    }
   }
 
   // rw: the four s16_rawSpeedRpm (FL, BL, BR, FR) packed in 8 bytes.  Returns the packed
@@ -233,7 +240,8 @@ struct CtrlLane {
 #pragma unroll
     for (int w = 0; w < 4; w++)
 #pragma unroll
-      for (int k = 0; k < PD_TGT; k++) PD.st(w * kPidF + k, i, po[w][k]);
+      for (int k = PD_INTEG; k < PD_TGT; k++) PD.st(w * kPidF + k, i, po[w][k]);
+    reinterpret_cast<uint2 *>(c.rpm_prev)[i] = on ? rw : make_uint2(0u, 0u);  // now_val's rpm
     if (p.store_derived) {
 #pragma unroll
       for (int w = 0; w < 4; w++) {
@@ -273,10 +281,15 @@ __device__ __forceinline__ void ctrl_derive_lane(const CtrlDev &c, const CtrlPrm
 #pragma unroll
   for (int a = 0; a < 3; a++) v[a] = AX.ld(a * kAxF + IV_V, i);
   float pv[4][3];
+  const uint2 rp = reinterpret_cast<const uint2 *>(c.rpm_prev)[i];
+  const int16_t r[4] = {(int16_t)(rp.x & 0xFFFFu), (int16_t)(rp.x >> 16), (int16_t)(rp.y & 0xFFFFu),
+                        (int16_t)(rp.y >> 16)};
 #pragma unroll
-  for (int w = 0; w < 4; w++)
+  for (int w = 0; w < 4; w++) {
+    pv[w][PD_VAL] = rpm_to_mvel(r[w]) * 36.0f;  // now_val, as the step formed it
 #pragma unroll
-    for (int k = 0; k < 3; k++) pv[w][k] = PD.ld(w * kPidF + k, i);  // PD_VAL, PD_INTEG, PD_LY
+    for (int k = PD_INTEG; k < 3; k++) pv[w][k] = PD.ld(w * kPidF + k, i);  // PD_INTEG, PD_LY
+  }
   vdir_to_mdir(v, mt);
 #pragma unroll
   for (int w = 0; w < 4; w++) {
@@ -289,7 +302,7 @@ __device__ __forceinline__ void ctrl_derive_lane(const CtrlDev &c, const CtrlPrm
 }
 
 // bytes of the per-robot control state the step streams (interpolators + wheel loops)
-inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * 4ull * (3 * kAxF + 4 * kPidF); }
+inline uint64_t ctrl_state_bytes(const CtrlDev &c) { return c.n * (4ull * (3 * kAxF + 4 * kPidF) + 8ull); }
 
 // C610 0x200 payload of one robot: bytes (hi, lo) per wheel -> swap the bytes of every 16-bit half
 __device__ __forceinline__ uint2 tx_frame(uint2 c) {

@@ -233,6 +233,10 @@ struct CtrlDev {
   float *ax = nullptr;
   float *pid = nullptr;
   float *vel_tgt = nullptr;
+  // [N][4] the rpm the last step ran on (0 after a power-off reset): FF_PI_D's now_val is
+  // rpm_to_mvel(rpm) * GEAR_RATIO, so the step keeps the 8-byte record instead of the four float
+  // now_val planes (round 6; the pid planes' now_val row is no longer used)
+  int16_t *rpm_prev = nullptr;
   int16_t *curr = nullptr;
   uint8_t *power = nullptr;
 };

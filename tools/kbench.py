@@ -346,7 +346,7 @@ def bench_io(args, e, n, R, dev, rpm, st):
         run = (lambda k: e.control(rpm[k % R])) if args.op == "control" else (lambda k: e.can_tx(frames))
         # control: power 1 + interpolators 3x12 + FF_PI_D 4x4 read, rpm 8 read; writes
         # interpolator dt/v/a 3x3, FF_PI_D 4x6, vel_tgt 3, currents 8 (power on)
-        bpr = (1 + 4 * 33 + 4 * 16 + 8 + 4 * 9 + 4 * 16 + 8) if args.op == "control" else 16  # round 6: 313 B
+        bpr = (1 + 4 * 33 + 4 * 12 + 8 + 8 + 4 * 9 + 4 * 12 + 8 + 8) if args.op == "control" else 16  # round 6: 297 B
     elif args.op == "wt901":
         # one 10 ms poll per robot: acc, gyro, angle, quaternion frames (44 B), ring of R polls
         stride = 48

@@ -103,30 +103,31 @@ PATHS = [
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 60, 42),
     ("can_ingest_2p20", "k_can4", 104, 80),
-    # the control step (k_ctrl_step): power 1, interpolators 132, FF_PI_D 64, rpm 8 read; the
-    # interpolators' time / speed / accel 36, FF_PI_D 64 and the currents 8 written (round 6)
-    ("control_step_2p20", "k_ctrl_step", 1 + 132 + 64 + 8, 36 + 64 + 8),
+    # the control step (k_ctrl_step): power 1, interpolators 132, FF_PI_D 48, the last step's rpm 8,
+    # rpm 8 read; the interpolators' time / speed / accel 36, FF_PI_D 48, the rpm 8 and the
+    # currents 8 written (round 6)
+    ("control_step_2p20", "k_ctrl_step", 1 + 132 + 48 + 8 + 8, 36 + 48 + 8 + 8),
     ("cfg2_kf6_comp_pos_2p20", "k_kf6p", 144, 128),
     # the fused KF6 ISR (k_isr_kf6, planes): the tick's 124 / 108, the control step's reads
-    # without its rpm (197; 209 before round 6 also read the interpolators' acceleration) and
-    # writes (108; 152 before round 6 formed vel_tgt / now_tgt / now_ctrl on demand), the 0x200
-    # frame (8 w)
-    ("isr_kf6_2p20", "k_isr_kf6", 124 + 197, 108 + 108 + 8),
+    # without its rpm (189; 209 before round 6 also read the interpolators' acceleration and the
+    # four float now_val) and writes (100; 152 before round 6 formed vel_tgt / now_tgt / now_ctrl
+    # on demand and kept now_val as the step's rpm), the 0x200 frame (8 w)
+    ("isr_kf6_2p20", "k_isr_kf6", 124 + 189, 108 + 100 + 8),
     # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 120 / 96, the rpm
     # plane no longer read
-    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 197 + 104, 108 + 108 + 8 + 80),
+    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 189 + 104, 108 + 100 + 8 + 80),
     # the reference-semantics ISR (k_isr_rs) on the motor state: the RS tick's 84 / 56 with the
-    # control step's 197 / 108 and the frame; with the CAN RX fused in, the rpm and sums not read
-    ("isr_rs_2p20", "k_isr_rs", 84 + 197, 56 + 108 + 8),
+    # control step's 189 / 100 and the frame; with the CAN RX fused in, the rpm and sums not read
+    ("isr_rs_2p20", "k_isr_rs", 84 + 189, 56 + 100 + 8),
     # the EKF9 ISR (k_isr_ekf9): the tick's 232 / 216 (cfg 3's count; the heading's hidden row,
-    # 4 + 4 B, is traffic above it) with the control step's 205 / 108 (its own rpm plane) and the
+    # 4 + 4 B, is traffic above it) with the control step's 197 / 100 (its own rpm plane) and the
     # frame
-    ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 205, 216 + 108 + 8),
+    ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 197, 216 + 100 + 8),
     # round 6: the previous sums neither read nor written while they equal the motor sums (PS)
-    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 197 + 104, 56 - 32 + 108 + 8 + 80),
+    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 189 + 104, 56 - 32 + 100 + 8 + 80),
     # the EKF9 ISR with the tick's CAN RX fused in: + the CAN row's 120 / 96, the control step's
     # rpm plane no longer read
-    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 205 - 8 + 104, 216 + 108 + 8 + 80),
+    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 197 - 8 + 104, 216 + 100 + 8 + 80),
 ]
 
 
