@@ -341,7 +341,7 @@ def secondary_configs(dev, stream, ticks: int, trig):
 # the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20) and the C610 RX of four wheels
 # (can_ingest_2p20)
 WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4
-CAN_RX_BYTES = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)
+CAN_RX_BYTES = 4 * (10 + (2 + 2 + 2 + 2 + 4 + 4) + (2 + 2 + 4 + 4) + 2 + 2)
 # the vehicle control step (control_step_2p20): power 1, interpolators 132 (every field but the
 # acceleration, which update() writes before it reads it), FF_PI_D integral / LPF 48, the last
 # step's rpm 8 (FF_PI_D now_val is formed from it), rpm 8 read; interpolator time / speed / accel
@@ -367,10 +367,12 @@ PATH_BYTES = {
     # the yaw / gyro z floats, then 102)
     "wt901_ingest_2p20": WT901_POLL_BYTES,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
-    # output y and the low word of the int64 sum read and written (round 6: the high word only on
-    # a carry across 2^32); rpm and curr written (the speed is the IIR state y; Status's dlt is
-    # formed at readout from the angle and the previous one; the IIR input state x is formed from
-    # the previous frame's angle and stamp (round 5: 224 -> 216 B; round 6: 216 -> 184 B))
+    # output y and the low word of the int64 sum read; the new stamp and angle (over the older
+    # history slots: the current ones become the previous ones where they lie, round 6), IIR y and
+    # the sum's low word written (round 6: the high word only on a carry across 2^32); rpm and curr
+    # written (the speed is the IIR state y; Status's dlt is formed at readout from the angle and
+    # the previous one; the IIR input state x is formed from the previous frame's angle and stamp
+    # (round 5: 224 -> 216 B; round 6: 216 -> 184 -> 168 B))
     "can_ingest_2p20": CAN_RX_BYTES,
     # control step: power 1, interpolators 132, FF_PI_D 48 + 8, rpm 8 r; 36 + 48 + 8 + 8 w (round 6: the
     # outputs nothing reads back -- vel_tgt 12, FF_PI_D now_tgt / now_ctrl 32 -- formed on demand)

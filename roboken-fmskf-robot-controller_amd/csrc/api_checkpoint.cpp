@@ -72,7 +72,8 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_qprev, (size_t)4 * n * 4});
   }
   if (groups & 4) {
-    for (void *p : {(void *)s.m_micro, (void *)s.m_angle, (void *)s.m_prev, (void *)s.m_prev_micro,
+    const MotorSlots ms = motor_slots(s);  // newest first, whichever slots hold them (DevState::m_par)
+    for (void *p : {(void *)ms.micro, (void *)ms.angle, (void *)ms.prev, (void *)ms.prev_micro,
                     (void *)s.m_rpm, (void *)s.m_curr})
       v.push_back({p, (size_t)4 * n * 2});
     v.push_back({s.m_sum_lo, (size_t)4 * n * 4});

@@ -316,13 +316,17 @@ int fmskf_isr_tick_can(fmskf_handle h, const uint8_t *can_frames, const int16_t 
         h->rs_prev_stale = h->rs_prev_stale || ps;
       }
     }
-    if (fused != (int)hipErrorNotSupported) launch_check(fused, "isr+can launch");
+    if (fused != (int)hipErrorNotSupported) {
+      launch_check(fused, "isr+can launch");
+      h->s.m_par ^= 1u;  // the frames' stamps and angles went over the older history slots
+    }
     if (fused == (int)hipErrorNotSupported) {  // CAN RX, then the ISR of fmskf_isr_tick
       h->isr_can_split++;
       rs_prev_materialize(h);  // the CAN RX rewrites the motor sums
       h->rs_prev_synced = false;
       launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, nullptr, h->cfg.motor_dir, h->stream),
                    "can launch");
+      h->s.m_par ^= 1u;
       isr_launches(h, t, dst);
     }
     h->time_end();

@@ -181,6 +181,8 @@ struct fmskf_ctx {
   // reads the power flags the step ran with.  Inside a graph capture the step stores them itself
   // (the host cannot follow the replays): graph_has_ctrl marks a captured sequence with a step.
   bool ctrl_derived_stale = false, graph_has_ctrl = false;
+  // the motor history order (DevState::m_par) at the start and the end of the captured sequence
+  uint32_t graph_par0 = 0, graph_par_end = 0;
   fmskf::CtrlPrm ctrl_prm_last{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -590,6 +590,7 @@ int fmskf_graph_begin(fmskf_handle h) {
     // before the capture are formed now, while the host still knows their parameters
     ctrl_materialize(h);
     h->graph_has_ctrl = false;
+    h->graph_par0 = h->s.m_par;  // the motor history order the captured CAN RX calls start from
     hip_check(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal),
               "hipStreamBeginCapture");
     h->capturing = true;
@@ -603,6 +604,10 @@ int fmskf_graph_end(fmskf_handle h) {
     DeviceGuard g(h->cfg.device);
     h->capturing = false;
     h->rs_prev_synced = false;  // the captured calls moved host-side flags the replays do not
+    // nor has any captured CAN RX run: the order is back where the capture started, and each
+    // replay leaves it where the capture ended
+    h->graph_par_end = h->s.m_par;
+    h->s.m_par = h->graph_par0;
     hipGraph_t gnew = nullptr;
     hip_check(hipStreamEndCapture(h->stream, &gnew), "hipStreamEndCapture");
     if (h->graph_exec) hip_check(hipGraphExecDestroy(h->graph_exec), "hipGraphExecDestroy");
@@ -620,8 +625,14 @@ int fmskf_graph_launch(fmskf_handle h, uint32_t times) {
     if (!h->graph_exec) fail(FMSKF_EINVAL, "no graph captured");
     if (h->capturing) fail(FMSKF_EINVAL, "capture still open");
     DeviceGuard g(h->cfg.device);
-    for (uint32_t k = 0; k < times; k++)
+    for (uint32_t k = 0; k < times; k++) {
+      if (h->s.m_par != h->graph_par0) {  // replays start from the capture's motor history order
+        launch_check(launch_motor_swap(h->s, h->stream), "motor history order");
+        h->s.m_par ^= 1u;
+      }
       hip_check(hipGraphLaunch(h->graph_exec, h->stream), "hipGraphLaunch");
+      h->s.m_par = h->graph_par_end;
+    }
     h->rs_prev_synced = false;
     if (h->graph_has_ctrl && times > 0) h->ctrl_derived_stale = false;  // the replayed steps stored them
   });
@@ -684,6 +695,7 @@ int fmskf_ingest_can(fmskf_handle h, const uint8_t *frames, const int16_t *stamp
     launch_check(launch_can(h->s, (const uint8_t *)f, (const int16_t *)s, (const uint8_t *)p,
                             h->cfg.motor_dir, h->stream),
                  "can launch");
+    h->s.m_par ^= 1u;  // the frames' stamps and angles went over the older history slots
     h->rs_prev_synced = false;
   });
 }

@@ -60,7 +60,7 @@ int fmskf_get_motors(fmskf_handle h, int16_t *angle, int16_t *rpm, int16_t *curr
     if (mem != FMSKF_MEM_HOST && mem != FMSKF_MEM_DEVICE) fail(FMSKF_EINVAL, "bad mem flag");
     const uint64_t n = h->s.n;
     ensure_motors(h);
-    copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
+    copy_out(h, angle, motor_slots(h->s).angle, 4 * n * 2, mem);
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
     if (angle_sum) {  // the split sums as whole int64 [4][N] planes
@@ -98,13 +98,14 @@ int fmskf_get_motor_status(fmskf_handle h, int16_t *microsec_id, int16_t *angle,
     DeviceGuard g(h->cfg.device);
     const uint64_t n = h->s.n;
     ensure_motors(h);
-    copy_out(h, microsec_id, h->s.m_micro, 4 * n * 2, mem);
-    copy_out(h, angle, h->s.m_angle, 4 * n * 2, mem);
+    const MotorSlots ms = motor_slots(h->s);
+    copy_out(h, microsec_id, ms.micro, 4 * n * 2, mem);
+    copy_out(h, angle, ms.angle, 4 * n * 2, mem);
     copy_out(h, rpm, h->s.m_rpm, 4 * n * 2, mem);
     copy_out(h, curr, h->s.m_curr, 4 * n * 2, mem);
     if (dlt_out_angle_rad) {
       float *dst = mem == FMSKF_MEM_DEVICE ? dlt_out_angle_rad : (float *)h->out_for(4 * n * 4);
-      launch_check(launch_motor_dlt(h->s.m_angle, h->s.m_prev, dst, 4 * n, h->stream), "motor dlt");
+      launch_check(launch_motor_dlt(ms.angle, ms.prev, dst, 4 * n, h->stream), "motor dlt");
       if (mem == FMSKF_MEM_HOST) copy_out(h, dlt_out_angle_rad, dst, 4 * n * 4, mem);
     }
     // Status::flt_SpeedRadPS [N][4]: the IIR1 output rows as the device keeps them

@@ -18,6 +18,8 @@ struct CanArgs {
   const int16_t *stamps;
   const uint8_t *present;
   int8_t dir[4];
+  // the newest frame's stamps and angles, and the ones before (DevState::m_par, motor_slots): a
+  // frame's stamp and angle go over the older slot (prev_micro / prev), the host flips the order
   int16_t *micro, *angle, *rpm, *curr;
   int16_t *prev;  // [N][4] the angle before this frame (Status::flt_dltOutAngle_rad at readout)
   int16_t *prev_micro;  // [N][4] the stamp before this frame (the IIR1's previous sample, speed_x)
@@ -128,10 +130,11 @@ inline bool can_args(const DevState &s, const uint8_t *can_frames, const int16_t
   ca.stamps = can_stamps;
   ca.present = nullptr;
   for (int w = 0; w < 4; w++) ca.dir[w] = dir[w];
-  ca.micro = s.m_micro;
-  ca.angle = s.m_angle;
-  ca.prev = s.m_prev;
-  ca.prev_micro = s.m_prev_micro;
+  const MotorSlots ms = motor_slots(s);
+  ca.micro = ms.micro;
+  ca.angle = ms.angle;
+  ca.prev = ms.prev;
+  ca.prev_micro = ms.prev_micro;
   ca.rpm = s.m_rpm;
   ca.curr = s.m_curr;
   ca.sum_lo = s.m_sum_lo;
@@ -229,10 +232,10 @@ struct Can4Lane {
       __builtin_amdgcn_raw_buffer_store_b128(ol, rsrc_span(a.sum_lo + hb * 4), li * 16u, 0, SP);
       __builtin_amdgcn_raw_buffer_store_b128(oy, rsrc_span(a.iir_y + hb * 4), li * 16u, 0, SP);
       const auto pk = [](uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; };
-      st_span<uint64_t, SP>(rsrc_span(a.prev_micro + hb * 4), li, 0, mv);
-      st_span<uint64_t, SP>(rsrc_span(a.micro + hb * 4), li, 0, pk(st.x, st.y));
-      st_span<uint64_t, SP>(rsrc_span(a.angle + hb * 4), li, 0, pk(na[0], na[1]));
-      st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, av);
+      // the new stamps and angles over the older slots: the current ones become the previous
+      // ones where they lie (DevState::m_par)
+      st_span<uint64_t, SP>(rsrc_span(a.prev_micro + hb * 4), li, 0, pk(st.x, st.y));
+      st_span<uint64_t, SP>(rsrc_span(a.prev + hb * 4), li, 0, pk(na[0], na[1]));
       st_span<uint64_t, SP>(rsrc_span(a.rpm + hb * 4), li, 0, pk(nr[0], nr[1]));
       st_span<uint64_t, SP>(rsrc_span(a.curr + hb * 4), li, 0, pk(nc[0], nc[1]));
     }

@@ -73,9 +73,25 @@ struct DevState {
   float *m_iir_y = nullptr;    // [N][4] (one 16-byte access per robot in k_can4)
   int16_t *m_prev_micro = nullptr;  // [N][4] the stamp of the frame before (the IIR1's previous
                                     // sample x is formed from it: kernels_ingest.hip can_wheel)
+  // Round 6: (m_micro, m_prev_micro) and (m_angle, m_prev) are two-slot histories.  A CAN RX writes
+  // the new stamp and angle over the older slot and nothing else (16 B per robot instead of 32:
+  // the newest pair becomes the previous one where it lies), and the host flips m_par: 0, the
+  // newest are m_micro / m_angle (the checkpoint's order), 1, they are m_prev_micro / m_prev.
+  // The launchers and readers take the slots through motor_slots().
+  uint32_t m_par = 0;
   unsigned long long *counters = nullptr;  // [8]
   float *sintab = nullptr;                 // [513]
 };
+
+// the motor state's stamp / angle history slots in the current order (DevState::m_par): the newest
+// frame's stamps and angles, and the ones before
+struct MotorSlots {
+  int16_t *micro, *angle, *prev_micro, *prev;
+};
+inline MotorSlots motor_slots(const DevState &s) {
+  return s.m_par ? MotorSlots{s.m_prev_micro, s.m_prev, s.m_micro, s.m_angle}
+                 : MotorSlots{s.m_micro, s.m_angle, s.m_prev_micro, s.m_prev};
+}
 
 // Per-tick input planes, already resolved to device pointers.  `stride` is the
 // per-tick advance (in instances) for fmskf_tick_many.
@@ -428,5 +444,7 @@ int launch_tile(const void *dense, void *tiled, uint32_t rows, uint64_t n, uint3
 int launch_readout(const DevState &s, float *out, hipStream_t st);
 // Status::flt_dltOutAngle_rad [N][4] from the last two raw angles (count = 4 N)
 int launch_motor_dlt(const int16_t *angle, const int16_t *prev, float *out, uint64_t count, hipStream_t st);
+// exchange the two motor history slots of every wheel (the caller flips DevState::m_par)
+int launch_motor_swap(const DevState &s, hipStream_t st);
 
 }  // namespace fmskf

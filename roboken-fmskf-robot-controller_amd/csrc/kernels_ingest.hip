@@ -455,7 +455,16 @@ int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const
 __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t g) {
   const uint64_t i = g >> 2;
   const int w = (int)(g & 3);
-  if (a.present && !((a.present[i] >> w) & 1)) return;
+  if (a.present && !((a.present[i] >> w) & 1)) {
+    // no frame: the wheel's state stays, so its two history slots trade places with the order
+    // the host flips for every wheel (DevState::m_par)
+    const int16_t m0 = a.micro[g], m1 = a.prev_micro[g], a0 = a.angle[g], a1 = a.prev[g];
+    a.micro[g] = m1;
+    a.prev_micro[g] = m0;
+    a.angle[g] = a1;
+    a.prev[g] = a0;
+    return;
+  }
   const uint2 f = reinterpret_cast<const uint2 *>(a.frames)[g];
   const CanWheel o = can_wheel(f.x, f.y, a.stamps[g], a.dir[w], a.micro[g], a.angle[g], a.prev_micro[g],
                                a.prev[g], a.iir_y[g]);
@@ -463,10 +472,8 @@ __device__ __forceinline__ void can_lane(const CanArgs &a, uint64_t n, uint64_t 
   int32_t cy;
   a.sum_lo[g] = sum_add(a.sum_lo[g], o.d, cy);
   if (cy != 0) a.sum_hi[g] += cy;
-  a.prev_micro[g] = a.micro[g];
-  a.micro[g] = a.stamps[g];
-  a.prev[g] = a.angle[g];
-  a.angle[g] = o.angle;
+  a.prev_micro[g] = a.stamps[g];  // over the older slots (DevState::m_par)
+  a.prev[g] = o.angle;
   a.rpm[g] = o.rpm;
   a.curr[g] = o.curr;
 }
@@ -515,15 +522,16 @@ int launch_can(const DevState &s, const uint8_t *frames, const int16_t *stamps,
   a.stamps = stamps;
   a.present = present;
   for (int w = 0; w < 4; w++) a.dir[w] = dir[w];
-  a.micro = s.m_micro;
-  a.angle = s.m_angle;
-  a.prev = s.m_prev;
+  const MotorSlots ms = motor_slots(s);
+  a.micro = ms.micro;
+  a.angle = ms.angle;
+  a.prev = ms.prev;
   a.rpm = s.m_rpm;
   a.curr = s.m_curr;
   a.sum_lo = s.m_sum_lo;
   a.sum_hi = s.m_sum_hi;
   a.iir_y = s.m_iir_y;
-  a.prev_micro = s.m_prev_micro;
+  a.prev_micro = ms.prev_micro;
   // every wheel present and the caller's frames / stamps aligned for the wide loads: one robot
   // per lane; a `present` mask or unaligned buffers: one wheel per lane
   if (!present && ((uintptr_t)frames & 15) == 0 && ((uintptr_t)stamps & 7) == 0) {

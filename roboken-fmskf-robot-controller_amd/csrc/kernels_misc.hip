@@ -306,6 +306,24 @@ __global__ __launch_bounds__(kBlock) void k_motor_dlt(const int16_t *angle, cons
     out[g] = (float)((int32_t)angle[g] - (int32_t)prev[g]) * K::out_rad_per_raw * K::gear_ratio_inv;
 }
 
+// the two stamp / angle history slots of every wheel traded (DevState::m_par), one robot per lane
+__global__ __launch_bounds__(kBlock) void k_motor_swap(uint2 *m0, uint2 *m1, uint2 *a0, uint2 *a1, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint2 x = m0[i], y = m1[i], p = a0[i], q = a1[i];
+  m0[i] = y;
+  m1[i] = x;
+  a0[i] = q;
+  a1[i] = p;
+}
+
+int launch_motor_swap(const DevState &s, hipStream_t st) {
+  if (s.n == 0 || !s.m_micro) return 0;
+  k_motor_swap<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
+      (uint2 *)s.m_micro, (uint2 *)s.m_prev_micro, (uint2 *)s.m_angle, (uint2 *)s.m_prev, s.n);
+  return (int)hipGetLastError();
+}
+
 int launch_motor_dlt(const int16_t *angle, const int16_t *prev, float *out, uint64_t count, hipStream_t st) {
   if (count == 0) return 0;
   const uint64_t b = (count + kBlock - 1) / kBlock;

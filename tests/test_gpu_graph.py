@@ -144,6 +144,11 @@ def test_graph_isr_tick_can_kf6():
         ma, mb = a.get_motors(), b.get_motors()
         for k in ma:
             np.testing.assert_array_equal(ma[k], mb[k], err_msg=k)
+        # the Status fields, incl. the stamps and dlt from the two history slots (round 6: each
+        # replay of the one-call graph starts from the order the capture began with)
+        sa, sb = a.get_motor_status(), b.get_motor_status()
+        for k in sa:
+            np.testing.assert_array_equal(np.asarray(sa[k]).view(np.uint8), np.asarray(sb[k]).view(np.uint8), err_msg=k)
 
 
 def test_graph_errors():

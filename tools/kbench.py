@@ -374,7 +374,7 @@ def bench_io(args, e, n, R, dev, rpm, st):
             e.ingest_can(fr[0], stp[0], torch.from_numpy(rng.integers(0, 16, n).astype(np.uint8)).to(dev))
         # per wheel: frame 8 + stamp 2 in; micro, angle (2 + 2), IIR y / x (4 + 4) and the int64
         # sum read and written; rpm, curr, the previous angle (2 + 2 + 2) written
-        bpr = 4 * (10 + 2 * (2 + 2 + 2 + 2 + 4 + 4) + 2 + 2)  # round 6: 184 B (the sums' low words)
+        bpr = 4 * (10 + (2 + 2 + 2 + 2 + 4 + 4) + (2 + 2 + 4 + 4) + 2 + 2)  # round 6: 168 B
     for k in range(10):
         run(k)
     torch.cuda.synchronize()

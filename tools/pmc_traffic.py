@@ -89,11 +89,11 @@ def secondary(root, out):
 # The rows either side of the tick at 2^20 (bench path_rows): (bench key, kernel substring,
 # kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
 # written (56); WT901 standard poll: row, len, parser count / flags, magnetometer read (60),
-# flags, error, 4 registers (round 6: the other eleven only in the snapshot row), snapshot row,
-# yaw / gyro z written (50; the empty parser window is neither read nor written); CAN RX, four
-# wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y, the sums' low words read
-# (104), those state fields plus rpm and curr written (80; round 6: the sums' high words only on
-# a carry); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
+# flags, error, 2 registers (round 6: the other thirteen only in the snapshot row and the Yaw /
+# GZ words), snapshot row, the Yaw / GZ words written (42; the empty parser window is neither read
+# nor written); CAN RX, four wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y,
+# the sums' low words read (104), the new stamp and angle over the older history slots, IIR y, the
+# sums' low words, rpm and curr written (64; round 6: the sums' high words only on a carry); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128); the fused
 # ISR with and without the CAN RX (below).  The
 # counters are corrected with the KF6 calibration of profiles/pmc_traffic.json (the same
@@ -102,7 +102,7 @@ PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
     ("wt901_ingest_2p20", "k_wt901", 60, 42),
-    ("can_ingest_2p20", "k_can4", 104, 80),
+    ("can_ingest_2p20", "k_can4", 104, 64),
     # the control step (k_ctrl_step): power 1, interpolators 132, FF_PI_D 48, the last step's rpm 8,
     # rpm 8 read; the interpolators' time / speed / accel 36, FF_PI_D 48, the rpm 8 and the
     # currents 8 written (round 6)
@@ -113,9 +113,9 @@ PATHS = [
     # four float now_val) and writes (100; 152 before round 6 formed vel_tgt / now_tgt / now_ctrl
     # on demand and kept now_val as the step's rpm), the 0x200 frame (8 w)
     ("isr_kf6_2p20", "k_isr_kf6", 124 + 189, 108 + 100 + 8),
-    # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 120 / 96, the rpm
+    # with the tick's CAN RX fused in (fmskf_isr_tick_can): + the CAN row's 104 / 64, the rpm
     # plane no longer read
-    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 189 + 104, 108 + 100 + 8 + 80),
+    ("isr_can_kf6_2p20", "k_isr_kf6", 124 - 8 + 189 + 104, 108 + 100 + 8 + 64),
     # the reference-semantics ISR (k_isr_rs) on the motor state: the RS tick's 84 / 56 with the
     # control step's 189 / 100 and the frame; with the CAN RX fused in, the rpm and sums not read
     ("isr_rs_2p20", "k_isr_rs", 84 + 189, 56 + 100 + 8),
@@ -124,10 +124,10 @@ PATHS = [
     # frame
     ("isr_ekf9_2p20", "k_isr_ekf9", 232 + 197, 216 + 100 + 8),
     # round 6: the previous sums neither read nor written while they equal the motor sums (PS)
-    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 189 + 104, 56 - 32 + 100 + 8 + 80),
-    # the EKF9 ISR with the tick's CAN RX fused in: + the CAN row's 120 / 96, the control step's
+    ("isr_can_rs_2p20", "k_isr_rs", 84 - 8 - 32 - 32 + 189 + 104, 56 - 32 + 100 + 8 + 64),
+    # the EKF9 ISR with the tick's CAN RX fused in: + the CAN row's 104 / 64, the control step's
     # rpm plane no longer read
-    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 197 - 8 + 104, 216 + 100 + 8 + 80),
+    ("isr_can_ekf9_2p20", "k_isr_ekf9", 232 + 197 - 8 + 104, 216 + 100 + 8 + 64),
 ]
 
 
