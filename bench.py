@@ -340,7 +340,7 @@ def secondary_configs(dev, stream, ticks: int, trig):
 
 # the WT901 standard poll's bytes (PATH_BYTES wt901_ingest_2p20) and the C610 RX of four wheels
 # (can_ingest_2p20)
-WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4
+WT901_POLL_BYTES = 48 + 4 + 2 + 2 + 4 + 24 + 4
 CAN_RX_BYTES = 4 * (10 + (2 + 2 + 2 + 2 + 4 + 4) + (2 + 2 + 4 + 4) + 2 + 2)
 # the vehicle control step (control_step_2p20): power 1, interpolators 132 (every field but the
 # acceleration, which update() writes before it reads it), FF_PI_D integral / LPF 48, the last
@@ -358,13 +358,14 @@ PATH_BYTES = {
     "rs_tick_2p20_device_state": 140,
     # WT901 standard poll: row 48 + len 4, the parser count and update flags 2 r, flags and error
     # 2 w, 2 registers 4 w (TEMP, VERSION: of the other thirteen the poll writes, eleven live in
-    # the snapshot row and GZ / Yaw in the Yaw / GZ dword, round 6), magnetometer 6 r, the
-    # snapshot row 32 w (the words updateData reads: the Data page is formed at readout), the Yaw
-    # / GZ words 4 w (what the tick reads as its yaw and gyro z); the parser window is empty
+    # the snapshot row and GZ / Yaw in the Yaw / GZ dword, round 6), the snapshot row 24 w (the
+    # words updateData reads but the magnetometer's, which the standard poll does not carry and
+    # the snapshot takes from sReg: round 6; the Data page is formed at readout), the Yaw / GZ
+    # words 4 w (what the tick reads as its yaw and gyro z); the parser window is empty
     # before and after such a poll, so its words are neither read nor written (round 4: 197 B,
     # with the window words, q_init read and the 64-byte page written; round 5: 132 B, the 15
     # registers written to sReg as well as to the row; round 6: 110 B with GZ / Yaw in sReg and
-    # the yaw / gyro z floats, then 102)
+    # the yaw / gyro z floats, then 102, then 88 without the magnetometer read and row words)
     "wt901_ingest_2p20": WT901_POLL_BYTES,
     # CAN RX, per wheel: frame 8 + stamp 2 in; micro, angle, previous angle, previous stamp, IIR
     # output y and the low word of the int64 sum read; the new stamp and angle (over the older

@@ -39,10 +39,11 @@ struct CkHeader {
   // rs_prev_at; [4][pitch] planes before); bit 1, the motor group's angle sums as split low /
   // high words (round 6, fmskf_internal.hpp m_sum_lo; int64 [4][pitch] planes before); bit 2, the
   // IMU group's yaw / gyro z as the Yaw / GZ register words (round 6, DevState::imu_yg; two float
-  // planes before); bit 3, the control group's rpm of the last step (round 6, CtrlDev::rpm_prev)
+  // planes before); bit 3, the control group's rpm of the last step (round 6, CtrlDev::rpm_prev);
+  // bit 4, the IMU snapshot as 12-word rows plus the detached magnetometer (round 6, kRowWords)
   uint32_t layout;
 };
-constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u, kCkImuYg = 4u, kCkRpmPrev = 8u;
+constexpr uint32_t kCkPrevRows = 1u, kCkSumSplit = 2u, kCkImuYg = 4u, kCkRpmPrev = 8u, kCkImuRow = 16u;
 struct CkSection {
   void *dev;
   size_t bytes;
@@ -67,7 +68,8 @@ std::vector<CkSection> ck_sections(fmskf_ctx *h, uint32_t groups) {
     v.push_back({s.imu_flags, (size_t)n});
     v.push_back({s.imu_err, (size_t)n});
     v.push_back({s.imu_qinit, (size_t)4 * n * 4});
-    v.push_back({s.imu_snap, (size_t)kSnapWords * n * 2});
+    v.push_back({s.imu_snap, (size_t)kRowWords * n * 2});
+    v.push_back({s.imu_mag, (size_t)4 * n * 2});
     v.push_back({s.imu_yg, (size_t)n * 4});
     v.push_back({s.imu_qprev, (size_t)4 * n * 4});
   }
@@ -103,7 +105,7 @@ void ck_layout(const fmskf_ctx *h, CkHeader *hd) {
   hd->elem = h->d.elem;
   hd->ctrl_tile = FMSKF_CTRL_TILED ? tile_w_elem(4) : 0;
   hd->m_pitch = plane_pitch(h->s.n);
-  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit | kCkImuYg | kCkRpmPrev;
+  hd->layout = (h->s.prev_sum ? kCkPrevRows : 0u) | kCkSumSplit | kCkImuYg | kCkRpmPrev | kCkImuRow;
   const uint64_t w = tile_w_elem(4);
   hd->ctrl_pitch = FMSKF_CTRL_TILED ? std::max(h->s.pitch, (h->s.n + w - 1) / w * w) : h->s.pitch;
 }

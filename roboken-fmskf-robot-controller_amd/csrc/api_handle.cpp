@@ -110,7 +110,8 @@ void zero_imu(fmskf_ctx *h) {
   hip_check(hipMemsetAsync(s.imu_flags, 0, n, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_err, 0, n, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_qinit, 0, 4 * n * 4, st), "reset imu");
-  hip_check(hipMemsetAsync(s.imu_snap, 0, kSnapWords * n * 2, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_snap, 0, kRowWords * n * 2, st), "reset imu");
+  hip_check(hipMemsetAsync(s.imu_mag, 0, 4 * n * 2, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_yg, 0, n * 4, st), "reset imu");
   hip_check(hipMemsetAsync(s.imu_qprev, 0, 4 * n * 4, st), "reset imu");
 }
@@ -140,7 +141,8 @@ void ensure_imu(fmskf_ctx *h) {
   s.imu_flags = h->alloc<uint8_t>(n);
   s.imu_err = h->alloc<uint8_t>(n);
   s.imu_qinit = h->alloc<float>(4 * n);
-  s.imu_snap = h->alloc<int16_t>(kSnapWords * n);
+  s.imu_snap = h->alloc<int16_t>(kRowWords * n);
+  s.imu_mag = h->alloc<int16_t>(4 * n);
   s.imu_yg = h->alloc<uint32_t>(n);
   s.imu_qprev = h->alloc<float>(4 * n);
   zero_imu(h);

@@ -176,6 +176,40 @@ __device__ __forceinline__ float tick_word_sel(bool word, uint32_t w, float conv
 __device__ __forceinline__ float tick_yaw(bool word, uint32_t w) { return tick_word_sel(word, w, imu_yaw_deg(w)); }
 __device__ __forceinline__ float tick_gz(bool word, uint32_t w) { return tick_word_sel(word, w, imu_gz_dps(w)); }
 
+// the snapshot row of robot i (DevState::imu_snap: 12 int16 words, AX AY AZ GX GY Roll Pitch
+// Q0-Q3 and the flags) as six dwords (three 8-byte loads), and the page's 16 words in
+// imu_data_page's order with the snapshot's magnetometer words
+__device__ __forceinline__ void snap_row_load(const int16_t *snap, uint64_t i, uint32_t rw[6]) {
+  const uint2 *p = reinterpret_cast<const uint2 *>(snap + 12 * i);
+  const uint2 a = p[0], b = p[1], c = p[2];
+  rw[0] = a.x;
+  rw[1] = a.y;
+  rw[2] = b.x;
+  rw[3] = b.y;
+  rw[4] = c.x;
+  rw[5] = c.y;
+}
+__device__ __forceinline__ void snap_page_words(const uint32_t rw[6], int16_t hx, int16_t hy, int16_t hz,
+                                                int16_t w[16]) {
+  int16_t r[12];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    r[2 * k] = (int16_t)(rw[k] & 0xFFFFu);
+    r[2 * k + 1] = (int16_t)(rw[k] >> 16);
+  }
+#pragma unroll
+  for (int k = 0; k < 5; k++) w[k] = r[k];
+  w[5] = hx;
+  w[6] = hy;
+  w[7] = hz;
+  w[8] = r[5];
+  w[9] = r[6];
+#pragma unroll
+  for (int k = 0; k < 4; k++) w[10 + k] = r[7 + k];
+  w[14] = r[11];
+  w[15] = 0;
+}
+
 // the Data page of a snapshot row (same operations and order as updateData): yaw = angle[2]
 // and gz = gyro[2] from the Yaw / GZ words; qi: q_init as it was when the poll ran
 __device__ __forceinline__ void imu_data_page(const int16_t *w, float yaw, float gz, const float qi[4],

@@ -12,9 +12,13 @@ namespace fmskf {
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
-// WT901 snapshot rows (DevState::imu_snap, fmskf_device.hpp imu_data_page): int16 words per
-// robot, and word 14's flags: a successful poll happened / that poll latched q_init
-constexpr int kSnapWords = 16;
+// WT901 snapshot (fmskf_device.hpp imu_data_page): the page's 16 int16 words per robot, word 14
+// the flags: a successful poll happened / that poll latched q_init.  Stored (round 6) as a
+// 12-word row (DevState::imu_snap: AX AY AZ GX GY Roll Pitch Q0-Q3, the flags; kRowWords) plus the
+// magnetometer, which a standard poll does not carry: the snapshot's HX-HZ are the sReg ones
+// unless a poll after the last successful one wrote them (then DevState::imu_mag holds the
+// snapshot's; kernels_ingest.hip F_MAGDET)
+constexpr int kSnapWords = 16, kRowWords = 12;
 enum : int { kSnapValid = 1, kSnapLatched = 2 };
 
 // Device-resident state of one handle.  Every array is plane-major (SoA): element k of
@@ -47,7 +51,8 @@ struct DevState {
   float *imu_qinit = nullptr;     // q_init [4][N]
   // IMU_IF::Data is not stored: the WT901 kernel keeps the register words updateData reads
   // (fmskf_device.hpp imu_data_page), and the readers form the page
-  int16_t *imu_snap = nullptr;    // snapshot rows [N][16] of the last successful poll
+  int16_t *imu_snap = nullptr;    // snapshot rows [N][12] of the last successful poll (kRowWords)
+  int16_t *imu_mag = nullptr;     // [N][4] the snapshot's HX-HZ while sReg's moved on (F_MAGDET)
   // the Yaw (low half) and GZ (high half) register words of the last successful poll [N]: what
   // the tick reads as its yaw and gyro z (Data.angle[2], Data.gyro[2]: fmskf_device.hpp
   // imu_yaw_deg / imu_gz_dps, exact both ways).  Round 6: one dword plane instead of the two

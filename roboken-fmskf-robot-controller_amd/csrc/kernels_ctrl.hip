@@ -238,15 +238,10 @@ __global__ __launch_bounds__(kBlock) void k_vehicle_info(const float *ro, ImuVie
     float d[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) d[k] = 0.0f;
-    const uint4 r0 = reinterpret_cast<const uint4 *>(im.snap + (uint64_t)kSnapWords * i)[0];
-    const uint4 r1 = reinterpret_cast<const uint4 *>(im.snap + (uint64_t)kSnapWords * i)[1];
-    const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint32_t rw[6];
+    snap_row_load(im.snap, i, rw);
     int16_t w[kSnapWords];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      w[2 * k] = (int16_t)(rw[k] & 0xFFFFu);
-      w[2 * k + 1] = (int16_t)(rw[k] >> 16);
-    }
+    snap_page_words(rw, 0, 0, 0, w);  // (the record takes no magnetometer field)
     if (!err && (w[14] & kSnapValid)) {
       const float *q = (w[14] & kSnapLatched) ? im.qprev : im.qinit;
       const float qi[4] = {q[i], q[n + i], q[2 * n + i], q[3 * n + i]};

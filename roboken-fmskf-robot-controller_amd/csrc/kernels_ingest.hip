@@ -35,26 +35,30 @@ enum : uint32_t { F_ACC = 0x01, F_GYRO = 0x02, F_ANGLE = 0x04, F_MAG = 0x08, F_Q
 // poll writes them once, into the row and the dword).  Any other poll, fmskf_get_imu_regs and a
 // checkpoint write them back first (row_regs_out).
 enum : uint32_t { F_ROWREGS = 0x40 };
+// not a firmware flag either (round 6): the snapshot's magnetometer words are DevState::imu_mag's,
+// since a poll after the last successful one wrote HX-HZ (it saved their earlier values there);
+// otherwise they are sReg's (a standard poll carries no magnetometer frame, so its snapshot
+// takes the registers as they are, and neither reads nor writes them)
+enum : uint32_t { F_MAGDET = 0x20 };
 // bit k of a register's row-resident index (AX AY AZ GX GY Roll Pitch Q0-Q3 -> 0..10, GZ 11,
-// Yaw 12), or 0
+// Yaw 12), or for HX-HZ bits 13-15 (not row-resident: a poll that writes them), or 0
 __device__ __forceinline__ uint32_t rowreg_bit(uint32_t r) {
   return r >= R_AX && r < R_GZ ? 1u << (r - R_AX)
          : r == R_ROLL || r == R_ROLL + 1 ? 1u << (5 + r - R_ROLL)
          : r >= R_Q0 && r <= R_Q3 ? 1u << (7 + r - R_Q0)
-         : r == R_GZ ? 1u << 11 : r == R_YAW ? 1u << 12 : 0u;
+         : r == R_GZ ? 1u << 11 : r == R_YAW ? 1u << 12
+         : r >= R_HX && r <= R_HZ ? 1u << (13 + r - R_HX) : 0u;
 }
-// the row-resident registers (words 0-4, 8-13 of imu_data_page's row in snapshot-row order, then
-// the imu_yg dword's GZ and Yaw) written back to sReg, except those in `skip` (rowreg_bit mask:
-// registers written since)
+// the row-resident registers (snapshot-row words 0-10, then the imu_yg dword's GZ and Yaw)
+// written back to sReg, except those in `skip` (rowreg_bit mask: registers written since)
 __device__ __forceinline__ void row_regs_out(const int16_t *snap, const uint32_t *yg, int16_t *reg, uint64_t n,
                                              uint64_t i, uint32_t skip = 0) {
-  const uint4 r0 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[0];
-  const uint4 r1 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[1];
-  const uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};  // word k in w[k / 2]
+  uint32_t w[6];  // word k in w[k / 2]
+  snap_row_load(snap, i, w);
   // (register, snapshot word) of the eleven, in rowreg_bit order
   constexpr uint32_t kReg[11] = {R_AX, R_AX + 1, R_AX + 2, R_GX, R_GX + 1, R_ROLL, R_ROLL + 1,
                                  R_Q0, R_Q0 + 1, R_Q0 + 2, R_Q0 + 3};
-  constexpr int kWord[11] = {0, 1, 2, 3, 4, 8, 9, 10, 11, 12, 13};
+  constexpr int kWord[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10};
 #pragma unroll
   for (int k = 0; k < 11; k++) {
     const uint32_t v = w[kWord[k] / 2];
@@ -89,7 +93,8 @@ struct Wt901Args {
   uint8_t *flags;
   uint8_t *err;
   float *qinit;
-  int16_t *snap;  // [N][16] snapshot rows (fmskf_device.hpp imu_data_page)
+  int16_t *snap;  // [N][12] snapshot rows (fmskf_device.hpp snap_row_load)
+  int16_t *mag;   // [N][4] the snapshot's HX-HZ while F_MAGDET
   uint32_t *yg;   // [N] Yaw / GZ words of the snapshot (DevState::imu_yg)
   float *qprev;
 };
@@ -208,16 +213,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   if (i >= n) return;
   Wt901Parser ps;
   const uint8_t *p = a.bytes + i * (uint64_t)a.stride;
-  // Every unconditional load first -- the count, flags, length, the poll row and the
-  // magnetometer registers -- so a wave waits for memory once before parsing (the parser words,
-  // read only when bytes are pending, and a non-standard poll's register reads come after)
+  // Every unconditional load first -- the count, flags, length and the poll row -- so a wave
+  // waits for memory once before parsing (the parser words, read only when bytes are pending, and
+  // a non-standard poll's register reads come after)
   const uint32_t cnt_in = a.cnt[i];
   const uint32_t flags_in = a.flags[i];
   const uint32_t len_in = a.len[i];
   int16_t *reg = a.reg;
-  int16_t rm[3];
+  // the magnetometer registers before this poll: a poll that is not the standard one may write
+  // them and fail, and the snapshot must then keep these (F_MAGDET; read before its frames land)
+  int16_t rm[3] = {0, 0, 0};
+  const auto load_mag = [&] {
 #pragma unroll
-  for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+    for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
+  };
   uint4 ch[4];
   if constexpr (VEC) {
     const uint32_t nch = (a.stride + 15) / 16;  // <= 4, wave-uniform
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
     ps.lo = (uint64_t)a.parser[i] | ((uint64_t)a.parser[n + i] << 32);
     ps.hi = (uint64_t)a.parser[2 * n + i];
   }
-  ps.flags = flags_in & ~F_ROWREGS;
+  ps.flags = flags_in & ~(F_ROWREGS | F_MAGDET);  // the firmware's update flags
   const bool row_regs = (flags_in & F_ROWREGS) != 0;
   const uint32_t len = len_in < a.stride ? len_in : a.stride;
   // the standard 10 ms poll (0x51 acc, 0x52 gyro, 0x53 angle, 0x59 quaternion)
@@ -273,6 +282,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
       if ((uint32_t)f < nfr) fast = fast && ok;
     }
     std4 = fast && nfr == 4 && rb(1) == 0x51u && rb(12) == 0x52u && rb(23) == 0x53u && rb(34) == 0x59u;
+    if (!std4) load_mag();
     if (std4) {
       // CopeWitData of the four frames with their register runs known statically.  Round 6: of
       // the 15 registers the four frames write, thirteen are written once (F_ROWREGS): AX AY AZ
@@ -314,6 +324,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
     }
     }
   } else {
+    load_mag();
     for (uint32_t b = 0; b < len; b++) ps.byte(p[b], a, i);
   }
   // any other poll worked on the register file itself: the row-resident registers its frames did
@@ -329,6 +340,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   a.err[i] = ok ? 0 : 1;
   // the standard poll (always a successful one) leaves its row-resident registers in the row
   if (std4) flags |= F_ROWREGS;
+  // a successful poll's snapshot takes the magnetometer registers as they are (F_MAGDET clear);
+  // after a failed one that wrote them the snapshot's are the ones before, kept in imu_mag (once:
+  // if they were detached already, imu_mag holds the snapshot's)
+  if (!ok) {
+    if (flags_in & F_MAGDET) {
+      flags |= F_MAGDET;
+    } else if ((ps.roww >> 13) & 7u) {
+      reinterpret_cast<uint2 *>(a.mag)[i] = make_uint2((uint32_t)(uint16_t)rm[0] | ((uint32_t)(uint16_t)rm[1] << 16),
+                                                       (uint32_t)(uint16_t)rm[2]);
+      flags |= F_MAGDET;
+    }
+  }
   if (cnt_in != 0 || cnt != 0) {
     a.parser[i] = (uint32_t)lo;
     a.parser[n + i] = (uint32_t)(lo >> 32);
@@ -338,7 +361,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
   a.flags[i] = (uint8_t)flags;
   if (!ok) return;
   // updateData, imu_if_wt901c.cpp:91-129: the page is not formed here.  Its 16 words are kept
-  // (the snapshot row: one 32-byte row, two 16-byte stores) and the yaw and gyro z the tick reads;
+  // (the snapshot row: 24 bytes, three 8-byte stores -- round 6: the magnetometer's stay in sReg --
+  // and the Yaw / GZ words the tick reads);
   // fmskf_get_imu and VehicleInfo form the page from them (imu_data_page), so a poll moves 157 B
   // instead of 197 (the 64-byte page written, q_init read; 132 B with the empty-window rule above).  Only a latching poll reads q_init,
   // to keep it (qprev) for the page of that very poll, which used the old one.
@@ -361,9 +385,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) rq[k] = reg[(R_Q0 + k) * n + i];
-    // any other poll may have carried a magnetometer frame: read the registers as it left them
-#pragma unroll
-    for (int k = 0; k < 3; k++) rm[k] = reg[(R_HX + k) * n + i];
   }
   // Data.angle[2] / Data.gyro[2] as their register words (fmskf_device.hpp imu_yaw_deg)
   a.yg[i] = (uint32_t)(uint16_t)rr[2] | ((uint32_t)(uint16_t)rg[2] << 16);
@@ -377,9 +398,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(FMSKF_WT
     }
   }
   const auto u = [](int16_t lo, int16_t hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
-  uint4 *row = reinterpret_cast<uint4 *>(a.snap + (uint64_t)kSnapWords * i);
-  row[0] = make_uint4(u(ra[0], ra[1]), u(ra[2], rg[0]), u(rg[1], rm[0]), u(rm[1], rm[2]));
-  row[1] = make_uint4(u(rr[0], rr[1]), u(rq[0], rq[1]), u(rq[2], rq[3]), snapf);
+  uint2 *row = reinterpret_cast<uint2 *>(a.snap + (uint64_t)kRowWords * i);  // fmskf_device.hpp snap_row_load
+  row[0] = make_uint2(u(ra[0], ra[1]), u(ra[2], rg[0]));
+  row[1] = make_uint2(u(rg[1], rr[0]), u(rr[1], rq[0]));
+  row[2] = make_uint2(u(rq[1], rq[2]), u(rq[3], (int16_t)snapf));
 }
 
 // the register file made whole (fmskf_get_imu_regs, a checkpoint): robots whose row-resident
@@ -403,19 +425,26 @@ int launch_wt901_regs_sync(const DevState &s, hipStream_t st) {
 
 // IMU_IF::Data [16][N] of every robot from its snapshot (fmskf_get_imu): zeros until the first
 // successful poll, like the firmware's zero-initialised page
-__global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const uint32_t *yg, const float *qinit,
+__global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const int16_t *mag, const int16_t *reg,
+                                                     const uint8_t *flags, const uint32_t *yg, const float *qinit,
                                                      const float *qprev, uint64_t n, float *out) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  int16_t w[kSnapWords];
-  const uint4 r0 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[0];
-  const uint4 r1 = reinterpret_cast<const uint4 *>(snap + (uint64_t)kSnapWords * i)[1];
-  const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+  uint32_t rw[6];
+  snap_row_load(snap, i, rw);
+  // the snapshot's magnetometer: sReg's, or the ones a later failed poll displaced (F_MAGDET)
+  int16_t hm[3];
+  if (flags[i] & F_MAGDET) {
+    const uint2 m = reinterpret_cast<const uint2 *>(mag)[i];
+    hm[0] = (int16_t)(m.x & 0xFFFFu);
+    hm[1] = (int16_t)(m.x >> 16);
+    hm[2] = (int16_t)(m.y & 0xFFFFu);
+  } else {
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    w[2 * k] = (int16_t)(rw[k] & 0xFFFFu);
-    w[2 * k + 1] = (int16_t)(rw[k] >> 16);
+    for (int k = 0; k < 3; k++) hm[k] = reg[(R_HX + k) * n + i];
   }
+  int16_t w[kSnapWords];
+  snap_page_words(rw, hm[0], hm[1], hm[2], w);
   float d[16];
   if (w[14] & kSnapValid) {
     const float *q = (w[14] & kSnapLatched) ? qprev : qinit;
@@ -432,7 +461,8 @@ __global__ __launch_bounds__(kBlock) void k_imu_data(const int16_t *snap, const 
 
 int launch_imu_data(const DevState &s, float *out, hipStream_t st) {
   if (s.n == 0) return 0;
-  k_imu_data<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_yg, s.imu_qinit,
+  k_imu_data<<<dim3((unsigned)((s.n + kBlock - 1) / kBlock)), kBlock, 0, st>>>(s.imu_snap, s.imu_mag, s.imu_reg,
+                                                                                s.imu_flags, s.imu_yg, s.imu_qinit,
                                                                                 s.imu_qprev, s.n, out);
   return (int)hipGetLastError();
 }
@@ -440,8 +470,8 @@ int launch_imu_data(const DevState &s, float *out, hipStream_t st) {
 int launch_wt901(const DevState &s, const uint8_t *bytes, uint32_t stride, const uint32_t *len,
                  int latch_qinit, uint32_t read_reg_index, hipStream_t st) {
   Wt901Args a{s.n,       bytes,      stride,   len,        latch_qinit,  read_reg_index, s.imu_reg,
-              s.imu_parser, s.imu_cnt, s.imu_flags, s.imu_err, s.imu_qinit, s.imu_snap, s.imu_yg,
-              s.imu_qprev};
+              s.imu_parser, s.imu_cnt, s.imu_flags, s.imu_err, s.imu_qinit, s.imu_snap, s.imu_mag,
+              s.imu_yg,    s.imu_qprev};
   const dim3 g((unsigned)((s.n + kBlock - 1) / kBlock));
   const bool vec = stride % 16 == 0 && stride <= 64 && ((uintptr_t)bytes & 15) == 0;
   if (vec) k_wt901<true><<<g, kBlock, 0, st>>>(a);

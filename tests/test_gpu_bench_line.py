@@ -17,10 +17,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SECONDARY_BYTES = {"cfg3_ekf9_2p22": 448, "cfg5_kf12d_2p20": 1504, "cfg2_kf6_2p24": 232,
                    "cfg2_kf6_comp_pos_2p20": 272, "cfg3_ekf9_comp_pos_2p22": 488, "cfg4_shard_kf6_2p21": 232}
 PATH_BYTES = {"rs_tick_2p20": 140, "rs_tick_2p20_padded_sums": 140, "rs_tick_2p20_device_state": 140,
-              "wt901_ingest_2p20": 102, "can_ingest_2p20": 168, "control_step_2p20": 297,
-              "isr_kf6_2p20": 529, "firmware_loop_kf6_2p20": 703.2, "isr_can_kf6_2p20": 689,
+              "wt901_ingest_2p20": 88, "can_ingest_2p20": 168, "control_step_2p20": 297,
+              "isr_kf6_2p20": 529, "firmware_loop_kf6_2p20": 701.8, "isr_can_kf6_2p20": 689,
               "isr_ekf9_2p20": 753, "isr_can_ekf9_2p20": 913, "isr_rs_2p20": 437, "isr_can_rs_2p20": 501,
-              "firmware_loop_rs_fused_2p20": 511.2, "firmware_loop_kf6_fused_2p20": 695.2}
+              "firmware_loop_rs_fused_2p20": 509.8, "firmware_loop_kf6_fused_2p20": 693.8}
 
 
 def test_driver_bench_line_contract():

@@ -577,8 +577,10 @@ def test_wt901_data_page_across_latches(orc, stride):
                     ts = (0x51, 0x52, 0x53)
                 elif r < 0.7:  # the standard poll (fast path)
                     ts = (0x51, 0x52, 0x53, 0x59)
-                elif r < 0.85:  # no quaternion frame: the poll fails, the page stays
+                elif r < 0.80:  # no quaternion frame: the poll fails, the page stays
                     ts = (0x51, 0x53)
+                elif r < 0.85:  # a failed poll that writes the magnetometer: the page keeps the
+                    ts = (0x54, 0x51)  # earlier HX-HZ (round 6: F_MAGDET, imu_mag)
                 elif r < 0.92:  # a register-read reply (0x5F at imu_read_reg 0x51: Q0-Q3) alone
                     ts = (0x5F,)
                 else:  # a quaternion frame among others, through the parser

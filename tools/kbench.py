@@ -363,7 +363,7 @@ def bench_io(args, e, n, R, dev, rpm, st):
         run = lambda k: e.ingest_wt901(polls[k % len(polls)], lens)  # noqa: E731
         # the standard poll (bench.py PATH_BYTES): row 48 + len 4, parser window / count / flags r+w,
         # error, 15 registers, magnetometer + q_init read, Data page written
-        bpr = 48 + 4 + 2 + 2 + 4 + 6 + 32 + 4  # round 6: 13 registers only in the snapshot row / Yaw-GZ words
+        bpr = 48 + 4 + 2 + 2 + 4 + 24 + 4  # round 6: 88 B (13 registers only in the row / Yaw-GZ words, no magnetometer)
     else:  # can
         rng = np.random.default_rng(2)
         fr = [torch.from_numpy(rng.integers(0, 256, (n, 4, 8)).astype(np.uint8)).to(dev) for _ in range(4)]

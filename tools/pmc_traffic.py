@@ -88,10 +88,10 @@ def secondary(root, out):
 
 # The rows either side of the tick at 2^20 (bench path_rows): (bench key, kernel substring,
 # kernel read / write bytes per robot).  RS: px, py, prev, sums, yaw, rpm read (84), x and prev
-# written (56); WT901 standard poll: row, len, parser count / flags, magnetometer read (60),
+# written (56); WT901 standard poll: row, len, parser count / flags read (54),
 # flags, error, 2 registers (round 6: the other thirteen only in the snapshot row and the Yaw /
-# GZ words), snapshot row, the Yaw / GZ words written (42; the empty parser window is neither read
-# nor written); CAN RX, four wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y,
+# GZ words), the 24-byte snapshot row, the Yaw / GZ words written (34; the empty parser window is
+# neither read nor written, and round 6 reads no magnetometer register); CAN RX, four wheels: frame, stamp, micro, angle, previous angle / stamp, IIR y,
 # the sums' low words read (104), the new stamp and angle over the older history slots, IIR y, the
 # sums' low words, rpm and curr written (64; round 6: the sums' high words only on a carry); the KF6 with FMSKF_CFG_COMP_POS (k_kf6p at
 # 2^20): the tick's 124 / 108 plus the five low-part rows read and written (144 / 128); the fused
@@ -101,7 +101,7 @@ def secondary(root, out):
 PATHS = [
     ("rs_tick_2p20", "k_rs2", 84, 56),
     ("rs_tick_2p20_padded_sums", "k_rs2", 84, 56),
-    ("wt901_ingest_2p20", "k_wt901", 60, 42),
+    ("wt901_ingest_2p20", "k_wt901", 54, 34),
     ("can_ingest_2p20", "k_can4", 104, 64),
     # the control step (k_ctrl_step): power 1, interpolators 132, FF_PI_D 48, the last step's rpm 8,
     # rpm 8 read; the interpolators' time / speed / accel 36, FF_PI_D 48, the rpm 8 and the
