@@ -202,7 +202,8 @@ struct Wt901Parser {
 // (kbench, three passes, profiles/r5_ab.json); capped at 7 or 8 waves it spills (29.4, 34.8 us).
 // Round 6, the bytes read from the chunk registers where used (62 VGPRs, 103 SGPRs: 7 waves per
 // SIMD): 6 here (7 waves) against 8 (63 VGPRs, 78 SGPRs, 8 waves) 21.3 / 21.3-21.6 us at 2^20,
-// 84.3 / 86.4 at 2^22 (two passes, one box)
+// 84.3 / 86.4 at 2^22 (two passes, one box); with the 88-byte poll (54 VGPRs) 17.7-17.8 / 17.9-18.0 us
+// at 2^20, 65.0-65.1 / 65.3-65.6 at 2^22 (three passes, profiles/r6_ab.json `wt901_wpe_after_row_split`)
 #ifndef FMSKF_WT901_WPE
 #define FMSKF_WT901_WPE 6
 #endif
