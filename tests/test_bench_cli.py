@@ -58,3 +58,25 @@ def test_mall_regime_and_traffic_provenance():
     for f in tj["source"]["committed_as"]:
         assert os.path.exists(os.path.join(ROOT, f)), f
     assert bench.traffic_of({"kernel": "x"}) == (None, None)
+
+
+def test_path_byte_models_agree():
+    """The path rows' algorithmic bytes per robot (bench.PATH_BYTES, the `roofline.achieved`
+    numerator) and the read / write split tools/pmc_traffic.py checks the FETCH / WRITE counters
+    against are one model: every row both name sums to the same bytes, and so does the committed
+    profiles/pmc_traffic_paths.json (bytes per launch at 2^20 robots)."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic  # noqa: E402
+    secondary = {"cfg2_kf6_comp_pos_2p20": 272}
+    seen = 0
+    for key, _kernel, rd, wr in pmc_traffic.PATHS:
+        want = bench.PATH_BYTES.get(key, secondary.get(key))
+        assert want is not None, key
+        assert rd + wr == want, (key, rd, wr, want)
+        seen += 1
+    assert seen >= 10
+    committed = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_paths.json")))
+    for key, _kernel, rd, wr in pmc_traffic.PATHS:
+        if key in committed:
+            assert committed[key]["algorithmic_bytes_per_launch"] == (rd + wr) << 20, key
